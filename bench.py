@@ -1,0 +1,289 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident throughput of the MI355X rx classifier.
+
+One "step" = one pass of the hot path (mOS ProcessPacket checks + ip_fast_csum
++ TCPCalcChecksum + Toeplitz RSS / queue map) over one batch per GPU, inputs
+already resident in HBM.  The headline workload is BASELINE config #3
+(1500 B MTU TCP segments, 1M flows, batch 64K) whose GB/s the north star
+prices against the HBM roofline; the same run also measures config #2
+(64 B, 1 flow, batch 32K; Mpkts/s) and config #4 (IMIX, batch 256K).
+
+Multi-GPU (torchrun, one process per GPU): batches are split round-robin over
+the GPUs with no collective on the data path (`scaling: weak`); gloo carries
+only the barrier and the max-over-ranks of the timed region.
+
+Each rank cycles over several copies of its batch at distinct HBM addresses so
+the working set exceeds the 256 MiB Infinity Cache: every timed pass reads HBM.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mos-networking-stack_amd"))
+
+import numpy as np  # noqa: E402
+
+import mosrx  # noqa: E402  (loads libmosrx.so before torch so one HIP runtime is used)
+
+METRIC = "Mpkts/s + GB/s device-resident checksum+RSS classify, 64B & 1500B batches"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+DESC_BYTES, RESULT_BYTES = 6, 16
+L3_BYTES = 256 << 20
+
+WORKLOADS = {
+    # key: (trace kind, batch, label)
+    "M1500": (mosrx.TRACE_M1500, 65_536, "1xMI355X 1500B MTU TCP segments, 1M distinct 5-tuples, batch=64K (BASELINE config #3)"),
+    "S64": (mosrx.TRACE_S64, 32_768, "1xMI355X 64B TCP, 1 flow, batch=32K (BASELINE config #2), full verdict"),
+    "S64_hdr": (mosrx.TRACE_S64, 32_768, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum)"),
+    "IMIX": (mosrx.TRACE_IMIX, 262_144, "IMIX 60/590/1514 7:4:1, 1M flows, batch=256K (BASELINE config #4)"),
+}
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+class Dist:
+    """Barrier + max-reduce over ranks (gloo, CPU); nothing on the data path."""
+
+    def __init__(self, ws: int, rank: int):
+        self.ws, self.rank, self.pg = ws, rank, None
+        if ws > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=rank, world_size=ws)
+            self.dist = dist
+
+    def barrier(self):
+        if self.ws > 1:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.ws == 1:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.ws > 1:
+            self.dist.destroy_process_group()
+
+
+def algo_bytes(tr: mosrx.Trace) -> int:
+    """B_i = caplen_i + 6 (offset+len descriptor) + 16 (result record)."""
+    return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES)
+
+
+def load_pmc(key: str):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d.get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def measure(ctx, dist, key, steps, warmup, rank):
+    kind, batch, label = WORKLOADS[key]
+    params = mosrx.default_params(skip_tcp_csum=1 if key == "S64_hdr" else 0)
+    ctx.set_params(params)
+    # rank r owns the batches b = r, r+N, ... of the job's round-robin split; the
+    # synthetic content differs per rank (seed), the shape does not.
+    tr = mosrx.Trace(kind, batch, seed=0 if rank == 0 else 0x6D4F5321 + kind + 1000 * rank)
+    ncopy = max(2, -(-2 * L3_BYTES // max(tr.frames_bytes, 1)))
+    ncopy = min(ncopy, 256)
+    dbs = [ctx.upload(tr.frames, tr.off, tr.len, frames_bytes=tr.frames_bytes, max_len=tr.max_len)
+           for _ in range(ncopy)]
+    ab = algo_bytes(tr)
+    # warmup (untimed)
+    if warmup:
+        ctx.time_dev(dbs, warmup)
+    ctx.device_sync()
+    dist.barrier()
+    t0 = time.perf_counter()
+    dev_ms = ctx.time_dev(dbs, steps)          # K back-to-back launches, HIP events on the kernel stream
+    ctx.device_sync()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    wall_max = dist.max(wall)
+    # roofline: average duration of one launch, HIP events around each launch
+    kern_ms = ctx.time_dev_kernels(dbs, min(steps, 200))
+    for d in dbs:
+        d.free()
+    n = dist.ws
+    out = {
+        "workload": label,
+        "batch": batch,
+        "frames_bytes_per_batch": tr.frames_bytes,
+        "algo_bytes_per_batch": ab,
+        "resident_copies": ncopy,
+        "wall_s": wall_max,
+        "ms_per_step": 1e3 * wall_max / steps,
+        "gbps": n * ab * steps / wall_max / 1e9,
+        "mpkts": n * batch * steps / wall_max / 1e6,
+        "device_ms_per_batch": dev_ms / steps,
+        "kernel_ms": kern_ms,
+    }
+    achieved = ab / (kern_ms * 1e-3) / 1e9
+    pmc = load_pmc(key)
+    out["roofline"] = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+    }
+    if pmc:
+        out["roofline"]["traffic_source"] = pmc.get("source")
+    return out, tr
+
+
+def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0):
+    """The oracle (bit-exact C restatement, oracle/mosrx_oracle.c) on this host's cores.
+
+    Reported baseline only; never the measured product path."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O
+    p = O.params(skip_tcp_csum=1 if key == "S64_hdr" else 0)
+    ab = algo_bytes(tr)
+    cores_avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores_all = max(1, min(16, cores_avail))
+
+    def run(nt):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            O.classify(tr.frames, tr.off, tr.len, p, nthreads=nt)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= min_s:
+                return reps, el
+
+    r1, e1 = run(1)
+    rn, en = run(cores_all)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    gb1, gbn = r1 * ab / e1 / 1e9, rn * ab / en / 1e9
+    return {
+        "value": round(gb1, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+        "mpkts": round(r1 * tr.n / e1 / 1e6, 3),
+        "sample": f"{r1} passes over one {tr.n}-frame batch of this workload ({e1:.1f} s), "
+                  f"oracle/mosrx_oracle.c mo_classify, 1 thread; host '{model}', nproc {os.cpu_count()}",
+        "all_cores": {"value": round(gbn, 3), "unit": "GB/s", "cores": cores_all,
+                      "mpkts": round(rn * tr.n / en / 1e6, 3),
+                      "sample": f"{rn} passes, {cores_all} pthreads over disjoint slices ({en:.1f} s)"},
+    }
+
+
+def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
+    """End-to-end host->HBM->host rate (pinned staging, 2 slots); recorded in DESIGN.md."""
+    ctx.set_params(mosrx.default_params())
+    fb = tr.frames_bytes + 64
+    bufs, outs, batches = [], [], []
+    for _ in range(2):
+        pf, af = ctx.host_alloc(fb)
+        af[:] = tr.frames[:fb]
+        po, ao = ctx.host_alloc(tr.n * 4)
+        ao.view(np.uint32)[:] = tr.off
+        pl, al = ctx.host_alloc(tr.n * 2)
+        al.view(np.uint16)[:] = tr.len
+        pr, _ = ctx.host_alloc(tr.n * 16)
+        bufs += [pf, po, pl, pr]
+        outs.append(pr)
+        batches.append(mosrx.Batch(pf, tr.frames_bytes, po, pl, tr.n, tr.max_len))
+    ctx.time_host(batches, outs, 2)
+    ms = ctx.time_host(batches, outs, iters)
+    for p in bufs:
+        ctx.host_free(p)
+    ab = algo_bytes(tr)
+    return {"gbps": ab * iters / (ms * 1e-3) / 1e9, "mpkts": tr.n * iters / (ms * 1e-3) / 1e6,
+            "ms_per_batch": ms / iters,
+            "method": "pinned hipHostMalloc staging, H2D frames+descriptors, kernel, D2H records; 2 streams"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workloads", default="M1500,S64,S64_hdr,IMIX")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (PCIe) leg")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    if ws != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {ws}", file=sys.stderr)
+    dist = Dist(ws, rank)
+    ctx = mosrx.Context(local)
+    keys = [k for k in args.workloads.split(",") if k]
+    results, traces = {}, {}
+    for k in keys:
+        results[k], traces[k] = measure(ctx, dist, k, args.steps, args.warmup, rank)
+        if rank == 0:
+            r = results[k]
+            print(f"[bench] {k}: {r['gbps']:.1f} GB/s {r['mpkts']:.1f} Mpkts/s "
+                  f"kernel {r['kernel_ms']*1e3:.1f} us roofline {r['roofline']['frac']:.3f}",
+                  file=sys.stderr, flush=True)
+    e2e = None
+    if not args.no_e2e and "M1500" in traces:
+        e2e = {k: measure_e2e(ctx, traces[k], 20) for k in ("M1500", "S64") if k in traces}
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu:
+        head = "M1500" if "M1500" in traces else keys[0]
+        cpu = cpu_baseline(traces[head], head)
+        for k in keys:
+            if k != head:
+                results[k]["cpu_baseline"] = cpu_baseline(traces[k], k, min_s=2.0)
+    ctx.close()
+    dist.close()
+    if rank != 0:
+        return
+    head = "M1500" if "M1500" in results else keys[0]
+    h = results[head]
+    line = {
+        "metric": METRIC,
+        "value": round(h["gbps"], 2),
+        "unit": "GB/s",
+        "mpkts_per_s": round(h["mpkts"], 2),
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(h["ms_per_step"], 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded splitmix64 traces, BASELINE.md §3)",
+        "config": {"workload": h["workload"], "batch": h["batch"],
+                   "algo_bytes_per_batch": h["algo_bytes_per_batch"],
+                   "parallelism": f"replicas x{ws}: batches round-robin per GPU, no collectives",
+                   "resident_copies": h["resident_copies"]},
+        "roofline": h["roofline"],
+        "cpu_baseline": cpu,
+        "secondary": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in r.items()}
+                      for k, r in results.items() if k != head},
+        "e2e": e2e,
+    }
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,189 @@
+/*
+ * mosrx.h — C ABI of the MI355X receive-path classifier for mOS.
+ *
+ * One call classifies a batch of received Ethernet frames on a gfx950 GPU and
+ * emits one 16-byte result record per frame.  The per-frame transform is the
+ * part of mOS's software receive path that runs before the stateful flow
+ * engine:
+ *
+ *   ProcessPacket          core/src/eth_in.c:27-87      (ethertype dispatch)
+ *   ProcessInIPv4Packet    core/src/ip_in.c:30-101      (IPv4 checks)
+ *   ip_fast_csum           core/src/include/ip_in.h:10-38
+ *   ProcessInTCPPacket     core/src/tcp.c:408-445       (prefix up to FindStream)
+ *   FillPacketContextTCPInfo core/src/tcp.c:258-270
+ *   TCPCalcChecksum        core/src/tcp_util.c:157-190
+ *   GetRSSHash/BuildKeyCache core/src/util.c:27-99     (Toeplitz RSS)
+ *   GetRSSCPUCore          core/src/util.c:114-131     (queue map)
+ *
+ * The verdict in each record is bit-identical to ProcessPacket()'s return value
+ * (1 / 0 / -1) for the same frame and the same stack state (num_msp, num_esp,
+ * forward); `reason` distinguishes the causes that share a return value.
+ *
+ * Conventions (mirroring the reference's io_module_func, io_module.h:63-78):
+ *   - every function returns 0 on success or a negative errno value;
+ *   - the caller owns every buffer; the library never frees caller memory;
+ *   - one mosrx_ctx per host thread (mOS runs one mTCP thread per core, and
+ *     all io_module calls for a context come from that thread, core.c:1282-1349).
+ *
+ * No HIP, torch or C++ types appear in this header: streams are passed as
+ * `void *` (a hipStream_t), device buffers as plain pointers.
+ */
+#ifndef MOSRX_H
+#define MOSRX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MOSRX_ABI_VERSION 1
+
+/* ---- per-frame result record (16 bytes) -------------------- */
+
+/* reason codes */
+enum {
+	MOSRX_R_TCP_OK        = 0,  /* TCP segment passed every check        -> 1  (tcp.c:445)      */
+	MOSRX_R_ARP           = 1,  /* ARP ethertype (RUN_ARP) or forwarded  -> 1  (eth_in.c:63-66) */
+	MOSRX_R_NON_IPV4      = 2,  /* other ethertype: -1, or 1 if forward && num_msp (eth_in.c:62-77) */
+	MOSRX_R_IP_SHORT      = 3,  /* tot_len < 20                          -> -1 (ip_in.c:42-45)  */
+	MOSRX_R_IP_BADVER     = 4,  /* version != 4                          -> 0  (ip_in.c:47-51)  */
+	MOSRX_R_NOVERIFY_PASS = 5,  /* num_msp == 0 && num_esp == 0          -> 1  (ip_in.c:67-72)  */
+	MOSRX_R_IP_BADCSUM    = 6,  /* ip_fast_csum != 0                     -> -1 (ip_in.c:74-77)  */
+	MOSRX_R_NOT_TCP       = 7,  /* protocol != TCP                       -> 0  (ip_in.c:82-93)  */
+	MOSRX_R_TCP_SHORT     = 8,  /* ip_len < (ihl + doff) * 4             -> -1 (tcp.c:429-430)  */
+	MOSRX_R_TCP_BADCSUM   = 9,  /* TCPCalcChecksum != 0                  -> -1 (tcp.c:432-444)  */
+	MOSRX_R_TRUNCATED     = 10, /* build-only: a byte the reference reads lies past caplen -> -1 */
+	MOSRX_R_TCP_LEN_OK    = 11, /* skip_tcp_csum mode: length check passed -> 1                 */
+	MOSRX_R_COUNT         = 12
+};
+
+typedef struct mosrx_result {
+	uint32_t rss;         /* GetRSSHash(ntohl(saddr), ntohl(daddr), ntohs(sport), ntohs(dport)); ports 0 if not TCP */
+	uint16_t ip_csum;     /* raw ip_fast_csum() value (0 == valid); 0 if not computed */
+	uint16_t tcp_csum;    /* raw TCPCalcChecksum() value (0 == valid); 0 if not computed */
+	uint16_t payloadlen;  /* pkt_info.payloadlen (tcp.c:262, u16 arithmetic, may wrap) */
+	uint8_t  payload_off; /* 14 + ihl*4 + doff*4 (<= 134); 0 if not TCP */
+	int8_t   verdict;     /* ProcessPacket() return value: 1, 0 or -1 */
+	uint8_t  reason;      /* MOSRX_R_* */
+	uint8_t  queue;       /* GetRSSCPUCore() queue for rss */
+	uint8_t  tcp_flags;   /* TCP flags byte (header byte 13); 0 if not TCP */
+	uint8_t  ihl_doff;    /* (ihl << 4) | doff; doff 0 if not TCP */
+} mosrx_result;
+
+/* ---- parameters: the reference stack state the verdict depends on --------- */
+
+enum { MOSRX_QMAP_I40E = 1, MOSRX_QMAP_IXGBE = 0 };  /* FetchEndianType() values, config.c:1261-1278 */
+
+#define MOSRX_RSS_KEY_MAX 52   /* the DPDK backend programs a 52-byte key (dpdk_module.c:652-662) */
+
+typedef struct mosrx_params {
+	uint32_t num_msp;        /* # MOS_SOCK_MONITOR_STREAM sockets (mtcp.h:243); simple_firewall: 1 */
+	uint32_t num_esp;        /* # MOS_SOCK_STREAM sockets (mtcp.h:244) */
+	int32_t  forward;        /* mos.conf `forward` (config.c:608); setup.sh writes 1 */
+	int32_t  num_queues;     /* GetRSSCPUCore num_queues, 1..256 (pcap: 1, pcap_module.c:159) */
+	int32_t  queue_mode;     /* MOSRX_QMAP_I40E (non-DPDK default) or MOSRX_QMAP_IXGBE */
+	int32_t  skip_tcp_csum;  /* 1: header parse + IP checksum + RSS only (BASELINE config #2) */
+	uint32_t rss_key_len;    /* >= 16; only key bytes 0..15 affect a 12-byte input (util.c:47-57) */
+	uint8_t  rss_key[MOSRX_RSS_KEY_MAX];
+} mosrx_params;
+
+/* simple_firewall's state: num_msp=1, num_esp=0, forward=1, num_queues=1,
+ * i40e map, the all-0x05 40-byte key of util.c:36-42. */
+void mosrx_params_default(mosrx_params *p);
+/* The Microsoft reference Toeplitz key (util/rss.c:75-81), for the MSDN vectors. */
+void mosrx_params_set_ms_key(mosrx_params *p);
+
+/* ---- a batch of frames ---------------------------------------------------- */
+
+/* Frame i occupies frames[off[i] .. off[i]+len[i]).  The fast layout puts each
+ * frame at a 16-byte boundary + 2 (IP header 16-byte aligned); any offset is
+ * accepted.  Offsets are relative to `frames`; frames_bytes bounds every read
+ * (the kernel never touches memory outside [frames, frames+frames_bytes)). */
+typedef struct mosrx_batch {
+	const uint8_t  *frames;       /* device pointer (classify_dev) or host pointer (classify_host) */
+	uint64_t        frames_bytes; /* < 4 GiB */
+	const uint32_t *off;          /* n frame offsets */
+	const uint16_t *len;          /* n capture lengths (pcap caplen / get_rptr *len, core.c:903-905) */
+	uint32_t        n;            /* frames in the batch */
+	uint32_t        max_len;      /* max(len[]) if known, else 0 (selects the kernel variant) */
+} mosrx_batch;
+
+typedef struct mosrx_ctx mosrx_ctx;
+
+/* Open a context on HIP device `device`.  Fails with -ENODEV when no GPU or
+ * the HIP kernels are unavailable: there is no CPU fallback. */
+int  mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out);
+int  mosrx_set_params(mosrx_ctx *c, const mosrx_params *p);
+void mosrx_close(mosrx_ctx *c);
+
+/* Device-resident classification: `b` points at device memory, results go to
+ * device memory `d_out[n]`.  Enqueued on `stream` (a hipStream_t, NULL = the
+ * context's own stream); returns after enqueue.  Graph-capturable. */
+int  mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, void *stream);
+
+/* Device-resident classification of `nb` batches in one launch sequence. */
+int  mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
+                             mosrx_result *const *d_out, void *stream);
+
+/* End-to-end: host frames -> pinned staging -> H2D -> kernel -> D2H -> h_out.
+ * Blocks until h_out is filled. */
+int  mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out);
+
+/* Asynchronous end-to-end form for pipelining: two slots per context, each
+ * with its own stream.  submit enqueues H2D -> kernel -> D2H and returns; wait
+ * blocks until that slot's h_out is filled.  The host buffers must stay valid
+ * (and unmodified) until the wait returns; pinned buffers (mosrx_host_alloc)
+ * make the copies asynchronous. */
+#define MOSRX_NSLOT 2
+int  mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out);
+int  mosrx_classify_host_wait(mosrx_ctx *c, int slot);
+
+/* Per-reason counters of the last completed end-to-end batch (MOSRX_R_COUNT
+ * entries), the NETSTAT rx view of eth_in.c:42-45,80-84. */
+int  mosrx_last_counters(mosrx_ctx *c, uint64_t counts[MOSRX_R_COUNT]);
+
+/* Synchronise the context's stream. */
+int  mosrx_sync(mosrx_ctx *c);
+
+/* Device memory helpers so callers need no HIP headers. */
+int  mosrx_dev_alloc(mosrx_ctx *c, size_t bytes, void **dptr);
+int  mosrx_dev_free(mosrx_ctx *c, void *dptr);
+/* Pinned (page-locked) host memory: the staging a backend fills from the wire
+ * so H2D copies run at full PCIe rate. */
+int  mosrx_host_alloc(mosrx_ctx *c, size_t bytes, void **hptr);
+int  mosrx_host_free(mosrx_ctx *c, void *hptr);
+int  mosrx_memcpy_h2d(mosrx_ctx *c, void *dst, const void *src, size_t bytes);
+int  mosrx_memcpy_d2h(mosrx_ctx *c, void *dst, const void *src, size_t bytes);
+void *mosrx_stream(mosrx_ctx *c);
+
+/* ---- timing helpers (HIP events on the context stream) -------------------- */
+/* Run `iters` classify_dev calls cycling over `nb` resident batches and return
+ * the elapsed device time in milliseconds between events recorded on the same
+ * stream the kernels run on.  Used by bench.py for the live roofline figure. */
+int  mosrx_time_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
+                    mosrx_result *const *d_out, uint32_t iters, float *ms);
+/* Average duration of one classify kernel over `iters` launches, each bracketed
+ * by its own pair of HIP events on the stream it runs on (the roofline figure). */
+int  mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
+                            mosrx_result *const *d_out, uint32_t iters, float *avg_ms);
+/* hipDeviceSynchronize on the context's device. */
+int  mosrx_device_sync(mosrx_ctx *c);
+/* Same, end-to-end from host buffers through pinned staging, double-buffered. */
+int  mosrx_time_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
+                     mosrx_result *const *h_out, uint32_t iters, float *ms);
+
+/* ---- RSS helpers (host-side table build; the hash itself runs on the GPU) -- */
+/* Toeplitz nibble tables: 24 tables x 16 u32 for the 12-byte tuple
+ * saddr|daddr|sport|dport (wire order).  Built from the key cache of
+ * BuildKeyCache (util.c:27-58). */
+int  mosrx_rss_tables(const uint8_t *key, uint32_t key_len, uint32_t tables[24 * 16]);
+
+int  mosrx_abi_version(void);
+const char *mosrx_strerror(int err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MOSRX_H */

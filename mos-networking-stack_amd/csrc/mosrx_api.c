@@ -1,0 +1,560 @@
+/*
+ * mosrx_api.c — C host side of the MI355X rx classifier (include/mosrx.h).
+ *
+ * Plain C over the HIP runtime API.  It owns the per-context device state
+ * (lookup tables, staging for the end-to-end path, the stream) and enqueues the
+ * kernels in mosrx_kernels.hip.  There is no CPU fallback: without a usable GPU
+ * mosrx_open() fails with -ENODEV.
+ */
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mosrx_internal.h"
+
+#define HIPCHK(x) do { if ((x) != hipSuccess) return -EIO; } while (0)
+
+/* pipeline slots for the end-to-end path (double-buffered H2D | kernel | D2H) */
+#define NSLOT MOSRX_NSLOT
+
+struct slot {
+	uint8_t *d_frames;
+	uint32_t *d_off;
+	uint16_t *d_len;
+	mosrx_result *d_res;
+	uint32_t *d_cnt;
+	uint64_t cap_frames;
+	uint32_t cap_n;
+	hipStream_t stream;
+	hipEvent_t done;
+	uint32_t h_cnt[MOSRX_R_COUNT];
+	int busy;
+};
+
+struct mosrx_ctx {
+	int device;
+	hipStream_t stream;
+	mosrx_params params;
+	uint32_t kflags;
+	uint32_t *d_tables;
+	struct slot slot[NSLOT];
+	uint32_t h_cnt[MOSRX_R_COUNT];   /* counters of the last waited batch */
+	hipEvent_t ev0, ev1;
+};
+
+int mosrx_abi_version(void) { return MOSRX_ABI_VERSION; }
+
+const char *mosrx_strerror(int err)
+{
+	switch (err) {
+	case 0: return "success";
+	case -EINVAL: return "invalid argument";
+	case -ENODEV: return "no usable gfx950 device / HIP runtime";
+	case -ENOMEM: return "out of memory";
+	case -EIO: return "HIP runtime error";
+	case -E2BIG: return "batch too large";
+	default: return "unknown error";
+	}
+}
+
+void mosrx_params_default(mosrx_params *p)
+{
+	memset(p, 0, sizeof(*p));
+	p->num_msp = 1;           /* simple_firewall opens one MONITOR_STREAM socket (socket.c:77-78) */
+	p->num_esp = 0;
+	p->forward = 1;           /* setup.sh:135 */
+	p->num_queues = 1;        /* pcap_module.c:159 */
+	p->queue_mode = MOSRX_QMAP_I40E;   /* FetchEndianType() without DPDK, config.c:1277 */
+	p->skip_tcp_csum = 0;
+	p->rss_key_len = 40;      /* util.c:36-42 */
+	memset(p->rss_key, 0x05, 40);
+}
+
+void mosrx_params_set_ms_key(mosrx_params *p)
+{
+	static const uint8_t ms[40] = {
+		0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+		0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+		0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+	memset(p->rss_key, 0, sizeof(p->rss_key));
+	memcpy(p->rss_key, ms, sizeof(ms));
+	p->rss_key_len = sizeof(ms);
+}
+
+/* Key cache of BuildKeyCache (util.c:27-58): cache[i] = the 32 key bits starting
+ * at bit i.  The 96-bit input bit i (MSB-first over saddr|daddr|sport|dport)
+ * contributes cache[i]; grouping input bits by nibble gives 24 tables of 16. */
+int mosrx_rss_tables(const uint8_t *key, uint32_t key_len, uint32_t tables[24 * 16])
+{
+	uint32_t cache[96];
+	uint32_t result, idx = 32;
+	int i, k, v, b;
+
+	if (!key || !tables || key_len < 16)
+		return -EINVAL;
+	result = ((uint32_t)key[0] << 24) | ((uint32_t)key[1] << 16) | ((uint32_t)key[2] << 8) | key[3];
+	for (i = 0; i < 96; i++, idx++) {
+		cache[i] = result;
+		result = (result << 1) | (((key[idx / 8] << (idx % 8)) & 0x80) ? 1u : 0u);
+	}
+	for (k = 0; k < 24; k++)
+		for (v = 0; v < 16; v++) {
+			uint32_t h = 0;
+			for (b = 0; b < 4; b++)
+				if (v & (8 >> b))
+					h ^= cache[4 * k + b];
+			tables[k * 16 + v] = h;
+		}
+	return 0;
+}
+
+static int check_params(const mosrx_params *p)
+{
+	if (!p || p->rss_key_len < 16 || p->rss_key_len > MOSRX_RSS_KEY_MAX)
+		return -EINVAL;
+	if (p->num_queues < 1 || p->num_queues > 256)
+		return -EINVAL;
+	if (p->queue_mode != MOSRX_QMAP_I40E && p->queue_mode != MOSRX_QMAP_IXGBE)
+		return -EINVAL;
+	return 0;
+}
+
+/* GetRSSCPUCore (util.c:114-131) evaluated for every (hash & 0x1FF). */
+static void build_qlut(const mosrx_params *p, uint8_t lut[512])
+{
+	static const uint32_t offs[4] = {3, 1, (uint32_t)-1, (uint32_t)-3};
+	uint32_t x;
+	for (x = 0; x < 512; x++) {
+		uint32_t m;
+		if (p->queue_mode == MOSRX_QMAP_I40E) {
+			m = x & 0x1FF;
+			m += offs[m & 3];
+		} else {
+			m = x & 0x7F;
+		}
+		lut[x] = (uint8_t)(m % (uint32_t)p->num_queues);
+	}
+}
+
+int mosrx_set_params(mosrx_ctx *c, const mosrx_params *p)
+{
+	uint32_t tab[MOSRX_TAB_WORDS];
+	int rc;
+
+	if (!c)
+		return -EINVAL;
+	if ((rc = check_params(p)))
+		return rc;
+	memset(tab, 0, sizeof(tab));
+	if ((rc = mosrx_rss_tables(p->rss_key, p->rss_key_len, tab)))
+		return rc;
+	build_qlut(p, (uint8_t *)(tab + MOSRX_TAB_RSS_WORDS));
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipMemcpyAsync(c->d_tables, tab, sizeof(tab), hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	c->params = *p;
+	c->kflags = ((p->num_msp || p->num_esp) ? MOSRX_KF_VERIFY : 0) |
+	            ((p->num_msp && p->forward) ? MOSRX_KF_FWD_NONIP : 0) |
+	            (p->skip_tcp_csum ? MOSRX_KF_SKIP_TCP : 0);
+	return 0;
+}
+
+int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
+{
+	mosrx_ctx *c;
+	int ndev = 0, rc, i;
+	hipDeviceProp_t prop;
+
+	if (!out)
+		return -EINVAL;
+	*out = NULL;
+	if ((rc = check_params(p)))
+		return rc;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+		return -ENODEV;
+	if (hipGetDeviceProperties(&prop, device) != hipSuccess || strncmp(prop.gcnArchName, "gfx950", 6))
+		return -ENODEV;
+	c = calloc(1, sizeof(*c));
+	if (!c)
+		return -ENOMEM;
+	c->device = device;
+	if (hipSetDevice(device) != hipSuccess ||
+	    hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+	    hipMalloc((void **)&c->d_tables, MOSRX_TAB_WORDS * 4) != hipSuccess ||
+	    hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+		mosrx_close(c);
+		return -ENODEV;
+	}
+	for (i = 0; i < NSLOT; i++) {
+		if (hipStreamCreateWithFlags(&c->slot[i].stream, hipStreamNonBlocking) != hipSuccess ||
+		    hipEventCreateWithFlags(&c->slot[i].done, hipEventDisableTiming) != hipSuccess ||
+		    hipMalloc((void **)&c->slot[i].d_cnt, MOSRX_R_COUNT * 4) != hipSuccess) {
+			mosrx_close(c);
+			return -ENODEV;
+		}
+	}
+	if ((rc = mosrx_set_params(c, p))) {
+		mosrx_close(c);
+		return rc;
+	}
+	*out = c;
+	return 0;
+}
+
+static void slot_free(struct slot *s)
+{
+	if (s->d_frames) hipFree(s->d_frames);
+	if (s->d_off) hipFree(s->d_off);
+	if (s->d_len) hipFree(s->d_len);
+	if (s->d_res) hipFree(s->d_res);
+	s->d_frames = NULL; s->d_off = NULL; s->d_len = NULL; s->d_res = NULL;
+	s->cap_frames = 0; s->cap_n = 0;
+}
+
+void mosrx_close(mosrx_ctx *c)
+{
+	int i;
+	if (!c)
+		return;
+	hipSetDevice(c->device);
+	if (c->stream)
+		hipStreamSynchronize(c->stream);
+	for (i = 0; i < NSLOT; i++) {
+		if (c->slot[i].stream) {
+			hipStreamSynchronize(c->slot[i].stream);
+			hipStreamDestroy(c->slot[i].stream);
+		}
+		if (c->slot[i].done) hipEventDestroy(c->slot[i].done);
+		if (c->slot[i].d_cnt) hipFree(c->slot[i].d_cnt);
+		slot_free(&c->slot[i]);
+	}
+	if (c->d_tables) hipFree(c->d_tables);
+	if (c->ev0) hipEventDestroy(c->ev0);
+	if (c->ev1) hipEventDestroy(c->ev1);
+	if (c->stream) hipStreamDestroy(c->stream);
+	free(c);
+}
+
+static int check_batch(const mosrx_batch *b, int dev)
+{
+	if (!b)
+		return -EINVAL;
+	if (b->n == 0)
+		return 0;
+	if (!b->frames || !b->off || !b->len || (dev && ((uintptr_t)b->frames & 15)))
+		return -EINVAL;
+	if (b->frames_bytes >= (1ull << 32))
+		return -E2BIG;
+	return 0;
+}
+
+static int tile_for(const mosrx_batch *b)
+{
+	return (b->max_len && b->max_len <= MOSRX_WINDOW_END) ? MOSRX_TILE_SMALL : MOSRX_TILE_LARGE;
+}
+
+static int launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
+                  const uint16_t *len, mosrx_result *out, uint32_t *cnt, hipStream_t s)
+{
+	mosrx_kparams kp;
+	kp.frames = frames;
+	kp.off = off;
+	kp.len = len;
+	kp.out = out;
+	kp.tables = c->d_tables;
+	kp.counters = cnt;
+	kp.frames_bytes = (uint32_t)b->frames_bytes;
+	kp.n = b->n;
+	kp.flags = c->kflags;
+	kp.pad = 0;
+	return mosrx_launch_classify(&kp, tile_for(b), (void *)s);
+}
+
+int mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, void *stream)
+{
+	int rc;
+	if (!c || (rc = check_batch(b, 1)))
+		return c ? rc : -EINVAL;
+	if (b->n == 0)
+		return 0;
+	if (!d_out || ((uintptr_t)d_out & 15))
+		return -EINVAL;
+	return launch(c, b, b->frames, b->off, b->len, d_out, NULL,
+	              stream ? (hipStream_t)stream : c->stream);
+}
+
+int mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
+                            mosrx_result *const *d_out, void *stream)
+{
+	uint32_t i;
+	int rc;
+	if (!c || !b || !d_out)
+		return -EINVAL;
+	for (i = 0; i < nb; i++)
+		if ((rc = mosrx_classify_dev(c, &b[i], d_out[i], stream)))
+			return rc;
+	return 0;
+}
+
+static int slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uint32_t n)
+{
+	if (frames_bytes > s->cap_frames || n > s->cap_n) {
+		uint64_t fb = frames_bytes > s->cap_frames ? frames_bytes + (frames_bytes >> 2) : s->cap_frames;
+		uint32_t nn = n > s->cap_n ? n + (n >> 2) : s->cap_n;
+		hipStreamSynchronize(s->stream);
+		slot_free(s);
+		fb = (fb + 255) & ~(uint64_t)255;
+		if (hipMalloc((void **)&s->d_frames, fb) != hipSuccess ||
+		    hipMalloc((void **)&s->d_off, (size_t)nn * 4) != hipSuccess ||
+		    hipMalloc((void **)&s->d_len, (size_t)nn * 2) != hipSuccess ||
+		    hipMalloc((void **)&s->d_res, (size_t)nn * sizeof(mosrx_result)) != hipSuccess) {
+			slot_free(s);
+			return -ENOMEM;
+		}
+		s->cap_frames = fb;
+		s->cap_n = nn;
+	}
+	(void)c;
+	return 0;
+}
+
+/* Enqueue one end-to-end batch on slot s: H2D frames+descriptors, kernel, D2H results. */
+static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosrx_result *h_out)
+{
+	int rc;
+	if ((rc = slot_reserve(c, s, b->frames_bytes, b->n)))
+		return rc;
+	HIPCHK(hipMemcpyAsync(s->d_frames, b->frames, b->frames_bytes, hipMemcpyHostToDevice, s->stream));
+	HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
+	HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
+	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_R_COUNT * 4, s->stream));
+	if ((rc = launch(c, b, s->d_frames, s->d_off, s->d_len, s->d_res, s->d_cnt, s->stream)))
+		return rc;
+	HIPCHK(hipMemcpyAsync(h_out, s->d_res, (size_t)b->n * sizeof(mosrx_result), hipMemcpyDeviceToHost,
+	                      s->stream));
+	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_R_COUNT * 4, hipMemcpyDeviceToHost, s->stream));
+	HIPCHK(hipEventRecord(s->done, s->stream));
+	s->busy = 1;
+	return 0;
+}
+
+int mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out)
+{
+	int rc;
+	if (!c || (rc = check_batch(b, 0)))
+		return c ? rc : -EINVAL;
+	if ((rc = mosrx_classify_host_submit(c, 0, b, h_out)))
+		return rc;
+	return mosrx_classify_host_wait(c, 0);
+}
+
+int mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out)
+{
+	int rc;
+	if (!c || slot < 0 || slot >= NSLOT)
+		return -EINVAL;
+	if ((rc = check_batch(b, 0)))
+		return rc;
+	if (c->slot[slot].busy)
+		return -EBUSY;
+	if (b->n == 0) {
+		memset(c->slot[slot].h_cnt, 0, sizeof(c->slot[slot].h_cnt));
+		c->slot[slot].busy = 2;   /* nothing enqueued */
+		return 0;
+	}
+	if (!h_out)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	return host_enqueue(c, &c->slot[slot], b, h_out);
+}
+
+int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
+{
+	struct slot *s;
+	if (!c || slot < 0 || slot >= NSLOT)
+		return -EINVAL;
+	s = &c->slot[slot];
+	if (!s->busy)
+		return -EINVAL;
+	if (s->busy == 1)
+		HIPCHK(hipEventSynchronize(s->done));
+	memcpy(c->h_cnt, s->h_cnt, sizeof(c->h_cnt));
+	s->busy = 0;
+	return 0;
+}
+
+int mosrx_last_counters(mosrx_ctx *c, uint64_t counts[MOSRX_R_COUNT])
+{
+	int i;
+	if (!c || !counts)
+		return -EINVAL;
+	for (i = 0; i < MOSRX_R_COUNT; i++)
+		counts[i] = c->h_cnt[i];
+	return 0;
+}
+
+int mosrx_sync(mosrx_ctx *c)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int mosrx_dev_alloc(mosrx_ctx *c, size_t bytes, void **dptr)
+{
+	if (!c || !dptr)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess)
+		return -ENOMEM;
+	return 0;
+}
+
+int mosrx_dev_free(mosrx_ctx *c, void *dptr)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipFree(dptr));
+	return 0;
+}
+
+int mosrx_host_alloc(mosrx_ctx *c, size_t bytes, void **hptr)
+{
+	if (!c || !hptr)
+		return -EINVAL;
+	if (hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+		return -ENOMEM;
+	return 0;
+}
+
+int mosrx_host_free(mosrx_ctx *c, void *hptr)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipHostFree(hptr));
+	return 0;
+}
+
+int mosrx_memcpy_h2d(mosrx_ctx *c, void *dst, const void *src, size_t bytes)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int mosrx_memcpy_d2h(mosrx_ctx *c, void *dst, const void *src, size_t bytes)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+void *mosrx_stream(mosrx_ctx *c) { return c ? (void *)c->stream : NULL; }
+
+int mosrx_time_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
+                   uint32_t iters, float *ms)
+{
+	uint32_t i;
+	int rc;
+	if (!c || !b || !d_out || !ms || nb == 0)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipEventRecord(c->ev0, c->stream));
+	for (i = 0; i < iters; i++)
+		if ((rc = mosrx_classify_dev(c, &b[i % nb], d_out[i % nb], c->stream)))
+			return rc;
+	HIPCHK(hipEventRecord(c->ev1, c->stream));
+	HIPCHK(hipEventSynchronize(c->ev1));
+	HIPCHK(hipEventElapsedTime(ms, c->ev0, c->ev1));
+	return 0;
+}
+
+int mosrx_time_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *h_out,
+                    uint32_t iters, float *ms)
+{
+	uint32_t i;
+	int rc, k;
+	if (!c || !b || !h_out || !ms || nb == 0)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	for (i = 0; i < nb; i++)   /* size both slots before timing */
+		for (k = 0; k < NSLOT; k++)
+			if ((rc = slot_reserve(c, &c->slot[k], b[i].frames_bytes, b[i].n)))
+				return rc;
+	HIPCHK(hipDeviceSynchronize());
+	HIPCHK(hipEventRecord(c->ev0, c->stream));
+	for (k = 0; k < NSLOT; k++)
+		HIPCHK(hipStreamWaitEvent(c->slot[k].stream, c->ev0, 0));
+	for (k = 0; k < NSLOT; k++)
+		if (c->slot[k].busy)
+			return -EBUSY;
+	for (i = 0; i < iters; i++) {
+		struct slot *s = &c->slot[i % NSLOT];
+		if ((rc = host_enqueue(c, s, &b[i % nb], h_out[i % nb])))
+			return rc;
+	}
+	for (k = 0; k < NSLOT; k++) {
+		HIPCHK(hipEventRecord(c->slot[k].done, c->slot[k].stream));
+		HIPCHK(hipStreamWaitEvent(c->stream, c->slot[k].done, 0));
+		c->slot[k].busy = 0;
+	}
+	HIPCHK(hipEventRecord(c->ev1, c->stream));
+	HIPCHK(hipEventSynchronize(c->ev1));
+	HIPCHK(hipEventElapsedTime(ms, c->ev0, c->ev1));
+	return 0;
+}
+
+int mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
+                           uint32_t iters, float *avg_ms)
+{
+	hipEvent_t *ev;
+	uint32_t i;
+	int rc = 0;
+	double tot = 0;
+	if (!c || !b || !d_out || !avg_ms || nb == 0 || iters == 0)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	ev = calloc((size_t)iters * 2, sizeof(*ev));
+	if (!ev)
+		return -ENOMEM;
+	for (i = 0; i < iters * 2 && !rc; i++)
+		if (hipEventCreate(&ev[i]) != hipSuccess)
+			rc = -EIO;
+	for (i = 0; i < iters && !rc; i++) {
+		if (hipEventRecord(ev[2 * i], c->stream) != hipSuccess) { rc = -EIO; break; }
+		if ((rc = mosrx_classify_dev(c, &b[i % nb], d_out[i % nb], c->stream)))
+			break;
+		if (hipEventRecord(ev[2 * i + 1], c->stream) != hipSuccess) { rc = -EIO; break; }
+	}
+	if (!rc && hipStreamSynchronize(c->stream) != hipSuccess)
+		rc = -EIO;
+	for (i = 0; i < iters && !rc; i++) {
+		float ms = 0;
+		if (hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]) != hipSuccess) { rc = -EIO; break; }
+		tot += ms;
+	}
+	for (i = 0; i < iters * 2; i++)
+		if (ev[i])
+			hipEventDestroy(ev[i]);
+	free(ev);
+	if (!rc)
+		*avg_ms = (float)(tot / iters);
+	return rc;
+}
+
+int mosrx_device_sync(mosrx_ctx *c)
+{
+	if (!c)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipDeviceSynchronize());
+	return 0;
+}

@@ -1,0 +1,54 @@
+/*
+ * mosrx_internal.h — shared between the C host library (mosrx_api.c) and the
+ * HIP kernels (mosrx_kernels.hip).  Plain C layout, no HIP types except the
+ * launcher's stream argument.
+ */
+#ifndef MOSRX_INTERNAL_H
+#define MOSRX_INTERNAL_H
+
+#include <stdint.h>
+#include "../../include/mosrx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Device-side lookup tables, one 2 KiB block per context:
+ *   [0, 384)   Toeplitz nibble tables, 24 x 16 u32 (mosrx_rss_tables)
+ *   [384, 512) GetRSSCPUCore queue LUT, 512 x u8 indexed by (rss & 0x1FF) */
+#define MOSRX_TAB_RSS_WORDS   384
+#define MOSRX_TAB_QLUT_WORDS  128
+#define MOSRX_TAB_WORDS       512
+
+enum {
+	MOSRX_KF_VERIFY    = 1u << 0,  /* num_msp || num_esp: checksums verified (ip_in.c:67) */
+	MOSRX_KF_FWD_NONIP = 1u << 1,  /* num_msp && forward: non-IPv4 frames forwarded (eth_in.c:62) */
+	MOSRX_KF_SKIP_TCP  = 1u << 2,  /* skip TCPCalcChecksum (BASELINE config #2 mode) */
+};
+
+typedef struct mosrx_kparams {
+	const uint8_t  *frames;
+	const uint32_t *off;
+	const uint16_t *len;
+	mosrx_result   *out;
+	const uint32_t *tables;     /* MOSRX_TAB_WORDS */
+	uint32_t       *counters;   /* MOSRX_R_COUNT u32, accumulated with atomics; may be NULL */
+	uint32_t        frames_bytes;
+	uint32_t        n;
+	uint32_t        flags;      /* MOSRX_KF_* */
+	uint32_t        pad;
+} mosrx_kparams;
+
+/* Kernel variants: tile = frames per 256-thread workgroup. */
+enum { MOSRX_TILE_SMALL = 256, MOSRX_TILE_LARGE = 64 };
+/* Frames whose IP datagram ends at or before this frame byte are finished in
+ * the per-lane header window; longer ones stream their tail cooperatively. */
+#define MOSRX_WINDOW_END 94
+
+/* Launch one classify kernel; returns 0 or -EINVAL / -EIO.  `stream` is a hipStream_t. */
+int mosrx_launch_classify(const mosrx_kparams *kp, int tile, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,427 @@
+"""mosrx — Python mirror of the MI355X rx classifier's C ABI (include/mosrx.h).
+
+Thin ctypes binding over the in-tree ``libmosrx.so``; every call goes to the
+HIP path.  There is no CPU fallback: when the library or a gfx950 GPU is
+missing, ``Context()`` raises.
+
+The names mirror mOS's receive path: ``classify`` is ProcessPacket
+(core/src/eth_in.c:27) over a batch, records carry the verdict it returns plus
+the raw ip_fast_csum / TCPCalcChecksum values and the GetRSSHash /
+GetRSSCPUCore outputs (core/src/util.c:61-131).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libmosrx.so")
+
+RESULT_DTYPE = np.dtype([
+    ("rss", "<u4"), ("ip_csum", "<u2"), ("tcp_csum", "<u2"), ("payloadlen", "<u2"),
+    ("payload_off", "u1"), ("verdict", "i1"), ("reason", "u1"), ("queue", "u1"),
+    ("tcp_flags", "u1"), ("ihl_doff", "u1"),
+])
+assert RESULT_DTYPE.itemsize == 16
+
+REASONS = ["TCP_OK", "ARP", "NON_IPV4", "IP_SHORT", "IP_BADVER", "NOVERIFY_PASS", "IP_BADCSUM",
+           "NOT_TCP", "TCP_SHORT", "TCP_BADCSUM", "TRUNCATED", "TCP_LEN_OK"]
+R = {name: i for i, name in enumerate(REASONS)}
+
+QMAP_I40E, QMAP_IXGBE = 1, 0
+TRACE_FW64, TRACE_S64, TRACE_M1500, TRACE_IMIX = 0, 1, 2, 3
+WINDOW_END = 94
+
+MS_KEY = bytes([0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+                0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+                0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa])
+
+
+class Params(C.Structure):
+    """mosrx_params: the mOS stack state the verdict depends on."""
+    _fields_ = [("num_msp", C.c_uint32), ("num_esp", C.c_uint32), ("forward", C.c_int32),
+                ("num_queues", C.c_int32), ("queue_mode", C.c_int32), ("skip_tcp_csum", C.c_int32),
+                ("rss_key_len", C.c_uint32), ("rss_key", C.c_uint8 * 52)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("frames_bytes", C.c_uint64), ("off", C.c_void_p),
+                ("len", C.c_void_p), ("n", C.c_uint32), ("max_len", C.c_uint32)]
+
+
+class TraceC(C.Structure):
+    _fields_ = [("frames", C.c_void_p), ("frames_bytes", C.c_uint64), ("off", C.c_void_p),
+                ("len", C.c_void_p), ("n", C.c_uint32), ("max_len", C.c_uint32),
+                ("caplen_sum", C.c_uint64)]
+
+
+class RxStats(C.Structure):
+    _fields_ = [("rx_packets", C.c_uint64), ("rx_bytes", C.c_uint64), ("rx_errors", C.c_uint64),
+                ("rounds", C.c_uint64), ("batches", C.c_uint64), ("by_reason", C.c_uint64 * 12)]
+
+
+class ModuleCfg(C.Structure):
+    _fields_ = [("num_ifs", C.c_uint32), ("if_names", (C.c_char * 16) * 16),
+                ("src", C.c_void_p * 16), ("batch", C.c_uint32), ("max_frame", C.c_uint32),
+                ("gpu_base", C.c_int32), ("ngpu", C.c_int32), ("pipeline", C.c_int32),
+                ("params", Params)]
+
+
+class MosrxError(OSError):
+    pass
+
+
+_lib = None
+
+
+def build():
+    """Compile libmosrx.so in-tree (hipcc --offload-arch=gfx950 + gcc)."""
+    subprocess.check_call(["make", "-s", "-C", PKG_DIR])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MosrxError(2, f"{LIB_PATH} missing: run build() / `make -C {PKG_DIR}`")
+        L = C.CDLL(LIB_PATH)
+        P, U32, U64, I = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+        sig = {
+            "mosrx_abi_version": (I, []),
+            "mosrx_strerror": (C.c_char_p, [I]),
+            "mosrx_params_default": (None, [C.POINTER(Params)]),
+            "mosrx_params_set_ms_key": (None, [C.POINTER(Params)]),
+            "mosrx_open": (I, [I, C.POINTER(Params), C.POINTER(P)]),
+            "mosrx_set_params": (I, [P, C.POINTER(Params)]),
+            "mosrx_close": (None, [P]),
+            "mosrx_classify_dev": (I, [P, C.POINTER(Batch), P, P]),
+            "mosrx_classify_host": (I, [P, C.POINTER(Batch), P]),
+            "mosrx_classify_host_submit": (I, [P, I, C.POINTER(Batch), P]),
+            "mosrx_classify_host_wait": (I, [P, I]),
+            "mosrx_last_counters": (I, [P, C.POINTER(U64)]),
+            "mosrx_sync": (I, [P]),
+            "mosrx_dev_alloc": (I, [P, C.c_size_t, C.POINTER(P)]),
+            "mosrx_dev_free": (I, [P, P]),
+            "mosrx_host_alloc": (I, [P, C.c_size_t, C.POINTER(P)]),
+            "mosrx_host_free": (I, [P, P]),
+            "mosrx_memcpy_h2d": (I, [P, P, P, C.c_size_t]),
+            "mosrx_memcpy_d2h": (I, [P, P, P, C.c_size_t]),
+            "mosrx_stream": (P, [P]),
+            "mosrx_time_dev": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
+            "mosrx_time_dev_kernels": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
+            "mosrx_device_sync": (I, [P]),
+            "mosrx_time_host": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
+            "mosrx_rss_tables": (I, [C.c_char_p, U32, C.POINTER(U32)]),
+            "mosrx_trace_gen": (I, [I, U32, U32, U64, C.POINTER(TraceC)]),
+            "mosrx_trace_free": (None, [C.POINTER(TraceC)]),
+            "mosrx_source_mem": (P, [P, P, P, U32, U32]),
+            "mosrx_source_pcap": (P, [C.c_char_p, U32]),
+            "mosrx_source_afpacket": (P, [C.c_char_p]),
+            "mosrx_source_close": (None, [P]),
+            "mosrx_source_next": (I, [P, P, U32]),
+            "mosrx_gpu_module_cfg_default": (None, [C.POINTER(ModuleCfg)]),
+            "mosrx_gpu_module_configure": (I, [C.POINTER(ModuleCfg)]),
+            "mosrx_gpu_module_bind": (I, [P, I]),
+            "mosrx_rx_loop": (I, [P, P, I, U64, P, P, C.POINTER(RxStats)]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _chk(rc: int, what: str):
+    if rc:
+        raise MosrxError(-rc, f"{what}: {lib().mosrx_strerror(rc).decode()}")
+
+
+def default_params(**kw) -> Params:
+    p = Params()
+    lib().mosrx_params_default(C.byref(p))
+    key = kw.pop("key", None)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    if key is not None:
+        if not 16 <= len(key) <= 52:
+            raise ValueError("rss key must be 16..52 bytes")
+        for i in range(52):
+            p.rss_key[i] = key[i] if i < len(key) else 0
+        p.rss_key_len = len(key)
+    return p
+
+
+class Trace:
+    """A seeded synthetic batch (include/mosrx_trace.h) held as numpy arrays."""
+
+    def __init__(self, kind: int, n: int, nflows: int = 1_000_000, seed: int = 0):
+        t = TraceC()
+        _chk(lib().mosrx_trace_gen(kind, n, nflows, seed, C.byref(t)), "mosrx_trace_gen")
+        try:
+            fb = int(t.frames_bytes)
+            self.frames = np.ctypeslib.as_array(C.cast(t.frames, C.POINTER(C.c_uint8)), (fb + 64,)).copy()
+            self.off = np.ctypeslib.as_array(C.cast(t.off, C.POINTER(C.c_uint32)), (t.n,)).copy() if t.n else np.zeros(0, np.uint32)
+            self.len = np.ctypeslib.as_array(C.cast(t.len, C.POINTER(C.c_uint16)), (t.n,)).copy() if t.n else np.zeros(0, np.uint16)
+            self.frames_bytes = fb
+            self.n = int(t.n)
+            self.max_len = int(t.max_len)
+            self.caplen_sum = int(t.caplen_sum)
+        finally:
+            lib().mosrx_trace_free(C.byref(t))
+
+
+class DevBuffer:
+    """Device allocation owned by a Context (hipMalloc through the C ABI)."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        p = C.c_void_p()
+        _chk(lib().mosrx_dev_alloc(ctx.handle, max(self.nbytes, 1), C.byref(p)), "mosrx_dev_alloc")
+        self.ptr = p.value
+
+    def upload(self, arr: np.ndarray):
+        a = np.ascontiguousarray(arr)
+        assert a.nbytes <= self.nbytes
+        _chk(lib().mosrx_memcpy_h2d(self.ctx.handle, self.ptr, a.ctypes.data, a.nbytes), "h2d")
+
+    def download(self, arr: np.ndarray):
+        assert arr.flags.c_contiguous and arr.nbytes <= self.nbytes
+        _chk(lib().mosrx_memcpy_d2h(self.ctx.handle, arr.ctypes.data, self.ptr, arr.nbytes), "d2h")
+        return arr
+
+    def free(self):
+        if self.ptr:
+            lib().mosrx_dev_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+
+class DevBatch:
+    """A batch resident in HBM: frames + off + len, and its result buffer."""
+
+    def __init__(self, ctx: "Context", frames: np.ndarray, off: np.ndarray, ln: np.ndarray,
+                 frames_bytes: int | None = None, max_len: int | None = None):
+        frames = np.ascontiguousarray(frames, np.uint8)
+        off = np.ascontiguousarray(off, np.uint32)
+        ln = np.ascontiguousarray(ln, np.uint16)
+        self.n = len(off)
+        self.frames_bytes = int(frames_bytes if frames_bytes is not None else len(frames))
+        self.d_frames = DevBuffer(ctx, max(len(frames), 16))
+        self.d_frames.upload(frames)
+        self.d_off = DevBuffer(ctx, max(off.nbytes, 4))
+        self.d_off.upload(off)
+        self.d_len = DevBuffer(ctx, max(ln.nbytes, 2))
+        self.d_len.upload(ln)
+        self.d_out = DevBuffer(ctx, max(self.n * 16, 16))
+        self.max_len = int(max_len if max_len is not None else (int(ln.max()) if self.n else 0))
+        self.caplen_sum = int(ln.astype(np.uint64).sum())
+
+    def batch(self) -> Batch:
+        return Batch(self.d_frames.ptr, self.frames_bytes, self.d_off.ptr, self.d_len.ptr, self.n,
+                     self.max_len)
+
+    def results(self) -> np.ndarray:
+        out = np.zeros(self.n, RESULT_DTYPE)
+        if self.n:
+            self.d_out.download(out)
+        return out
+
+    def free(self):
+        for b in (self.d_frames, self.d_off, self.d_len, self.d_out):
+            b.free()
+
+
+class Context:
+    """mosrx_ctx: one per host thread, bound to one GPU."""
+
+    def __init__(self, device: int = 0, params: Params | None = None):
+        self.params = params or default_params()
+        h = C.c_void_p()
+        _chk(lib().mosrx_open(device, C.byref(self.params), C.byref(h)), "mosrx_open")
+        self.handle = h.value
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib().mosrx_close(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_params(self, params: Params):
+        _chk(lib().mosrx_set_params(self.handle, C.byref(params)), "mosrx_set_params")
+        self.params = params
+
+    # ---- end-to-end from host memory ----
+    def classify_host(self, frames, off, ln, frames_bytes=None, max_len=0) -> np.ndarray:
+        frames = np.ascontiguousarray(frames, np.uint8)
+        off = np.ascontiguousarray(off, np.uint32)
+        ln = np.ascontiguousarray(ln, np.uint16)
+        out = np.zeros(len(off), RESULT_DTYPE)
+        b = Batch(frames.ctypes.data, int(frames_bytes if frames_bytes is not None else len(frames)),
+                  off.ctypes.data, ln.ctypes.data, len(off), max_len)
+        _chk(lib().mosrx_classify_host(self.handle, C.byref(b), out.ctypes.data), "mosrx_classify_host")
+        return out
+
+    def last_counters(self) -> np.ndarray:
+        c = (C.c_uint64 * 12)()
+        _chk(lib().mosrx_last_counters(self.handle, c), "mosrx_last_counters")
+        return np.array(c[:], np.uint64)
+
+    # ---- device resident ----
+    def upload(self, frames, off, ln, frames_bytes=None, max_len=None) -> DevBatch:
+        return DevBatch(self, frames, off, ln, frames_bytes, max_len)
+
+    def classify_dev(self, db: DevBatch, sync: bool = True) -> None:
+        b = db.batch()
+        _chk(lib().mosrx_classify_dev(self.handle, C.byref(b), db.d_out.ptr, None), "mosrx_classify_dev")
+        if sync:
+            _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
+
+    def time_dev(self, dbs: list[DevBatch], iters: int) -> float:
+        bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
+        outs = (C.c_void_p * len(dbs))(*[d.d_out.ptr for d in dbs])
+        ms = C.c_float()
+        _chk(lib().mosrx_time_dev(self.handle, bs, len(dbs), outs, iters, C.byref(ms)), "mosrx_time_dev")
+        return float(ms.value)
+
+    def time_dev_kernels(self, dbs: list[DevBatch], iters: int) -> float:
+        """Average kernel duration (ms), HIP events around every launch."""
+        bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
+        outs = (C.c_void_p * len(dbs))(*[d.d_out.ptr for d in dbs])
+        ms = C.c_float()
+        _chk(lib().mosrx_time_dev_kernels(self.handle, bs, len(dbs), outs, iters, C.byref(ms)),
+             "mosrx_time_dev_kernels")
+        return float(ms.value)
+
+    def device_sync(self):
+        _chk(lib().mosrx_device_sync(self.handle), "mosrx_device_sync")
+
+    def host_alloc(self, nbytes: int) -> tuple[int, np.ndarray]:
+        p = C.c_void_p()
+        _chk(lib().mosrx_host_alloc(self.handle, max(int(nbytes), 1), C.byref(p)), "mosrx_host_alloc")
+        arr = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), (max(int(nbytes), 1),))
+        return p.value, arr
+
+    def host_free(self, ptr: int):
+        lib().mosrx_host_free(self.handle, ptr)
+
+    def time_host(self, batches: list[Batch], outs: list[int], iters: int) -> float:
+        bs = (Batch * len(batches))(*batches)
+        os_ = (C.c_void_p * len(outs))(*outs)
+        ms = C.c_float()
+        _chk(lib().mosrx_time_host(self.handle, bs, len(batches), os_, iters, C.byref(ms)), "mosrx_time_host")
+        return float(ms.value)
+
+
+def rss_tables(key: bytes) -> np.ndarray:
+    out = (C.c_uint32 * 384)()
+    _chk(lib().mosrx_rss_tables(key, len(key), out), "mosrx_rss_tables")
+    return np.array(out[:], np.uint32)
+
+
+# ---------------------------------------------------------------------------
+# io_module_func backend (include/mosrx_io_module.h): gpu_module_func behind a
+# raw-socket / loopback source, driven by the RunMainLoop-shaped rx loop.
+# ---------------------------------------------------------------------------
+_VOIDFN = C.CFUNCTYPE(None)
+_CTXFN = C.CFUNCTYPE(None, C.c_void_p)
+_IOCTLFN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int, C.c_int, C.c_void_p)
+_RECVFN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int)
+_RPTRFN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint16))
+PKT_RX_RSS, DRV_NAME, PKT_RX_RESULTS = 0x03, 0x08, 0x10
+
+
+class IoModuleFunc(C.Structure):
+    """io_module_func (core/src/include/io_module.h:63-78): 14 function pointers."""
+    _fields_ = [(n, C.c_void_p) for n in (
+        "load_module_upper_half", "load_module_lower_half", "init_handle", "link_devices",
+        "release_pkt", "get_wptr", "set_wptr", "send_pkts", "get_rptr", "get_nif", "recv_pkts",
+        "select", "destroy_handle", "dev_ioctl")]
+
+
+class RssInfo(C.Structure):
+    _fields_ = [("pktidx", C.c_int8), ("hash_value", C.c_uint32)]
+
+
+def gpu_module() -> IoModuleFunc:
+    return IoModuleFunc.in_dll(lib(), "gpu_module_func")
+
+
+class GpuBackend:
+    """One mTCP-thread's view of gpu_module_func over in-memory / pcap sources."""
+
+    def __init__(self, sources: list[int], params: Params | None = None, batch: int = 32768,
+                 max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
+                 ngpu: int = 1):
+        cfg = ModuleCfg()
+        lib().mosrx_gpu_module_cfg_default(C.byref(cfg))
+        cfg.num_ifs = len(sources)
+        for i, s in enumerate(sources):
+            cfg.src[i] = s
+            cfg.if_names[i].value = f"gpu{i}".encode()
+        cfg.batch, cfg.max_frame, cfg.pipeline = batch, max_frame, int(pipeline)
+        cfg.gpu_base, cfg.ngpu = gpu_base, ngpu
+        if params is not None:
+            cfg.params = params
+        _chk(lib().mosrx_gpu_module_configure(C.byref(cfg)), "mosrx_gpu_module_configure")
+        self.nif = len(sources)
+        self.sources = list(sources)
+        self.m = gpu_module()
+        self._ctx_obj = C.c_uint64(0xC0DE0000 + cpu)      # stands in for struct mtcp_thread_context *
+        self.ctx = C.addressof(self._ctx_obj)
+        _chk(lib().mosrx_gpu_module_bind(self.ctx, cpu), "mosrx_gpu_module_bind")
+        _VOIDFN(self.m.load_module_upper_half)()
+        _CTXFN(self.m.init_handle)(self.ctx)
+        self._recv = _RECVFN(self.m.recv_pkts)
+        self._rptr = _RPTRFN(self.m.get_rptr)
+        self._ioctl = _IOCTLFN(self.m.dev_ioctl)
+
+    def recv_pkts(self, ifidx: int = 0) -> int:
+        return self._recv(self.ctx, ifidx)
+
+    def get_rptr(self, ifidx: int, index: int) -> bytes | None:
+        ln = C.c_uint16()
+        p = self._rptr(self.ctx, ifidx, index, C.byref(ln))
+        return C.string_at(p, ln.value) if p else None
+
+    def results(self, ifidx: int, n: int) -> np.ndarray:
+        p = C.c_void_p()
+        if self._ioctl(self.ctx, ifidx, PKT_RX_RESULTS, C.byref(p)):
+            raise MosrxError(5, "dev_ioctl(MOSRX_PKT_RX_RESULTS)")
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), (n * 16,)).view(RESULT_DTYPE).copy()
+
+    def rss_of(self, ifidx: int, pktidx: int) -> int | None:
+        ri = RssInfo(pktidx, 0)
+        return None if self._ioctl(self.ctx, ifidx, PKT_RX_RSS, C.byref(ri)) else ri.hash_value
+
+    def run_loop(self, max_pkts: int = 0) -> RxStats:
+        st = RxStats()
+        _chk(lib().mosrx_rx_loop(C.addressof(self.m), self.ctx, self.nif, max_pkts, None, None,
+                                 C.byref(st)), "mosrx_rx_loop")
+        return st
+
+    def close(self):
+        if self.ctx:
+            _CTXFN(self.m.destroy_handle)(self.ctx)
+            self.ctx = None
+            for s in self.sources:
+                lib().mosrx_source_close(s)
+            self.sources = []
+
+
+def mem_source(frames: np.ndarray, off: np.ndarray, ln: np.ndarray, loops: int = 1) -> int:
+    frames = np.ascontiguousarray(frames, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    ln = np.ascontiguousarray(ln, np.uint16)
+    s = lib().mosrx_source_mem(frames.ctypes.data, off.ctypes.data, ln.ctypes.data, len(off), loops)
+    if not s:
+        raise MosrxError(12, "mosrx_source_mem")
+    return s

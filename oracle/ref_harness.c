@@ -1,0 +1,161 @@
+/*
+ * ref_harness.c — TEST INFRASTRUCTURE ONLY.
+ *
+ * Drives mOS's OWN compiled receive path (core/src objects built by
+ * oracle/ref.mk from /root/reference, output in oracle/_ref/) over a trace
+ * file, to pin the C restatement in mosrx_oracle.c and to generate the golden
+ * vectors under tests/golden/.  It follows the reference's fake-backend test
+ * pattern (core/test/scalable_event/test.c:21-43): a static mtcp_manager and
+ * a zeroed io_module_func instead of a running stack.
+ *
+ * Usage: mosref <trace.in> <results.out>
+ *   trace.in : "MRXT" | u32 ver=1 | u32 n | u64 frames_bytes |
+ *              u32 num_msp | u32 num_esp | i32 forward | i32 num_queues | i32 queue_mode |
+ *              u32 off[n] | u16 len[n] | u8 frames[frames_bytes]
+ *   results  : n x { i8 verdict, u8 have, u16 ip_csum, u16 tcp_csum, u16 pad, u32 rss, i32 queue }
+ *              then u64 rx_packets, rx_bytes, rx_errors (NETSTAT, eth_in.c:42-45,80-84)
+ *   have bit0: ip_csum computed, bit1: tcp_csum computed, bit2: rss computed,
+ *        bit3: frame skipped (would make the reference read past caplen).
+ *
+ * forward must be 0: ForwardIPPacket/ForwardEthernetFrame need route/ARP
+ * tables and TX buffers.
+ */
+#include <arpa/inet.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mtcp.h"
+#include "config.h"
+#include "io_module.h"
+#include "ip_in.h"
+#include "eth_in.h"
+#include "tcp_util.h"
+#include "fhash.h"
+#include "logger.h"
+#include "mtcp_util.h"
+
+int ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index,
+                  uint32_t cur_ts, unsigned char *pkt_data, int len);
+uint16_t TCPCalcChecksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t daddr);
+
+static int g_qmode = 1;
+int __wrap_FetchEndianType(void) { return g_qmode; }
+
+struct rec {
+	int8_t verdict;
+	uint8_t have;
+	uint16_t ip_csum, tcp_csum, pad;
+	uint32_t rss;
+	int32_t queue;
+};
+
+static int rd(FILE *f, void *p, size_t n) { return fread(p, 1, n, f) == n ? 0 : -1; }
+
+int main(int argc, char **argv)
+{
+	FILE *in, *out;
+	char magic[4];
+	uint32_t ver, n, i;
+	uint64_t fb;
+	uint32_t num_msp, num_esp;
+	int32_t forward, nq, qmode;
+	uint32_t *off;
+	uint16_t *len;
+	uint8_t *frames;
+	static struct mtcp_manager m;
+	static struct mtcp_thread_context tctx;
+	static struct mos_conf mc;
+	static struct netdev_conf nd;
+	static io_module_func null_iom;
+	static log_thread_context lg;
+
+	if (argc != 3) {
+		fprintf(stderr, "usage: %s trace.in results.out\n", argv[0]);
+		return 2;
+	}
+	in = fopen(argv[1], "rb");
+	if (!in || rd(in, magic, 4) || memcmp(magic, "MRXT", 4) || rd(in, &ver, 4) || ver != 1 ||
+	    rd(in, &n, 4) || rd(in, &fb, 8) || rd(in, &num_msp, 4) || rd(in, &num_esp, 4) ||
+	    rd(in, &forward, 4) || rd(in, &nq, 4) || rd(in, &qmode, 4)) {
+		fprintf(stderr, "bad trace header\n");
+		return 1;
+	}
+	if (forward != 0 || nq < 1) {
+		fprintf(stderr, "forward must be 0 and num_queues >= 1\n");
+		return 1;
+	}
+	off = malloc((size_t)n * 4 + 1);
+	len = malloc((size_t)n * 2 + 1);
+	frames = calloc(fb + 64, 1); /* +64: the masked odd-tail read may touch one byte past a frame */
+	if (!off || !len || !frames || rd(in, off, (size_t)n * 4) || rd(in, len, (size_t)n * 2) ||
+	    rd(in, frames, fb)) {
+		fprintf(stderr, "short trace\n");
+		return 1;
+	}
+	fclose(in);
+	g_qmode = qmode;
+
+	/* stack state: core.c:1079-1110 InitializeMTCPManager, reduced */
+	nd.num = 0;
+	mc.forward = forward;
+	mc.netdev_table = &nd;
+	g_config.mos = &mc;
+	tctx.cpu = 0;
+	TAILQ_INIT(&m.monitors);
+	m.num_msp = num_msp;
+	m.num_esp = num_esp;
+	m.tcp_flow_table = CreateHashtable();
+	m.iom = &null_iom;
+	m.ctx = &tctx;
+	InitLogThreadContext(&lg, 0);
+	m.logger = &lg;
+	m.log_fp = fopen("/dev/null", "w");
+
+	out = fopen(argv[2], "wb");
+	if (!out)
+		return 1;
+	for (i = 0; i < n; i++) {
+		uint8_t *f = frames + off[i];
+		uint32_t cap = len[i];
+		struct rec r;
+		memset(&r, 0, sizeof(r));
+		if (cap < 14) {
+			r.have = 8;
+		} else if (f[12] == 0x08 && f[13] == 0x00) {
+			struct iphdr *iph = (struct iphdr *)(f + 14);
+			if (cap < 34) {
+				r.have = 8;
+			} else {
+				unsigned ihl = iph->ihl, ip_len = ntohs(iph->tot_len), proto = iph->protocol;
+				if (14 + ihl * 4 > cap || 14 + ip_len > cap || (proto == 6 && 14 + ihl * 4 + 20 > cap)) {
+					r.have = 8;
+				} else {
+					struct tcphdr *th = (struct tcphdr *)((uint8_t *)iph + ihl * 4);
+					uint16_t sp = proto == 6 ? ntohs(th->source) : 0;
+					uint16_t dp = proto == 6 ? ntohs(th->dest) : 0;
+					r.ip_csum = ip_fast_csum(iph, ihl);
+					r.have |= 1;
+					if (proto == 6 && ip_len >= (ihl + th->doff) * 4) {
+						uint16_t payloadlen = ip_len - (ihl * 4 + th->doff * 4);
+						r.tcp_csum = TCPCalcChecksum((uint16_t *)th, (th->doff << 2) + payloadlen,
+						                             iph->saddr, iph->daddr);
+						r.have |= 2;
+					}
+					r.rss = GetRSSHash(ntohl(iph->saddr), ntohl(iph->daddr), sp, dp);
+					r.queue = GetRSSCPUCore(ntohl(iph->saddr), ntohl(iph->daddr), sp, dp, nq);
+					r.have |= 4;
+				}
+			}
+		}
+		if (!(r.have & 8))
+			r.verdict = (int8_t)ProcessPacket(&m, 0, (int)i, 0, f, (int)cap);
+		fwrite(&r, sizeof(r), 1, out);
+	}
+	fwrite(&m.nstat.rx_packets[0], 8, 1, out);
+	fwrite(&m.nstat.rx_bytes[0], 8, 1, out);
+	fwrite(&m.nstat.rx_errors[0], 8, 1, out);
+	fclose(out);
+	return 0;
+}

@@ -1,0 +1,191 @@
+"""Generate the golden vectors in tests/golden/ from mOS's OWN compiled rx path.
+
+Run in the build container (needs /root/reference):
+    make -C oracle ref && python tests/golden/make_golden.py
+
+For every fixture trace it runs oracle/_ref/mosref (core/src objects compiled
+from /root/reference by oracle/ref.mk + oracle/ref_harness.c) under several
+stack states and stores inputs and the reference's outputs as .npz data:
+  verdict  = ProcessPacket() return (eth_in.c:27)
+  ip_csum  = ip_fast_csum(iph, ihl) (include/ip_in.h:10)
+  tcp_csum = TCPCalcChecksum(...)   (tcp_util.c:157)
+  rss      = GetRSSHash(ntohl(saddr), ntohl(daddr), ntohs(sp), ntohs(dp)) (util.c:61)
+  queue    = GetRSSCPUCore(...)     (util.c:114, FetchEndianType wrapped for ixgbe)
+  have     = which of those the harness computed (bit3: frame skipped, see harness)
+plus the NETSTAT rx counters.  The MSDN Toeplitz KAT (util/rss.c:177-193) is
+stored as its own fixture.  Nothing here is reference source: only data.
+"""
+from __future__ import annotations
+
+import os
+import random
+import struct
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from pktlib import ETH_ARP, pack_frames, tcp_frame  # noqa: E402
+import oracle_py as O  # noqa: E402
+
+STATES = [  # (name, num_msp, num_esp, num_queues, queue_mode)
+    ("msp1", 1, 0, 1, 1),
+    ("noverify", 0, 0, 1, 1),
+    ("esp1", 0, 1, 1, 1),
+    ("q2_i40e", 1, 0, 2, 1),
+    ("q4_i40e", 1, 0, 4, 1),
+    ("q8_i40e", 1, 0, 8, 1),
+    ("q3_ixgbe", 1, 0, 3, 0),
+    ("q8_ixgbe", 1, 0, 8, 0),
+]
+
+
+def edge_frames() -> list[bytes]:
+    """Hand-made frames for the edges listed in SURVEY.md §8a."""
+    f = []
+    f.append(tcp_frame(payload=b"abcdef"))                              # valid 64B-class
+    f.append(tcp_frame(payload=b"abcde"))                               # odd length valid
+    odd = bytearray(tcp_frame(payload=b"abcde")); odd[-1] ^= 0x40
+    f.append(bytes(odd))                                                # odd payload corrupted
+    f.append(tcp_frame(payload=b"abcde", pad_to=60))                    # odd, byte after end = 0
+    odd2 = bytearray(tcp_frame(payload=b"abcde", pad_to=60)); odd2[14 + 45] = 0x77
+    f.append(bytes(odd2))                                               # byte after odd end changed
+    th = bytearray(tcp_frame(payload=b"xyz!")); th[14 + 20 + 4] ^= 1
+    f.append(bytes(th))                                                 # TCP header corrupted
+    for ihl in range(0, 5):
+        f.append(tcp_frame(ihl=ihl, pad_to=60))                         # ihl 0..4 quirk
+    f.append(tcp_frame(version=6))
+    f.append(tcp_frame(tot_len=19, pad_to=60))
+    f.append(tcp_frame(tot_len=0, pad_to=60))
+    f.append(tcp_frame(tot_len=20, pad_to=60))
+    f.append(tcp_frame(tot_len=39, pad_to=60))
+    f.append(tcp_frame(proto=17, payload=b"udpudpudp"))
+    f.append(tcp_frame(proto=17, payload=b"udp", ip_csum=0x1234))       # UDP bad IP csum
+    f.append(tcp_frame(proto=1, payload=b"\x08\x00icmp"))               # ICMP, no local IP
+    f.append(tcp_frame(ip_csum=0xBEEF))                                 # bad IP checksum
+    f.append(tcp_frame(ethertype=ETH_ARP, pad_to=60))
+    f.append(tcp_frame(ethertype=0x86DD, pad_to=60))
+    f.append(tcp_frame(ethertype=0x8100, pad_to=60))
+    f.append(tcp_frame(doff=4))
+    f.append(tcp_frame(doff=0))
+    f.append(tcp_frame(doff=15, tot_len=46, pad_to=100))
+    f.append(tcp_frame(ihl=6, payload=b"opts"))
+    f.append(tcp_frame(ihl=15, payload=b"maxopts"))
+    f.append(tcp_frame(ihl=15, doff=15, payload=b"both max"))
+    v = tcp_frame(payload=b"complement")
+    vv = bytearray(v); c = struct.unpack("!H", vv[14 + 20 + 16:14 + 20 + 18])[0]
+    vv[14 + 20 + 16:14 + 20 + 18] = struct.pack("!H", (~c) & 0xFFFF)
+    f.append(bytes(vv))                                                 # TCP check complemented
+    big = tcp_frame(payload=bytes(range(256)) * 5 + bytes(168), doff=8)
+    f.append(big)                                                       # 1514 B valid
+    bb = bytearray(big); bb[700] ^= 0x10
+    f.append(bytes(bb))                                                 # one payload bit flipped
+    sw = bytearray(big); sw[600:602], sw[602:604] = sw[602:604], sw[600:602]
+    f.append(bytes(sw))                                                 # two aligned words swapped
+    pad = bytearray(tcp_frame(payload=b"ab", pad_to=60)); pad[58] = 0xAA
+    f.append(bytes(pad))                                                # Ethernet pad byte corrupted
+    f.append(tcp_frame(payload=bytes(1), flags=0x02))                   # SYN, 1 byte
+    f.append(tcp_frame(src="255.255.255.255", dst="255.255.255.255", sport=65535, dport=65535))
+    f.append(tcp_frame(src="0.0.0.0", dst="0.0.0.0", sport=0, dport=0))
+    # ip_fast_csum carry-chain corner: header words summing to 0 / 0xFFFF classes
+    f.append(tcp_frame(src="255.255.255.255", dst="255.255.255.255", tos=0xFF, ip_id=0xFFFF, ttl=255))
+    return f
+
+
+def random_frames(rng: random.Random, n: int, size_class: int) -> list[bytes]:
+    """Valid frames with random mutations of every header field the path reads."""
+    out = []
+    for _ in range(n):
+        if size_class == 0:
+            plen = rng.randint(0, 26)
+        elif size_class == 1:
+            plen = rng.randint(400, 560)
+        else:
+            plen = rng.randint(1300, 1460)
+        ihl = 5 if rng.random() < 0.7 else rng.randint(5, 15)
+        doff = 5 if rng.random() < 0.5 else rng.randint(5, 15)
+        ip = lambda: ".".join(str(rng.randint(0, 255)) for _ in range(4))  # noqa: E731
+        fr = bytearray(tcp_frame(ip(), ip(), rng.randint(0, 65535), rng.randint(0, 65535),
+                                 bytes(rng.getrandbits(8) for _ in range(plen)), ihl=ihl, doff=doff,
+                                 flags=rng.choice([0x02, 0x10, 0x18, 0x11, 0x04]),
+                                 seq=rng.getrandbits(32), ack=rng.getrandbits(32),
+                                 window=rng.getrandbits(16), ip_id=rng.getrandbits(16),
+                                 tos=rng.getrandbits(8), ttl=rng.randint(1, 255)))
+        m = rng.random()
+        tot = len(fr) - 14
+        if m < 0.25:
+            pass                                                       # valid
+        elif m < 0.35:
+            fr[rng.randint(14 + ihl * 4, len(fr) - 1)] ^= 1 << rng.randint(0, 7)   # payload flip
+        elif m < 0.42:
+            fr[rng.randint(14, 14 + ihl * 4 - 1)] ^= 1 << rng.randint(0, 7)        # IP header flip
+        elif m < 0.50:                                                 # shorter tot_len (Ethernet pad)
+            nt = rng.randint(0, tot)
+            fr[16:18] = struct.pack("!H", nt)
+        elif m < 0.56:
+            fr[14] = (fr[14] & 0xF0) | rng.randint(0, 15)              # ihl
+        elif m < 0.62:
+            fr[14] = (rng.randint(0, 15) << 4) | (fr[14] & 0xF)        # version
+        elif m < 0.68:
+            fr[14 + ihl * 4 + 12] = (rng.randint(0, 15) << 4) | (fr[14 + ihl * 4 + 12] & 0xF)  # doff
+        elif m < 0.72:
+            fr[23] = rng.choice([1, 17, 47, 0, 255])                   # protocol
+        elif m < 0.76:
+            fr[12:14] = struct.pack("!H", rng.choice([0x0806, 0x86DD, 0x8100, 0x0000, 0x0801]))
+        elif m < 0.88:                                                 # fix up IP csum after a field change
+            nt = rng.randint(20, tot)
+            fr[16:18] = struct.pack("!H", nt)
+            fr[24:26] = b"\0\0"
+            from pktlib import csum16
+            fr[24:26] = struct.pack("!H", csum16(bytes(fr[14:14 + ihl * 4])))
+        else:
+            fr[14 + ihl * 4 + 16] ^= rng.getrandbits(8)                # TCP check field
+        if rng.random() < 0.1:
+            fr += bytes(rng.getrandbits(8) for _ in range(rng.randint(1, 9)))  # trailing bytes in caplen
+        out.append(bytes(fr))
+    return out
+
+
+def run_states(frames: list[bytes], name: str, phase: int = 2):
+    buf, off, ln = pack_frames(frames, phase=phase)
+    res = {}
+    for st, msp, esp, nq, qm in STATES:
+        rec, stats = O.run_ref(buf, off, ln, num_msp=msp, num_esp=esp, num_queues=nq, queue_mode=qm)
+        res[st] = rec
+        res[st + "_stats"] = np.array([stats["rx_packets"], stats["rx_bytes"], stats["rx_errors"]],
+                                      np.uint64)
+    out = {"frames": buf, "off": off, "len": ln}
+    for st, *_ in STATES:
+        r = res[st]
+        for fld in ("verdict", "have", "ip_csum", "tcp_csum", "rss", "queue"):
+            out[f"{st}__{fld}"] = np.ascontiguousarray(r[fld])
+        out[f"{st}__stats"] = res[st + "_stats"]
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(f"{name}: {len(frames)} frames, {len(buf)} bytes")
+
+
+def main():
+    if not O.have_ref():
+        sys.exit("oracle/_ref/mosref missing: run `make -C oracle ref` first (needs /root/reference)")
+    rng = random.Random(0x6D4F5321)
+    run_states(edge_frames(), "edge")
+    run_states(random_frames(rng, 256, 0), "rand_small")
+    run_states(random_frames(rng, 256, 1), "rand_mid", phase=7)   # odd frame starts: byte-swap path
+    run_states(random_frames(rng, 256, 2), "rand_large")
+    # MSDN Toeplitz vectors (util/rss.c:177-193), Microsoft key (util/rss.c:75-81)
+    kat = np.array([
+        (0x420995bb, 0xa18e6450, 2794, 1766, 0x51ccc178),
+        (0xc75c6f02, 0x41458c53, 14230, 4739, 0xc626b0ea),
+        (0x1813c65f, 0x0c16cfb8, 12898, 38024, 0x5c2b394a),
+        (0x261bcd1e, 0xd18ea306, 48228, 2217, 0xafc7327f),
+        (0x9927a3bf, 0xcabc7f02, 44251, 1303, 0x10e828a2),
+    ], dtype=[("sip", "<u4"), ("dip", "<u4"), ("sp", "<u2"), ("dp", "<u2"), ("hash", "<u4")])
+    np.savez_compressed(os.path.join(HERE, "rss_msdn_kat.npz"), kat=kat,
+                        key=np.frombuffer(O.MS_KEY, np.uint8))
+    print("rss_msdn_kat: 5 vectors")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,102 @@
+"""ctypes access to the oracle (TEST INFRASTRUCTURE ONLY).
+
+Loads oracle/libmosrx_oracle.so (the C restatement) and, when it was built in
+this container, runs oracle/_ref/mosref (mOS's own compiled rx path).  Only
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+
+from pktlib import RESULT_DTYPE, read_ref_results, write_ref_trace
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "libmosrx_oracle.so")
+REF_BIN = os.path.join(ROOT, "oracle", "_ref", "mosref")
+
+MS_KEY = bytes([0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+                0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+                0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa])
+
+
+class Params(C.Structure):
+    _fields_ = [("num_msp", C.c_uint32), ("num_esp", C.c_uint32), ("forward", C.c_int32),
+                ("num_queues", C.c_int32), ("queue_mode", C.c_int32), ("skip_tcp_csum", C.c_int32),
+                ("rss_key_len", C.c_uint32), ("rss_key", C.c_uint8 * 52)]
+
+
+def params(num_msp=1, num_esp=0, forward=1, num_queues=1, queue_mode=1, skip_tcp_csum=0,
+           key=b"\x05" * 40) -> Params:
+    p = Params()
+    p.num_msp, p.num_esp, p.forward = num_msp, num_esp, forward
+    p.num_queues, p.queue_mode, p.skip_tcp_csum = num_queues, queue_mode, skip_tcp_csum
+    p.rss_key_len = len(key)
+    for i, b in enumerate(key):
+        p.rss_key[i] = b
+    return p
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = C.CDLL(ORACLE_SO)
+        L.mo_ip_fast_csum.restype = C.c_uint16
+        L.mo_ip_fast_csum.argtypes = [C.c_char_p, C.c_uint]
+        L.mo_tcp_csum.restype = C.c_uint16
+        L.mo_tcp_csum.argtypes = [C.c_char_p, C.c_uint16, C.c_uint32, C.c_uint32]
+        L.mo_rss_key_cache.argtypes = [C.c_char_p, C.POINTER(C.c_uint32)]
+        L.mo_rss_hash.restype = C.c_uint32
+        L.mo_rss_hash.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32, C.c_uint16, C.c_uint16]
+        L.mo_rss_queue.restype = C.c_int
+        L.mo_rss_queue.argtypes = [C.c_uint32, C.c_int, C.c_int]
+        L.mo_classify.restype = C.c_int
+        L.mo_classify.argtypes = [C.POINTER(Params), C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                  C.c_uint32, C.c_void_p]
+        L.mo_classify_mt.restype = C.c_int
+        L.mo_classify_mt.argtypes = L.mo_classify.argtypes + [C.c_int]
+        _lib = L
+    return _lib
+
+
+def rss_hash(key: bytes, sip: int, dip: int, sp: int, dp: int) -> int:
+    cache = (C.c_uint32 * 96)()
+    lib().mo_rss_key_cache(key, cache)
+    return lib().mo_rss_hash(cache, sip, dip, sp, dp)
+
+
+def classify(buf, off, ln, p: Params | None = None, nthreads: int = 1) -> np.ndarray:
+    p = p or params()
+    buf = np.ascontiguousarray(buf, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    ln = np.ascontiguousarray(ln, np.uint16)
+    out = np.zeros(len(off), RESULT_DTYPE)
+    args = (C.byref(p), buf.ctypes.data, len(buf), off.ctypes.data, ln.ctypes.data, len(off),
+            out.ctypes.data)
+    rc = lib().mo_classify_mt(*args, nthreads) if nthreads > 1 else lib().mo_classify(*args)
+    if rc:
+        raise OSError(-rc, "mo_classify failed")
+    return out
+
+
+def have_ref() -> bool:
+    return os.path.exists(REF_BIN)
+
+
+def run_ref(buf, off, ln, *, num_msp=1, num_esp=0, num_queues=1, queue_mode=1):
+    """Run mOS's own compiled rx path (forward=0) over the frames."""
+    with tempfile.TemporaryDirectory() as d:
+        tin, tout = os.path.join(d, "t.in"), os.path.join(d, "t.out")
+        write_ref_trace(tin, buf, off, ln, num_msp=num_msp, num_esp=num_esp, forward=0,
+                        num_queues=num_queues, queue_mode=queue_mode)
+        subprocess.run([REF_BIN, tin, tout], check=True, stdout=subprocess.DEVNULL)
+        return read_ref_results(tout, len(off))

@@ -1,0 +1,109 @@
+"""Frame construction and trace (de)serialisation helpers for the tests.
+
+Pure Python, standard RFC 1071 arithmetic written independently of both the
+HIP kernels and the oracle, used only to BUILD input frames (valid or
+deliberately broken).  Expected outputs always come from the oracle / the
+reference harness, never from this file.
+"""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+
+ETH_IP = 0x0800
+ETH_ARP = 0x0806
+RESULT_DTYPE = np.dtype([
+    ("rss", "<u4"), ("ip_csum", "<u2"), ("tcp_csum", "<u2"), ("payloadlen", "<u2"),
+    ("payload_off", "u1"), ("verdict", "i1"), ("reason", "u1"), ("queue", "u1"),
+    ("tcp_flags", "u1"), ("ihl_doff", "u1"),
+])
+assert RESULT_DTYPE.itemsize == 16
+
+R = dict(TCP_OK=0, ARP=1, NON_IPV4=2, IP_SHORT=3, IP_BADVER=4, NOVERIFY_PASS=5, IP_BADCSUM=6,
+         NOT_TCP=7, TCP_SHORT=8, TCP_BADCSUM=9, TRUNCATED=10, TCP_LEN_OK=11)
+
+
+def csum16(data: bytes) -> int:
+    """RFC 1071 one's-complement checksum of big-endian 16-bit words."""
+    if len(data) % 2:
+        data = data + b"\0"
+    s = sum(struct.unpack("!%dH" % (len(data) // 2), data))
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return (~s) & 0xFFFF
+
+
+def ip4(a: str) -> bytes:
+    return bytes(int(x) for x in a.split("."))
+
+
+def tcp_frame(src="10.0.0.1", dst="10.0.0.2", sport=1234, dport=80, payload=b"", *,
+              ihl=5, doff=5, flags=0x10, seq=1, ack=1, window=65535, ttl=64, ip_id=0,
+              proto=6, version=4, tot_len=None, ip_opts=None, tcp_opts=None,
+              ip_csum=None, tcp_csum=None, pad_to=0, ethertype=ETH_IP, tos=0) -> bytes:
+    """Build an Ethernet/IPv4/TCP frame.  Checksums are valid unless overridden."""
+    ip_opts = ip_opts if ip_opts is not None else b"\x01" * (ihl * 4 - 20 if ihl > 5 else 0)
+    tcp_opts = tcp_opts if tcp_opts is not None else b"\x01" * (doff * 4 - 20 if doff > 5 else 0)
+    tcph_wo = struct.pack("!HHIIBBHHH", sport, dport, seq, ack, (doff & 0xF) << 4, flags, window, 0, 0)
+    seg = tcph_wo + tcp_opts + payload
+    hdr_len = 20 + len(ip_opts)
+    if tot_len is None:
+        tot_len = hdr_len + len(seg)
+    s, d = ip4(src), ip4(dst)
+    iph = struct.pack("!BBHHHBBH4s4s", ((version & 0xF) << 4) | (ihl & 0xF), tos, tot_len & 0xFFFF,
+                      ip_id & 0xFFFF, 0x4000, ttl, proto, 0, s, d) + ip_opts
+    if ip_csum is None:
+        ip_csum = csum16(iph)
+    iph = iph[:10] + struct.pack("!H", ip_csum) + iph[12:]
+    if proto == 6 and tcp_csum is None:
+        pseudo = s + d + struct.pack("!BBH", 0, 6, len(seg))
+        tcp_csum = csum16(pseudo + seg)
+    if proto == 6:
+        seg = seg[:16] + struct.pack("!H", tcp_csum) + seg[18:]
+    eth = b"\x02\x00\x00\x00\x00\x02" + b"\x02\x00\x00\x00\x00\x01" + struct.pack("!H", ethertype)
+    frame = eth + iph + seg
+    if len(frame) < pad_to:
+        frame += b"\0" * (pad_to - len(frame))
+    return frame
+
+
+def pack_frames(frames: list[bytes], align: int = 16, phase: int = 2, gap: int = 0):
+    """Pack frames into one buffer; frame i starts at a multiple of `align` plus `phase`.
+
+    Returns (buf: uint8[], off: uint32[], len: uint16[]).  The buffer gets 64 zero
+    bytes of tail padding (the reference's masked odd-tail read may touch one byte
+    past a frame).
+    """
+    offs, pos = [], phase
+    for f in frames:
+        offs.append(pos)
+        pos += len(f) + gap
+        if align > 1:
+            pos = ((pos - phase + align - 1) // align) * align + phase
+    buf = np.zeros(pos + 64, np.uint8)
+    for o, f in zip(offs, frames):
+        buf[o:o + len(f)] = np.frombuffer(f, np.uint8)
+    return buf, np.asarray(offs, np.uint32), np.asarray([len(f) for f in frames], np.uint16)
+
+
+def write_ref_trace(path, buf, off, ln, *, num_msp=1, num_esp=0, forward=0, num_queues=1,
+                    queue_mode=1):
+    """Trace file consumed by oracle/_ref/mosref (format in oracle/ref_harness.c)."""
+    with open(path, "wb") as fh:
+        fh.write(b"MRXT" + struct.pack("<IIQIIiii", 1, len(off), len(buf), num_msp, num_esp,
+                                       forward, num_queues, queue_mode))
+        fh.write(np.asarray(off, "<u4").tobytes())
+        fh.write(np.asarray(ln, "<u2").tobytes())
+        fh.write(np.asarray(buf, np.uint8).tobytes())
+
+
+REF_DTYPE = np.dtype([("verdict", "i1"), ("have", "u1"), ("ip_csum", "<u2"), ("tcp_csum", "<u2"),
+                      ("pad", "<u2"), ("rss", "<u4"), ("queue", "<i4")])
+
+
+def read_ref_results(path, n):
+    raw = open(path, "rb").read()
+    rec = np.frombuffer(raw[: n * 16], REF_DTYPE)
+    stats = struct.unpack("<QQQ", raw[n * 16: n * 16 + 24])
+    return rec, dict(rx_packets=stats[0], rx_bytes=stats[1], rx_errors=stats[2])

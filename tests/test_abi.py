@@ -1,0 +1,155 @@
+"""CPU-side checks of the C ABI: the library loads, exports every declared
+symbol, validates arguments, fails loudly without a GPU, and its host-side
+logic (RSS tables, queue LUT inputs, trace generator, frame sources) agrees
+with the oracle.  No kernel is launched here."""
+import ctypes as C
+import os
+import re
+import struct
+import tempfile
+
+import numpy as np
+import pytest
+
+import mosrx
+import oracle_py as O
+from pktlib import R, pack_frames, tcp_frame
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    names = set()
+    for h in ("mosrx.h", "mosrx_io_module.h", "mosrx_trace.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b(mosrx_[a-z0-9_]+)\s*\(", txt))
+    return sorted(names)
+
+
+def test_every_declared_symbol_is_exported():
+    lib = C.CDLL(mosrx.LIB_PATH)
+    syms = declared_symbols()
+    assert len(syms) > 30
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert hasattr(lib, "gpu_module_func")
+    assert mosrx.lib().mosrx_abi_version() == 1
+
+
+def test_no_oracle_in_product_library():
+    lib = C.CDLL(mosrx.LIB_PATH)
+    for s in ("mo_classify", "mo_tcp_csum", "mo_ip_fast_csum", "mo_rss_hash"):
+        assert not hasattr(lib, s)
+    src = open(os.path.join(ROOT, "mos-networking-stack_amd", "mosrx", "__init__.py")).read()
+    assert "oracle" not in src
+
+
+def test_struct_layouts():
+    assert C.sizeof(mosrx.Params) == 80
+    assert C.sizeof(mosrx.Batch) == 40
+    assert mosrx.RESULT_DTYPE.itemsize == 16
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK),
+                    reason="a GPU is visible")
+def test_open_without_gpu_fails_loudly():
+    with pytest.raises(mosrx.MosrxError) as e:
+        mosrx.Context(0)
+    assert e.value.errno == 19  # ENODEV: no CPU fallback
+
+
+def test_param_validation_before_device():
+    h = C.c_void_p()
+    for kw in (dict(num_queues=0), dict(num_queues=257), dict(queue_mode=5)):
+        p = mosrx.default_params(**kw)
+        assert mosrx.lib().mosrx_open(0, C.byref(p), C.byref(h)) == -22
+    p = mosrx.default_params()
+    p.rss_key_len = 8
+    assert mosrx.lib().mosrx_open(0, C.byref(p), C.byref(h)) == -22
+    assert mosrx.lib().mosrx_classify_dev(None, None, None, None) == -22
+
+
+def test_defaults_match_simple_firewall_state():
+    p = mosrx.default_params()
+    assert (p.num_msp, p.num_esp, p.forward, p.num_queues, p.queue_mode) == (1, 0, 1, 1, 1)
+    assert bytes(p.rss_key[:40]) == b"\x05" * 40 and p.rss_key_len == 40
+
+
+@pytest.mark.parametrize("key", [b"\x05" * 40, mosrx.MS_KEY, bytes(range(1, 53))])
+def test_rss_nibble_tables_equal_key_cache_hash(key):
+    tab = mosrx.rss_tables(key).reshape(24, 16)
+    rng = np.random.default_rng(7)
+    for _ in range(200):
+        sip, dip = (int(x) for x in rng.integers(0, 2**32, 2, dtype=np.uint64))
+        sp, dp = (int(x) for x in rng.integers(0, 2**16, 2))
+        tup = struct.pack("!IIHH", sip, dip, sp, dp)
+        h = 0
+        for k, b in enumerate(tup):
+            h ^= int(tab[2 * k][b >> 4]) ^ int(tab[2 * k + 1][b & 15])
+        assert h == O.rss_hash(key, sip, dip, sp, dp)
+
+
+def test_trace_generator_layout_and_content():
+    for kind, n, cap in [(mosrx.TRACE_S64, 3000, {60}), (mosrx.TRACE_M1500, 700, {1514}),
+                         (mosrx.TRACE_IMIX, 2400, {60, 590, 1514})]:
+        t = mosrx.Trace(kind, n, nflows=5000)
+        assert t.n == n and set(np.unique(t.len).tolist()) == cap
+        assert np.all(t.off % 16 == 2)
+        assert np.all(t.off[1:] >= t.off[:-1] + t.len[:-1])
+        assert t.off[-1] + t.len[-1] <= t.frames_bytes
+        res = O.classify(t.frames, t.off, t.len, O.params())
+        idx = np.arange(n)
+        bad_ip, bad_tcp = idx % 1024 == 511, idx % 1024 == 1023
+        assert np.all(res["reason"][bad_ip] == R["IP_BADCSUM"])
+        assert np.all(res["reason"][bad_tcp] == R["TCP_BADCSUM"])
+        assert np.all(res["reason"][~bad_ip & ~bad_tcp] == R["TCP_OK"])
+    imix = mosrx.Trace(mosrx.TRACE_IMIX, 12000, nflows=1000)
+    assert abs(imix.caplen_sum / imix.n - 357.83) < 0.01
+
+
+def test_trace_is_deterministic():
+    a = mosrx.Trace(mosrx.TRACE_IMIX, 500, nflows=100)
+    b = mosrx.Trace(mosrx.TRACE_IMIX, 500, nflows=100)
+    assert np.array_equal(a.frames, b.frames) and np.array_equal(a.off, b.off)
+    c = mosrx.Trace(mosrx.TRACE_IMIX, 500, nflows=100, seed=99)
+    assert not np.array_equal(a.frames, c.frames)
+
+
+def _drain(src, cap=4096):
+    buf = np.zeros(cap, np.uint8)
+    out = []
+    while True:
+        n = mosrx.lib().mosrx_source_next(src, buf.ctypes.data, cap)
+        if n <= 0:
+            return out
+        out.append(bytes(buf[:n]))
+
+
+def test_mem_source_replays_frames():
+    frames = [tcp_frame(payload=bytes([i]) * i) for i in range(1, 9)]
+    buf, off, ln = pack_frames(frames)
+    src = mosrx.lib().mosrx_source_mem(buf.ctypes.data, off.ctypes.data, ln.ctypes.data, len(frames), 2)
+    assert src
+    got = _drain(src)
+    mosrx.lib().mosrx_source_close(src)
+    assert got == frames * 2
+
+
+@pytest.mark.parametrize("swap,nsec", [(False, False), (True, False), (False, True)])
+def test_pcap_source_reads_classic_pcap(swap, nsec):
+    frames = [tcp_frame(payload=b"p" * i) for i in range(0, 40, 7)]
+    e = ">" if swap else "<"
+    magic = 0xA1B23C4D if nsec else 0xA1B2C3D4
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "t.pcap")
+        with open(path, "wb") as fh:
+            fh.write(struct.pack(e + "IHHiIII", magic, 2, 4, 0, 0, 65535, 1))
+            for i, f in enumerate(frames):
+                fh.write(struct.pack(e + "IIII", i, 0, len(f), len(f)) + f)
+        src = mosrx.lib().mosrx_source_pcap(path.encode(), 1)
+        assert src
+        got = _drain(src)
+        mosrx.lib().mosrx_source_close(src)
+    assert got == frames
+    assert not mosrx.lib().mosrx_source_pcap(b"/nonexistent.pcap", 1)

@@ -1,0 +1,135 @@
+"""Pin the oracle (C restatement) against mOS's own outputs.
+
+The fixtures in tests/golden/ were produced by mOS's compiled core/src rx path
+(oracle/_ref/mosref, see tests/golden/make_golden.py); the MSDN Toeplitz KAT
+comes from util/rss.c:177-193.  When oracle/_ref/mosref exists (this build
+container) the oracle is also fuzzed against the reference directly.
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from pktlib import R, pack_frames, tcp_frame
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = ["edge", "rand_small", "rand_mid", "rand_large"]
+STATES = {  # name -> (num_msp, num_esp, num_queues, queue_mode)
+    "msp1": (1, 0, 1, 1), "noverify": (0, 0, 1, 1), "esp1": (0, 1, 1, 1),
+    "q2_i40e": (1, 0, 2, 1), "q4_i40e": (1, 0, 4, 1), "q8_i40e": (1, 0, 8, 1),
+    "q3_ixgbe": (1, 0, 3, 0), "q8_ixgbe": (1, 0, 8, 0),
+}
+
+
+def compare_with_ref(res, ref, p):
+    """Field-by-field agreement of oracle records with the reference harness output."""
+    trunc = res["reason"] == R["TRUNCATED"]
+    skipped = (ref["have"] & 8) != 0
+    np.testing.assert_array_equal(trunc, skipped, err_msg="TRUNCATED set differs from reference skips")
+    live = ~trunc
+    np.testing.assert_array_equal(res["verdict"][live], ref["verdict"][live], err_msg="verdict")
+    # header fields are defined once the version check passed
+    fields = live & ~np.isin(res["reason"], [R["ARP"], R["NON_IPV4"], R["IP_SHORT"], R["IP_BADVER"]])
+    np.testing.assert_array_equal(res["rss"][fields], ref["rss"][fields], err_msg="rss")
+    np.testing.assert_array_equal(res["queue"][fields], ref["queue"][fields].astype(np.uint8), err_msg="queue")
+    if p.num_msp or p.num_esp:
+        np.testing.assert_array_equal(res["ip_csum"][fields], ref["ip_csum"][fields], err_msg="ip_csum")
+    tcp = live & np.isin(res["reason"], [R["TCP_OK"], R["TCP_BADCSUM"]])
+    assert np.all(ref["have"][tcp] & 2)
+    np.testing.assert_array_equal(res["tcp_csum"][tcp], ref["tcp_csum"][tcp], err_msg="tcp_csum")
+    np.testing.assert_array_equal(res["tcp_csum"][tcp] == 0, res["verdict"][tcp] == 1)
+
+
+@pytest.mark.parametrize("fix", FIXTURES)
+@pytest.mark.parametrize("state", list(STATES))
+def test_oracle_matches_reference_fixture(fix, state):
+    z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
+    msp, esp, nq, qm = STATES[state]
+    p = O.params(num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm)
+    res = O.classify(z["frames"], z["off"], z["len"], p)
+    ref = {k: z[f"{state}__{k}"] for k in ("verdict", "have", "ip_csum", "tcp_csum", "rss", "queue")}
+    compare_with_ref(res, ref, p)
+    # NETSTAT view (eth_in.c:42-45, 80-84) over the frames the reference processed
+    live = res["reason"] != R["TRUNCATED"]
+    st = z[f"{state}__stats"]
+    assert st[0] == live.sum()
+    assert st[1] == (z["len"][live].astype(np.uint64) + 24).sum()
+    assert st[2] == (res["verdict"][live] < 0).sum()
+
+
+def test_fixtures_cover_every_reason():
+    seen = set()
+    for fix in FIXTURES:
+        z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
+        for state, (msp, esp, nq, qm) in STATES.items():
+            p = O.params(num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm)
+            seen |= set(np.unique(O.classify(z["frames"], z["off"], z["len"], p)["reason"]).tolist())
+    missing = {k for k, v in R.items() if v not in seen} - {"TCP_LEN_OK"}
+    assert not missing, missing
+
+
+def test_msdn_rss_kat():
+    z = np.load(os.path.join(GOLDEN, "rss_msdn_kat.npz"))
+    key = bytes(z["key"])
+    for v in z["kat"]:
+        assert O.rss_hash(key, int(v["sip"]), int(v["dip"]), int(v["sp"]), int(v["dp"])) == int(v["hash"])
+
+
+def test_default_key_survey_values():
+    # 10.0.0.1:1234 -> 10.0.0.2:80 hashes to 0x27272727 with the 0x05 key;
+    # num_queues=8 gives queue 4 with the i40e map and 7 with ixgbe.
+    cache_key = b"\x05" * 40
+    h = O.rss_hash(cache_key, 0x0A000001, 0x0A000002, 1234, 80)
+    assert h == 0x27272727
+    assert O.lib().mo_rss_queue(h, 1, 8) == 4
+    assert O.lib().mo_rss_queue(h, 0, 8) == 7
+    # symmetric key: swapping the endpoints keeps the hash
+    assert O.rss_hash(cache_key, 0x0A000002, 0x0A000001, 80, 1234) == h
+
+
+def test_ip_fast_csum_quirk():
+    f = tcp_frame(ihl=4, pad_to=60)
+    for ihl in range(5):
+        assert O.lib().mo_ip_fast_csum(f[14:], ihl) == (f[14] | (f[15] << 8))
+
+
+def test_forward_nonip_verdicts():
+    # eth_in.c:62-77: forward && num_msp makes every non-IPv4 frame 1 (read from the code:
+    # the reference harness cannot run ForwardEthernetFrame without TX tables).
+    frames = [tcp_frame(ethertype=0x86DD, pad_to=60), tcp_frame(ethertype=0x0806, pad_to=60)]
+    buf, off, ln = pack_frames(frames)
+    a = O.classify(buf, off, ln, O.params(num_msp=1, forward=1))
+    assert list(a["verdict"]) == [1, 1]
+    b = O.classify(buf, off, ln, O.params(num_msp=0, num_esp=1, forward=1))
+    assert list(b["verdict"]) == [-1, 1]
+
+
+@pytest.mark.skipif(not O.have_ref(), reason="oracle/_ref/mosref not built (needs /root/reference)")
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_oracle_fuzz_vs_reference(seed):
+    from golden.make_golden import random_frames
+    rng = random.Random(seed)
+    frames = random_frames(rng, 300, seed % 3)
+    buf, off, ln = pack_frames(frames, phase=rng.choice([2, 3, 6, 9]))
+    for msp, esp, nq, qm in [(1, 0, 1, 1), (0, 1, 5, 0), (1, 1, 7, 1)]:
+        p = O.params(num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm)
+        rec, _ = O.run_ref(buf, off, ln, num_msp=msp, num_esp=esp, num_queues=nq, queue_mode=qm)
+        compare_with_ref(O.classify(buf, off, ln, p), rec, p)
+
+
+@pytest.mark.skipif(not O.have_ref(), reason="oracle/_ref/mosref not built (needs /root/reference)")
+def test_oracle_vs_reference_on_seeded_trace():
+    import mosrx
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 6000, nflows=1000)
+    p = O.params(forward=0)
+    rec, _ = O.run_ref(t.frames, t.off, t.len)
+    res = O.classify(t.frames, t.off, t.len, p)
+    compare_with_ref(res, rec, p)
+    # corruption schedule of the generator: 1/1024 IP, 1/1024 TCP
+    idx = np.arange(t.n)
+    assert np.all(res["reason"][idx % 1024 == 511] == R["IP_BADCSUM"])
+    assert np.all(res["reason"][idx % 1024 == 1023] == R["TCP_BADCSUM"])
+    ok = (idx % 1024 != 511) & (idx % 1024 != 1023)
+    assert np.all(res["reason"][ok] == R["TCP_OK"])

@@ -43,7 +43,9 @@ WORKLOADS = {
     "S64": (mosrx.TRACE_S64, 32_768, "1xMI355X 64B TCP, 1 flow, batch=32K (BASELINE config #2), full verdict"),
     "S64_hdr": (mosrx.TRACE_S64, 32_768, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum)"),
     "IMIX": (mosrx.TRACE_IMIX, 262_144, "IMIX 60/590/1514 7:4:1, 1M flows, batch=256K (BASELINE config #4)"),
+    "S64_queue": (mosrx.TRACE_S64, 32_768, "config #2, 64 batches of 32K per launch (device batch queue)"),
 }
+QUEUE_DEPTH = 64
 
 
 def dist_env():
@@ -108,19 +110,39 @@ def measure(ctx, dist, key, steps, warmup, rank):
     dbs = [ctx.upload(tr.frames, tr.off, tr.len, frames_bytes=tr.frames_bytes, max_len=tr.max_len)
            for _ in range(ncopy)]
     ab = algo_bytes(tr)
-    # warmup (untimed)
-    if warmup:
-        ctx.time_dev(dbs, warmup)
-    ctx.device_sync()
-    dist.barrier()
-    t0 = time.perf_counter()
-    dev_ms = ctx.time_dev(dbs, steps)          # K back-to-back launches, HIP events on the kernel stream
-    ctx.device_sync()
-    dist.barrier()
-    wall = time.perf_counter() - t0
-    wall_max = dist.max(wall)
-    # roofline: average duration of one launch, HIP events around each launch
-    kern_ms = ctx.time_dev_kernels(dbs, min(steps, 200))
+    if key.endswith("_queue"):
+        # each step = one launch over QUEUE_DEPTH distinct resident 32K batches
+        # several queues over disjoint batch copies: the working set exceeds the L3
+        qs = [ctx.queue(dbs[i:i + QUEUE_DEPTH]) for i in range(0, len(dbs) - QUEUE_DEPTH + 1, QUEUE_DEPTH)]
+        ab *= QUEUE_DEPTH
+        batch *= QUEUE_DEPTH
+        if warmup:
+            qs[0].time(warmup, qs[1:])
+        ctx.device_sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        dev_ms, _ = qs[0].time(steps, qs[1:])
+        ctx.device_sync()
+        dist.barrier()
+        wall = time.perf_counter() - t0
+        wall_max = dist.max(wall)
+        _, kern_ms = qs[0].time(min(steps, 64), qs[1:])
+        for q in qs:
+            q.destroy()
+    else:
+        # warmup (untimed)
+        if warmup:
+            ctx.time_dev(dbs, warmup)
+        ctx.device_sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        dev_ms = ctx.time_dev(dbs, steps)          # K back-to-back launches, HIP events on the kernel stream
+        ctx.device_sync()
+        dist.barrier()
+        wall = time.perf_counter() - t0
+        wall_max = dist.max(wall)
+        # roofline: average duration of one launch, HIP events around each launch
+        kern_ms = ctx.time_dev_kernels(dbs, min(steps, 200))
     for d in dbs:
         d.free()
     n = dist.ws
@@ -223,7 +245,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workloads", default="M1500,S64,S64_hdr,IMIX")
+    ap.add_argument("--workloads", default="M1500,S64,S64_hdr,S64_queue,IMIX")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (PCIe) leg")
     args = ap.parse_args()

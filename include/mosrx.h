@@ -127,6 +127,20 @@ int  mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out,
 int  mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
                              mosrx_result *const *d_out, void *stream);
 
+/* Batch queue: a device-resident descriptor table of `nb` resident batches
+ * that ONE kernel launch classifies (a workgroup finds its batch by binary
+ * search).  Amortises launch latency for small batches (64 B frames, 32K per
+ * batch); every batch keeps its own frames, descriptors and result buffer. */
+typedef struct mosrx_queue mosrx_queue;
+int  mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
+                        mosrx_result *const *d_out, mosrx_queue **q);
+int  mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream);
+void mosrx_queue_destroy(mosrx_ctx *c, mosrx_queue *q);
+/* `iters` back-to-back launches cycling over `nq` queues; HIP events on the
+ * kernel stream (total, and per launch for the average kernel duration). */
+int  mosrx_time_queue(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq, uint32_t iters,
+                      float *total_ms, float *avg_kernel_ms);
+
 /* End-to-end: host frames -> pinned staging -> H2D -> kernel -> D2H -> h_out.
  * Blocks until h_out is filled. */
 int  mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out);

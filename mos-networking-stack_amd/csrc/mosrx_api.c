@@ -558,3 +558,122 @@ int mosrx_device_sync(mosrx_ctx *c)
 	HIPCHK(hipDeviceSynchronize());
 	return 0;
 }
+
+/* ---- batch queue (one launch over many resident batches) ---- */
+struct mosrx_queue {
+	mosrx_qdesc *d_desc;
+	uint32_t nb;
+	uint32_t total_tiles;
+	int tile;
+};
+
+int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
+                       mosrx_queue **q)
+{
+	mosrx_qdesc *h;
+	mosrx_queue *qq;
+	uint32_t i, tiles = 0, maxl = 0;
+	int rc, unknown = 0, tile;
+	if (!c || !b || !d_out || !q || nb == 0)
+		return -EINVAL;
+	*q = NULL;
+	for (i = 0; i < nb; i++) {
+		if ((rc = check_batch(&b[i], 1)))
+			return rc;
+		if (b[i].n && (!d_out[i] || ((uintptr_t)d_out[i] & 15)))
+			return -EINVAL;
+		if (!b[i].max_len)
+			unknown = 1;
+		if (b[i].max_len > maxl)
+			maxl = b[i].max_len;
+	}
+	tile = (!unknown && maxl <= MOSRX_WINDOW_END) ? MOSRX_TILE_SMALL : MOSRX_TILE_LARGE;
+	h = calloc(nb, sizeof(*h));
+	qq = calloc(1, sizeof(*qq));
+	if (!h || !qq) {
+		free(h);
+		free(qq);
+		return -ENOMEM;
+	}
+	for (i = 0; i < nb; i++) {
+		h[i].frames = b[i].frames;
+		h[i].off = b[i].off;
+		h[i].len = b[i].len;
+		h[i].out = d_out[i];
+		h[i].frames_bytes = (uint32_t)b[i].frames_bytes;
+		h[i].n = b[i].n;
+		h[i].tile_base = tiles;
+		tiles += (b[i].n + (uint32_t)tile - 1) / (uint32_t)tile;
+	}
+	if (hipSetDevice(c->device) != hipSuccess ||
+	    hipMalloc((void **)&qq->d_desc, (size_t)nb * sizeof(*h)) != hipSuccess ||
+	    hipMemcpy(qq->d_desc, h, (size_t)nb * sizeof(*h), hipMemcpyHostToDevice) != hipSuccess) {
+		if (qq->d_desc)
+			hipFree(qq->d_desc);
+		free(h);
+		free(qq);
+		return -ENOMEM;
+	}
+	free(h);
+	qq->nb = nb;
+	qq->total_tiles = tiles;
+	qq->tile = tile;
+	*q = qq;
+	return 0;
+}
+
+int mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream)
+{
+	mosrx_qparams qp;
+	if (!c || !q)
+		return -EINVAL;
+	qp.desc = q->d_desc;
+	qp.tables = c->d_tables;
+	qp.counters = NULL;
+	qp.nb = q->nb;
+	qp.flags = c->kflags;
+	return mosrx_launch_queue(&qp, q->total_tiles, q->tile, stream ? stream : (void *)c->stream);
+}
+
+void mosrx_queue_destroy(mosrx_ctx *c, mosrx_queue *q)
+{
+	if (!q)
+		return;
+	if (c)
+		hipSetDevice(c->device);
+	if (q->d_desc)
+		hipFree(q->d_desc);
+	free(q);
+}
+
+int mosrx_time_queue(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq, uint32_t iters,
+                     float *total_ms, float *avg_kernel_ms)
+{
+	uint32_t i;
+	int rc;
+	if (!c || !q || nq == 0 || !total_ms || iters == 0)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipEventRecord(c->ev0, c->stream));
+	for (i = 0; i < iters; i++)
+		if ((rc = mosrx_queue_run(c, q[i % nq], c->stream)))
+			return rc;
+	HIPCHK(hipEventRecord(c->ev1, c->stream));
+	HIPCHK(hipEventSynchronize(c->ev1));
+	HIPCHK(hipEventElapsedTime(total_ms, c->ev0, c->ev1));
+	if (avg_kernel_ms) {
+		double tot = 0;
+		for (i = 0; i < iters && i < 64; i++) {
+			float ms = 0;
+			HIPCHK(hipEventRecord(c->ev0, c->stream));
+			if ((rc = mosrx_queue_run(c, q[i % nq], c->stream)))
+				return rc;
+			HIPCHK(hipEventRecord(c->ev1, c->stream));
+			HIPCHK(hipEventSynchronize(c->ev1));
+			HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+			tot += ms;
+		}
+		*avg_kernel_ms = (float)(tot / (i ? i : 1));
+	}
+	return 0;
+}

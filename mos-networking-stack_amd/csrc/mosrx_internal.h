@@ -45,6 +45,28 @@ enum { MOSRX_TILE_SMALL = 256, MOSRX_TILE_LARGE = 64 };
  * the per-lane header window; longer ones stream their tail cooperatively. */
 #define MOSRX_WINDOW_END 94
 
+/* Batch-queue descriptor (device resident), 48 bytes. */
+typedef struct mosrx_qdesc {
+	const uint8_t  *frames;
+	const uint32_t *off;
+	const uint16_t *len;
+	mosrx_result   *out;
+	uint32_t        frames_bytes;
+	uint32_t        n;
+	uint32_t        tile_base;   /* first workgroup of this batch in the launch */
+	uint32_t        pad;
+} mosrx_qdesc;
+
+typedef struct mosrx_qparams {
+	const mosrx_qdesc *desc;     /* nb entries */
+	const uint32_t    *tables;
+	uint32_t          *counters;
+	uint32_t           nb;
+	uint32_t           flags;
+} mosrx_qparams;
+
+int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles, int tile, void *stream);
+
 /* Launch one classify kernel; returns 0 or -EINVAL / -EIO.  `stream` is a hipStream_t. */
 int mosrx_launch_classify(const mosrx_kparams *kp, int tile, void *stream);
 

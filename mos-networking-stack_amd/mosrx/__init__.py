@@ -113,6 +113,10 @@ def lib():
             "mosrx_time_dev": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_time_dev_kernels": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_device_sync": (I, [P]),
+            "mosrx_queue_create": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
+            "mosrx_queue_run": (I, [P, P, P]),
+            "mosrx_queue_destroy": (None, [P, P]),
+            "mosrx_time_queue": (I, [P, C.POINTER(P), U32, U32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
             "mosrx_time_host": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_rss_tables": (I, [C.c_char_p, U32, C.POINTER(U32)]),
             "mosrx_trace_gen": (I, [I, U32, U32, U64, C.POINTER(TraceC)]),
@@ -301,6 +305,9 @@ class Context:
              "mosrx_time_dev_kernels")
         return float(ms.value)
 
+    def queue(self, dbs: list[DevBatch]) -> "Queue":
+        return Queue(self, dbs)
+
     def device_sync(self):
         _chk(lib().mosrx_device_sync(self.handle), "mosrx_device_sync")
 
@@ -319,6 +326,37 @@ class Context:
         ms = C.c_float()
         _chk(lib().mosrx_time_host(self.handle, bs, len(batches), os_, iters, C.byref(ms)), "mosrx_time_host")
         return float(ms.value)
+
+
+class Queue:
+    """mosrx_queue: one launch classifies every batch of the queue."""
+
+    def __init__(self, ctx: Context, dbs: list[DevBatch]):
+        self.ctx = ctx
+        bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
+        outs = (C.c_void_p * len(dbs))(*[d.d_out.ptr for d in dbs])
+        h = C.c_void_p()
+        _chk(lib().mosrx_queue_create(ctx.handle, bs, len(dbs), outs, C.byref(h)), "mosrx_queue_create")
+        self.handle = h.value
+
+    def run(self, sync: bool = True):
+        _chk(lib().mosrx_queue_run(self.ctx.handle, self.handle, None), "mosrx_queue_run")
+        if sync:
+            _chk(lib().mosrx_sync(self.ctx.handle), "mosrx_sync")
+
+    def time(self, iters: int, others: list["Queue"] = ()) -> tuple[float, float]:
+        """(total ms, average kernel ms) of `iters` launches cycling over self + others."""
+        qs = [self] + list(others)
+        arr = (C.c_void_p * len(qs))(*[q.handle for q in qs])
+        tot, kern = C.c_float(), C.c_float()
+        _chk(lib().mosrx_time_queue(self.ctx.handle, arr, len(qs), iters, C.byref(tot), C.byref(kern)),
+             "mosrx_time_queue")
+        return float(tot.value), float(kern.value)
+
+    def destroy(self):
+        if self.handle:
+            lib().mosrx_queue_destroy(self.ctx.handle, self.handle)
+            self.handle = None
 
 
 def rss_tables(key: bytes) -> np.ndarray:
@@ -425,3 +463,25 @@ def mem_source(frames: np.ndarray, off: np.ndarray, ln: np.ndarray, loops: int =
     if not s:
         raise MosrxError(12, "mosrx_source_mem")
     return s
+
+
+def shard_plan(nbatches: int, world: int, rank: int) -> list[int]:
+    """Round-robin split of a job's batches over GPUs: batch b -> GPU b % world.
+
+    No exchange step exists between GPUs, so the plan is the whole multi-GPU protocol:
+    each rank classifies its own batches; results land in disjoint slices."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    return list(range(rank, nbatches, world))
+
+
+def split_batches(frames: np.ndarray, off: np.ndarray, ln: np.ndarray, batch: int):
+    """Cut a packed trace into consecutive batches of `batch` frames (views re-based
+    so every batch is self-contained: its own frames buffer and offsets)."""
+    out = []
+    for s in range(0, len(off), batch):
+        o, l = off[s:s + batch], ln[s:s + batch]
+        lo = int(o.min()) & ~15 if len(o) else 0
+        hi = int((o.astype(np.uint64) + l).max()) if len(o) else 0
+        out.append((frames[lo:hi + 64], (o - lo).astype(np.uint32), l.copy(), hi - lo))
+    return out

@@ -1,0 +1,69 @@
+"""World-size-2 gloo test of the multi-GPU protocol on CPU.
+
+Batches are split round-robin with no data-path collective; the only
+communication is the barrier and the max-over-ranks of the timed region that
+bench.py uses.  Each rank classifies its shard with the oracle (the CPU checker;
+the GPU path is exercised by the -m gpu tests) and the union must equal the
+single-process result."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import mosrx
+import oracle_py as O
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    d = bench.Dist(world, rank)
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 12_000, nflows=3000)
+    batches = mosrx.split_batches(t.frames, t.off, t.len, 1000)
+    mine = mosrx.shard_plan(len(batches), world, rank)
+    d.barrier()
+    res = {b: O.classify(batches[b][0], batches[b][1], batches[b][2]) for b in mine}
+    d.barrier()
+    m = d.max(float(rank + 1))
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), m=m,
+             **{f"b{b}": r.view(np.uint8) for b, r in res.items()})
+    d.close()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_round_robin_shards_cover_job(tmp_path, world):
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 12_000, nflows=3000)
+    whole = O.classify(t.frames, t.off, t.len)
+    got = {}
+    for r in range(world):
+        z = np.load(tmp_path / f"r{r}.npz")
+        assert float(z["m"]) == world          # max over ranks
+        for k in z.files:
+            if k.startswith("b"):
+                b = int(k[1:])
+                assert b not in got              # disjoint
+                got[b] = z[k]
+    assert sorted(got) == list(range(12))        # complete
+    joined = np.concatenate([got[b] for b in range(12)]).view(mosrx.RESULT_DTYPE)
+    assert np.array_equal(joined.view(np.uint8), whole.view(np.uint8))
+
+
+def test_shard_plan():
+    assert mosrx.shard_plan(10, 4, 1) == [1, 5, 9]
+    allb = sorted(b for r in range(8) for b in mosrx.shard_plan(37, 8, r))
+    assert allb == list(range(37))
+    with pytest.raises(ValueError):
+        mosrx.shard_plan(4, 2, 2)

@@ -222,3 +222,17 @@ def test_gpu_io_module_batches_and_ioctl():
         assert be.recv_pkts(5) == -1          # bad ifidx, pcap_module.c:37-38
     finally:
         be.close()
+
+
+@pytest.mark.parametrize("kind,n,nb", [(mosrx.TRACE_S64, 32_768, 8), (mosrx.TRACE_IMIX, 9_000, 5)])
+def test_batch_queue_one_launch(gpu_ctx, kind, n, nb):
+    gpu_ctx.set_params(mosrx.default_params())
+    trs = [mosrx.Trace(kind, n - 7 * i, nflows=4000, seed=100 + i) for i in range(nb)]
+    dbs = [gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len) for t in trs]
+    q = gpu_ctx.queue(dbs)
+    q.run()
+    for t, d in zip(trs, dbs):
+        assert_records_equal(d.results(), O.classify(t.frames, t.off, t.len, O.params()), "queue")
+    q.destroy()
+    for d in dbs:
+        d.free()

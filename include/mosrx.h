@@ -116,6 +116,10 @@ typedef struct mosrx_ctx mosrx_ctx;
  * the HIP kernels are unavailable: there is no CPU fallback. */
 int  mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out);
 int  mosrx_set_params(mosrx_ctx *c, const mosrx_params *p);
+/* Tuning knob: cache policy of the frame loads (bit 0: header windows
+ * non-temporal, bit 1: tail stream non-temporal).  Results never depend on it.
+ * Default from measurements; env MOSRX_KVARIANT overrides at open. */
+int  mosrx_set_variant(mosrx_ctx *c, int variant);
 void mosrx_close(mosrx_ctx *c);
 
 /* Device-resident classification: `b` points at device memory, results go to
@@ -182,6 +186,10 @@ int  mosrx_time_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
  * by its own pair of HIP events on the stream it runs on (the roofline figure). */
 int  mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
                             mosrx_result *const *d_out, uint32_t iters, float *avg_ms);
+/* The device's streaming-read ceiling: `iters` coalesced 16-byte-load passes
+ * cycling over `nbuf` buffers of `bytes` each (sized past the 256 MiB Infinity
+ * Cache), in GB/s.  The roofline figure next to the 8 TB/s spec peak. */
+int  mosrx_probe_read_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, float *gbps);
 /* hipDeviceSynchronize on the context's device. */
 int  mosrx_device_sync(mosrx_ctx *c);
 /* Same, end-to-end from host buffers through pinned staging, double-buffered. */

@@ -43,7 +43,20 @@ struct mosrx_ctx {
 	struct slot slot[NSLOT];
 	uint32_t h_cnt[MOSRX_R_COUNT];   /* counters of the last waited batch */
 	hipEvent_t ev0, ev1;
+	int variant;                     /* kernel cache-policy variant (mosrx_set_variant) */
 };
+
+/* Default cache policy per access class (bit 0: header windows non-temporal,
+ * bit 1: tail stream non-temporal), chosen from measurements on MI355X. */
+#define MOSRX_DEFAULT_VARIANT 2   /* tails nt, windows default: scripts/tune.py, profiles/r01_tune_variants.log */
+
+int mosrx_set_variant(mosrx_ctx *c, int variant)
+{
+	if (!c || variant < 0 || variant > 15)
+		return -EINVAL;
+	c->variant = variant;
+	return 0;
+}
 
 int mosrx_abi_version(void) { return MOSRX_ABI_VERSION; }
 
@@ -181,6 +194,9 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 	if (!c)
 		return -ENOMEM;
 	c->device = device;
+	c->variant = MOSRX_DEFAULT_VARIANT;
+	if (getenv("MOSRX_KVARIANT"))
+		c->variant = atoi(getenv("MOSRX_KVARIANT")) & 15;
 	if (hipSetDevice(device) != hipSuccess ||
 	    hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
 	    hipMalloc((void **)&c->d_tables, MOSRX_TAB_WORDS * 4) != hipSuccess ||
@@ -269,8 +285,8 @@ static int launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, con
 	kp.frames_bytes = (uint32_t)b->frames_bytes;
 	kp.n = b->n;
 	kp.flags = c->kflags;
-	kp.pad = 0;
-	return mosrx_launch_classify(&kp, tile_for(b), (void *)s);
+	kp.grid_cap = 0;
+	return mosrx_launch_classify(&kp, tile_for(b), c->variant, (void *)s);
 }
 
 int mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, void *stream)
@@ -550,6 +566,47 @@ int mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosr
 	return rc;
 }
 
+int mosrx_probe_read_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, float *gbps)
+{
+	void **bufs;
+	uint32_t *sink = NULL;
+	uint32_t i;
+	float ms = 0;
+	int rc = 0;
+	if (!c || !gbps || nbuf == 0 || iters == 0 || bytes < 16)
+		return -EINVAL;
+	bytes &= ~(uint64_t)15;
+	HIPCHK(hipSetDevice(c->device));
+	bufs = calloc(nbuf, sizeof(*bufs));
+	if (!bufs)
+		return -ENOMEM;
+	for (i = 0; i < nbuf && !rc; i++)
+		if (hipMalloc(&bufs[i], bytes) != hipSuccess ||
+		    hipMemsetAsync(bufs[i], (int)(i + 1), bytes, c->stream) != hipSuccess)
+			rc = -ENOMEM;
+	if (!rc && hipMalloc((void **)&sink, 4) != hipSuccess)
+		rc = -ENOMEM;
+	for (i = 0; i < nbuf && !rc; i++)   /* warm-up pass */
+		rc = mosrx_launch_read_bw(bufs[i], bytes, sink, c->stream);
+	if (!rc && hipEventRecord(c->ev0, c->stream) != hipSuccess)
+		rc = -EIO;
+	for (i = 0; i < iters && !rc; i++)
+		rc = mosrx_launch_read_bw(bufs[i % nbuf], bytes, sink, c->stream);
+	if (!rc && (hipEventRecord(c->ev1, c->stream) != hipSuccess || hipEventSynchronize(c->ev1) != hipSuccess ||
+	            hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess))
+		rc = -EIO;
+	if (!rc)
+		*gbps = (float)((double)bytes * iters / (ms * 1e-3) / 1e9);
+	hipStreamSynchronize(c->stream);
+	for (i = 0; i < nbuf; i++)
+		if (bufs[i])
+			hipFree(bufs[i]);
+	if (sink)
+		hipFree(sink);
+	free(bufs);
+	return rc;
+}
+
 int mosrx_device_sync(mosrx_ctx *c)
 {
 	if (!c)
@@ -632,7 +689,7 @@ int mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream)
 	qp.counters = NULL;
 	qp.nb = q->nb;
 	qp.flags = c->kflags;
-	return mosrx_launch_queue(&qp, q->total_tiles, q->tile, stream ? stream : (void *)c->stream);
+	return mosrx_launch_queue(&qp, q->total_tiles, q->tile, c->variant, stream ? stream : (void *)c->stream);
 }
 
 void mosrx_queue_destroy(mosrx_ctx *c, mosrx_queue *q)

@@ -36,7 +36,7 @@ typedef struct mosrx_kparams {
 	uint32_t        frames_bytes;
 	uint32_t        n;
 	uint32_t        flags;      /* MOSRX_KF_* */
-	uint32_t        pad;
+	uint32_t        grid_cap;   /* large tiles: max workgroups (persistent walk), 0 = one per tile */
 } mosrx_kparams;
 
 /* Kernel variants: tile = frames per 256-thread workgroup. */
@@ -65,10 +65,11 @@ typedef struct mosrx_qparams {
 	uint32_t           flags;
 } mosrx_qparams;
 
-int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles, int tile, void *stream);
+int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles, int tile, int variant, void *stream);
+int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sink, void *stream);
 
 /* Launch one classify kernel; returns 0 or -EINVAL / -EIO.  `stream` is a hipStream_t. */
-int mosrx_launch_classify(const mosrx_kparams *kp, int tile, void *stream);
+int mosrx_launch_classify(const mosrx_kparams *kp, int tile, int variant, void *stream);
 
 #ifdef __cplusplus
 }

@@ -6,24 +6,31 @@
 // (tcp_util.c:157-190) and the Toeplitz RSS hash + queue map (util.c:27-131).
 // Integer byte work, HBM-bound: no MFMA.
 //
-// Workgroup = 256 threads (4 waves) over a tile of TILE frames:
-//   phase 0  lane-per-frame.  Each lane loads a 96-byte window of its frame
-//            (6 x buffer_load_dwordx4 from frame byte 2, realigned with
-//            v_alignbyte so the IP header sits dword-aligned in registers),
-//            parses every header field, runs the ip_fast_csum carry chain, the
-//            Toeplitz hash (24 nibble-table lookups in LDS) and the TCP
-//            one's-complement sum of the segment bytes up to the frame's first
-//            16-byte-aligned address past byte 78 ("split").  64-byte frames
-//            finish here.
-//   phase 1  wave-per-frame.  Frames whose IP datagram extends past the split
-//            stream the rest ("tail") with coalesced, 16-byte-aligned loads,
-//            1 KiB per wave instruction; each wave keeps four tails in flight
-//            (8 loads) before reducing.  Lanes sum 16-bit words on the absolute
-//            even grid with v_dot2_u32_u16; only the last chunk is masked.  A
-//            DPP row reduction + 4 readlanes gives each tail sum.
-//   phase 2  lane-per-frame: tail sum folded in (byte-swapped when the frame
-//            starts at an odd address: 256 * x == bswap16(x) mod 0xFFFF), final
-//            fold/complement, verdict, one 16-byte record store.
+// Header work is lane-per-frame ("hdr" below): each lane loads a 96-byte window
+// of its frame (6 x buffer_load_dwordx4 from frame byte 2, realigned with
+// v_alignbyte so the IP header sits dword-aligned in registers), parses every
+// field, runs the ip_fast_csum carry chain, the Toeplitz hash (24 nibble-table
+// lookups in LDS) and the TCP one's-complement sum of the segment bytes before
+// the frame's "split": the first 16-byte-aligned buffer offset at or below
+// frame byte 94.  64-byte frames finish there.
+//
+// Bytes past the split (the "tail") are streamed wave-per-frame with
+// coalesced 16-byte-aligned loads, 1 KiB per wave instruction, summed as
+// 16-bit words on the absolute even address grid with v_dot2_u32_u16 and
+// reduced with DPP row steps + 4 readlanes.  The segment-grid sum is the
+// absolute-grid sum, byte-swapped when the frame starts at an odd address
+// (256 * x == bswap16(x) mod 0xFFFF).
+//
+// Two tile shapes (256-thread workgroups):
+//   small (TILE 256): every lane owns a frame; frames that do have a tail are
+//     compacted into an LDS list and streamed by the four waves.  Used when
+//     every frame fits the header window (64-byte configs).
+//   large (TILE 64): every wave loads the tile's 64 descriptors; wave w owns
+//     the tails of frames w, w+4, ... and issues their loads SPECULATIVELY from
+//     the capture length (hi = off + caplen) right after the descriptor load,
+//     so HBM streams while wave 0 parses the headers.  After one barrier the
+//     exact end (off + 14 + tot_len) masks the sums; the next group of four
+//     tails is in flight while the current one is reduced (double buffered).
 //
 // All frame loads go through a buffer resource whose range is the batch
 // buffer: a bad offset can never fault, out-of-range dwords read as zero.
@@ -39,29 +46,37 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 #define WIN_RAW 24     // raw dwords per lane window (96 B)
 #define WIN_DW  23     // realigned dwords: frame bytes [2, 94)
-#define TAIL_G  4      // tails in flight per wave
-#define TAIL_U  2      // 1 KiB loads per tail issued up front (tails <= 2 KiB finish in one pass)
+#define TAIL_G  4      // tails per group
+#define TAIL_U  2      // 1 KiB loads per tail issued up front (tails <= 2 KiB need no extra pass)
 
 static_assert(2 + 4 * WIN_DW == MOSRX_WINDOW_END, "window end");
 static_assert(sizeof(mosrx_result) == 16, "record size");
+static_assert(MOSRX_TILE_LARGE == 64, "large tile is one descriptor per lane");
+// small tile: 4 waves, one frame per lane; large tile: header wave + 4 streamer waves
+#define WG_THREADS(tile) ((tile) == MOSRX_TILE_SMALL ? 256 : 320)
 
+// The resource range is frames_bytes rounded up to 16: the 16-byte chunk that
+// holds the buffer's last byte is readable whole (it cannot cross a page the
+// buffer does not touch), and every byte past the last frame's end is masked.
+// Loads at or past the range read zero with no memory traffic; the range check
+// is per dword (tested by test_buffer_end_exact on misaligned layouts).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t *base, uint32_t nbytes)
 {
-	return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)nbytes, 0x00020000);
+	return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)((nbytes + 15u) & ~15u), 0x00020000);
 }
 
-// 16 bytes at byte offset c.  A chunk that straddles the end of the buffer is
-// assembled from byte loads so that in-range bytes are never dropped by the
-// range check; offsets at or past the end read zero with no memory traffic.
+// 16 bytes at byte offset c (OOB offsets read zero).  No data-dependent branch:
+// the compiler can then count outstanding loads (s_waitcnt vmcnt(N)) across groups.
+// AUX = cache policy (0 default, 2 = non-temporal).  Kernel variant VAR picks it
+// per access class: bit 0 the header windows, bit 1 the tail stream.
+template <int AUX>
 __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t c, uint32_t nbytes)
 {
-	if (__builtin_expect(c + 16u <= nbytes || c >= nbytes, 1))
-		return __builtin_amdgcn_raw_buffer_load_b128(r, c, 0, 0);
-	uint32_t d[4] = {0, 0, 0, 0};
-	for (uint32_t b = 0; b < 16u && c + b < nbytes; b++)
-		d[b >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, c + b, 0, 0) << (8 * (b & 3));
-	return (u32x4){d[0], d[1], d[2], d[3]};
+	(void)nbytes;
+	return __builtin_amdgcn_raw_buffer_load_b128(r, c, 0, AUX);
 }
+#define WIN_AUX(v)  (((v) & 1) ? 2 : 0)
+#define TAIL_AUX(v) (((v) & 2) ? 2 : 0)
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 __device__ __forceinline__ uint32_t be16hi(uint32_t w) { return ((w >> 8) & 0xFF00u) | (w >> 24); } // bytes 2,3
@@ -110,57 +125,61 @@ __device__ __forceinline__ uint32_t chunk_sum(u32x4 v, uint32_t c, uint32_t hi, 
 	return add16x2(acc, v.w);
 }
 
-template <int TILE>
-__device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t tile)
+// Sum of a tail [lo, hi) (lo 16-aligned) beyond its first TAIL_U KiB.
+template <int AUX>
+__device__ __forceinline__ uint32_t tail_rest(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo,
+                                              uint32_t hi, uint32_t lane, uint32_t acc)
 {
-	static_assert(TILE % 64 == 0 && TILE <= 256, "tile");
-	__shared__ uint32_t s_tab[MOSRX_TAB_WORDS];
-	__shared__ uint32_t s_tail_lo[TILE];
-	__shared__ uint32_t s_tail_hi[TILE];
-	__shared__ uint32_t s_tail_sum[TILE];
-	__shared__ uint32_t s_tail_pkt[TILE];
-	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];   // [MOSRX_R_COUNT] = number of tails
-
-	const uint32_t t = threadIdx.x;
-	const uint32_t lane = t & 63u;
-	const uint32_t wave = t >> 6;
-
-	// tables: RSS nibble tables + queue LUT (2 KiB, L2-resident)
-	s_tab[t] = kp.tables[t];
-	s_tab[t + 256] = kp.tables[t + 256];
-	if (t <= MOSRX_R_COUNT)
-		s_cnt[t] = 0;
-
-	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
-	const uint32_t nbytes = kp.frames_bytes;
-
-	// ---------------- phase 0: lane per frame ----------------
-	const uint32_t p = tile * TILE + t;
-	const bool active = (t < (uint32_t)TILE) && (p < kp.n);
-	uint32_t o = 0, cap = 0;
-	if (active) {
-		o = kp.off[p];
-		cap = kp.len[p];
-		cap = (o >= nbytes) ? 0u : min(cap, nbytes - o);   // eff_caplen
+#pragma unroll 1
+	for (uint32_t base = lo + 1024u * TAIL_U; base < hi; base += 1024u) {
+		const uint32_t c = base + 16u * lane;
+		acc = chunk_sum(load16<AUX>(rs, c < hi ? c : nbytes, nbytes), c, hi, acc);
 	}
-	// window: raw dwords from (o+2)&~3, realigned to frame bytes [2+4j, 6+4j)
-	const uint32_t a2 = o + 2u;
-	const uint32_t wbase = active ? (a2 & ~3u) : nbytes;  // inactive lanes read out of range -> 0
-	const uint32_t rsh = a2 & 3u;
+	return acc;
+}
+
+// ---------------------------------------------------------------------------
+// Per-frame header state (lane per frame)
+// ---------------------------------------------------------------------------
+struct hdr_t {
+	uint32_t o, fend, split_abs;
+	uint32_t wsum;                 // segment-grid sum of the segment bytes before the split
+	uint32_t saddr, daddr, ip_len, ihl, doff, th3;
+	uint32_t rss, queue, ipc, reason;
+	int verdict;
+	bool fields, need_tcp, has_tail, is_tcp;
+};
+
+struct hdr_win_t {
 	uint32_t raw[WIN_RAW];
+};
+
+template <int AUX>
+__device__ __forceinline__ void hdr_load(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t o, bool active,
+                                         hdr_win_t &win)
+{
+	const uint32_t wbase = active ? ((o + 2u) & ~3u) : nbytes;   // inactive lanes read out of range -> 0
 #pragma unroll
 	for (int m = 0; m < WIN_RAW / 4; m++) {
-		u32x4 v = load16(rs, wbase + 16u * m, nbytes);
-		raw[4 * m + 0] = v.x; raw[4 * m + 1] = v.y; raw[4 * m + 2] = v.z; raw[4 * m + 3] = v.w;
+		u32x4 v = load16<AUX>(rs, wbase + 16u * m, nbytes);
+		win.raw[4 * m + 0] = v.x; win.raw[4 * m + 1] = v.y; win.raw[4 * m + 2] = v.z; win.raw[4 * m + 3] = v.w;
 	}
+}
+
+// Parse + checks + IP checksum + RSS + in-window TCP sum.  Mirrors
+// ProcessPacket (eth_in.c:27) -> ProcessInIPv4Packet (ip_in.c:30) ->
+// ProcessInTCPPacket prefix (tcp.c:408-445); see oracle/mosrx_oracle.c.
+__device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uint32_t cap, bool active,
+                                           uint32_t kflags, const uint32_t *s_tab)
+{
+	hdr_t h;
 	uint32_t w[WIN_DW];
+	const uint32_t rsh = (o + 2u) & 3u;
 #pragma unroll
 	for (int j = 0; j < WIN_DW; j++)
-		w[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], rsh);
+		w[j] = __builtin_amdgcn_alignbyte(win.raw[j + 1], win.raw[j], rsh);
 
-	__syncthreads();   // s_tab, s_cnt ready
-
-	// header fields (frame byte f sits in byte (f-2)&3 of w[(f-2)>>2])
+	// frame byte f sits in byte (f-2)&3 of w[(f-2)>>2]
 	const uint32_t h_proto = be16hi(w[2]);            // frame bytes 12,13  (eth_in.c:34)
 	const uint32_t vi = w[3] & 0xFFu;                 // frame byte 14: version/ihl
 	const uint32_t ver = vi >> 4, ihl = vi & 0xFu;
@@ -178,9 +197,8 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 	const bool is_tcp = (proto == 6u);
 	const uint32_t doff = is_tcp ? ((th3 >> 4) & 0xFu) : 0u;
 	const uint32_t fend = 14u + ip_len;                // frame byte after the IP datagram
-	// split: first 16-byte-aligned buffer offset at or below o+94 (frame byte 79..94)
 	const uint32_t split_abs = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
-	const uint32_t split = split_abs - o;
+	const uint32_t split = split_abs - o;              // frame byte 79..94
 
 	// ip_fast_csum (ip_in.h:10-38): 32-bit adc chain, final carry added once, fold, not.
 	uint32_t ipc;
@@ -205,8 +223,8 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 		}
 	}
 
-	// TCP segment sum over frame bytes [14+4*ihl, min(fend, split)) (segment grid
-	// == realigned grid, dword j holds frame bytes [4j+2, 4j+6)).
+	// TCP segment sum over frame bytes [14+4*ihl, min(fend, split)); the
+	// realigned grid (dword j = frame bytes [4j+2, 4j+6)) is the segment grid.
 	uint32_t wsum = 0;
 	{
 		const int wend = (int)min(fend, split);
@@ -219,7 +237,7 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 		}
 	}
 
-	// Toeplitz over saddr|daddr|sport|dport in wire order (util.c:61-99 with host-order args)
+	// Toeplitz over saddr|daddr|sport|dport in wire order (util.c:61-99, host-order args)
 	uint32_t rss = 0;
 	{
 		const uint32_t tup[3] = {saddr, daddr, is_tcp ? th0 : 0u};
@@ -231,8 +249,8 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 	}
 	const uint32_t queue = (s_tab[MOSRX_TAB_RSS_WORDS + ((rss & 0x1FFu) >> 2)] >> (8 * (rss & 3u))) & 0xFFu;
 
-	// ---------------- verdict chain (eth_in.c:27 -> ip_in.c:30 -> tcp.c:408) ----------------
-	const bool verify = kp.flags & MOSRX_KF_VERIFY;
+	// verdict chain (eth_in.c:27 -> ip_in.c:30 -> tcp.c:408)
+	const bool verify = kflags & MOSRX_KF_VERIFY;
 	int verdict = -1;
 	uint32_t reason = MOSRX_R_TRUNCATED;
 	bool fields = false, need_tcp = false;
@@ -240,7 +258,7 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 		verdict = -1; reason = MOSRX_R_TRUNCATED;
 	} else if (h_proto != 0x0800u) {
 		reason = (h_proto == 0x0806u) ? MOSRX_R_ARP : MOSRX_R_NON_IPV4;
-		verdict = ((kp.flags & MOSRX_KF_FWD_NONIP) || h_proto == 0x0806u) ? 1 : -1;
+		verdict = ((kflags & MOSRX_KF_FWD_NONIP) || h_proto == 0x0806u) ? 1 : -1;
 	} else if (cap < 34u || 14u + ihl * 4u > cap || fend > cap || (is_tcp && 14u + ihl * 4u + 20u > cap)) {
 		verdict = -1; reason = MOSRX_R_TRUNCATED;
 	} else if (ip_len < 20u) {
@@ -257,7 +275,7 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 			verdict = 0; reason = MOSRX_R_NOT_TCP;
 		} else if (ip_len < (ihl + doff) * 4u) {
 			verdict = -1; reason = MOSRX_R_TCP_SHORT;
-		} else if (kp.flags & MOSRX_KF_SKIP_TCP) {
+		} else if (kflags & MOSRX_KF_SKIP_TCP) {
 			verdict = 1; reason = MOSRX_R_TCP_LEN_OK;
 		} else {
 			need_tcp = true;   // verdict decided after the tail sum
@@ -265,95 +283,77 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 	}
 	if (!active)
 		need_tcp = false;
-	const bool has_tail = need_tcp && fend > split;
-	if (has_tail) {
-		const uint32_t k = atomicAdd(&s_cnt[MOSRX_R_COUNT], 1u);
-		s_tail_pkt[k] = t;
-		s_tail_lo[k] = split_abs;
-		s_tail_hi[k] = o + fend;
-	}
-	__syncthreads();
 
-	// ---------------- phase 1: wave per tail, TAIL_G tails in flight ----------------
-	{
-		const uint32_t ntail = __builtin_amdgcn_readfirstlane(s_cnt[MOSRX_R_COUNT]);
-#pragma unroll 1
-		for (uint32_t k0 = wave * TAIL_G; k0 < ntail; k0 += 4u * TAIL_G) {
-			uint32_t lo[TAIL_G], hi[TAIL_G], acc[TAIL_G];
-			u32x4 v[TAIL_G][TAIL_U];
-#pragma unroll
-			for (int u = 0; u < TAIL_G; u++) {
-				const bool ok = k0 + u < ntail;
-				lo[u] = ok ? __builtin_amdgcn_readfirstlane(s_tail_lo[k0 + u]) : 0u;
-				hi[u] = ok ? __builtin_amdgcn_readfirstlane(s_tail_hi[k0 + u]) : 0u;
-#pragma unroll
-				for (int q = 0; q < TAIL_U; q++) {
-					const uint32_t c = lo[u] + 1024u * q + 16u * lane;
-					v[u][q] = load16(rs, c < hi[u] ? c : nbytes, nbytes);
-				}
-			}
-#pragma unroll
-			for (int u = 0; u < TAIL_G; u++) {
-				acc[u] = 0;
-#pragma unroll
-				for (int q = 0; q < TAIL_U; q++)
-					acc[u] = chunk_sum(v[u][q], lo[u] + 1024u * q + 16u * lane, hi[u], acc[u]);
-				// jumbo tails: the rest, 1 KiB per step
-#pragma unroll 1
-				for (uint32_t base = lo[u] + 1024u * TAIL_U; base < hi[u]; base += 1024u) {
-					const uint32_t c = base + 16u * lane;
-					acc[u] = chunk_sum(load16(rs, c < hi[u] ? c : nbytes, nbytes), c, hi[u], acc[u]);
-				}
-			}
-#pragma unroll
-			for (int u = 0; u < TAIL_G; u++) {
-				const uint32_t s = wave_sum(acc[u]);
-				if (k0 + u < ntail && lane == 0)
-					s_tail_sum[__builtin_amdgcn_readfirstlane(s_tail_pkt[k0 + u])] = s;
-			}
-		}
-	}
-	__syncthreads();
+	h.o = o; h.fend = fend; h.split_abs = split_abs; h.wsum = wsum;
+	h.saddr = saddr; h.daddr = daddr; h.ip_len = ip_len; h.ihl = ihl; h.doff = doff; h.th3 = th3;
+	h.rss = rss; h.queue = queue; h.ipc = ipc; h.reason = reason; h.verdict = verdict;
+	h.fields = fields; h.need_tcp = need_tcp; h.has_tail = need_tcp && fend > split; h.is_tcp = is_tcp;
+	return h;
+}
 
-	// ---------------- phase 2: finalise and store ----------------
-	if (active) {
-		uint32_t tcpc = 0;
-		if (need_tcp) {
-			const uint32_t seglen = (ip_len - ihl * 4u) & 0xFFFFu;    // (doff<<2) + payloadlen, u16
-			uint32_t s = wsum + (saddr & 0xFFFFu) + (saddr >> 16) + (daddr & 0xFFFFu) + (daddr >> 16) +
-			             bswap16(seglen) + 0x0600u;
-			if (has_tail) {
-				const uint32_t ts = fold16(s_tail_sum[t]);
-				s += (o & 1u) ? bswap16(ts) : ts;
-			}
-			s = (s >> 16) + (s & 0xFFFFu);
-			s += s >> 16;
-			tcpc = (~s) & 0xFFFFu;
-			verdict = tcpc ? -1 : 1;
-			reason = tcpc ? MOSRX_R_TCP_BADCSUM : MOSRX_R_TCP_OK;
+// Fold in the tail sum, decide the TCP verdict, build the 16-byte record.
+__device__ __forceinline__ u32x4 hdr_finish(hdr_t h, uint32_t tail_sum, uint32_t kflags)
+{
+	uint32_t tcpc = 0;
+	if (h.need_tcp) {
+		const uint32_t seglen = (h.ip_len - h.ihl * 4u) & 0xFFFFu;   // (doff<<2) + payloadlen, u16
+		uint32_t s = h.wsum + (h.saddr & 0xFFFFu) + (h.saddr >> 16) + (h.daddr & 0xFFFFu) + (h.daddr >> 16) +
+		             bswap16(seglen) + 0x0600u;                       // tcp_util.c:178-181
+		if (h.has_tail) {
+			const uint32_t ts = fold16(tail_sum);
+			s += (h.o & 1u) ? bswap16(ts) : ts;
 		}
-		uint32_t r_rss = 0, r_ipc = 0, r_plen = 0, r_poff = 0, r_q = 0, r_flags = 0, r_ihld = 0;
-		if (fields) {
-			r_rss = rss;
-			r_q = queue;
-			r_ihld = (ihl << 4) | doff;
-			if (verify)
-				r_ipc = ipc;
-			if (is_tcp) {
-				r_flags = (th3 >> 8) & 0xFFu;
-				r_plen = (ip_len - (ihl * 4u + doff * 4u)) & 0xFFFFu;   // tcp.c:262
-				r_poff = 14u + ihl * 4u + doff * 4u;
-			}
-		}
-		u32x4 rec;
-		rec.x = r_rss;
-		rec.y = r_ipc | (tcpc << 16);
-		rec.z = r_plen | (r_poff << 16) | (((uint32_t)verdict & 0xFFu) << 24);
-		rec.w = reason | (r_q << 8) | (r_flags << 16) | (r_ihld << 24);
-		*reinterpret_cast<u32x4 *>(kp.out + p) = rec;
-		if (kp.counters)
-			atomicAdd(&s_cnt[reason], 1u);
+		s = (s >> 16) + (s & 0xFFFFu);
+		s += s >> 16;
+		tcpc = (~s) & 0xFFFFu;
+		h.verdict = tcpc ? -1 : 1;
+		h.reason = tcpc ? MOSRX_R_TCP_BADCSUM : MOSRX_R_TCP_OK;
 	}
+	uint32_t r_rss = 0, r_ipc = 0, r_plen = 0, r_poff = 0, r_q = 0, r_flags = 0, r_ihld = 0;
+	if (h.fields) {
+		r_rss = h.rss;
+		r_q = h.queue;
+		r_ihld = (h.ihl << 4) | h.doff;
+		if (kflags & MOSRX_KF_VERIFY)
+			r_ipc = h.ipc;
+		if (h.is_tcp) {
+			r_flags = (h.th3 >> 8) & 0xFFu;
+			r_plen = (h.ip_len - (h.ihl * 4u + h.doff * 4u)) & 0xFFFFu;   // tcp.c:262
+			r_poff = 14u + h.ihl * 4u + h.doff * 4u;
+		}
+	}
+	u32x4 rec;
+	rec.x = r_rss;
+	rec.y = r_ipc | (tcpc << 16);
+	rec.z = r_plen | (r_poff << 16) | (((uint32_t)h.verdict & 0xFFu) << 24);
+	rec.w = h.reason | (r_q << 8) | (r_flags << 16) | (r_ihld << 24);
+	return rec;
+}
+
+__device__ __forceinline__ void tables_to_lds(const mosrx_kparams &kp, uint32_t *s_tab, uint32_t *s_cnt, uint32_t t)
+{
+	if (t < 256) {                            // RSS nibble tables + queue LUT (2 KiB, L2-resident)
+		s_tab[t] = kp.tables[t];
+		s_tab[t + 256] = kp.tables[t + 256];
+	}
+	if (t <= MOSRX_R_COUNT)
+		s_cnt[t] = 0;
+}
+
+__device__ __forceinline__ uint32_t eff_caplen(uint32_t o, uint32_t len, uint32_t nbytes)
+{
+	return (o >= nbytes) ? 0u : min(len, nbytes - o);
+}
+
+__device__ __forceinline__ void store_record(const mosrx_kparams &kp, uint32_t p, u32x4 rec, uint32_t *s_cnt)
+{
+	*reinterpret_cast<u32x4 *>(kp.out + p) = rec;
+	if (kp.counters)
+		atomicAdd(&s_cnt[rec.w & 0xFFu], 1u);
+}
+
+__device__ __forceinline__ void flush_counters(const mosrx_kparams &kp, const uint32_t *s_cnt, uint32_t t)
+{
 	if (kp.counters) {
 		__syncthreads();
 		if (t < MOSRX_R_COUNT && s_cnt[t])
@@ -361,16 +361,274 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 	}
 }
 
-template <int TILE>
-__global__ __launch_bounds__(256) void mosrx_classify_kernel(mosrx_kparams kp)
+// ---------------------------------------------------------------------------
+// small tile: 256 frames, lane per frame, compacted tails
+// ---------------------------------------------------------------------------
+template <int VAR>
+__device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uint32_t tile)
 {
-	classify_tile<TILE>(kp, blockIdx.x);
+	constexpr uint32_t TILE = MOSRX_TILE_SMALL;
+	constexpr int AUX = TAIL_AUX(VAR);
+	__shared__ uint32_t s_tab[MOSRX_TAB_WORDS];
+	__shared__ uint32_t s_tail_lo[TILE], s_tail_hi[TILE], s_tail_sum[TILE], s_tail_pkt[TILE];
+	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];   // [MOSRX_R_COUNT] = number of tails
+
+	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
+	const uint32_t nbytes = kp.frames_bytes;
+	tables_to_lds(kp, s_tab, s_cnt, t);
+
+	const uint32_t p = tile * TILE + t;
+	const bool active = p < kp.n;
+	uint32_t o = 0, cap = 0;
+	if (active) {
+		o = kp.off[p];
+		cap = eff_caplen(o, kp.len[p], nbytes);
+	}
+	hdr_win_t win;
+	hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
+	__syncthreads();   // s_tab, s_cnt ready
+	const hdr_t h = hdr_parse(win, o, cap, active, kp.flags, s_tab);
+	if (h.has_tail) {
+		const uint32_t k = atomicAdd(&s_cnt[MOSRX_R_COUNT], 1u);
+		s_tail_pkt[k] = t;
+		s_tail_lo[k] = h.split_abs;
+		s_tail_hi[k] = o + h.fend;
+	}
+	__syncthreads();
+
+	const uint32_t ntail = __builtin_amdgcn_readfirstlane(s_cnt[MOSRX_R_COUNT]);
+#pragma unroll 1
+	for (uint32_t k0 = wave * TAIL_G; k0 < ntail; k0 += 4u * TAIL_G) {
+		uint32_t lo[TAIL_G], hi[TAIL_G];
+		u32x4 v[TAIL_G][TAIL_U];
+#pragma unroll
+		for (int u = 0; u < TAIL_G; u++) {
+			const bool ok = k0 + u < ntail;
+			lo[u] = ok ? __builtin_amdgcn_readfirstlane(s_tail_lo[k0 + u]) : 0u;
+			hi[u] = ok ? __builtin_amdgcn_readfirstlane(s_tail_hi[k0 + u]) : 0u;
+#pragma unroll
+			for (int q = 0; q < TAIL_U; q++) {
+				const uint32_t c = lo[u] + 1024u * q + 16u * lane;
+				v[u][q] = load16<AUX>(rs, c < hi[u] ? c : nbytes, nbytes);
+			}
+		}
+#pragma unroll
+		for (int u = 0; u < TAIL_G; u++) {
+			uint32_t acc = 0;
+#pragma unroll
+			for (int q = 0; q < TAIL_U; q++)
+				acc = chunk_sum(v[u][q], lo[u] + 1024u * q + 16u * lane, hi[u], acc);
+			acc = tail_rest<AUX>(rs, nbytes, lo[u], hi[u], lane, acc);
+			const uint32_t s = wave_sum(acc);
+			if (k0 + u < ntail && lane == 0)
+				s_tail_sum[__builtin_amdgcn_readfirstlane(s_tail_pkt[k0 + u])] = s;
+		}
+	}
+	__syncthreads();
+	if (active)
+		store_record(kp, p, hdr_finish(h, h.has_tail ? s_tail_sum[t] : 0u, kp.flags), s_cnt);
+	flush_counters(kp, s_cnt, t);
+}
+
+// ---------------------------------------------------------------------------
+// large tile: 64 frames, headers by wave 0, speculative tail streaming by all waves
+// ---------------------------------------------------------------------------
+struct tail_grp_t {
+	u32x4 v[TAIL_G][TAIL_U];
+};
+
+// Frame of this wave's j-th tail candidate.  Candidates (frames whose capture
+// reaches past the split) are ranked in frame order; group g of the workgroup
+// takes candidates [16g, 16g+16), four consecutive ones per wave, so each wave
+// streams ~6 KB of contiguous frames and the workgroup a ~24 KB run per group.
+// Returns 64 when there is no such candidate.
+__device__ __forceinline__ uint32_t cand_frame(bool cand, uint32_t rank_l, uint32_t wave, uint32_t j)
+{
+	const uint32_t r = 4u * TAIL_G * (j / TAIL_G) + TAIL_G * wave + (j % TAIL_G);
+	const uint64_t m = __ballot(cand && rank_l == r);
+	return m ? (uint32_t)__builtin_ctzll(m) : 64u;
+}
+
+// Issue the loads of group g of this wave's tail candidates (speculative bounds).
+template <int AUX>
+__device__ __forceinline__ void tail_issue(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
+                                           uint32_t hi_l, bool cand, uint32_t rank_l, uint32_t wave,
+                                           uint32_t lane, int g, tail_grp_t &b, uint32_t (&fr)[TAIL_G])
+{
+#pragma unroll
+	for (int u = 0; u < TAIL_G; u++) {
+		const uint32_t f = cand_frame(cand, rank_l, wave, TAIL_G * g + u);
+		fr[u] = f;
+		const uint32_t lo = f < 64u ? __builtin_amdgcn_readlane(lo_l, f) : 0u;
+		const uint32_t hi = f < 64u ? __builtin_amdgcn_readlane(hi_l, f) : 0u;
+#pragma unroll
+		for (int q = 0; q < TAIL_U; q++) {
+			const uint32_t c = lo + 1024u * q + 16u * lane;
+			b.v[u][q] = load16<AUX>(rs, c < hi ? c : nbytes, nbytes);   // empty slots read out of range: no traffic
+		}
+	}
+}
+
+// Reduce a group over its speculative range [split, off + caplen) into s_spec.
+template <int AUX>
+__device__ __forceinline__ void tail_consume(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
+                                             uint32_t hi_l, uint32_t lane, const tail_grp_t &b,
+                                             const uint32_t (&fr)[TAIL_G], uint32_t *s_spec)
+{
+#pragma unroll
+	for (int u = 0; u < TAIL_G; u++) {
+		const uint32_t f = fr[u];
+		if (f < 64u) {
+			const uint32_t lo = __builtin_amdgcn_readlane(lo_l, f);
+			const uint32_t hi = __builtin_amdgcn_readlane(hi_l, f);
+			uint32_t acc = 0;
+#pragma unroll
+			for (int q = 0; q < TAIL_U; q++)
+				acc = chunk_sum(b.v[u][q], lo + 1024u * q + 16u * lane, hi, acc);
+			if (hi - lo > 1024u * TAIL_U)
+				acc = tail_rest<AUX>(rs, nbytes, lo, hi, lane, acc);
+			const uint32_t s = wave_sum(acc);
+			if (lane == 0)
+				s_spec[f] = s;
+		}
+	}
+}
+
+// Absolute-grid word sum of the bytes [a, b) (any alignment), whole wave.
+__device__ __forceinline__ uint32_t range_sum(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t a, uint32_t b,
+                                              uint32_t lane)
+{
+	uint32_t acc = 0;
+#pragma unroll 1
+	for (uint32_t base = a & ~15u; base < b; base += 1024u) {
+		const uint32_t c = base + 16u * lane;
+		u32x4 v = load16<0>(rs, c < b ? c : nbytes, nbytes);
+		const int h = (int)(a - c);   // bytes to drop at the front
+		v.x &= ~keep_lo(h);
+		v.y &= ~keep_lo(h - 4);
+		v.z &= ~keep_lo(h - 8);
+		v.w &= ~keep_lo(h - 12);
+		acc = chunk_sum(v, c, b, acc);
+	}
+	return wave_sum(acc);
+}
+
+// One tile per workgroup of 5 waves: wave 0 parses the 64 headers while waves
+// 1..4 stream the tails over their SPECULATIVE ranges [split, off + caplen)
+// (known from the descriptors alone), so the header work is off the streaming
+// critical path and the workgroup has a single barrier between loads and
+// records.  (A persistent walk over tiles with the next tile's descriptors
+// prefetched measured slower at every grid cap: per-workgroup concurrency, not
+// launch startup, bounds this kernel; profiles/r01_tune_persistent.log.)
+template <int VAR>
+__device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uint32_t tile)
+{
+	constexpr uint32_t TILE = MOSRX_TILE_LARGE;
+	constexpr int AUX = TAIL_AUX(VAR);
+	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
+	__shared__ uint32_t s_spec[TILE];
+	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
+
+	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
+	const uint32_t nbytes = kp.frames_bytes;
+
+	// every wave reads the tile's descriptors (lane = frame)
+	const uint32_t p = tile * TILE + lane;
+	const bool active = p < kp.n;
+	uint32_t o = 0, cap = 0;
+	if (active) {
+		o = kp.off[p];
+		cap = eff_caplen(o, kp.len[p], nbytes);
+	}
+	// speculative tail bounds from the capture length: [split, off + caplen)
+	const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
+	const uint32_t hi_l = active ? o + cap : 0u;
+	const bool cand = hi_l > lo_l;
+	const uint64_t cmask = __ballot(cand);
+	const uint32_t rank_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(cmask >> 32),
+	                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)cmask, 0u));
+
+	if (wave == 0) {
+		// ---- header wave: parse while the streamers pull the tails.  It fills the
+		// LDS tables itself (no barrier: a wave's LDS accesses are ordered) ----
+		hdr_win_t win;
+		hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
+		{
+			const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
+			const u32x4 a = tg[lane], b = tg[lane + 64];
+			reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
+			reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
+			if (lane <= MOSRX_R_COUNT)
+				s_cnt[lane] = 0;
+		}
+		const hdr_t h = hdr_parse(win, o, cap, active, kp.flags, s_tab);
+		__syncthreads();   // B: s_spec ready
+		uint32_t tail = h.has_tail ? s_spec[lane] : 0u;
+		// Bytes between the datagram end and the capture end (Ethernet padding of
+		// a long capture) were summed speculatively: subtract them (exact integer
+		// sums, so the difference is the true tail sum).  Rare: a wave-wide pass
+		// per such frame.
+		const uint32_t true_hi = o + h.fend;
+		uint64_t fm = __ballot(h.has_tail && true_hi < hi_l);
+#pragma unroll 1
+		while (fm) {
+			const uint32_t f = (uint32_t)__builtin_ctzll(fm);
+			fm &= fm - 1;
+			const uint32_t a = max(__builtin_amdgcn_readlane(lo_l, f), __builtin_amdgcn_readlane(true_hi, f));
+			const uint32_t s = range_sum(rs, nbytes, a, __builtin_amdgcn_readlane(hi_l, f), lane);
+			if (lane == f)
+				tail -= s;
+		}
+		if (active)
+			store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
+	} else {
+		// ---- streamer waves 1..4: candidates [16g + 4(w-1), +4) of group g ----
+		// up to 16 candidates per wave in four groups; groups past the count are
+		// issued anyway (out-of-range loads, no traffic) so the load counts stay
+		// static and every wait is a counted vmcnt(N), never a drain.
+		const uint32_t sw = wave - 1u;
+		static_assert(TILE / 4 == 4 * TAIL_G, "four groups of four tails per streamer");
+		const uint32_t ngrp = (__builtin_popcountll(cmask) + 4u * TAIL_G - 1u) / (4u * TAIL_G);
+		tail_grp_t b0, b1;
+		uint32_t f0[TAIL_G], f1[TAIL_G];
+		tail_issue<AUX>(rs, nbytes, lo_l, hi_l, cand, rank_l, sw, lane, 0, b0, f0);
+		tail_issue<AUX>(rs, nbytes, lo_l, hi_l, cand, rank_l, sw, lane, 1, b1, f1);
+		tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b0, f0, s_spec);
+		if (ngrp > 2) {
+			tail_issue<AUX>(rs, nbytes, lo_l, hi_l, cand, rank_l, sw, lane, 2, b0, f0);
+			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, s_spec);
+			tail_issue<AUX>(rs, nbytes, lo_l, hi_l, cand, rank_l, sw, lane, 3, b1, f1);
+			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b0, f0, s_spec);
+			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, s_spec);
+		} else {
+			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, s_spec);
+		}
+		__syncthreads();   // B
+	}
+	flush_counters(kp, s_cnt, t);
+}
+
+template <int TILE, int VAR>
+__device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t tile)
+{
+	if constexpr (TILE == MOSRX_TILE_SMALL)
+		classify_tile_small<VAR>(kp, tile);
+	else
+		classify_tile_large<VAR>(kp, tile);
+}
+
+template <int TILE, int VAR>
+__global__ __launch_bounds__(WG_THREADS(TILE)) void mosrx_classify_kernel(mosrx_kparams kp)
+{
+	classify_tile<TILE, VAR>(kp, blockIdx.x);
 }
 
 // Batch queue: one launch over nb resident batches (descriptor table in HBM).
 // Workgroup b finds its batch by a binary search of tile_base[] (scalar loads).
-template <int TILE>
-__global__ __launch_bounds__(256) void mosrx_classify_queue_kernel(mosrx_qparams qp)
+template <int TILE, int VAR>
+__global__ __launch_bounds__(WG_THREADS(TILE)) void mosrx_classify_queue_kernel(mosrx_qparams qp)
 {
 	const uint32_t b = blockIdx.x;
 	uint32_t lo = 0, hi = qp.nb;               // find k: tile_base[k] <= b < tile_base[k+1]
@@ -392,33 +650,79 @@ __global__ __launch_bounds__(256) void mosrx_classify_queue_kernel(mosrx_qparams
 	kp.frames_bytes = d->frames_bytes;
 	kp.n = d->n;
 	kp.flags = qp.flags;
-	kp.pad = 0;
-	classify_tile<TILE>(kp, b - d->tile_base);
+	kp.grid_cap = 0;
+	classify_tile<TILE, VAR>(kp, b - d->tile_base);
 }
 
-extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles, int tile, void *stream)
+// Streaming-read ceiling of the box: each workgroup streams one contiguous slab
+// with coalesced non-temporal 16-byte loads, 4 in flight per lane; a
+// data-dependent sink keeps them live.  The fastest shape found by
+// scripts/probe_bw.hip (6.4 TB/s, vs 5.3 for a grid-stride default-policy
+// loop).  Diagnostic for the roofline report.
+__global__ __launch_bounds__(256) void mosrx_read_bw_kernel(const u32x4 *p, uint64_t n16, uint32_t *sink)
+{
+	uint32_t acc = 0;
+	const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+	const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n16, lo + per);
+	for (uint64_t i = lo + threadIdx.x; i < hi; i += 1024u) {
+		u32x4 v[4];
+#pragma unroll
+		for (int u = 0; u < 4; u++) {
+			const uint64_t j = i + 256u * u;
+			v[u] = j < hi ? __builtin_nontemporal_load(p + j) : (u32x4){0, 0, 0, 0};
+		}
+#pragma unroll
+		for (int u = 0; u < 4; u++)
+			acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+	}
+	if (acc == 0x9E3779B9u)
+		sink[0] = acc;
+}
+
+extern "C" int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sink, void *stream)
+{
+	hipLaunchKernelGGL(mosrx_read_bw_kernel, dim3(256 * 8), dim3(256), 0, (hipStream_t)stream,
+	                   (const u32x4 *)p, bytes / 16, sink);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+template <int TILE, int VAR>
+static void launch_queue_v(const mosrx_qparams *qp, uint32_t total_tiles, hipStream_t s)
+{
+	hipLaunchKernelGGL((mosrx_classify_queue_kernel<TILE, VAR>), dim3(total_tiles), dim3(WG_THREADS(TILE)), 0, s, *qp);
+}
+
+template <int TILE, int VAR>
+static void launch_v(const mosrx_kparams *kp, hipStream_t s)
+{
+	hipLaunchKernelGGL((mosrx_classify_kernel<TILE, VAR>), dim3((kp->n + TILE - 1) / TILE), dim3(WG_THREADS(TILE)), 0,
+	                   s, *kp);
+}
+
+extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles, int tile, int variant, void *stream)
 {
 	if (!qp || qp->nb == 0 || total_tiles == 0)
 		return qp ? 0 : -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-	if (tile == MOSRX_TILE_SMALL)
-		hipLaunchKernelGGL(mosrx_classify_queue_kernel<MOSRX_TILE_SMALL>, dim3(total_tiles), dim3(256), 0, s, *qp);
-	else
-		hipLaunchKernelGGL(mosrx_classify_queue_kernel<MOSRX_TILE_LARGE>, dim3(total_tiles), dim3(256), 0, s, *qp);
+	static void (*const tab[2][4])(const mosrx_qparams *, uint32_t, hipStream_t) = {
+		{launch_queue_v<MOSRX_TILE_SMALL, 0>, launch_queue_v<MOSRX_TILE_SMALL, 1>,
+		 launch_queue_v<MOSRX_TILE_SMALL, 2>, launch_queue_v<MOSRX_TILE_SMALL, 3>},
+		{launch_queue_v<MOSRX_TILE_LARGE, 0>, launch_queue_v<MOSRX_TILE_LARGE, 1>,
+		 launch_queue_v<MOSRX_TILE_LARGE, 2>, launch_queue_v<MOSRX_TILE_LARGE, 3>}};
+	tab[tile == MOSRX_TILE_SMALL ? 0 : 1][variant & 3](qp, total_tiles, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int tile, void *stream)
+extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int tile, int variant, void *stream)
 {
 	if (!kp || kp->n == 0)
 		return kp ? 0 : -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-	if (tile == MOSRX_TILE_SMALL) {
-		const dim3 grid((kp->n + MOSRX_TILE_SMALL - 1) / MOSRX_TILE_SMALL);
-		hipLaunchKernelGGL(mosrx_classify_kernel<MOSRX_TILE_SMALL>, grid, dim3(256), 0, s, *kp);
-	} else {
-		const dim3 grid((kp->n + MOSRX_TILE_LARGE - 1) / MOSRX_TILE_LARGE);
-		hipLaunchKernelGGL(mosrx_classify_kernel<MOSRX_TILE_LARGE>, grid, dim3(256), 0, s, *kp);
-	}
+	static void (*const tab[2][4])(const mosrx_kparams *, hipStream_t) = {
+		{launch_v<MOSRX_TILE_SMALL, 0>, launch_v<MOSRX_TILE_SMALL, 1>,
+		 launch_v<MOSRX_TILE_SMALL, 2>, launch_v<MOSRX_TILE_SMALL, 3>},
+		{launch_v<MOSRX_TILE_LARGE, 0>, launch_v<MOSRX_TILE_LARGE, 1>,
+		 launch_v<MOSRX_TILE_LARGE, 2>, launch_v<MOSRX_TILE_LARGE, 3>}};
+	tab[tile == MOSRX_TILE_SMALL ? 0 : 1][variant & 3](kp, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

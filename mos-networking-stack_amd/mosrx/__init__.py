@@ -96,6 +96,7 @@ def lib():
             "mosrx_params_set_ms_key": (None, [C.POINTER(Params)]),
             "mosrx_open": (I, [I, C.POINTER(Params), C.POINTER(P)]),
             "mosrx_set_params": (I, [P, C.POINTER(Params)]),
+            "mosrx_set_variant": (I, [P, I]),
             "mosrx_close": (None, [P]),
             "mosrx_classify_dev": (I, [P, C.POINTER(Batch), P, P]),
             "mosrx_classify_host": (I, [P, C.POINTER(Batch), P]),
@@ -113,6 +114,7 @@ def lib():
             "mosrx_time_dev": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_time_dev_kernels": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_device_sync": (I, [P]),
+            "mosrx_probe_read_bw": (I, [P, U64, U32, U32, C.POINTER(C.c_float)]),
             "mosrx_queue_create": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
             "mosrx_queue_run": (I, [P, P, P]),
             "mosrx_queue_destroy": (None, [P, P]),
@@ -259,6 +261,9 @@ class Context:
     def __exit__(self, *a):
         self.close()
 
+    def set_variant(self, variant: int):
+        _chk(lib().mosrx_set_variant(self.handle, variant), "mosrx_set_variant")
+
     def set_params(self, params: Params):
         _chk(lib().mosrx_set_params(self.handle, C.byref(params)), "mosrx_set_params")
         self.params = params
@@ -307,6 +312,12 @@ class Context:
 
     def queue(self, dbs: list[DevBatch]) -> "Queue":
         return Queue(self, dbs)
+
+    def probe_read_bw(self, nbytes: int = 128 << 20, nbuf: int = 6, iters: int = 60) -> float:
+        """Measured streaming-read ceiling (GB/s) of this device."""
+        g = C.c_float()
+        _chk(lib().mosrx_probe_read_bw(self.handle, nbytes, nbuf, iters, C.byref(g)), "mosrx_probe_read_bw")
+        return float(g.value)
 
     def device_sync(self):
         _chk(lib().mosrx_device_sync(self.handle), "mosrx_device_sync")

@@ -46,6 +46,7 @@ WORKLOADS = {
     "S64_queue": (mosrx.TRACE_S64, 32_768, "config #2, 64 batches of 32K per launch (device batch queue)"),
 }
 QUEUE_DEPTH = 64
+STREAMS = 2   # rx batches in flight per GPU (scripts/tune_streams.py: 2 beats 1 and 4)
 
 
 def dist_env():
@@ -132,16 +133,19 @@ def measure(ctx, dist, key, steps, warmup, rank):
     else:
         # warmup (untimed)
         if warmup:
-            ctx.time_dev(dbs, warmup)
+            ctx.time_dev_streams(dbs, warmup, STREAMS)
         ctx.device_sync()
         dist.barrier()
         t0 = time.perf_counter()
-        dev_ms = ctx.time_dev(dbs, steps)          # K back-to-back launches, HIP events on the kernel stream
+        # K back-to-back batches, batch i on stream i % STREAMS (independent rx
+        # batches overlap launch and drain); HIP events on the kernel streams
+        dev_ms = ctx.time_dev_streams(dbs, steps, STREAMS)
         ctx.device_sync()
         dist.barrier()
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
-        # roofline: average duration of one launch, HIP events around each launch
+        # roofline: average duration of ONE launch alone on its stream, HIP
+        # events around each launch (the rocprofv3 kernel-trace figure)
         kern_ms = ctx.time_dev_kernels(dbs, min(steps, 200))
     for d in dbs:
         d.free()

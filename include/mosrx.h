@@ -127,6 +127,14 @@ void mosrx_close(mosrx_ctx *c);
  * context's own stream); returns after enqueue.  Graph-capturable. */
 int  mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, void *stream);
 
+/* Same, plus the flow-table hash of every frame into device memory
+ * `d_fhash[n]`: SuperFastHash of FindStream's reversed tuple (tcp.c:185-190,
+ * fhash.c:25-92) before the NUM_BINS mask, i.e. HashFlow() == d_fhash[i] &
+ * 0x1FFFF.  0 where payload_off == 0 (no TCP header).  Replaces the per-packet
+ * HashFlow call of HTSearch (fhash.c:184-203) with a precomputed bucket. */
+int  mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,
+                           void *stream);
+
 /* Device-resident classification of `nb` batches in one launch sequence. */
 int  mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
                              mosrx_result *const *d_out, void *stream);
@@ -148,6 +156,8 @@ int  mosrx_time_queue(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq, uint32_t
 /* End-to-end: host frames -> pinned staging -> H2D -> kernel -> D2H -> h_out.
  * Blocks until h_out is filled. */
 int  mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out);
+/* Same, plus the flow hashes into h_fhash[n] (see mosrx_classify_dev_fh). */
+int  mosrx_classify_host_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_fhash);
 
 /* Asynchronous end-to-end form for pipelining: two slots per context, each
  * with its own stream.  submit enqueues H2D -> kernel -> D2H and returns; wait
@@ -182,6 +192,11 @@ void *mosrx_stream(mosrx_ctx *c);
  * stream the kernels run on.  Used by bench.py for the live roofline figure. */
 int  mosrx_time_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
                     mosrx_result *const *d_out, uint32_t iters, float *ms);
+/* Same, with batch i enqueued on stream i % nstreams (1..MOSRX_MAX_STREAMS):
+ * independent batches overlap launch and drain, as several rx queues would. */
+#define MOSRX_MAX_STREAMS 8
+int  mosrx_time_dev_streams(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
+                            mosrx_result *const *d_out, uint32_t iters, uint32_t nstreams, float *ms);
 /* Average duration of one classify kernel over `iters` launches, each bracketed
  * by its own pair of HIP events on the stream it runs on (the roofline figure). */
 int  mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,

@@ -25,6 +25,7 @@ struct slot {
 	uint32_t *d_off;
 	uint16_t *d_len;
 	mosrx_result *d_res;
+	uint32_t *d_fh;
 	uint32_t *d_cnt;
 	uint64_t cap_frames;
 	uint32_t cap_n;
@@ -226,7 +227,8 @@ static void slot_free(struct slot *s)
 	if (s->d_off) hipFree(s->d_off);
 	if (s->d_len) hipFree(s->d_len);
 	if (s->d_res) hipFree(s->d_res);
-	s->d_frames = NULL; s->d_off = NULL; s->d_len = NULL; s->d_res = NULL;
+	if (s->d_fh) hipFree(s->d_fh);
+	s->d_frames = NULL; s->d_off = NULL; s->d_len = NULL; s->d_res = NULL; s->d_fh = NULL;
 	s->cap_frames = 0; s->cap_n = 0;
 }
 
@@ -267,13 +269,26 @@ static int check_batch(const mosrx_batch *b, int dev)
 	return 0;
 }
 
-static int tile_for(const mosrx_batch *b)
+/* Kernel shape from what the caller knows cheaply: max_len (every frame fits
+ * the header window -> SMALL) and the mean buffer bytes per frame (large frames
+ * -> LARGE, mixed/small -> MID).  Variant bits 2-3 force a shape (tuning). */
+static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_t n)
 {
-	return (b->max_len && b->max_len <= MOSRX_WINDOW_END) ? MOSRX_TILE_SMALL : MOSRX_TILE_LARGE;
+	const int force = (c->variant >> 2) & 3;
+	if (force)
+		return force - 1;
+	if (max_len && max_len <= MOSRX_WINDOW_END)
+		return MOSRX_KIND_SMALL;
+	return (n && bytes / n >= MOSRX_LARGE_AVG_BYTES) ? MOSRX_KIND_LARGE : MOSRX_KIND_MID;
+}
+
+static int tile_for(const mosrx_ctx *c, const mosrx_batch *b)
+{
+	return kind_of(c, b->max_len, b->frames_bytes, b->n);
 }
 
 static int launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
-                  const uint16_t *len, mosrx_result *out, uint32_t *cnt, hipStream_t s)
+                  const uint16_t *len, mosrx_result *out, uint32_t *cnt, uint32_t *fhash, hipStream_t s)
 {
 	mosrx_kparams kp;
 	kp.frames = frames;
@@ -282,24 +297,31 @@ static int launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, con
 	kp.out = out;
 	kp.tables = c->d_tables;
 	kp.counters = cnt;
+	kp.fhash = fhash;
 	kp.frames_bytes = (uint32_t)b->frames_bytes;
 	kp.n = b->n;
 	kp.flags = c->kflags;
 	kp.grid_cap = 0;
-	return mosrx_launch_classify(&kp, tile_for(b), c->variant, (void *)s);
+	return mosrx_launch_classify(&kp, tile_for(c, b), c->variant, (void *)s);
 }
 
-int mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, void *stream)
+int mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,
+                          void *stream)
 {
 	int rc;
 	if (!c || (rc = check_batch(b, 1)))
 		return c ? rc : -EINVAL;
 	if (b->n == 0)
 		return 0;
-	if (!d_out || ((uintptr_t)d_out & 15))
+	if (!d_out || ((uintptr_t)d_out & 15) || ((uintptr_t)d_fhash & 3))
 		return -EINVAL;
-	return launch(c, b, b->frames, b->off, b->len, d_out, NULL,
+	return launch(c, b, b->frames, b->off, b->len, d_out, NULL, d_fhash,
 	              stream ? (hipStream_t)stream : c->stream);
+}
+
+int mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, void *stream)
+{
+	return mosrx_classify_dev_fh(c, b, d_out, NULL, stream);
 }
 
 int mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
@@ -326,7 +348,8 @@ static int slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uin
 		if (hipMalloc((void **)&s->d_frames, fb) != hipSuccess ||
 		    hipMalloc((void **)&s->d_off, (size_t)nn * 4) != hipSuccess ||
 		    hipMalloc((void **)&s->d_len, (size_t)nn * 2) != hipSuccess ||
-		    hipMalloc((void **)&s->d_res, (size_t)nn * sizeof(mosrx_result)) != hipSuccess) {
+		    hipMalloc((void **)&s->d_res, (size_t)nn * sizeof(mosrx_result)) != hipSuccess ||
+		    hipMalloc((void **)&s->d_fh, (size_t)nn * 4) != hipSuccess) {
 			slot_free(s);
 			return -ENOMEM;
 		}
@@ -338,7 +361,8 @@ static int slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uin
 }
 
 /* Enqueue one end-to-end batch on slot s: H2D frames+descriptors, kernel, D2H results. */
-static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosrx_result *h_out)
+static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosrx_result *h_out,
+                        uint32_t *h_fhash)
 {
 	int rc;
 	if ((rc = slot_reserve(c, s, b->frames_bytes, b->n)))
@@ -347,10 +371,13 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 	HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
 	HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
 	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_R_COUNT * 4, s->stream));
-	if ((rc = launch(c, b, s->d_frames, s->d_off, s->d_len, s->d_res, s->d_cnt, s->stream)))
+	if ((rc = launch(c, b, s->d_frames, s->d_off, s->d_len, s->d_res, s->d_cnt, h_fhash ? s->d_fh : NULL,
+	                 s->stream)))
 		return rc;
 	HIPCHK(hipMemcpyAsync(h_out, s->d_res, (size_t)b->n * sizeof(mosrx_result), hipMemcpyDeviceToHost,
 	                      s->stream));
+	if (h_fhash)
+		HIPCHK(hipMemcpyAsync(h_fhash, s->d_fh, (size_t)b->n * 4, hipMemcpyDeviceToHost, s->stream));
 	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_R_COUNT * 4, hipMemcpyDeviceToHost, s->stream));
 	HIPCHK(hipEventRecord(s->done, s->stream));
 	s->busy = 1;
@@ -363,6 +390,25 @@ int mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out)
 	if (!c || (rc = check_batch(b, 0)))
 		return c ? rc : -EINVAL;
 	if ((rc = mosrx_classify_host_submit(c, 0, b, h_out)))
+		return rc;
+	return mosrx_classify_host_wait(c, 0);
+}
+
+int mosrx_classify_host_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_fhash)
+{
+	int rc;
+	if (!c || (rc = check_batch(b, 0)))
+		return c ? rc : -EINVAL;
+	if (!h_fhash)
+		return mosrx_classify_host(c, b, h_out);
+	if (c->slot[0].busy)
+		return -EBUSY;
+	if (b->n == 0)
+		return 0;
+	if (!h_out)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	if ((rc = host_enqueue(c, &c->slot[0], b, h_out, h_fhash)))
 		return rc;
 	return mosrx_classify_host_wait(c, 0);
 }
@@ -384,7 +430,7 @@ int mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mos
 	if (!h_out)
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
-	return host_enqueue(c, &c->slot[slot], b, h_out);
+	return host_enqueue(c, &c->slot[slot], b, h_out, NULL);
 }
 
 int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
@@ -514,7 +560,7 @@ int mosrx_time_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_resul
 			return -EBUSY;
 	for (i = 0; i < iters; i++) {
 		struct slot *s = &c->slot[i % NSLOT];
-		if ((rc = host_enqueue(c, s, &b[i % nb], h_out[i % nb])))
+		if ((rc = host_enqueue(c, s, &b[i % nb], h_out[i % nb], NULL)))
 			return rc;
 	}
 	for (k = 0; k < NSLOT; k++) {
@@ -563,6 +609,43 @@ int mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosr
 	free(ev);
 	if (!rc)
 		*avg_ms = (float)(tot / iters);
+	return rc;
+}
+
+int mosrx_time_dev_streams(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
+                           uint32_t iters, uint32_t nstreams, float *ms)
+{
+	hipStream_t st[MOSRX_MAX_STREAMS];
+	hipEvent_t done[MOSRX_MAX_STREAMS];
+	uint32_t i, k, made = 0;
+	int rc = 0;
+	if (!c || !b || !d_out || !ms || nb == 0 || nstreams == 0 || nstreams > MOSRX_MAX_STREAMS)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	for (k = 0; k < nstreams && !rc; k++, made++)
+		if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess ||
+		    hipEventCreateWithFlags(&done[k], hipEventDisableTiming) != hipSuccess)
+			rc = -EIO;
+	if (!rc && hipEventRecord(c->ev0, c->stream) != hipSuccess)
+		rc = -EIO;
+	for (k = 0; k < nstreams && !rc; k++)
+		if (hipStreamWaitEvent(st[k], c->ev0, 0) != hipSuccess)
+			rc = -EIO;
+	/* batch i on stream i % nstreams: independent batches overlap their
+	 * launch/drain phases the way several rx queues would */
+	for (i = 0; i < iters && !rc; i++)
+		rc = mosrx_classify_dev(c, &b[i % nb], d_out[i % nb], st[i % nstreams]);
+	for (k = 0; k < nstreams && !rc; k++)
+		if (hipEventRecord(done[k], st[k]) != hipSuccess || hipStreamWaitEvent(c->stream, done[k], 0) != hipSuccess)
+			rc = -EIO;
+	if (!rc && (hipEventRecord(c->ev1, c->stream) != hipSuccess || hipEventSynchronize(c->ev1) != hipSuccess ||
+	            hipEventElapsedTime(ms, c->ev0, c->ev1) != hipSuccess))
+		rc = -EIO;
+	hipDeviceSynchronize();
+	for (k = 0; k < made; k++) {
+		hipStreamDestroy(st[k]);
+		hipEventDestroy(done[k]);
+	}
 	return rc;
 }
 
@@ -629,8 +712,9 @@ int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_re
 {
 	mosrx_qdesc *h;
 	mosrx_queue *qq;
-	uint32_t i, tiles = 0, maxl = 0;
-	int rc, unknown = 0, tile;
+	uint32_t i, tiles = 0, maxl = 0, tile;
+	uint64_t bytes = 0, frames = 0;
+	int rc, unknown = 0, kind;
 	if (!c || !b || !d_out || !q || nb == 0)
 		return -EINVAL;
 	*q = NULL;
@@ -643,8 +727,11 @@ int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_re
 			unknown = 1;
 		if (b[i].max_len > maxl)
 			maxl = b[i].max_len;
+		bytes += b[i].frames_bytes;
+		frames += b[i].n;
 	}
-	tile = (!unknown && maxl <= MOSRX_WINDOW_END) ? MOSRX_TILE_SMALL : MOSRX_TILE_LARGE;
+	kind = kind_of(c, unknown ? 0 : maxl, bytes, frames);   /* one shape for the whole queue */
+	tile = MOSRX_KIND_FRAMES(kind);
 	h = calloc(nb, sizeof(*h));
 	qq = calloc(1, sizeof(*qq));
 	if (!h || !qq) {
@@ -674,7 +761,7 @@ int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_re
 	free(h);
 	qq->nb = nb;
 	qq->total_tiles = tiles;
-	qq->tile = tile;
+	qq->tile = kind;
 	*q = qq;
 	return 0;
 }

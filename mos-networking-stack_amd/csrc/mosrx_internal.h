@@ -33,14 +33,21 @@ typedef struct mosrx_kparams {
 	mosrx_result   *out;
 	const uint32_t *tables;     /* MOSRX_TAB_WORDS */
 	uint32_t       *counters;   /* MOSRX_R_COUNT u32, accumulated with atomics; may be NULL */
+	uint32_t       *fhash;      /* n flow hashes (HashFlow before the NUM_BINS mask); may be NULL */
 	uint32_t        frames_bytes;
 	uint32_t        n;
 	uint32_t        flags;      /* MOSRX_KF_* */
 	uint32_t        grid_cap;   /* large tiles: max workgroups (persistent walk), 0 = one per tile */
 } mosrx_kparams;
 
-/* Kernel variants: tile = frames per 256-thread workgroup. */
-enum { MOSRX_TILE_SMALL = 256, MOSRX_TILE_LARGE = 64 };
+/* Kernel shapes ("kinds"):
+ *   SMALL  256 frames / 4 waves, every frame fits the header window (64 B configs)
+ *   LARGE   64 frames / 1 header wave + 4 streamer waves (large frames)
+ *   MID    256 frames / 4 header waves + 4 streamer waves (mixed sizes, IMIX) */
+enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_LARGE = 1, MOSRX_KIND_MID = 2 };
+#define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_LARGE ? 64u : 256u)
+/* Average captured bytes per frame at or above which LARGE beats MID. */
+#define MOSRX_LARGE_AVG_BYTES 1000u
 /* Frames whose IP datagram ends at or before this frame byte are finished in
  * the per-lane header window; longer ones stream their tail cooperatively. */
 #define MOSRX_WINDOW_END 94

@@ -51,9 +51,8 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 static_assert(2 + 4 * WIN_DW == MOSRX_WINDOW_END, "window end");
 static_assert(sizeof(mosrx_result) == 16, "record size");
-static_assert(MOSRX_TILE_LARGE == 64, "large tile is one descriptor per lane");
-// small tile: 4 waves, one frame per lane; large tile: header wave + 4 streamer waves
-#define WG_THREADS(tile) ((tile) == MOSRX_TILE_SMALL ? 256 : 320)
+// small: 4 waves, one frame per lane; large: 1 header + 4 streamer waves; mid: 4 + 4
+#define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? 256 : ((kind) == MOSRX_KIND_LARGE ? 320 : 512))
 
 // The resource range is frames_bytes rounded up to 16: the 16-byte chunk that
 // holds the buffer's last byte is readable whole (it cannot cross a page the
@@ -144,7 +143,7 @@ __device__ __forceinline__ uint32_t tail_rest(__amdgpu_buffer_rsrc_t rs, uint32_
 struct hdr_t {
 	uint32_t o, fend, split_abs;
 	uint32_t wsum;                 // segment-grid sum of the segment bytes before the split
-	uint32_t saddr, daddr, ip_len, ihl, doff, th3;
+	uint32_t saddr, daddr, ip_len, ihl, doff, th0, th3;
 	uint32_t rss, queue, ipc, reason;
 	int verdict;
 	bool fields, need_tcp, has_tail, is_tcp;
@@ -285,7 +284,7 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 		need_tcp = false;
 
 	h.o = o; h.fend = fend; h.split_abs = split_abs; h.wsum = wsum;
-	h.saddr = saddr; h.daddr = daddr; h.ip_len = ip_len; h.ihl = ihl; h.doff = doff; h.th3 = th3;
+	h.saddr = saddr; h.daddr = daddr; h.ip_len = ip_len; h.ihl = ihl; h.doff = doff; h.th0 = th0; h.th3 = th3;
 	h.rss = rss; h.queue = queue; h.ipc = ipc; h.reason = reason; h.verdict = verdict;
 	h.fields = fields; h.need_tcp = need_tcp; h.has_tail = need_tcp && fend > split; h.is_tcp = is_tcp;
 	return h;
@@ -330,6 +329,30 @@ __device__ __forceinline__ u32x4 hdr_finish(hdr_t h, uint32_t tail_sum, uint32_t
 	return rec;
 }
 
+// Flow-table hash of FindStream's reversed tuple (tcp.c:185-190): SuperFastHash
+// (fhash.c:25-69) over the 12-byte key {daddr, saddr, dport, sport} of
+// tcp_stream (tcp_stream.h:239-242) as three little-endian dwords; HashFlow
+// (fhash.c:72-92) masks it to NUM_BINS.  Defined where payload_off != 0.
+__device__ __forceinline__ uint32_t flow_hash(const hdr_t &h)
+{
+	const uint32_t key[3] = {h.daddr, h.saddr, __builtin_amdgcn_alignbit(h.th0, h.th0, 16)};
+	uint32_t hash = 12u;
+#pragma unroll
+	for (int k = 0; k < 3; k++) {
+		hash += key[k] & 0xFFFFu;
+		const uint32_t tmp = ((key[k] >> 16) << 11) ^ hash;
+		hash = (hash << 16) ^ tmp;
+		hash += hash >> 11;
+	}
+	hash ^= hash << 3;
+	hash += hash >> 5;
+	hash ^= hash << 4;
+	hash += hash >> 17;
+	hash ^= hash << 25;
+	hash += hash >> 6;
+	return (h.fields && h.is_tcp) ? hash : 0u;
+}
+
 __device__ __forceinline__ void tables_to_lds(const mosrx_kparams &kp, uint32_t *s_tab, uint32_t *s_cnt, uint32_t t)
 {
 	if (t < 256) {                            // RSS nibble tables + queue LUT (2 KiB, L2-resident)
@@ -367,7 +390,7 @@ __device__ __forceinline__ void flush_counters(const mosrx_kparams &kp, const ui
 template <int VAR>
 __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uint32_t tile)
 {
-	constexpr uint32_t TILE = MOSRX_TILE_SMALL;
+	constexpr uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL);
 	constexpr int AUX = TAIL_AUX(VAR);
 	__shared__ uint32_t s_tab[MOSRX_TAB_WORDS];
 	__shared__ uint32_t s_tail_lo[TILE], s_tail_hi[TILE], s_tail_sum[TILE], s_tail_pkt[TILE];
@@ -428,6 +451,8 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	__syncthreads();
 	if (active)
 		store_record(kp, p, hdr_finish(h, h.has_tail ? s_tail_sum[t] : 0u, kp.flags), s_cnt);
+	if (active && kp.fhash)
+		kp.fhash[p] = flow_hash(h);
 	flush_counters(kp, s_cnt, t);
 }
 
@@ -438,27 +463,28 @@ struct tail_grp_t {
 	u32x4 v[TAIL_G][TAIL_U];
 };
 
-// Frame of this wave's j-th tail candidate.  Candidates (frames whose capture
-// reaches past the split) are ranked in frame order; group g of the workgroup
-// takes candidates [16g, 16g+16), four consecutive ones per wave, so each wave
-// streams ~6 KB of contiguous frames and the workgroup a ~24 KB run per group.
-// Returns 64 when there is no such candidate.
-__device__ __forceinline__ uint32_t cand_frame(bool cand, uint32_t rank_l, uint32_t wave, uint32_t j)
+// Frame of streamer q's j-th tail candidate within a 64-frame subtile served by
+// SP streamers.  Candidates (frames whose capture reaches past the split) are
+// ranked in frame order; group g takes candidates [SP*4g, SP*4(g+1)), four
+// consecutive ones per streamer, so each streamer reads ~6 KB of contiguous
+// frames per group.  Returns 64 when there is no such candidate.
+template <int SP>
+__device__ __forceinline__ uint32_t cand_frame(bool cand, uint32_t rank_l, uint32_t q, uint32_t j)
 {
-	const uint32_t r = 4u * TAIL_G * (j / TAIL_G) + TAIL_G * wave + (j % TAIL_G);
+	const uint32_t r = SP * TAIL_G * (j / TAIL_G) + TAIL_G * q + (j % TAIL_G);
 	const uint64_t m = __ballot(cand && rank_l == r);
 	return m ? (uint32_t)__builtin_ctzll(m) : 64u;
 }
 
-// Issue the loads of group g of this wave's tail candidates (speculative bounds).
-template <int AUX>
+// Issue the loads of group g of this streamer's tail candidates (speculative bounds).
+template <int AUX, int SP>
 __device__ __forceinline__ void tail_issue(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
-                                           uint32_t hi_l, bool cand, uint32_t rank_l, uint32_t wave,
-                                           uint32_t lane, int g, tail_grp_t &b, uint32_t (&fr)[TAIL_G])
+                                           uint32_t hi_l, bool cand, uint32_t rank_l, uint32_t q,
+                                           uint32_t lane, uint32_t g, tail_grp_t &b, uint32_t (&fr)[TAIL_G])
 {
 #pragma unroll
 	for (int u = 0; u < TAIL_G; u++) {
-		const uint32_t f = cand_frame(cand, rank_l, wave, TAIL_G * g + u);
+		const uint32_t f = cand_frame<SP>(cand, rank_l, q, TAIL_G * g + u);
 		fr[u] = f;
 		const uint32_t lo = f < 64u ? __builtin_amdgcn_readlane(lo_l, f) : 0u;
 		const uint32_t hi = f < 64u ? __builtin_amdgcn_readlane(hi_l, f) : 0u;
@@ -521,11 +547,18 @@ __device__ __forceinline__ uint32_t range_sum(__amdgpu_buffer_rsrc_t rs, uint32_
 // records.  (A persistent walk over tiles with the next tile's descriptors
 // prefetched measured slower at every grid cap: per-workgroup concurrency, not
 // launch startup, bounds this kernel; profiles/r01_tune_persistent.log.)
-template <int VAR>
+//
+// H = header waves (64 frames each, TILE = 64 H); 4 streamer waves follow them.
+// H = 1 (large frames): the 4 streamers share the subtile's candidates.
+// H = 4 (mixed sizes, e.g. IMIX): streamer s serves subtile s, so a workgroup
+// covers 256 frames and keeps enough bytes in flight when most frames are small.
+template <int H, int VAR>
 __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uint32_t tile)
 {
-	constexpr uint32_t TILE = MOSRX_TILE_LARGE;
+	constexpr uint32_t TILE = 64u * H;
+	constexpr int SP = 4 / H;                 // streamers per 64-frame subtile
 	constexpr int AUX = TAIL_AUX(VAR);
+	static_assert(H == 1 || H == 4, "header waves");
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
 	__shared__ uint32_t s_spec[TILE];
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
@@ -533,9 +566,11 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
 	const uint32_t nbytes = kp.frames_bytes;
+	// subtile of this wave: header wave h -> h; streamer s -> s / SP
+	const uint32_t sub = wave < (uint32_t)H ? wave : (wave - H) / SP;
 
-	// every wave reads the tile's descriptors (lane = frame)
-	const uint32_t p = tile * TILE + lane;
+	// every wave reads its subtile's descriptors (lane = frame)
+	const uint32_t p = tile * TILE + 64u * sub + lane;
 	const bool active = p < kp.n;
 	uint32_t o = 0, cap = 0;
 	if (active) {
@@ -550,9 +585,10 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 	const uint32_t rank_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(cmask >> 32),
 	                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)cmask, 0u));
 
-	if (wave == 0) {
+	if (wave < (uint32_t)H) {
 		// ---- header wave: parse while the streamers pull the tails.  It fills the
-		// LDS tables itself (no barrier: a wave's LDS accesses are ordered) ----
+		// LDS tables itself (no barrier: a wave's LDS accesses are ordered; header
+		// waves write identical words) ----
 		hdr_win_t win;
 		hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
 		{
@@ -565,7 +601,7 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 		}
 		const hdr_t h = hdr_parse(win, o, cap, active, kp.flags, s_tab);
 		__syncthreads();   // B: s_spec ready
-		uint32_t tail = h.has_tail ? s_spec[lane] : 0u;
+		uint32_t tail = h.has_tail ? s_spec[64u * sub + lane] : 0u;
 		// Bytes between the datagram end and the capture end (Ethernet padding of
 		// a long capture) were summed speculatively: subtract them (exact integer
 		// sums, so the difference is the true tail sum).  Rare: a wave-wide pass
@@ -581,54 +617,71 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 			if (lane == f)
 				tail -= s;
 		}
-		if (active)
+		if (active) {
 			store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
+			if (kp.fhash)
+				kp.fhash[p] = flow_hash(h);
+		}
 	} else {
-		// ---- streamer waves 1..4: candidates [16g + 4(w-1), +4) of group g ----
-		// up to 16 candidates per wave in four groups; groups past the count are
-		// issued anyway (out-of-range loads, no traffic) so the load counts stay
-		// static and every wait is a counted vmcnt(N), never a drain.
-		const uint32_t sw = wave - 1u;
-		static_assert(TILE / 4 == 4 * TAIL_G, "four groups of four tails per streamer");
-		const uint32_t ngrp = (__builtin_popcountll(cmask) + 4u * TAIL_G - 1u) / (4u * TAIL_G);
+		// ---- streamer waves: streamer q of its subtile takes candidates
+		// [SP*4g + 4q, +4) of group g.  Groups come in pairs (double buffered);
+		// slots past the count are issued anyway (out-of-range loads, no traffic)
+		// so the load counts stay static and every wait is a counted vmcnt(N),
+		// never a drain.
+		const uint32_t q = (wave - H) % SP;
+		const uint32_t ngrp = (__builtin_popcountll(cmask) + SP * TAIL_G - 1u) / (SP * TAIL_G);
 		tail_grp_t b0, b1;
 		uint32_t f0[TAIL_G], f1[TAIL_G];
-		tail_issue<AUX>(rs, nbytes, lo_l, hi_l, cand, rank_l, sw, lane, 0, b0, f0);
-		tail_issue<AUX>(rs, nbytes, lo_l, hi_l, cand, rank_l, sw, lane, 1, b1, f1);
-		tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b0, f0, s_spec);
-		if (ngrp > 2) {
-			tail_issue<AUX>(rs, nbytes, lo_l, hi_l, cand, rank_l, sw, lane, 2, b0, f0);
-			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, s_spec);
-			tail_issue<AUX>(rs, nbytes, lo_l, hi_l, cand, rank_l, sw, lane, 3, b1, f1);
-			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b0, f0, s_spec);
-			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, s_spec);
+		uint32_t *spec = s_spec + 64u * sub;
+		tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 0, b0, f0);
+		tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 1, b1, f1);
+		if constexpr (H == 1) {
+			// at most 4 groups: straight-line code
+			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
+			if (ngrp > 2) {
+				tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 2, b0, f0);
+				tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+				tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 3, b1, f1);
+				tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
+				tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+			} else {
+				tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+			}
 		} else {
-			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, s_spec);
+#pragma unroll 1
+			for (uint32_t g = 0; g < ngrp; g += 2) {
+				tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
+				tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 2, b0, f0);
+				tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+				tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 3, b1, f1);
+			}
 		}
 		__syncthreads();   // B
 	}
 	flush_counters(kp, s_cnt, t);
 }
 
-template <int TILE, int VAR>
+template <int KIND, int VAR>
 __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t tile)
 {
-	if constexpr (TILE == MOSRX_TILE_SMALL)
+	if constexpr (KIND == MOSRX_KIND_SMALL)
 		classify_tile_small<VAR>(kp, tile);
+	else if constexpr (KIND == MOSRX_KIND_LARGE)
+		classify_tile_large<1, VAR>(kp, tile);
 	else
-		classify_tile_large<VAR>(kp, tile);
+		classify_tile_large<4, VAR>(kp, tile);
 }
 
-template <int TILE, int VAR>
-__global__ __launch_bounds__(WG_THREADS(TILE)) void mosrx_classify_kernel(mosrx_kparams kp)
+template <int KIND, int VAR>
+__global__ __launch_bounds__(WG_THREADS(KIND)) void mosrx_classify_kernel(mosrx_kparams kp)
 {
-	classify_tile<TILE, VAR>(kp, blockIdx.x);
+	classify_tile<KIND, VAR>(kp, blockIdx.x);
 }
 
 // Batch queue: one launch over nb resident batches (descriptor table in HBM).
 // Workgroup b finds its batch by a binary search of tile_base[] (scalar loads).
-template <int TILE, int VAR>
-__global__ __launch_bounds__(WG_THREADS(TILE)) void mosrx_classify_queue_kernel(mosrx_qparams qp)
+template <int KIND, int VAR>
+__global__ __launch_bounds__(WG_THREADS(KIND)) void mosrx_classify_queue_kernel(mosrx_qparams qp)
 {
 	const uint32_t b = blockIdx.x;
 	uint32_t lo = 0, hi = qp.nb;               // find k: tile_base[k] <= b < tile_base[k+1]
@@ -647,11 +700,12 @@ __global__ __launch_bounds__(WG_THREADS(TILE)) void mosrx_classify_queue_kernel(
 	kp.out = d->out;
 	kp.tables = qp.tables;
 	kp.counters = qp.counters;
+	kp.fhash = nullptr;
 	kp.frames_bytes = d->frames_bytes;
 	kp.n = d->n;
 	kp.flags = qp.flags;
 	kp.grid_cap = 0;
-	classify_tile<TILE, VAR>(kp, b - d->tile_base);
+	classify_tile<KIND, VAR>(kp, b - d->tile_base);
 }
 
 // Streaming-read ceiling of the box: each workgroup streams one contiguous slab
@@ -686,43 +740,50 @@ extern "C" int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sin
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-template <int TILE, int VAR>
+template <int KIND, int VAR>
 static void launch_queue_v(const mosrx_qparams *qp, uint32_t total_tiles, hipStream_t s)
 {
-	hipLaunchKernelGGL((mosrx_classify_queue_kernel<TILE, VAR>), dim3(total_tiles), dim3(WG_THREADS(TILE)), 0, s, *qp);
+	hipLaunchKernelGGL((mosrx_classify_queue_kernel<KIND, VAR>), dim3(total_tiles), dim3(WG_THREADS(KIND)), 0, s,
+	                   *qp);
 }
 
-template <int TILE, int VAR>
+template <int KIND, int VAR>
 static void launch_v(const mosrx_kparams *kp, hipStream_t s)
 {
-	hipLaunchKernelGGL((mosrx_classify_kernel<TILE, VAR>), dim3((kp->n + TILE - 1) / TILE), dim3(WG_THREADS(TILE)), 0,
-	                   s, *kp);
+	constexpr uint32_t tile = MOSRX_KIND_FRAMES(KIND);
+	hipLaunchKernelGGL((mosrx_classify_kernel<KIND, VAR>), dim3((kp->n + tile - 1) / tile), dim3(WG_THREADS(KIND)),
+	                   0, s, *kp);
 }
 
-extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles, int tile, int variant, void *stream)
+// Compiled variants: 0 = default cache policy, 2 = non-temporal tail stream
+// (the nt header-window variants 1 and 3 measured slower everywhere and are
+// folded onto 0 and 2).
+extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles, int kind, int variant, void *stream)
 {
 	if (!qp || qp->nb == 0 || total_tiles == 0)
 		return qp ? 0 : -EINVAL;
+	if (kind < 0 || kind > MOSRX_KIND_MID)
+		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-	static void (*const tab[2][4])(const mosrx_qparams *, uint32_t, hipStream_t) = {
-		{launch_queue_v<MOSRX_TILE_SMALL, 0>, launch_queue_v<MOSRX_TILE_SMALL, 1>,
-		 launch_queue_v<MOSRX_TILE_SMALL, 2>, launch_queue_v<MOSRX_TILE_SMALL, 3>},
-		{launch_queue_v<MOSRX_TILE_LARGE, 0>, launch_queue_v<MOSRX_TILE_LARGE, 1>,
-		 launch_queue_v<MOSRX_TILE_LARGE, 2>, launch_queue_v<MOSRX_TILE_LARGE, 3>}};
-	tab[tile == MOSRX_TILE_SMALL ? 0 : 1][variant & 3](qp, total_tiles, s);
+	static void (*const tab[3][2])(const mosrx_qparams *, uint32_t, hipStream_t) = {
+		{launch_queue_v<MOSRX_KIND_SMALL, 0>, launch_queue_v<MOSRX_KIND_SMALL, 2>},
+		{launch_queue_v<MOSRX_KIND_LARGE, 0>, launch_queue_v<MOSRX_KIND_LARGE, 2>},
+		{launch_queue_v<MOSRX_KIND_MID, 0>, launch_queue_v<MOSRX_KIND_MID, 2>}};
+	tab[kind][(variant >> 1) & 1](qp, total_tiles, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int tile, int variant, void *stream)
+extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int variant, void *stream)
 {
 	if (!kp || kp->n == 0)
 		return kp ? 0 : -EINVAL;
+	if (kind < 0 || kind > MOSRX_KIND_MID)
+		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-	static void (*const tab[2][4])(const mosrx_kparams *, hipStream_t) = {
-		{launch_v<MOSRX_TILE_SMALL, 0>, launch_v<MOSRX_TILE_SMALL, 1>,
-		 launch_v<MOSRX_TILE_SMALL, 2>, launch_v<MOSRX_TILE_SMALL, 3>},
-		{launch_v<MOSRX_TILE_LARGE, 0>, launch_v<MOSRX_TILE_LARGE, 1>,
-		 launch_v<MOSRX_TILE_LARGE, 2>, launch_v<MOSRX_TILE_LARGE, 3>}};
-	tab[tile == MOSRX_TILE_SMALL ? 0 : 1][variant & 3](kp, s);
+	static void (*const tab[3][2])(const mosrx_kparams *, hipStream_t) = {
+		{launch_v<MOSRX_KIND_SMALL, 0>, launch_v<MOSRX_KIND_SMALL, 2>},
+		{launch_v<MOSRX_KIND_LARGE, 0>, launch_v<MOSRX_KIND_LARGE, 2>},
+		{launch_v<MOSRX_KIND_MID, 0>, launch_v<MOSRX_KIND_MID, 2>}};
+	tab[kind][(variant >> 1) & 1](kp, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

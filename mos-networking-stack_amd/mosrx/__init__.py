@@ -100,6 +100,8 @@ def lib():
             "mosrx_close": (None, [P]),
             "mosrx_classify_dev": (I, [P, C.POINTER(Batch), P, P]),
             "mosrx_classify_host": (I, [P, C.POINTER(Batch), P]),
+            "mosrx_classify_dev_fh": (I, [P, C.POINTER(Batch), P, P, P]),
+            "mosrx_classify_host_fh": (I, [P, C.POINTER(Batch), P, P]),
             "mosrx_classify_host_submit": (I, [P, I, C.POINTER(Batch), P]),
             "mosrx_classify_host_wait": (I, [P, I]),
             "mosrx_last_counters": (I, [P, C.POINTER(U64)]),
@@ -114,6 +116,7 @@ def lib():
             "mosrx_time_dev": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_time_dev_kernels": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_device_sync": (I, [P]),
+            "mosrx_time_dev_streams": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, U32, C.POINTER(C.c_float)]),
             "mosrx_probe_read_bw": (I, [P, U64, U32, U32, C.POINTER(C.c_float)]),
             "mosrx_queue_create": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
             "mosrx_queue_run": (I, [P, P, P]),
@@ -222,6 +225,7 @@ class DevBatch:
         self.d_len = DevBuffer(ctx, max(ln.nbytes, 2))
         self.d_len.upload(ln)
         self.d_out = DevBuffer(ctx, max(self.n * 16, 16))
+        self.d_fhash = None   # allocated on the first classify_dev(..., flow_hash=True)
         self.max_len = int(max_len if max_len is not None else (int(ln.max()) if self.n else 0))
         self.caplen_sum = int(ln.astype(np.uint64).sum())
 
@@ -235,9 +239,16 @@ class DevBatch:
             self.d_out.download(out)
         return out
 
+    def flow_hashes(self) -> np.ndarray:
+        out = np.zeros(self.n, np.uint32)
+        if self.n:
+            self.d_fhash.download(out)
+        return out
+
     def free(self):
-        for b in (self.d_frames, self.d_off, self.d_len, self.d_out):
-            b.free()
+        for b in (self.d_frames, self.d_off, self.d_len, self.d_out, self.d_fhash):
+            if b is not None:
+                b.free()
 
 
 class Context:
@@ -279,6 +290,19 @@ class Context:
         _chk(lib().mosrx_classify_host(self.handle, C.byref(b), out.ctypes.data), "mosrx_classify_host")
         return out
 
+    def classify_host_fh(self, frames, off, ln, frames_bytes=None, max_len=0):
+        """Records plus the per-frame flow hash (HashFlow before the NUM_BINS mask)."""
+        frames = np.ascontiguousarray(frames, np.uint8)
+        off = np.ascontiguousarray(off, np.uint32)
+        ln = np.ascontiguousarray(ln, np.uint16)
+        out = np.zeros(len(off), RESULT_DTYPE)
+        fh = np.zeros(len(off), np.uint32)
+        b = Batch(frames.ctypes.data, int(frames_bytes if frames_bytes is not None else len(frames)),
+                  off.ctypes.data, ln.ctypes.data, len(off), max_len)
+        _chk(lib().mosrx_classify_host_fh(self.handle, C.byref(b), out.ctypes.data, fh.ctypes.data),
+             "mosrx_classify_host_fh")
+        return out, fh
+
     def last_counters(self) -> np.ndarray:
         c = (C.c_uint64 * 12)()
         _chk(lib().mosrx_last_counters(self.handle, c), "mosrx_last_counters")
@@ -288,9 +312,15 @@ class Context:
     def upload(self, frames, off, ln, frames_bytes=None, max_len=None) -> DevBatch:
         return DevBatch(self, frames, off, ln, frames_bytes, max_len)
 
-    def classify_dev(self, db: DevBatch, sync: bool = True) -> None:
+    def classify_dev(self, db: DevBatch, sync: bool = True, flow_hash: bool = False) -> None:
         b = db.batch()
-        _chk(lib().mosrx_classify_dev(self.handle, C.byref(b), db.d_out.ptr, None), "mosrx_classify_dev")
+        if flow_hash:
+            if db.d_fhash is None:
+                db.d_fhash = DevBuffer(self, max(db.n * 4, 4))
+            _chk(lib().mosrx_classify_dev_fh(self.handle, C.byref(b), db.d_out.ptr, db.d_fhash.ptr, None),
+                 "mosrx_classify_dev_fh")
+        else:
+            _chk(lib().mosrx_classify_dev(self.handle, C.byref(b), db.d_out.ptr, None), "mosrx_classify_dev")
         if sync:
             _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
 
@@ -299,6 +329,15 @@ class Context:
         outs = (C.c_void_p * len(dbs))(*[d.d_out.ptr for d in dbs])
         ms = C.c_float()
         _chk(lib().mosrx_time_dev(self.handle, bs, len(dbs), outs, iters, C.byref(ms)), "mosrx_time_dev")
+        return float(ms.value)
+
+    def time_dev_streams(self, dbs: list[DevBatch], iters: int, nstreams: int) -> float:
+        """Total ms for `iters` launches spread round-robin over `nstreams` streams."""
+        bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
+        outs = (C.c_void_p * len(dbs))(*[d.d_out.ptr for d in dbs])
+        ms = C.c_float()
+        _chk(lib().mosrx_time_dev_streams(self.handle, bs, len(dbs), outs, iters, nstreams, C.byref(ms)),
+             "mosrx_time_dev_streams")
         return float(ms.value)
 
     def time_dev_kernels(self, dbs: list[DevBatch], iters: int) -> float:

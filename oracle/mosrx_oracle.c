@@ -139,6 +139,82 @@ int mo_rss_queue(uint32_t hash, int mode, int num_queues)
 	return (int)(masked % (uint32_t)num_queues);
 }
 
+/* SuperFastHash, core/src/fhash.c:25-69 (get16bits = native little-endian
+ * 16-bit load on x86; the tail bytes are `signed char`). */
+uint32_t mo_superfasthash(const uint8_t *data, int len)
+{
+	uint32_t hash = (uint32_t)len, tmp;
+	int rem;
+
+	if (len <= 0 || data == NULL)
+		return 0;
+	rem = len & 3;
+	len >>= 2;
+	for (; len > 0; len--) {
+		hash += le16(data);
+		tmp = ((uint32_t)le16(data + 2) << 11) ^ hash;
+		hash = (hash << 16) ^ tmp;
+		data += 4;
+		hash += hash >> 11;
+	}
+	switch (rem) {
+	case 3:
+		hash += le16(data);
+		hash ^= hash << 16;
+		hash ^= (uint32_t)((int32_t)(signed char)data[2] << 18);
+		hash += hash >> 11;
+		break;
+	case 2:
+		hash += le16(data);
+		hash ^= hash << 11;
+		hash += hash >> 17;
+		break;
+	case 1:
+		hash += (uint32_t)(int32_t)(signed char)data[0];
+		hash ^= hash << 10;
+		hash += hash >> 1;
+	}
+	hash ^= hash << 3;
+	hash += hash >> 5;
+	hash ^= hash << 4;
+	hash += hash >> 17;
+	hash ^= hash << 25;
+	hash += hash >> 6;
+	return hash;
+}
+
+/* FindStream's key (tcp.c:185-190): the reversed tuple {daddr, saddr, dport,
+ * sport} as stored in tcp_stream (network order, tcp_stream.h:239-242), hashed
+ * by HashFlow (fhash.c:72-92); the flow-table bucket is hash & (NUM_BINS-1). */
+uint32_t mo_flow_hash(const uint8_t *iph, const uint8_t *tcph)
+{
+	uint8_t key[12];
+	memcpy(key, iph + 16, 4);      /* temp.saddr = iph->daddr */
+	memcpy(key + 4, iph + 12, 4);  /* temp.daddr = iph->saddr */
+	memcpy(key + 8, tcph + 2, 2);  /* temp.sport = tcph->dest */
+	memcpy(key + 10, tcph, 2);     /* temp.dport = tcph->source */
+	return mo_superfasthash(key, 12);
+}
+
+int mo_classify_fh(const mosrx_params *p, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
+                   const uint16_t *len, uint32_t n, mosrx_result *out, uint32_t *fhash)
+{
+	uint32_t i;
+	int rc = mo_classify(p, frames, frames_bytes, off, len, n, out);
+	if (rc || !fhash)
+		return rc;
+	for (i = 0; i < n; i++) {
+		/* defined for every TCP frame whose header fields are (payload_off != 0) */
+		if (out[i].payload_off) {
+			const uint8_t *iph = frames + off[i] + 14;
+			fhash[i] = mo_flow_hash(iph, iph + (out[i].ihl_doff >> 4) * 4);
+		} else {
+			fhash[i] = 0;
+		}
+	}
+	return 0;
+}
+
 void mo_params_default(mosrx_params *p)
 {
 	memset(p, 0, sizeof(*p));

@@ -33,6 +33,15 @@ uint32_t mo_rss_hash(const uint32_t cache[96], uint32_t sip, uint32_t dip, uint1
 /* GetRSSCPUCore, core/src/util.c:114-131, with FetchEndianType() == mode. */
 int      mo_rss_queue(uint32_t hash, int mode, int num_queues);
 
+/* SuperFastHash, core/src/fhash.c:25-69. */
+uint32_t mo_superfasthash(const uint8_t *data, int len);
+/* HashFlow of FindStream's reversed tuple (tcp.c:185-190, fhash.c:72-92), full
+ * 32 bits; bucket = value & 0x1FFFF (NUM_BINS, fhash.h:7). */
+uint32_t mo_flow_hash(const uint8_t *iph, const uint8_t *tcph);
+/* mo_classify + the flow hash per frame (0 unless a TCP frame with header fields). */
+int mo_classify_fh(const mosrx_params *p, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
+                   const uint16_t *len, uint32_t n, mosrx_result *out, uint32_t *fhash);
+
 /* ProcessPacket (eth_in.c:27-87) through the TCP prefix (tcp.c:408-445) plus
  * the RSS hash/queue, for one frame.  Fills all 16 bytes of *r. */
 void mo_classify_one(const mosrx_params *p, const uint32_t cache[96],

@@ -12,10 +12,12 @@
  *   trace.in : "MRXT" | u32 ver=1 | u32 n | u64 frames_bytes |
  *              u32 num_msp | u32 num_esp | i32 forward | i32 num_queues | i32 queue_mode |
  *              u32 off[n] | u16 len[n] | u8 frames[frames_bytes]
- *   results  : n x { i8 verdict, u8 have, u16 ip_csum, u16 tcp_csum, u16 pad, u32 rss, i32 queue }
+ *   results  : n x { i8 verdict, u8 have, u16 ip_csum, u16 tcp_csum, u16 pad, u32 rss, i32 queue,
+ *                    u32 fbucket }
  *              then u64 rx_packets, rx_bytes, rx_errors (NETSTAT, eth_in.c:42-45,80-84)
  *   have bit0: ip_csum computed, bit1: tcp_csum computed, bit2: rss computed,
- *        bit3: frame skipped (would make the reference read past caplen).
+ *        bit3: frame skipped (would make the reference read past caplen),
+ *        bit4: fbucket computed (TCP frames).
  *
  * forward must be 0: ForwardIPPacket/ForwardEthernetFrame need route/ARP
  * tables and TX buffers.
@@ -49,7 +51,10 @@ struct rec {
 	uint16_t ip_csum, tcp_csum, pad;
 	uint32_t rss;
 	int32_t queue;
+	uint32_t fbucket;   /* HashFlow() of FindStream's reversed tuple (tcp.c:185-190, fhash.c:72-92) */
 };
+
+unsigned int HashFlow(const tcp_stream *flow);
 
 static int rd(FILE *f, void *p, size_t n) { return fread(p, 1, n, f) == n ? 0 : -1; }
 
@@ -146,6 +151,15 @@ int main(int argc, char **argv)
 					r.rss = GetRSSHash(ntohl(iph->saddr), ntohl(iph->daddr), sp, dp);
 					r.queue = GetRSSCPUCore(ntohl(iph->saddr), ntohl(iph->daddr), sp, dp, nq);
 					r.have |= 4;
+					if (proto == 6) {   /* FindStream's temp stream, tcp.c:185-190 */
+						static tcp_stream ts;
+						ts.saddr = iph->daddr;
+						ts.sport = th->dest;
+						ts.daddr = iph->saddr;
+						ts.dport = th->source;
+						r.fbucket = HashFlow(&ts);
+						r.have |= 16;
+					}
 				}
 			}
 		}

@@ -11,7 +11,8 @@ stack states and stores inputs and the reference's outputs as .npz data:
   tcp_csum = TCPCalcChecksum(...)   (tcp_util.c:157)
   rss      = GetRSSHash(ntohl(saddr), ntohl(daddr), ntohs(sp), ntohs(dp)) (util.c:61)
   queue    = GetRSSCPUCore(...)     (util.c:114, FetchEndianType wrapped for ixgbe)
-  have     = which of those the harness computed (bit3: frame skipped, see harness)
+  fbucket  = HashFlow(&FindStream's reversed tuple) (fhash.c:72, tcp.c:185-190)
+  have     = which of those the harness computed (bit3: frame skipped, bit4: fbucket)
 plus the NETSTAT rx counters.  The MSDN Toeplitz KAT (util/rss.c:177-193) is
 stored as its own fixture.  Nothing here is reference source: only data.
 """
@@ -27,7 +28,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-from pktlib import ETH_ARP, pack_frames, tcp_frame  # noqa: E402
+from pktlib import ETH_ARP, REF_FIELDS, pack_frames, tcp_frame  # noqa: E402
 import oracle_py as O  # noqa: E402
 
 STATES = [  # (name, num_msp, num_esp, num_queues, queue_mode)
@@ -159,7 +160,7 @@ def run_states(frames: list[bytes], name: str, phase: int = 2):
     out = {"frames": buf, "off": off, "len": ln}
     for st, *_ in STATES:
         r = res[st]
-        for fld in ("verdict", "have", "ip_csum", "tcp_csum", "rss", "queue"):
+        for fld in REF_FIELDS:
             out[f"{st}__{fld}"] = np.ascontiguousarray(r[fld])
         out[f"{st}__stats"] = res[st + "_stats"]
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)

@@ -64,6 +64,10 @@ def lib():
                                   C.c_uint32, C.c_void_p]
         L.mo_classify_mt.restype = C.c_int
         L.mo_classify_mt.argtypes = L.mo_classify.argtypes + [C.c_int]
+        L.mo_classify_fh.restype = C.c_int
+        L.mo_classify_fh.argtypes = L.mo_classify.argtypes + [C.c_void_p]
+        L.mo_superfasthash.restype = C.c_uint32
+        L.mo_superfasthash.argtypes = [C.c_char_p, C.c_int]
         _lib = L
     return _lib
 
@@ -86,6 +90,21 @@ def classify(buf, off, ln, p: Params | None = None, nthreads: int = 1) -> np.nda
     if rc:
         raise OSError(-rc, "mo_classify failed")
     return out
+
+
+def classify_fh(buf, off, ln, p: Params | None = None):
+    """Records + the FindStream flow hash (HashFlow before masking) per frame."""
+    p = p or params()
+    buf = np.ascontiguousarray(buf, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    ln = np.ascontiguousarray(ln, np.uint16)
+    out = np.zeros(len(off), RESULT_DTYPE)
+    fh = np.zeros(len(off), np.uint32)
+    rc = lib().mo_classify_fh(C.byref(p), buf.ctypes.data, len(buf), off.ctypes.data, ln.ctypes.data,
+                              len(off), out.ctypes.data, fh.ctypes.data)
+    if rc:
+        raise OSError(-rc, "mo_classify_fh failed")
+    return out, fh
 
 
 def have_ref() -> bool:

@@ -99,11 +99,14 @@ def write_ref_trace(path, buf, off, ln, *, num_msp=1, num_esp=0, forward=0, num_
 
 
 REF_DTYPE = np.dtype([("verdict", "i1"), ("have", "u1"), ("ip_csum", "<u2"), ("tcp_csum", "<u2"),
-                      ("pad", "<u2"), ("rss", "<u4"), ("queue", "<i4")])
+                      ("pad", "<u2"), ("rss", "<u4"), ("queue", "<i4"), ("fbucket", "<u4")])
+# fields stored per stack state in the golden fixtures (fbucket = HashFlow bucket, have bit 4)
+REF_FIELDS = ("verdict", "have", "ip_csum", "tcp_csum", "rss", "queue", "fbucket")
 
 
 def read_ref_results(path, n):
     raw = open(path, "rb").read()
-    rec = np.frombuffer(raw[: n * 16], REF_DTYPE)
-    stats = struct.unpack("<QQQ", raw[n * 16: n * 16 + 24])
+    sz = REF_DTYPE.itemsize
+    rec = np.frombuffer(raw[: n * sz], REF_DTYPE)
+    stats = struct.unpack("<QQQ", raw[n * sz: n * sz + 24])
     return rec, dict(rx_packets=stats[0], rx_bytes=stats[1], rx_errors=stats[2])

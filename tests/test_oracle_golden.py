@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 import oracle_py as O
-from pktlib import R, pack_frames, tcp_frame
+from pktlib import R, REF_FIELDS, pack_frames, tcp_frame
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 FIXTURES = ["edge", "rand_small", "rand_mid", "rand_large"]
@@ -23,8 +23,11 @@ STATES = {  # name -> (num_msp, num_esp, num_queues, queue_mode)
 }
 
 
-def compare_with_ref(res, ref, p):
-    """Field-by-field agreement of oracle records with the reference harness output."""
+def compare_with_ref(res, ref, p, fh=None):
+    """Field-by-field agreement of oracle records with the reference harness output.
+
+    `fh` (optional) is the per-frame flow hash; its low 17 bits must equal the
+    reference's HashFlow() bucket wherever the reference computed one."""
     trunc = res["reason"] == R["TRUNCATED"]
     skipped = (ref["have"] & 8) != 0
     np.testing.assert_array_equal(trunc, skipped, err_msg="TRUNCATED set differs from reference skips")
@@ -40,6 +43,11 @@ def compare_with_ref(res, ref, p):
     assert np.all(ref["have"][tcp] & 2)
     np.testing.assert_array_equal(res["tcp_csum"][tcp], ref["tcp_csum"][tcp], err_msg="tcp_csum")
     np.testing.assert_array_equal(res["tcp_csum"][tcp] == 0, res["verdict"][tcp] == 1)
+    if fh is not None:
+        hashed = live & (res["payload_off"] != 0)
+        # the harness hashes every in-bounds TCP frame; the path defines it where FindStream runs
+        assert np.all(ref["have"][hashed] & 16), "flow hash defined where the reference has none"
+        np.testing.assert_array_equal(fh[hashed] & 0x1FFFF, ref["fbucket"][hashed], err_msg="fbucket")
 
 
 @pytest.mark.parametrize("fix", FIXTURES)
@@ -48,9 +56,9 @@ def test_oracle_matches_reference_fixture(fix, state):
     z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
     msp, esp, nq, qm = STATES[state]
     p = O.params(num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm)
-    res = O.classify(z["frames"], z["off"], z["len"], p)
-    ref = {k: z[f"{state}__{k}"] for k in ("verdict", "have", "ip_csum", "tcp_csum", "rss", "queue")}
-    compare_with_ref(res, ref, p)
+    res, fh = O.classify_fh(z["frames"], z["off"], z["len"], p)
+    ref = {k: z[f"{state}__{k}"] for k in REF_FIELDS}
+    compare_with_ref(res, ref, p, fh)
     # NETSTAT view (eth_in.c:42-45, 80-84) over the frames the reference processed
     live = res["reason"] != R["TRUNCATED"]
     st = z[f"{state}__stats"]
@@ -116,7 +124,8 @@ def test_oracle_fuzz_vs_reference(seed):
     for msp, esp, nq, qm in [(1, 0, 1, 1), (0, 1, 5, 0), (1, 1, 7, 1)]:
         p = O.params(num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm)
         rec, _ = O.run_ref(buf, off, ln, num_msp=msp, num_esp=esp, num_queues=nq, queue_mode=qm)
-        compare_with_ref(O.classify(buf, off, ln, p), rec, p)
+        res, fh = O.classify_fh(buf, off, ln, p)
+        compare_with_ref(res, rec, p, fh)
 
 
 @pytest.mark.skipif(not O.have_ref(), reason="oracle/_ref/mosref not built (needs /root/reference)")
@@ -125,8 +134,8 @@ def test_oracle_vs_reference_on_seeded_trace():
     t = mosrx.Trace(mosrx.TRACE_IMIX, 6000, nflows=1000)
     p = O.params(forward=0)
     rec, _ = O.run_ref(t.frames, t.off, t.len)
-    res = O.classify(t.frames, t.off, t.len, p)
-    compare_with_ref(res, rec, p)
+    res, fh = O.classify_fh(t.frames, t.off, t.len, p)
+    compare_with_ref(res, rec, p, fh)
     # corruption schedule of the generator: 1/1024 IP, 1/1024 TCP
     idx = np.arange(t.n)
     assert np.all(res["reason"][idx % 1024 == 511] == R["IP_BADCSUM"])

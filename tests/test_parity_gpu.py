@@ -11,7 +11,7 @@ import pytest
 
 import mosrx
 import oracle_py as O
-from pktlib import R, pack_frames, tcp_frame
+from pktlib import R, REF_FIELDS, pack_frames, tcp_frame
 from test_oracle_golden import FIXTURES, GOLDEN, STATES, compare_with_ref
 
 pytestmark = pytest.mark.gpu
@@ -55,7 +55,7 @@ def test_golden_fixtures(gpu_ctx, fix, state):
     p = mosrx.default_params(num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm)
     gpu_ctx.set_params(p)
     out = gpu_ctx.classify_host(z["frames"], z["off"], z["len"])
-    ref = {k: z[f"{state}__{k}"] for k in ("verdict", "have", "ip_csum", "tcp_csum", "rss", "queue")}
+    ref = {k: z[f"{state}__{k}"] for k in REF_FIELDS}
     compare_with_ref(out, ref, p)                                  # against mOS itself
     assert_records_equal(out, O.classify(z["frames"], z["off"], z["len"], oparams(p)), fix)
 
@@ -236,3 +236,56 @@ def test_batch_queue_one_launch(gpu_ctx, kind, n, nb):
     q.destroy()
     for d in dbs:
         d.free()
+
+
+# kernel shapes forced through variant bits 2-3 (value - 1: SMALL, LARGE, MID) with both
+# tail-load cache policies; every shape must be exact on every frame mix
+@pytest.mark.parametrize("variant", [2, 6, 10, 14, 0, 8, 12])
+@pytest.mark.parametrize("kind,n", [(mosrx.TRACE_S64, 20_000), (mosrx.TRACE_M1500, 9_000),
+                                    (mosrx.TRACE_IMIX, 30_000)])
+def test_forced_kernel_shapes(gpu_ctx, variant, kind, n):
+    t = mosrx.Trace(kind, n, seed=variant)
+    gpu_ctx.set_variant(variant)
+    try:
+        run_both(gpu_ctx, t.frames, t.off, t.len, mosrx.default_params(),
+                 frames_bytes=t.frames_bytes, max_len=t.max_len)
+        z = np.load(os.path.join(GOLDEN, "rand_mid.npz"))
+        run_both(gpu_ctx, z["frames"], z["off"], z["len"], mosrx.default_params(forward=0))
+    finally:
+        gpu_ctx.set_variant(2)
+
+
+@pytest.mark.parametrize("fix", FIXTURES)
+def test_flow_hash_golden(gpu_ctx, fix):
+    # HashFlow bucket (fhash.c:72-92) of FindStream's reversed tuple (tcp.c:185-190)
+    z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
+    p = mosrx.default_params(forward=0)
+    gpu_ctx.set_params(p)
+    out, fh = gpu_ctx.classify_host_fh(z["frames"], z["off"], z["len"])
+    ref = {k: z[f"msp1__{k}"] for k in REF_FIELDS}
+    compare_with_ref(out, ref, p, fh)                               # against mOS itself
+    ora, ofh = O.classify_fh(z["frames"], z["off"], z["len"], oparams(p))
+    assert_records_equal(out, ora, fix)
+    np.testing.assert_array_equal(fh, ofh)
+
+
+@pytest.mark.parametrize("variant", [2, 6, 10, 14])
+@pytest.mark.parametrize("kind,n", [(mosrx.TRACE_S64, 32_768), (mosrx.TRACE_M1500, 16_384),
+                                    (mosrx.TRACE_IMIX, 65_536)])
+def test_flow_hash_device(gpu_ctx, variant, kind, n):
+    t = mosrx.Trace(kind, n, nflows=5000)
+    p = mosrx.default_params()
+    gpu_ctx.set_params(p)
+    gpu_ctx.set_variant(variant)
+    try:
+        db = gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len)
+        gpu_ctx.classify_dev(db, flow_hash=True)
+        res, fh = db.results(), db.flow_hashes()
+        db.free()
+    finally:
+        gpu_ctx.set_variant(2)
+    ora, ofh = O.classify_fh(t.frames[:t.frames_bytes], t.off, t.len, oparams(p))
+    assert_records_equal(res, ora, "classify_dev_fh")
+    np.testing.assert_array_equal(fh, ofh)
+    # size-independent property: frames of one flow share a bucket; 5000 flows -> <= 5000 buckets
+    assert len(np.unique(fh[ora["payload_off"] != 0] & 0x1FFFF)) <= 5000

@@ -211,6 +211,51 @@ int  mosrx_device_sync(mosrx_ctx *c);
 int  mosrx_time_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
                      mosrx_result *const *h_out, uint32_t iters, float *ms);
 
+/* ---- batched BPF ---------------------------------------- */
+/* mOS evaluates classic-BPF programs per frame: raw-monitor filters on the
+ * whole frame (ip_in.c:56-63) and stream SYN / orphan filters on the IP
+ * datagram (tcp.c:42-56, 486-496), each through EVAL_BPFFILTER ->
+ * sfbpf_filter(insns, p, len, len) (include/bpf/sfbpf.h:84,
+ * bpf/sf_bpf_filter.c:214-536).  Programs still come from mOS's own compiler
+ * (SET_BPFFILTER -> sfbpf_compile, sfbpf.h:83); the GPU runs the batched
+ * evaluation of up to 32 of them over a batch and returns one match bitmask
+ * per frame. */
+typedef struct mosrx_bpf_insn {   /* layout of struct sfbpf_insn (include/bpf/sfbpf.h:174-179) */
+	uint16_t code;
+	uint8_t  jt;
+	uint8_t  jf;
+	uint32_t k;
+} mosrx_bpf_insn;
+
+enum {
+	MOSRX_BPF_LEN_FRAME = 0,  /* wirelen = buflen = caplen (raw monitor: ethh, eth_len) */
+	MOSRX_BPF_LEN_IP    = 1,  /* wirelen = buflen = 14 + ip tot_len (SYN/orphan filters);
+	                           * evaluated on IPv4 frames whose datagram lies inside caplen, else 0 */
+};
+#define MOSRX_BPF_MAX_PROGS 32
+#define MOSRX_BPF_MAX_INSNS 4096   /* total over all programs of a set */
+
+typedef struct mosrx_bpf_prog {
+	const mosrx_bpf_insn *insns;   /* NULL or len 0: no filter, matches every frame (sfbpf_filter(NULL) = ~0) */
+	uint32_t              len;     /* bf_len */
+	int32_t               len_mode;/* MOSRX_BPF_LEN_* */
+} mosrx_bpf_prog;
+
+/* The admission check of mosrx_bpf_set for one program (no GPU needed):
+ * 0 or -EINVAL. */
+int  mosrx_bpf_check(const mosrx_bpf_insn *insns, uint32_t len);
+/* Install a program set on the context (host arrays, copied).  Each program
+ * must pass sfbpf_validate (sf_bpf_filter.c:548-691) and, beyond it, use only
+ * opcodes sfbpf_filter executes (others abort() there) with jump targets that
+ * stay forward in 64-bit pointer arithmetic; otherwise -EINVAL, as
+ * SET_BPFFILTER failing makes mtcp_bind_monitor_filter return EINVAL
+ * (mos_api.c:127-155).  nprog = 0 clears the set. */
+int  mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog);
+/* Device-resident evaluation: d_match[i] bit j = (sfbpf_filter(prog j, frame i) != 0). */
+int  mosrx_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t *d_match, void *stream);
+/* End-to-end from host memory (blocking). */
+int  mosrx_bpf_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t *h_match);
+
 /* ---- RSS helpers (host-side table build; the hash itself runs on the GPU) -- */
 /* Toeplitz nibble tables: 24 tables x 16 u32 for the 12-byte tuple
  * saddr|daddr|sport|dport (wire order).  Built from the key cache of

@@ -1,0 +1,159 @@
+/*
+ * bpf_api.c — host side of the batched BPF row (include/mosrx.h).
+ *
+ * mosrx_bpf_set is the GPU-side counterpart of SET_BPFFILTER (sfbpf.h:83):
+ * mOS keeps compiling filter expressions with sfbpf_compile and hands the
+ * resulting struct sfbpf_program here; the check below admits exactly the
+ * programs sfbpf_filter (bpf/sf_bpf_filter.c:214-536) runs to a defined result.
+ */
+#include <errno.h>
+#include <string.h>
+
+#include "mosrx_ctx.h"
+
+enum {
+	LD = 0, LDX = 1, ST = 2, STX = 3, ALU = 4, JMP = 5, RET = 6, MISC = 7,
+	W = 0, H = 8, B = 0x10, IMM = 0, ABS = 0x20, IND = 0x40, MEM = 0x60, LEN = 0x80, MSH = 0xa0,
+	ADD = 0, SUB = 0x10, MUL = 0x20, DIV = 0x30, OR = 0x40, AND = 0x50, LSH = 0x60, RSH = 0x70, NEG = 0x80,
+	JA = 0, JEQ = 0x10, JGT = 0x20, JGE = 0x30, JSET = 0x40, K = 0, X = 8, A = 0x10, TAX = 0, TXA = 0x80,
+	MEMWORDS = 16
+};
+
+/* sfbpf_validate (sf_bpf_filter.c:548-691) tightened to what sfbpf_filter can
+ * execute on x86-64: only the opcodes of its switch (any other abort()s),
+ * memory slots < 16, no constant division by zero (validate misses it: it
+ * tests BPF_RVAL, :628, and the division traps), jump targets inside the
+ * program in 64-bit arithmetic (pc += k moves a pointer forward), and a
+ * return as the last instruction. */
+int mosrx_bpf_check(const mosrx_bpf_insn *f, uint32_t len)
+{
+	uint32_t i;
+	if (!f || len == 0 || len > MOSRX_BPF_MAX_INSNS)
+		return -EINVAL;
+	for (i = 0; i < len; i++) {
+		const uint32_t k = f[i].k;
+		const uint64_t from = (uint64_t)i + 1;
+		switch (f[i].code) {
+		case RET | K: case RET | A:
+		case LD | W | ABS: case LD | H | ABS: case LD | B | ABS: case LD | W | LEN: case LDX | W | LEN:
+		case LD | W | IND: case LD | H | IND: case LD | B | IND: case LDX | MSH | B:
+		case LD | IMM: case LDX | IMM:
+		case ALU | ADD | X: case ALU | SUB | X: case ALU | MUL | X: case ALU | DIV | X: case ALU | AND | X:
+		case ALU | OR | X: case ALU | LSH | X: case ALU | RSH | X:
+		case ALU | ADD | K: case ALU | SUB | K: case ALU | MUL | K: case ALU | AND | K: case ALU | OR | K:
+		case ALU | LSH | K: case ALU | RSH | K: case ALU | NEG:
+		case MISC | TAX: case MISC | TXA:
+			break;
+		case ALU | DIV | K:
+			if (k == 0)
+				return -EINVAL;
+			break;
+		case LD | MEM: case LDX | MEM: case ST: case STX:
+			if (k >= MEMWORDS)
+				return -EINVAL;
+			break;
+		case JMP | JA:
+			if (from + k >= len)
+				return -EINVAL;
+			break;
+		case JMP | JGT | K: case JMP | JGE | K: case JMP | JEQ | K: case JMP | JSET | K:
+		case JMP | JGT | X: case JMP | JGE | X: case JMP | JEQ | X: case JMP | JSET | X:
+			if (from + f[i].jt >= len || from + f[i].jf >= len)
+				return -EINVAL;
+			break;
+		default:
+			return -EINVAL;
+		}
+	}
+	return (f[len - 1].code & 7) == RET ? 0 : -EINVAL;
+}
+
+int mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
+{
+	mosrx_bparams t;
+	mosrx_bpf_insn staged[MOSRX_BPF_MAX_INSNS];
+	uint32_t j, total = 0;
+	int rc;
+	if (!c || nprog > MOSRX_BPF_MAX_PROGS || (nprog && !progs))
+		return -EINVAL;
+	memset(&t, 0, sizeof(t));
+	for (j = 0; j < nprog; j++) {
+		const uint32_t len = progs[j].insns ? progs[j].len : 0;
+		if (progs[j].len_mode != MOSRX_BPF_LEN_FRAME && progs[j].len_mode != MOSRX_BPF_LEN_IP)
+			return -EINVAL;
+		if (len && (rc = mosrx_bpf_check(progs[j].insns, len)))
+			return rc;
+		if (total + len > MOSRX_BPF_MAX_INSNS)
+			return -E2BIG;
+		if (len)
+			memcpy(staged + total, progs[j].insns, (size_t)len * sizeof(mosrx_bpf_insn));
+		t.prog_off[j] = (uint16_t)total;
+		t.prog_len[j] = (uint16_t)len;
+		if (progs[j].len_mode == MOSRX_BPF_LEN_IP)
+			t.ip_mode |= 1u << j;
+		total += len;
+	}
+	t.nprog = nprog;
+	HIPCHK(hipSetDevice(c->device));
+	if (!c->d_bpf)
+		HIPCHK(hipMalloc((void **)&c->d_bpf, MOSRX_BPF_MAX_INSNS * sizeof(mosrx_bpf_insn)));
+	/* the previous set may still be in use by enqueued launches */
+	HIPCHK(hipStreamSynchronize(c->stream));
+	HIPCHK(hipDeviceSynchronize());
+	if (total)
+		HIPCHK(hipMemcpy(c->d_bpf, staged, (size_t)total * sizeof(mosrx_bpf_insn), hipMemcpyHostToDevice));
+	c->bpf = t;
+	return 0;
+}
+
+static int bpf_launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
+                      const uint16_t *len, uint32_t *match, hipStream_t s)
+{
+	mosrx_bparams bp = c->bpf;
+	bp.frames = frames;
+	bp.off = off;
+	bp.len = len;
+	bp.match = match;
+	bp.insns = c->d_bpf;
+	bp.frames_bytes = (uint32_t)b->frames_bytes;
+	bp.n = b->n;
+	return mosrx_launch_bpf(&bp, (void *)s);
+}
+
+int mosrx_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t *d_match, void *stream)
+{
+	int rc;
+	if (!c || (rc = mosrx__check_batch(b, 1)))
+		return c ? rc : -EINVAL;
+	if (b->n == 0)
+		return 0;
+	if (!d_match || ((uintptr_t)d_match & 3))
+		return -EINVAL;
+	return bpf_launch(c, b, b->frames, b->off, b->len, d_match, stream ? (hipStream_t)stream : c->stream);
+}
+
+int mosrx_bpf_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t *h_match)
+{
+	struct slot *s;
+	int rc;
+	if (!c || (rc = mosrx__check_batch(b, 0)))
+		return c ? rc : -EINVAL;
+	if (b->n == 0)
+		return 0;
+	if (!h_match)
+		return -EINVAL;
+	s = &c->slot[0];
+	if (s->busy)
+		return -EBUSY;
+	HIPCHK(hipSetDevice(c->device));
+	if ((rc = mosrx__slot_reserve(c, s, b->frames_bytes, b->n)))
+		return rc;
+	HIPCHK(hipMemcpyAsync(s->d_frames, b->frames, b->frames_bytes, hipMemcpyHostToDevice, s->stream));
+	HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
+	HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
+	if ((rc = bpf_launch(c, b, s->d_frames, s->d_off, s->d_len, s->d_fh, s->stream)))
+		return rc;
+	HIPCHK(hipMemcpyAsync(h_match, s->d_fh, (size_t)b->n * 4, hipMemcpyDeviceToHost, s->stream));
+	HIPCHK(hipStreamSynchronize(s->stream));
+	return 0;
+}

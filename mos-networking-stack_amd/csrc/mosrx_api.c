@@ -6,46 +6,11 @@
  * kernels in mosrx_kernels.hip.  There is no CPU fallback: without a usable GPU
  * mosrx_open() fails with -ENODEV.
  */
-#define __HIP_PLATFORM_AMD__ 1
-#include <hip/hip_runtime_api.h>
-
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
 
-#include "mosrx_internal.h"
-
-#define HIPCHK(x) do { if ((x) != hipSuccess) return -EIO; } while (0)
-
-/* pipeline slots for the end-to-end path (double-buffered H2D | kernel | D2H) */
-#define NSLOT MOSRX_NSLOT
-
-struct slot {
-	uint8_t *d_frames;
-	uint32_t *d_off;
-	uint16_t *d_len;
-	mosrx_result *d_res;
-	uint32_t *d_fh;
-	uint32_t *d_cnt;
-	uint64_t cap_frames;
-	uint32_t cap_n;
-	hipStream_t stream;
-	hipEvent_t done;
-	uint32_t h_cnt[MOSRX_R_COUNT];
-	int busy;
-};
-
-struct mosrx_ctx {
-	int device;
-	hipStream_t stream;
-	mosrx_params params;
-	uint32_t kflags;
-	uint32_t *d_tables;
-	struct slot slot[NSLOT];
-	uint32_t h_cnt[MOSRX_R_COUNT];   /* counters of the last waited batch */
-	hipEvent_t ev0, ev1;
-	int variant;                     /* kernel cache-policy variant (mosrx_set_variant) */
-};
+#include "mosrx_ctx.h"
 
 /* Default cache policy per access class (bit 0: header windows non-temporal,
  * bit 1: tail stream non-temporal), chosen from measurements on MI355X. */
@@ -250,13 +215,14 @@ void mosrx_close(mosrx_ctx *c)
 		slot_free(&c->slot[i]);
 	}
 	if (c->d_tables) hipFree(c->d_tables);
+	if (c->d_bpf) hipFree(c->d_bpf);
 	if (c->ev0) hipEventDestroy(c->ev0);
 	if (c->ev1) hipEventDestroy(c->ev1);
 	if (c->stream) hipStreamDestroy(c->stream);
 	free(c);
 }
 
-static int check_batch(const mosrx_batch *b, int dev)
+int mosrx__check_batch(const mosrx_batch *b, int dev)
 {
 	if (!b)
 		return -EINVAL;
@@ -309,7 +275,7 @@ int mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_ou
                           void *stream)
 {
 	int rc;
-	if (!c || (rc = check_batch(b, 1)))
+	if (!c || (rc = mosrx__check_batch(b, 1)))
 		return c ? rc : -EINVAL;
 	if (b->n == 0)
 		return 0;
@@ -337,7 +303,7 @@ int mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
 	return 0;
 }
 
-static int slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uint32_t n)
+int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uint32_t n)
 {
 	if (frames_bytes > s->cap_frames || n > s->cap_n) {
 		uint64_t fb = frames_bytes > s->cap_frames ? frames_bytes + (frames_bytes >> 2) : s->cap_frames;
@@ -365,7 +331,7 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
                         uint32_t *h_fhash)
 {
 	int rc;
-	if ((rc = slot_reserve(c, s, b->frames_bytes, b->n)))
+	if ((rc = mosrx__slot_reserve(c, s, b->frames_bytes, b->n)))
 		return rc;
 	HIPCHK(hipMemcpyAsync(s->d_frames, b->frames, b->frames_bytes, hipMemcpyHostToDevice, s->stream));
 	HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
@@ -387,7 +353,7 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 int mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out)
 {
 	int rc;
-	if (!c || (rc = check_batch(b, 0)))
+	if (!c || (rc = mosrx__check_batch(b, 0)))
 		return c ? rc : -EINVAL;
 	if ((rc = mosrx_classify_host_submit(c, 0, b, h_out)))
 		return rc;
@@ -397,7 +363,7 @@ int mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out)
 int mosrx_classify_host_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_fhash)
 {
 	int rc;
-	if (!c || (rc = check_batch(b, 0)))
+	if (!c || (rc = mosrx__check_batch(b, 0)))
 		return c ? rc : -EINVAL;
 	if (!h_fhash)
 		return mosrx_classify_host(c, b, h_out);
@@ -418,7 +384,7 @@ int mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mos
 	int rc;
 	if (!c || slot < 0 || slot >= NSLOT)
 		return -EINVAL;
-	if ((rc = check_batch(b, 0)))
+	if ((rc = mosrx__check_batch(b, 0)))
 		return rc;
 	if (c->slot[slot].busy)
 		return -EBUSY;
@@ -549,7 +515,7 @@ int mosrx_time_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_resul
 	HIPCHK(hipSetDevice(c->device));
 	for (i = 0; i < nb; i++)   /* size both slots before timing */
 		for (k = 0; k < NSLOT; k++)
-			if ((rc = slot_reserve(c, &c->slot[k], b[i].frames_bytes, b[i].n)))
+			if ((rc = mosrx__slot_reserve(c, &c->slot[k], b[i].frames_bytes, b[i].n)))
 				return rc;
 	HIPCHK(hipDeviceSynchronize());
 	HIPCHK(hipEventRecord(c->ev0, c->stream));
@@ -719,7 +685,7 @@ int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_re
 		return -EINVAL;
 	*q = NULL;
 	for (i = 0; i < nb; i++) {
-		if ((rc = check_batch(&b[i], 1)))
+		if ((rc = mosrx__check_batch(&b[i], 1)))
 			return rc;
 		if (b[i].n && (!d_out[i] || ((uintptr_t)d_out[i] & 15)))
 			return -EINVAL;

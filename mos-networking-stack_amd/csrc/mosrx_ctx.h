@@ -1,0 +1,50 @@
+/*
+ * mosrx_ctx.h — host-side context layout shared by the C host files
+ * (mosrx_api.c, bpf_api.c).  Not part of the ABI.
+ */
+#ifndef MOSRX_CTX_H
+#define MOSRX_CTX_H
+
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+
+#include "mosrx_internal.h"
+
+#define HIPCHK(x) do { if ((x) != hipSuccess) return -EIO; } while (0)
+
+/* pipeline slots for the end-to-end path (double-buffered H2D | kernel | D2H) */
+#define NSLOT MOSRX_NSLOT
+
+struct slot {
+	uint8_t *d_frames;
+	uint32_t *d_off;
+	uint16_t *d_len;
+	mosrx_result *d_res;
+	uint32_t *d_fh;
+	uint32_t *d_cnt;
+	uint64_t cap_frames;
+	uint32_t cap_n;
+	hipStream_t stream;
+	hipEvent_t done;
+	uint32_t h_cnt[MOSRX_R_COUNT];
+	int busy;
+};
+
+struct mosrx_ctx {
+	int device;
+	hipStream_t stream;
+	mosrx_params params;
+	uint32_t kflags;
+	uint32_t *d_tables;
+	struct slot slot[NSLOT];
+	uint32_t h_cnt[MOSRX_R_COUNT];   /* counters of the last waited batch */
+	hipEvent_t ev0, ev1;
+	int variant;                     /* kernel cache-policy variant (mosrx_set_variant) */
+	mosrx_bpf_insn *d_bpf;           /* installed BPF programs (MOSRX_BPF_MAX_INSNS), NULL until set */
+	mosrx_bparams bpf;               /* program table of the installed set */
+};
+
+int mosrx__check_batch(const mosrx_batch *b, int dev);
+int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uint32_t n);
+
+#endif

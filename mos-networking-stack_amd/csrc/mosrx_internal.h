@@ -72,6 +72,24 @@ typedef struct mosrx_qparams {
 	uint32_t           flags;
 } mosrx_qparams;
 
+/* Batched BPF launch: the program table rides in the kernel arguments, the
+ * instructions sit in one device buffer read with scalar loads. */
+typedef struct mosrx_bparams {
+	const uint8_t        *frames;
+	const uint32_t       *off;
+	const uint16_t       *len;
+	uint32_t             *match;
+	const mosrx_bpf_insn *insns;      /* MOSRX_BPF_MAX_INSNS */
+	uint32_t              frames_bytes;
+	uint32_t              n;
+	uint32_t              nprog;
+	uint32_t              ip_mode;    /* bit j: program j uses MOSRX_BPF_LEN_IP */
+	uint16_t              prog_off[MOSRX_BPF_MAX_PROGS];
+	uint16_t              prog_len[MOSRX_BPF_MAX_PROGS];   /* 0: no filter (matches) */
+} mosrx_bparams;
+
+int mosrx_launch_bpf(const mosrx_bparams *bp, void *stream);
+
 int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles, int tile, int variant, void *stream);
 int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sink, void *stream);
 

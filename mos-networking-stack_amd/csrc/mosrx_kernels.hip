@@ -39,7 +39,7 @@
 #include <errno.h>
 #include <stdint.h>
 
-#include "mosrx_internal.h"
+#include "mosrx_device.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -54,15 +54,6 @@ static_assert(sizeof(mosrx_result) == 16, "record size");
 // small: 4 waves, one frame per lane; large: 1 header + 4 streamer waves; mid: 4 + 4
 #define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? 256 : ((kind) == MOSRX_KIND_LARGE ? 320 : 512))
 
-// The resource range is frames_bytes rounded up to 16: the 16-byte chunk that
-// holds the buffer's last byte is readable whole (it cannot cross a page the
-// buffer does not touch), and every byte past the last frame's end is masked.
-// Loads at or past the range read zero with no memory traffic; the range check
-// is per dword (tested by test_buffer_end_exact on misaligned layouts).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t *base, uint32_t nbytes)
-{
-	return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)((nbytes + 15u) & ~15u), 0x00020000);
-}
 
 // 16 bytes at byte offset c (OOB offsets read zero).  No data-dependent branch:
 // the compiler can then count outstanding loads (s_waitcnt vmcnt(N)) across groups.
@@ -363,10 +354,6 @@ __device__ __forceinline__ void tables_to_lds(const mosrx_kparams &kp, uint32_t 
 		s_cnt[t] = 0;
 }
 
-__device__ __forceinline__ uint32_t eff_caplen(uint32_t o, uint32_t len, uint32_t nbytes)
-{
-	return (o >= nbytes) ? 0u : min(len, nbytes - o);
-}
 
 __device__ __forceinline__ void store_record(const mosrx_kparams &kp, uint32_t p, u32x4 rec, uint32_t *s_cnt)
 {

@@ -52,6 +52,15 @@ class Batch(C.Structure):
                 ("len", C.c_void_p), ("n", C.c_uint32), ("max_len", C.c_uint32)]
 
 
+BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])   # mosrx_bpf_insn
+BPF_LEN_FRAME, BPF_LEN_IP = 0, 1
+BPF_MAX_PROGS = 32
+
+
+class BpfProg(C.Structure):
+    _fields_ = [("insns", C.c_void_p), ("len", C.c_uint32), ("len_mode", C.c_int32)]
+
+
 class TraceC(C.Structure):
     _fields_ = [("frames", C.c_void_p), ("frames_bytes", C.c_uint64), ("off", C.c_void_p),
                 ("len", C.c_void_p), ("n", C.c_uint32), ("max_len", C.c_uint32),
@@ -124,6 +133,10 @@ def lib():
             "mosrx_time_queue": (I, [P, C.POINTER(P), U32, U32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
             "mosrx_time_host": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_rss_tables": (I, [C.c_char_p, U32, C.POINTER(U32)]),
+            "mosrx_bpf_check": (I, [P, U32]),
+            "mosrx_bpf_set": (I, [P, C.POINTER(BpfProg), U32]),
+            "mosrx_bpf_dev": (I, [P, C.POINTER(Batch), P, P]),
+            "mosrx_bpf_host": (I, [P, C.POINTER(Batch), P]),
             "mosrx_trace_gen": (I, [I, U32, U32, U64, C.POINTER(TraceC)]),
             "mosrx_trace_free": (None, [C.POINTER(TraceC)]),
             "mosrx_source_mem": (P, [P, P, P, U32, U32]),
@@ -162,6 +175,12 @@ def default_params(**kw) -> Params:
             p.rss_key[i] = key[i] if i < len(key) else 0
         p.rss_key_len = len(key)
     return p
+
+
+def bpf_check(insns) -> int:
+    """mosrx_bpf_check: 0 if mosrx_bpf_set would admit the program, else -errno."""
+    ins = np.ascontiguousarray(insns, BPF_INSN)
+    return lib().mosrx_bpf_check(ins.ctypes.data if len(ins) else None, len(ins))
 
 
 class Trace:
@@ -226,6 +245,7 @@ class DevBatch:
         self.d_len.upload(ln)
         self.d_out = DevBuffer(ctx, max(self.n * 16, 16))
         self.d_fhash = None   # allocated on the first classify_dev(..., flow_hash=True)
+        self.d_match = None   # allocated on the first bpf_dev
         self.max_len = int(max_len if max_len is not None else (int(ln.max()) if self.n else 0))
         self.caplen_sum = int(ln.astype(np.uint64).sum())
 
@@ -239,6 +259,12 @@ class DevBatch:
             self.d_out.download(out)
         return out
 
+    def matches(self) -> np.ndarray:
+        out = np.zeros(self.n, np.uint32)
+        if self.n:
+            self.d_match.download(out)
+        return out
+
     def flow_hashes(self) -> np.ndarray:
         out = np.zeros(self.n, np.uint32)
         if self.n:
@@ -246,7 +272,7 @@ class DevBatch:
         return out
 
     def free(self):
-        for b in (self.d_frames, self.d_off, self.d_len, self.d_out, self.d_fhash):
+        for b in (self.d_frames, self.d_off, self.d_len, self.d_out, self.d_fhash, self.d_match):
             if b is not None:
                 b.free()
 
@@ -302,6 +328,35 @@ class Context:
         _chk(lib().mosrx_classify_host_fh(self.handle, C.byref(b), out.ctypes.data, fh.ctypes.data),
              "mosrx_classify_host_fh")
         return out, fh
+
+    # ---- batched BPF (mosrx_bpf_*) ----
+    def bpf_set(self, progs) -> None:
+        """progs: list of (insns, len_mode); insns None/empty = no filter (matches)."""
+        keep = [np.ascontiguousarray(i if i is not None else [], BPF_INSN) for i, _ in progs]
+        arr = (BpfProg * max(1, len(progs)))()
+        for j, ((_, mode), ins) in enumerate(zip(progs, keep)):
+            arr[j].insns = ins.ctypes.data if len(ins) else None
+            arr[j].len = len(ins)
+            arr[j].len_mode = mode
+        _chk(lib().mosrx_bpf_set(self.handle, arr, len(progs)), "mosrx_bpf_set")
+
+    def bpf_host(self, frames, off, ln, frames_bytes=None) -> np.ndarray:
+        frames = np.ascontiguousarray(frames, np.uint8)
+        off = np.ascontiguousarray(off, np.uint32)
+        ln = np.ascontiguousarray(ln, np.uint16)
+        out = np.zeros(len(off), np.uint32)
+        b = Batch(frames.ctypes.data, int(frames_bytes if frames_bytes is not None else len(frames)),
+                  off.ctypes.data, ln.ctypes.data, len(off), 0)
+        _chk(lib().mosrx_bpf_host(self.handle, C.byref(b), out.ctypes.data), "mosrx_bpf_host")
+        return out
+
+    def bpf_dev(self, db: "DevBatch", sync: bool = True) -> None:
+        if db.d_match is None:
+            db.d_match = DevBuffer(self, max(db.n * 4, 4))
+        b = db.batch()
+        _chk(lib().mosrx_bpf_dev(self.handle, C.byref(b), db.d_match.ptr, None), "mosrx_bpf_dev")
+        if sync:
+            _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
 
     def last_counters(self) -> np.ndarray:
         c = (C.c_uint64 * 12)()

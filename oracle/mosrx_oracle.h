@@ -42,6 +42,16 @@ uint32_t mo_flow_hash(const uint8_t *iph, const uint8_t *tcph);
 int mo_classify_fh(const mosrx_params *p, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
                    const uint16_t *len, uint32_t n, mosrx_result *out, uint32_t *fhash);
 
+/* sfbpf_filter (bpf/sf_bpf_filter.c:214-536) and sfbpf_validate (:548-691). */
+uint32_t mo_bpf_filter(const mosrx_bpf_insn *pc, const uint8_t *p, uint32_t wirelen, uint32_t buflen);
+int      mo_bpf_validate(const mosrx_bpf_insn *f, int len);
+/* One program's return value on every frame at a call-site length (0 where not evaluated). */
+int      mo_bpf_returns(const mosrx_bpf_insn *insns, uint32_t ninsn, int len_mode, const uint8_t *frames,
+                        uint64_t frames_bytes, const uint32_t *off, const uint16_t *len, uint32_t n, uint32_t *ret);
+/* Batched: out[i] bit j = program j matched frame i (lengths per MOSRX_BPF_LEN_*). */
+int      mo_bpf_eval(const mosrx_bpf_prog *progs, uint32_t nprog, const uint8_t *frames, uint64_t frames_bytes,
+                     const uint32_t *off, const uint16_t *len, uint32_t n, uint32_t *out);
+
 /* ProcessPacket (eth_in.c:27-87) through the TCP prefix (tcp.c:408-445) plus
  * the RSS hash/queue, for one frame.  Fills all 16 bytes of *r. */
 void mo_classify_one(const mosrx_params *p, const uint32_t cache[96],

@@ -18,6 +18,8 @@ from pktlib import RESULT_DTYPE, read_ref_results, write_ref_trace
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "libmosrx_oracle.so")
 REF_BIN = os.path.join(ROOT, "oracle", "_ref", "mosref")
+REF_BPF_BIN = os.path.join(ROOT, "oracle", "_ref", "mosbpf")
+BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])   # struct sfbpf_insn
 
 MS_KEY = bytes([0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
                 0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
@@ -68,6 +70,16 @@ def lib():
         L.mo_classify_fh.argtypes = L.mo_classify.argtypes + [C.c_void_p]
         L.mo_superfasthash.restype = C.c_uint32
         L.mo_superfasthash.argtypes = [C.c_char_p, C.c_int]
+        L.mo_bpf_filter.restype = C.c_uint32
+        L.mo_bpf_filter.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
+        L.mo_bpf_validate.restype = C.c_int
+        L.mo_bpf_validate.argtypes = [C.c_void_p, C.c_int]
+        L.mo_bpf_returns.restype = C.c_int
+        L.mo_bpf_returns.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_void_p, C.c_uint64, C.c_void_p,
+                                     C.c_void_p, C.c_uint32, C.c_void_p]
+        L.mo_bpf_eval.restype = C.c_int
+        L.mo_bpf_eval.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                  C.c_uint32, C.c_void_p]
         _lib = L
     return _lib
 
@@ -119,3 +131,85 @@ def run_ref(buf, off, ln, *, num_msp=1, num_esp=0, num_queues=1, queue_mode=1):
                         num_queues=num_queues, queue_mode=queue_mode)
         subprocess.run([REF_BIN, tin, tout], check=True, stdout=subprocess.DEVNULL)
         return read_ref_results(tout, len(off))
+
+
+class BpfProg(C.Structure):
+    """mosrx_bpf_prog (include/mosrx.h)."""
+    _fields_ = [("insns", C.c_void_p), ("len", C.c_uint32), ("len_mode", C.c_int32)]
+
+
+def bpf_filter(insns: np.ndarray, frame: bytes, length: int) -> int:
+    """sfbpf_filter(insns, frame, length, length) restated (None/empty = no filter)."""
+    insns = np.ascontiguousarray(insns, BPF_INSN)
+    ptr = insns.ctypes.data if len(insns) else None
+    return lib().mo_bpf_filter(ptr, bytes(frame) + bytes(8), length, length)
+
+
+def bpf_validate(insns: np.ndarray) -> int:
+    insns = np.ascontiguousarray(insns, BPF_INSN)
+    return lib().mo_bpf_validate(insns.ctypes.data if len(insns) else None, len(insns))
+
+
+def bpf_eval(progs: list, buf, off, ln) -> np.ndarray:
+    """progs: list of (insns ndarray, len_mode).  Returns the per-frame match mask."""
+    keep = [np.ascontiguousarray(i, BPF_INSN) for i, _ in progs]
+    arr = (BpfProg * max(1, len(progs)))()
+    for j, ((_, mode), ins) in enumerate(zip(progs, keep)):
+        arr[j].insns = ins.ctypes.data if len(ins) else None
+        arr[j].len = len(ins)
+        arr[j].len_mode = mode
+    buf = np.ascontiguousarray(buf, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    ln = np.ascontiguousarray(ln, np.uint16)
+    out = np.zeros(len(off), np.uint32)
+    rc = lib().mo_bpf_eval(arr, len(progs), buf.ctypes.data, len(buf), off.ctypes.data, ln.ctypes.data,
+                           len(off), out.ctypes.data)
+    if rc:
+        raise OSError(-rc, "mo_bpf_eval failed")
+    return out
+
+
+def bpf_returns(insns, len_mode: int, buf, off, ln) -> np.ndarray:
+    """sfbpf_filter's return value per frame at a call-site length (0 where not evaluated)."""
+    ins = np.ascontiguousarray(insns, BPF_INSN)
+    buf = np.ascontiguousarray(buf, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    ln = np.ascontiguousarray(ln, np.uint16)
+    out = np.zeros(len(off), np.uint32)
+    lib().mo_bpf_returns(ins.ctypes.data if len(ins) else None, len(ins), len_mode, buf.ctypes.data, len(buf),
+                         off.ctypes.data, ln.ctypes.data, len(off), out.ctypes.data)
+    return out
+
+
+def have_ref_bpf() -> bool:
+    return os.path.exists(REF_BPF_BIN)
+
+
+def run_ref_bpf(lines: list[str], buf, off, ln) -> list[dict]:
+    """Compile + evaluate with mOS's own BPF objects (oracle/_ref/mosbpf)."""
+    import struct
+    n = len(off)
+    with tempfile.TemporaryDirectory() as d:
+        te, tin, tout = (os.path.join(d, x) for x in ("e.txt", "t.in", "t.out"))
+        with open(te, "w") as fh:
+            fh.write("\n".join(lines) + "\n")
+        with open(tin, "wb") as fh:
+            fh.write(struct.pack("<II", n, len(buf)))
+            fh.write(np.asarray(off, "<u4").tobytes())
+            fh.write(np.asarray(ln, "<u2").tobytes())
+            fh.write(np.asarray(buf, np.uint8).tobytes())
+        subprocess.run([REF_BPF_BIN, te, tin, tout], check=True, stdout=subprocess.DEVNULL)
+        raw = open(tout, "rb").read()
+    out, p = [], 0
+    for _ in lines:
+        rc, val, ni = struct.unpack_from("<iiI", raw, p)
+        p += 12
+        insns = np.frombuffer(raw[p:p + 8 * ni], BPF_INSN).copy()
+        p += 8 * ni
+        rf = np.frombuffer(raw[p:p + 4 * n], "<u4").copy()
+        p += 4 * n
+        ri = np.frombuffer(raw[p:p + 4 * n], "<u4").copy()
+        p += 4 * n
+        out.append(dict(rc=rc, validate=val, insns=insns, ret_frame=rf, ret_ip=ri))
+    assert p == len(raw)
+    return out

@@ -1,0 +1,210 @@
+"""Batched BPF: mOS's sfbpf_filter per frame, on the GPU.
+
+tests/golden/bpf.npz holds programs compiled by mOS's own sfbpf_compile plus
+hand-assembled ones, mixed frames, and the return values of mOS's own
+sfbpf_filter at both call-site lengths (tests/golden/make_golden_bpf.py).
+CPU tests pin the oracle restatement to them; GPU tests compare the kernel
+(through the C ABI) with both, bit-exact on every match bit.
+"""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import mosrx
+import oracle_py as O
+from pktlib import pack_frames, tcp_frame
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load():
+    z = np.load(os.path.join(GOLDEN, "bpf.npz"))
+    progs = [z["insns"][o:o + n] for o, n in zip(z["prog_off"], z["prog_len"])]
+    return z, progs
+
+
+def runnable(z):
+    """Programs the reference compiled, validated and ran (ip6 fails to compile there)."""
+    return [j for j, v in enumerate(z["valid"]) if v == 1]
+
+
+def program_sets(z, progs):
+    """Sets of <= 32 programs, alternating the two call-site lengths, plus the
+    expected match masks from the reference's return values."""
+    js = runnable(z)
+    sets = []
+    for start in range(0, len(js), 32):
+        chunk = js[start:start + 32]
+        modes = [(start + b) % 2 for b in range(len(chunk))]
+        exp = np.zeros(len(z["off"]), np.uint32)
+        for b, (j, m) in enumerate(zip(chunk, modes)):
+            r = z["ret_ip"][j] if m == mosrx.BPF_LEN_IP else z["ret_frame"][j]
+            exp |= (r != 0).astype(np.uint32) << np.uint32(b)
+        sets.append(([(progs[j], m) for j, m in zip(chunk, modes)], exp))
+    return sets
+
+
+I_ = lambda code, k=0, jt=0, jf=0: (code, jt, jf, k & 0xFFFFFFFF)  # noqa: E731
+
+
+def prog(*ins):
+    return np.array(list(ins), mosrx.BPF_INSN)
+
+
+# ---------------------------------------------------------------- CPU: oracle pinned
+def test_oracle_bpf_filter_matches_reference_returns():
+    z, progs = load()
+    buf, off, ln = z["frames"], z["off"], z["len"]
+    for j in runnable(z):
+        for mode, key in ((mosrx.BPF_LEN_FRAME, "ret_frame"), (mosrx.BPF_LEN_IP, "ret_ip")):
+            np.testing.assert_array_equal(O.bpf_returns(progs[j], mode, buf, off, ln), z[key][j],
+                                          err_msg=f"{z['names'][j]} {key}")
+
+
+def test_oracle_bpf_filter_single_frame():
+    z, progs = load()
+    buf, off, ln = z["frames"], z["off"], z["len"]
+    for i in range(0, len(off), 37):
+        f = bytes(buf[off[i]:off[i] + ln[i]])
+        for j in runnable(z)[::5]:
+            assert O.bpf_filter(progs[j], f, int(ln[i])) == z["ret_frame"][j][i], (z["names"][j], i)
+        if f[12:14] == b"\x08\x00" and len(f) >= 18:
+            lip = 14 + struct.unpack("!H", f[16:18])[0]
+            if lip <= len(f):
+                assert O.bpf_filter(progs[0], f, lip) == z["ret_ip"][0][i]
+
+
+def test_oracle_validate_matches_reference():
+    z, progs = load()
+    for j, v in enumerate(z["valid"]):
+        if v >= 0:
+            assert O.bpf_validate(progs[j]) == v, z["names"][j]
+
+
+def test_oracle_batch_eval_masks():
+    z, progs = load()
+    for ps, exp in program_sets(z, progs):
+        np.testing.assert_array_equal(O.bpf_eval(ps, z["frames"], z["off"], z["len"]), exp)
+
+
+def test_reference_validate_accepts_constant_div0():
+    # sf_bpf_filter.c:628 tests BPF_RVAL (code & 0x18) instead of BPF_SRC, so ALU|DIV|K
+    # with k == 0 passes sfbpf_validate (and would SIGFPE in sfbpf_filter)
+    p = prog(I_(0x34, 0), I_(0x16))
+    assert O.bpf_validate(p) == 1
+    assert mosrx.bpf_check(p) == -22
+
+
+def test_fixture_coverage():
+    z, progs = load()
+    js = runnable(z)
+    assert len(js) >= 60
+    codes = set(np.concatenate([progs[j]["code"] for j in js]).tolist())
+    # every opcode sfbpf_filter executes appears in some runnable program
+    executable = {0x06, 0x16, 0x20, 0x28, 0x30, 0x80, 0x81, 0x40, 0x48, 0x50, 0xb1, 0x00, 0x01, 0x60, 0x61,
+                  0x02, 0x03, 0x05, 0x25, 0x35, 0x15, 0x45, 0x2d, 0x3d, 0x1d, 0x4d, 0x0c, 0x1c, 0x2c, 0x3c,
+                  0x5c, 0x4c, 0x6c, 0x7c, 0x04, 0x14, 0x24, 0x34, 0x54, 0x44, 0x64, 0x74, 0x84, 0x07, 0x87}
+    assert executable - codes == set()
+    # both outcomes occur for most programs
+    both = sum(1 for j in js if 0 < (z["ret_frame"][j] != 0).sum() < len(z["off"]))
+    assert both >= 40
+
+
+# ---------------------------------------------------------------- CPU: admission check
+@pytest.mark.parametrize("name,p,ok", [
+    ("ret", prog(I_(0x06, 1)), True),
+    ("empty", prog(), False),
+    ("no_ret_end", prog(I_(0x00, 1)), False),
+    ("jump_out", prog(I_(0x15, 1, 5, 0), I_(0x06, 1)), False),
+    ("ja_wrap", prog(I_(0x05, 0xFFFFFFFF), I_(0x06, 1)), False),     # u_int-wrap backward jump
+    ("mem16", prog(I_(0x60, 16), I_(0x16)), False),
+    ("div_k0", prog(I_(0x34, 0), I_(0x16)), False),
+    ("div_k1", prog(I_(0x34, 1), I_(0x16)), True),
+    ("ld_h_len", prog(I_(0x88), I_(0x16)), False),                   # validate ok, abort() in filter
+    ("neg_x", prog(I_(0x8c), I_(0x16)), False),
+    ("ret_x", prog(I_(0x0e)), False),
+    ("st_bits", prog(I_(0x22, 1), I_(0x16)), False),
+    ("misc_other", prog(I_(0x27), I_(0x16)), False),
+    ("alu_mod", prog(I_(0x94, 3), I_(0x16)), False),
+])
+def test_bpf_check(name, p, ok):
+    assert (mosrx.bpf_check(p) == 0) == ok, name
+    if ok:
+        assert O.bpf_validate(p) == 1
+
+
+def test_bpf_check_admits_every_reference_runnable_program():
+    z, progs = load()
+    for j in runnable(z):
+        assert mosrx.bpf_check(progs[j]) == 0, z["names"][j]
+    for j, v in enumerate(z["valid"]):
+        if v == 0:
+            assert mosrx.bpf_check(progs[j]) != 0, z["names"][j]
+
+
+# ---------------------------------------------------------------- GPU parity
+@pytest.mark.gpu
+def test_bpf_golden_sets(gpu_ctx):
+    z, progs = load()
+    for ps, exp in program_sets(z, progs):
+        gpu_ctx.bpf_set(ps)
+        got = gpu_ctx.bpf_host(z["frames"], z["off"], z["len"])
+        np.testing.assert_array_equal(got, exp)
+        db = gpu_ctx.upload(z["frames"], z["off"], z["len"])
+        gpu_ctx.bpf_dev(db)
+        np.testing.assert_array_equal(db.matches(), exp)
+        db.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("phase,align", [(0, 1), (1, 1), (3, 4), (7, 16), (13, 2)])
+def test_bpf_misaligned_layouts(gpu_ctx, phase, align):
+    z, progs = load()
+    frames = [bytes(z["frames"][o:o + n]) for o, n in zip(z["off"], z["len"])]
+    buf, off, ln = pack_frames(frames, align=align, phase=phase)
+    ps = program_sets(z, progs)[0][0]
+    gpu_ctx.bpf_set(ps)
+    np.testing.assert_array_equal(gpu_ctx.bpf_host(buf, off, ln), O.bpf_eval(ps, buf, off, ln))
+
+
+@pytest.mark.gpu
+def test_bpf_buffer_end_and_truncation(gpu_ctx):
+    # loads of the very last frame bytes, with frames_bytes ending mid-dword
+    last = prog(I_(0x81), I_(0x40, 0xFFFFFFFC), I_(0x16))
+    lastb = prog(I_(0x81), I_(0x50, 0xFFFFFFFF), I_(0x44, 0x100), I_(0x16))
+    ps = [(last, 0), (lastb, 0), (last, 1), (lastb, 1)]
+    gpu_ctx.bpf_set(ps)
+    for plen in range(0, 24):
+        f = tcp_frame(payload=bytes(range(1, plen + 1)))
+        buf, off, ln = pack_frames([tcp_frame(payload=b"x" * 50), f], phase=plen % 16)
+        fb = int(off[-1]) + int(ln[-1])
+        got = gpu_ctx.bpf_host(buf, off, ln, frames_bytes=fb)
+        np.testing.assert_array_equal(got, O.bpf_eval(ps, buf[:fb], off, ln))
+
+
+@pytest.mark.gpu
+def test_bpf_empty_and_nofilter(gpu_ctx):
+    buf, off, ln = pack_frames([tcp_frame(payload=b"a"), tcp_frame(ethertype=0x86DD, pad_to=60)])
+    gpu_ctx.bpf_set([(None, 0), (None, 1), (prog(I_(0x06, 0)), 0)])
+    assert gpu_ctx.bpf_host(buf, off, ln).tolist() == [0b011, 0b001]   # LEN_IP only on IPv4
+    gpu_ctx.bpf_set([])
+    assert gpu_ctx.bpf_host(buf, off, ln).tolist() == [0, 0]
+    with pytest.raises(mosrx.MosrxError):
+        gpu_ctx.bpf_set([(prog(I_(0x34, 0), I_(0x16)), 0)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n", [(mosrx.TRACE_IMIX, 262_144), (mosrx.TRACE_M1500, 65_536),
+                                    (mosrx.TRACE_S64, 32_768)])
+def test_bpf_full_size_traces(gpu_ctx, kind, n):
+    z, progs = load()
+    t = mosrx.Trace(kind, n, nflows=3000)
+    ps = program_sets(z, progs)[0][0]
+    gpu_ctx.bpf_set(ps)
+    db = gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len)
+    gpu_ctx.bpf_dev(db)
+    got = db.matches()
+    db.free()
+    np.testing.assert_array_equal(got, O.bpf_eval(ps, t.frames[:t.frames_bytes], t.off, t.len))

@@ -256,6 +256,23 @@ int  mosrx_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t *d_match, void *
 /* End-to-end from host memory (blocking). */
 int  mosrx_bpf_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t *h_match);
 
+/* ---- TX checksum generation ---------------------------- */
+/* The checksum rewrite mOS applies to a frame before it goes out again:
+ * mtcp_setlastpkt with MOS_UPDATE_IP_CHKSUM / MOS_UPDATE_TCP_CHKSUM
+ * (mos_api.c:1177-1193): iph->check = 0, iph->check = ip_fast_csum(iph, ihl);
+ * tcph->check = 0, tcph->check = TCPCalcChecksum(tcph, tot_len - ihl*4, saddr,
+ * daddr) -- the same arithmetic as the S/W fallback of ip_out.c:169-174 and
+ * tcp_out.c:207-218.  Flags use mos_api.h:107-108's values.  Frames are
+ * rewritten IN PLACE (b->frames is written through); frames must not overlap.
+ * IP check: IPv4 frames with ihl >= 5 and the datagram inside the capture.
+ * TCP check: those of them with protocol 6 and tot_len >= (ihl + doff) * 4.
+ * Other frames are left untouched. */
+#define MOSRX_TX_IP_CSUM  (1 << 4)   /* MOS_UPDATE_IP_CHKSUM */
+#define MOSRX_TX_TCP_CSUM (1 << 5)   /* MOS_UPDATE_TCP_CHKSUM */
+int  mosrx_tx_csum_dev(mosrx_ctx *c, const mosrx_batch *b, int flags, void *stream);
+/* End-to-end from host memory: frames go to the GPU and come back rewritten (blocking). */
+int  mosrx_tx_csum_host(mosrx_ctx *c, const mosrx_batch *b, int flags);
+
 /* ---- RSS helpers (host-side table build; the hash itself runs on the GPU) -- */
 /* Toeplitz nibble tables: 24 tables x 16 u32 for the 12-byte tuple
  * saddr|daddr|sport|dport (wire order).  Built from the key cache of

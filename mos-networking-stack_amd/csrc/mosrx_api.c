@@ -235,17 +235,20 @@ int mosrx__check_batch(const mosrx_batch *b, int dev)
 	return 0;
 }
 
-/* Kernel shape from what the caller knows cheaply: max_len (every frame fits
- * the header window -> SMALL) and the mean buffer bytes per frame (large frames
- * -> LARGE, mixed/small -> MID).  Variant bits 2-3 force a shape (tuning). */
+/* Kernel shape: SMALL when every frame fits the header window (max_len known
+ * and <= 94), else LARGE.  Measured on MI355X (profiles/r01_tune_kinds.log):
+ * LARGE beats MID for M1500 (22.7 vs 30.3 us) and for IMIX (43.5 vs 49.0 us);
+ * MID stays reachable for tuning.  Variant bits 2-3 force a shape (value - 1). */
 static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_t n)
 {
 	const int force = (c->variant >> 2) & 3;
+	(void)bytes;
+	(void)n;
 	if (force)
 		return force - 1;
 	if (max_len && max_len <= MOSRX_WINDOW_END)
 		return MOSRX_KIND_SMALL;
-	return (n && bytes / n >= MOSRX_LARGE_AVG_BYTES) ? MOSRX_KIND_LARGE : MOSRX_KIND_MID;
+	return MOSRX_KIND_LARGE;
 }
 
 static int tile_for(const mosrx_ctx *c, const mosrx_batch *b)
@@ -253,8 +256,9 @@ static int tile_for(const mosrx_ctx *c, const mosrx_batch *b)
 	return kind_of(c, b->max_len, b->frames_bytes, b->n);
 }
 
-static int launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
-                  const uint16_t *len, mosrx_result *out, uint32_t *cnt, uint32_t *fhash, hipStream_t s)
+static int launch_flags(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
+                        const uint16_t *len, mosrx_result *out, uint32_t *cnt, uint32_t *fhash, uint32_t kflags,
+                        hipStream_t s)
 {
 	mosrx_kparams kp;
 	kp.frames = frames;
@@ -266,9 +270,59 @@ static int launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, con
 	kp.fhash = fhash;
 	kp.frames_bytes = (uint32_t)b->frames_bytes;
 	kp.n = b->n;
-	kp.flags = c->kflags;
+	kp.flags = kflags;
 	kp.grid_cap = 0;
 	return mosrx_launch_classify(&kp, tile_for(c, b), c->variant, (void *)s);
+}
+
+static int launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
+                  const uint16_t *len, mosrx_result *out, uint32_t *cnt, uint32_t *fhash, hipStream_t s)
+{
+	return launch_flags(c, b, frames, off, len, out, cnt, fhash, c->kflags, s);
+}
+
+static uint32_t tx_kflags(int flags)
+{
+	return ((flags & MOSRX_TX_IP_CSUM) ? MOSRX_KF_TX_IP : 0u) | ((flags & MOSRX_TX_TCP_CSUM) ? MOSRX_KF_TX_TCP : 0u);
+}
+
+int mosrx_tx_csum_dev(mosrx_ctx *c, const mosrx_batch *b, int flags, void *stream)
+{
+	int rc;
+	if (!c || (rc = mosrx__check_batch(b, 1)))
+		return c ? rc : -EINVAL;
+	if (flags & ~(MOSRX_TX_IP_CSUM | MOSRX_TX_TCP_CSUM))
+		return -EINVAL;
+	if (b->n == 0 || !flags)
+		return 0;
+	return launch_flags(c, b, b->frames, b->off, b->len, NULL, NULL, NULL, tx_kflags(flags),
+	                    stream ? (hipStream_t)stream : c->stream);
+}
+
+int mosrx_tx_csum_host(mosrx_ctx *c, const mosrx_batch *b, int flags)
+{
+	struct slot *s;
+	int rc;
+	if (!c || (rc = mosrx__check_batch(b, 0)))
+		return c ? rc : -EINVAL;
+	if (flags & ~(MOSRX_TX_IP_CSUM | MOSRX_TX_TCP_CSUM))
+		return -EINVAL;
+	if (b->n == 0 || !flags)
+		return 0;
+	s = &c->slot[0];
+	if (s->busy)
+		return -EBUSY;
+	HIPCHK(hipSetDevice(c->device));
+	if ((rc = mosrx__slot_reserve(c, s, b->frames_bytes, b->n)))
+		return rc;
+	HIPCHK(hipMemcpyAsync(s->d_frames, b->frames, b->frames_bytes, hipMemcpyHostToDevice, s->stream));
+	HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
+	HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
+	if ((rc = launch_flags(c, b, s->d_frames, s->d_off, s->d_len, NULL, NULL, NULL, tx_kflags(flags), s->stream)))
+		return rc;
+	HIPCHK(hipMemcpyAsync((void *)b->frames, s->d_frames, b->frames_bytes, hipMemcpyDeviceToHost, s->stream));
+	HIPCHK(hipStreamSynchronize(s->stream));
+	return 0;
 }
 
 int mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,

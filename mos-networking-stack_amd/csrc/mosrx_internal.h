@@ -24,6 +24,8 @@ enum {
 	MOSRX_KF_VERIFY    = 1u << 0,  /* num_msp || num_esp: checksums verified (ip_in.c:67) */
 	MOSRX_KF_FWD_NONIP = 1u << 1,  /* num_msp && forward: non-IPv4 frames forwarded (eth_in.c:62) */
 	MOSRX_KF_SKIP_TCP  = 1u << 2,  /* skip TCPCalcChecksum (BASELINE config #2 mode) */
+	MOSRX_KF_TX_IP     = 1u << 3,  /* TX fill: write iph->check (no records) */
+	MOSRX_KF_TX_TCP    = 1u << 4,  /* TX fill: write tcph->check (no records) */
 };
 
 typedef struct mosrx_kparams {
@@ -46,8 +48,6 @@ typedef struct mosrx_kparams {
  *   MID    256 frames / 4 header waves + 4 streamer waves (mixed sizes, IMIX) */
 enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_LARGE = 1, MOSRX_KIND_MID = 2 };
 #define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_LARGE ? 64u : 256u)
-/* Average captured bytes per frame at or above which LARGE beats MID. */
-#define MOSRX_LARGE_AVG_BYTES 1000u
 /* Frames whose IP datagram ends at or before this frame byte are finished in
  * the per-lane header window; longer ones stream their tail cooperatively. */
 #define MOSRX_WINDOW_END 94

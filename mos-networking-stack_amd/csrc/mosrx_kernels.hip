@@ -67,6 +67,9 @@ __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t c, ui
 }
 #define WIN_AUX(v)  (((v) & 1) ? 2 : 0)
 #define TAIL_AUX(v) (((v) & 2) ? 2 : 0)
+// Variant bit 4: TX checksum fill (mosrx_tx_csum_dev) instead of classification.
+#define VAR_TX 16
+#define IS_TX(v) (((v) & VAR_TX) != 0)
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 __device__ __forceinline__ uint32_t be16hi(uint32_t w) { return ((w >> 8) & 0xFF00u) | (w >> 24); } // bytes 2,3
@@ -136,8 +139,9 @@ struct hdr_t {
 	uint32_t wsum;                 // segment-grid sum of the segment bytes before the split
 	uint32_t saddr, daddr, ip_len, ihl, doff, th0, th3;
 	uint32_t rss, queue, ipc, reason;
+	uint32_t tcw, ipc_tx;          // TX: segment-grid TCP check word, IP checksum with check = 0
 	int verdict;
-	bool fields, need_tcp, has_tail, is_tcp;
+	bool fields, need_tcp, has_tail, is_tcp, tx_ip;
 };
 
 struct hdr_win_t {
@@ -156,9 +160,33 @@ __device__ __forceinline__ void hdr_load(__amdgpu_buffer_rsrc_t rs, uint32_t nby
 	}
 }
 
+// ip_fast_csum (ip_in.h:10-38) over the realigned header (w[3] = IP dword 0):
+// 32-bit adc chain, the final carry added once (its own carry lost), fold, not.
+// w5 stands in for IP dword 2 (it carries the check field).
+__device__ __forceinline__ uint32_t ip_chain(const uint32_t *w, uint32_t ihl, uint32_t w5)
+{
+	uint32_t s = w[3];
+	if (ihl <= 4u)
+		return s & 0xFFFFu;
+	uint64_t tt = (uint64_t)s + w[4];
+	s = (uint32_t)tt; uint32_t c = (uint32_t)(tt >> 32);
+	tt = (uint64_t)s + w5 + c; s = (uint32_t)tt; c = (uint32_t)(tt >> 32);
+	tt = (uint64_t)s + w[6] + c; s = (uint32_t)tt; c = (uint32_t)(tt >> 32);
+#pragma unroll
+	for (int k = 4; k < 15; k++) {
+		tt = (uint64_t)s + w[3 + k] + c;
+		if ((uint32_t)k < ihl) { s = (uint32_t)tt; c = (uint32_t)(tt >> 32); }
+	}
+	s += c;
+	const uint32_t a = (s >> 16) + (s & 0xFFFFu);
+	const uint32_t rr = (a & 0xFFFFu) + (a >> 16);
+	return (~rr) & 0xFFFFu;
+}
+
 // Parse + checks + IP checksum + RSS + in-window TCP sum.  Mirrors
 // ProcessPacket (eth_in.c:27) -> ProcessInIPv4Packet (ip_in.c:30) ->
 // ProcessInTCPPacket prefix (tcp.c:408-445); see oracle/mosrx_oracle.c.
+template <int VAR>
 __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uint32_t cap, bool active,
                                            uint32_t kflags, const uint32_t *s_tab)
 {
@@ -176,12 +204,14 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	const uint32_t ip_len = be16hi(w[3]);             // frame bytes 16,17  (ip_in.c:39)
 	const uint32_t proto = (w[5] >> 8) & 0xFFu;       // frame byte 23
 	const uint32_t saddr = w[6], daddr = w[7];        // raw network-order words
-	uint32_t th0 = 0, th3 = 0;                         // TCP header dwords 0 and 3 at iph + ihl*4
+	uint32_t th0 = 0, th3 = 0, tcw = 0;                // TCP header dwords 0 and 3 at iph + ihl*4
 #pragma unroll
 	for (int k = 0; k < 16; k++) {
 		if (ihl == (uint32_t)k) {
 			th0 = w[3 + k];
 			th3 = w[6 + k];
+			if (IS_TX(VAR))
+				tcw = w[7 + k] & 0xFFFFu;                  // tcph->check (frame bytes 30+4ihl, +1)
 		}
 	}
 	const bool is_tcp = (proto == 6u);
@@ -190,28 +220,9 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	const uint32_t split_abs = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
 	const uint32_t split = split_abs - o;              // frame byte 79..94
 
-	// ip_fast_csum (ip_in.h:10-38): 32-bit adc chain, final carry added once, fold, not.
-	uint32_t ipc;
-	{
-		uint32_t s = w[3];
-		if (ihl <= 4u) {
-			ipc = s & 0xFFFFu;
-		} else {
-			uint64_t tt = (uint64_t)s + w[4];
-			s = (uint32_t)tt; uint32_t c = (uint32_t)(tt >> 32);
-			tt = (uint64_t)s + w[5] + c; s = (uint32_t)tt; c = (uint32_t)(tt >> 32);
-			tt = (uint64_t)s + w[6] + c; s = (uint32_t)tt; c = (uint32_t)(tt >> 32);
-#pragma unroll
-			for (int k = 4; k < 15; k++) {
-				tt = (uint64_t)s + w[3 + k] + c;
-				if ((uint32_t)k < ihl) { s = (uint32_t)tt; c = (uint32_t)(tt >> 32); }
-			}
-			s += c;
-			const uint32_t a = (s >> 16) + (s & 0xFFFFu);
-			const uint32_t rr = (a & 0xFFFFu) + (a >> 16);
-			ipc = (~rr) & 0xFFFFu;
-		}
-	}
+	const uint32_t ipc = ip_chain(w, ihl, w[5]);
+	// TX: iph->check = 0 first (mos_api.c:1180-1181): the check is frame bytes 24,25 = w[5] bytes 2,3
+	const uint32_t ipc_tx = IS_TX(VAR) ? ip_chain(w, ihl, w[5] & 0xFFFFu) : 0u;
 
 	// TCP segment sum over frame bytes [14+4*ihl, min(fend, split)); the
 	// realigned grid (dword j = frame bytes [4j+2, 4j+6)) is the segment grid.
@@ -271,12 +282,24 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 			need_tcp = true;   // verdict decided after the tail sum
 		}
 	}
-	if (!active)
+	// TX (mtcp_setlastpkt's MOS_UPDATE_*_CHKSUM, mos_api.c:1177-1193): every
+	// untruncated IPv4 frame with a full header gets the IP check; TCP frames
+	// whose length covers the header also get the TCP check.
+	bool tx_ip = false;
+	if (IS_TX(VAR)) {
+		tx_ip = h_proto == 0x0800u && cap >= 34u && ihl >= 5u && 14u + ihl * 4u <= cap && fend <= cap &&
+		        !(is_tcp && 14u + ihl * 4u + 20u > cap);
+		need_tcp = tx_ip && is_tcp && ip_len >= (ihl + doff) * 4u && (kflags & MOSRX_KF_TX_TCP);
+	}
+	if (!active) {
 		need_tcp = false;
+		tx_ip = false;
+	}
 
 	h.o = o; h.fend = fend; h.split_abs = split_abs; h.wsum = wsum;
 	h.saddr = saddr; h.daddr = daddr; h.ip_len = ip_len; h.ihl = ihl; h.doff = doff; h.th0 = th0; h.th3 = th3;
 	h.rss = rss; h.queue = queue; h.ipc = ipc; h.reason = reason; h.verdict = verdict;
+	h.tcw = tcw; h.ipc_tx = ipc_tx; h.tx_ip = tx_ip;
 	h.fields = fields; h.need_tcp = need_tcp; h.has_tail = need_tcp && fend > split; h.is_tcp = is_tcp;
 	return h;
 }
@@ -344,6 +367,37 @@ __device__ __forceinline__ uint32_t flow_hash(const hdr_t &h)
 	return (h.fields && h.is_tcp) ? hash : 0u;
 }
 
+// TX: write the fresh checksums into the frame (little-endian u16 stores, as
+// `iph->check = ip_fast_csum(..)` and `tcph->check = TCPCalcChecksum(..)` do).
+// The TCP value is the full-segment sum with the old check word taken out in
+// one's-complement arithmetic: TCPCalcChecksum depends only on the sum mod
+// 0xFFFF (the sum is > 0: the pseudo header holds 0x0600).
+__device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffer_rsrc_t rs, const hdr_t &h,
+                                         uint32_t tail_sum)
+{
+	if (h.tx_ip && (kp.flags & MOSRX_KF_TX_IP)) {
+		__builtin_amdgcn_raw_buffer_store_b8((uint8_t)h.ipc_tx, rs, h.o + 24u, 0, 0);
+		__builtin_amdgcn_raw_buffer_store_b8((uint8_t)(h.ipc_tx >> 8), rs, h.o + 25u, 0, 0);
+	}
+	if (h.need_tcp) {
+		const uint32_t seglen = (h.ip_len - h.ihl * 4u) & 0xFFFFu;
+		uint32_t s = h.wsum + (h.saddr & 0xFFFFu) + (h.saddr >> 16) + (h.daddr & 0xFFFFu) + (h.daddr >> 16) +
+		             bswap16(seglen) + 0x0600u;
+		if (h.has_tail) {
+			const uint32_t ts = fold16(tail_sum);
+			s += (h.o & 1u) ? bswap16(ts) : ts;
+		}
+		s = (s >> 16) + (s & 0xFFFFu);
+		s += s >> 16;                                   // low 16 bits in [1, 0xFFFF], == S mod 0xFFFF
+		uint32_t v = (s & 0xFFFFu) + (0xFFFFu - h.tcw); // - old check word
+		v = (v & 0xFFFFu) + (v >> 16);
+		const uint32_t c = (~v) & 0xFFFFu;
+		const uint32_t at = h.o + 30u + 4u * h.ihl;
+		__builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, rs, at, 0, 0);
+		__builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), rs, at + 1u, 0, 0);
+	}
+}
+
 __device__ __forceinline__ void tables_to_lds(const mosrx_kparams &kp, uint32_t *s_tab, uint32_t *s_cnt, uint32_t t)
 {
 	if (t < 256) {                            // RSS nibble tables + queue LUT (2 KiB, L2-resident)
@@ -398,7 +452,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	hdr_win_t win;
 	hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
 	__syncthreads();   // s_tab, s_cnt ready
-	const hdr_t h = hdr_parse(win, o, cap, active, kp.flags, s_tab);
+	const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab);
 	if (h.has_tail) {
 		const uint32_t k = atomicAdd(&s_cnt[MOSRX_R_COUNT], 1u);
 		s_tail_pkt[k] = t;
@@ -436,10 +490,14 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 		}
 	}
 	__syncthreads();
-	if (active)
-		store_record(kp, p, hdr_finish(h, h.has_tail ? s_tail_sum[t] : 0u, kp.flags), s_cnt);
-	if (active && kp.fhash)
-		kp.fhash[p] = flow_hash(h);
+	if constexpr (IS_TX(VAR)) {
+		tx_store(kp, rs, h, h.has_tail ? s_tail_sum[t] : 0u);
+	} else {
+		if (active)
+			store_record(kp, p, hdr_finish(h, h.has_tail ? s_tail_sum[t] : 0u, kp.flags), s_cnt);
+		if (active && kp.fhash)
+			kp.fhash[p] = flow_hash(h);
+	}
 	flush_counters(kp, s_cnt, t);
 }
 
@@ -586,7 +644,7 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 			if (lane <= MOSRX_R_COUNT)
 				s_cnt[lane] = 0;
 		}
-		const hdr_t h = hdr_parse(win, o, cap, active, kp.flags, s_tab);
+		const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab);
 		__syncthreads();   // B: s_spec ready
 		uint32_t tail = h.has_tail ? s_spec[64u * sub + lane] : 0u;
 		// Bytes between the datagram end and the capture end (Ethernet padding of
@@ -604,7 +662,9 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 			if (lane == f)
 				tail -= s;
 		}
-		if (active) {
+		if constexpr (IS_TX(VAR)) {
+			tx_store(kp, rs, h, tail);
+		} else if (active) {
 			store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 			if (kp.fhash)
 				kp.fhash[p] = flow_hash(h);
@@ -767,10 +827,10 @@ extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int vari
 	if (kind < 0 || kind > MOSRX_KIND_MID)
 		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-	static void (*const tab[3][2])(const mosrx_kparams *, hipStream_t) = {
-		{launch_v<MOSRX_KIND_SMALL, 0>, launch_v<MOSRX_KIND_SMALL, 2>},
-		{launch_v<MOSRX_KIND_LARGE, 0>, launch_v<MOSRX_KIND_LARGE, 2>},
-		{launch_v<MOSRX_KIND_MID, 0>, launch_v<MOSRX_KIND_MID, 2>}};
-	tab[kind][(variant >> 1) & 1](kp, s);
+	static void (*const tab[3][3])(const mosrx_kparams *, hipStream_t) = {
+		{launch_v<MOSRX_KIND_SMALL, 0>, launch_v<MOSRX_KIND_SMALL, 2>, launch_v<MOSRX_KIND_SMALL, 2 | VAR_TX>},
+		{launch_v<MOSRX_KIND_LARGE, 0>, launch_v<MOSRX_KIND_LARGE, 2>, launch_v<MOSRX_KIND_LARGE, 2 | VAR_TX>},
+		{launch_v<MOSRX_KIND_MID, 0>, launch_v<MOSRX_KIND_MID, 2>, launch_v<MOSRX_KIND_MID, 2 | VAR_TX>}};
+	tab[kind][(kp->flags & (MOSRX_KF_TX_IP | MOSRX_KF_TX_TCP)) ? 2 : (variant >> 1) & 1](kp, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -54,6 +54,7 @@ class Batch(C.Structure):
 
 BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])   # mosrx_bpf_insn
 BPF_LEN_FRAME, BPF_LEN_IP = 0, 1
+TX_IP_CSUM, TX_TCP_CSUM = 1 << 4, 1 << 5   # MOS_UPDATE_IP_CHKSUM / MOS_UPDATE_TCP_CHKSUM
 BPF_MAX_PROGS = 32
 
 
@@ -133,6 +134,8 @@ def lib():
             "mosrx_time_queue": (I, [P, C.POINTER(P), U32, U32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
             "mosrx_time_host": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_rss_tables": (I, [C.c_char_p, U32, C.POINTER(U32)]),
+            "mosrx_tx_csum_dev": (I, [P, C.POINTER(Batch), I, P]),
+            "mosrx_tx_csum_host": (I, [P, C.POINTER(Batch), I]),
             "mosrx_bpf_check": (I, [P, U32]),
             "mosrx_bpf_set": (I, [P, C.POINTER(BpfProg), U32]),
             "mosrx_bpf_dev": (I, [P, C.POINTER(Batch), P, P]),
@@ -259,6 +262,11 @@ class DevBatch:
             self.d_out.download(out)
         return out
 
+    def frames(self, nbytes: int | None = None) -> np.ndarray:
+        """The frame buffer as it is now in HBM (e.g. after tx_csum_dev)."""
+        out = np.zeros(self.frames_bytes if nbytes is None else nbytes, np.uint8)
+        return self.d_frames.download(out)
+
     def matches(self) -> np.ndarray:
         out = np.zeros(self.n, np.uint32)
         if self.n:
@@ -328,6 +336,23 @@ class Context:
         _chk(lib().mosrx_classify_host_fh(self.handle, C.byref(b), out.ctypes.data, fh.ctypes.data),
              "mosrx_classify_host_fh")
         return out, fh
+
+    # ---- TX checksum rewrite (mosrx_tx_csum_*) ----
+    def tx_csum_host(self, frames, off, ln, flags=TX_IP_CSUM | TX_TCP_CSUM, frames_bytes=None) -> np.ndarray:
+        """A rewritten copy of `frames` (the input array is left as it is)."""
+        out = np.array(frames, np.uint8, copy=True)
+        off = np.ascontiguousarray(off, np.uint32)
+        ln = np.ascontiguousarray(ln, np.uint16)
+        b = Batch(out.ctypes.data, int(frames_bytes if frames_bytes is not None else len(out)),
+                  off.ctypes.data, ln.ctypes.data, len(off), 0)
+        _chk(lib().mosrx_tx_csum_host(self.handle, C.byref(b), flags), "mosrx_tx_csum_host")
+        return out
+
+    def tx_csum_dev(self, db: "DevBatch", flags=TX_IP_CSUM | TX_TCP_CSUM, sync: bool = True) -> None:
+        b = db.batch()
+        _chk(lib().mosrx_tx_csum_dev(self.handle, C.byref(b), flags, None), "mosrx_tx_csum_dev")
+        if sync:
+            _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
 
     # ---- batched BPF (mosrx_bpf_*) ----
     def bpf_set(self, progs) -> None:

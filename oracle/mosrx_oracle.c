@@ -215,6 +215,44 @@ int mo_classify_fh(const mosrx_params *p, const uint8_t *frames, uint64_t frames
 	return 0;
 }
 
+/* TX checksum rewrite, mtcp_setlastpkt's MOS_UPDATE_IP_CHKSUM /
+ * MOS_UPDATE_TCP_CHKSUM branch (mos_api.c:1177-1193), IP first as there, on
+ * the frames include/mosrx.h defines for mosrx_tx_csum_dev.  In place. */
+int mo_tx_csum(uint8_t *frames, uint64_t frames_bytes, const uint32_t *off, const uint16_t *len, uint32_t n,
+               int flags)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++) {
+		uint8_t *f = frames + off[i], *iph = f + 14, *th;
+		uint32_t cap = (off[i] >= frames_bytes) ? 0 : (uint32_t)(frames_bytes - off[i] < len[i] ? frames_bytes - off[i] : len[i]);
+		unsigned ihl, ip_len, doff;
+		uint32_t saddr, daddr;
+		if (cap < 34 || f[12] != 0x08 || f[13] != 0x00)
+			continue;
+		ihl = iph[0] & 0xF;
+		ip_len = be16(iph + 2);
+		if (ihl < 5 || 14 + ihl * 4 > cap || 14 + ip_len > cap || (iph[9] == 6 && 14 + ihl * 4 + 20 > cap))
+			continue;
+		if (flags & MOSRX_TX_IP_CSUM) {
+			uint16_t v;
+			iph[10] = iph[11] = 0;
+			v = mo_ip_fast_csum(iph, ihl);
+			memcpy(iph + 10, &v, 2);
+		}
+		th = iph + ihl * 4;
+		doff = th[12] >> 4;
+		if ((flags & MOSRX_TX_TCP_CSUM) && iph[9] == 6 && ip_len >= (ihl + doff) * 4) {
+			uint16_t v;
+			memcpy(&saddr, iph + 12, 4);
+			memcpy(&daddr, iph + 16, 4);
+			th[16] = th[17] = 0;
+			v = mo_tcp_csum(th, (uint16_t)(ip_len - ihl * 4), saddr, daddr);
+			memcpy(th + 16, &v, 2);
+		}
+	}
+	return 0;
+}
+
 void mo_params_default(mosrx_params *p)
 {
 	memset(p, 0, sizeof(*p));

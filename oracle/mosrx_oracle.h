@@ -52,6 +52,10 @@ int      mo_bpf_returns(const mosrx_bpf_insn *insns, uint32_t ninsn, int len_mod
 int      mo_bpf_eval(const mosrx_bpf_prog *progs, uint32_t nprog, const uint8_t *frames, uint64_t frames_bytes,
                      const uint32_t *off, const uint16_t *len, uint32_t n, uint32_t *out);
 
+/* TX checksum rewrite of mosrx_tx_csum_dev (mos_api.c:1177-1193), in place. */
+int mo_tx_csum(uint8_t *frames, uint64_t frames_bytes, const uint32_t *off, const uint16_t *len, uint32_t n,
+               int flags);
+
 /* ProcessPacket (eth_in.c:27-87) through the TCP prefix (tcp.c:408-445) plus
  * the RSS hash/queue, for one frame.  Fills all 16 bytes of *r. */
 void mo_classify_one(const mosrx_params *p, const uint32_t cache[96],

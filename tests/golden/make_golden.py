@@ -167,6 +167,33 @@ def run_states(frames: list[bytes], name: str, phase: int = 2):
     print(f"{name}: {len(frames)} frames, {len(buf)} bytes")
 
 
+def tx_fixture(frames: list[bytes], name: str, phase: int):
+    """TX checksum rewrite vectors (mos_api.c:1177-1193).  The check fields are
+    zeroed first, as mtcp_setlastpkt does, and mOS's compiled path is run on
+    those frames: its ip_fast_csum / TCPCalcChecksum outputs are exactly the
+    values the rewrite stores.  Stored per frame: whether each check is
+    rewritten and the reference's value; the inputs keep their old checks."""
+    buf, off, ln = pack_frames(frames, phase=phase)
+    z = buf.copy()
+    for o, n in zip(off.tolist(), ln.tolist()):
+        f = z[o:o + n]
+        if n < 34 or f[12] != 0x08 or f[13] != 0x00 or (f[14] & 0xF) < 5:
+            continue
+        ihl = f[14] & 0xF
+        f[24:26] = 0
+        if f[23] == 6 and 14 + ihl * 4 + 18 <= n:
+            f[14 + ihl * 4 + 16:14 + ihl * 4 + 18] = 0
+    rec, _ = O.run_ref(z, off, ln, num_msp=1)
+    ihl = np.array([z[o + 14] & 0xF if n > 14 else 0 for o, n in zip(off.tolist(), ln.tolist())])
+    ipv4 = np.array([n >= 34 and z[o + 12] == 8 and z[o + 13] == 0 for o, n in zip(off.tolist(), ln.tolist())])
+    live = (rec["have"] & 8) == 0
+    ip_w = live & ipv4 & (ihl >= 5)
+    tcp_w = ip_w & ((rec["have"] & 2) != 0)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), frames=buf, off=off, len=ln,
+                        ip_w=ip_w, ip_check=rec["ip_csum"], tcp_w=tcp_w, tcp_check=rec["tcp_csum"])
+    print(f"{name}: {len(frames)} frames, {ip_w.sum()} IP / {tcp_w.sum()} TCP rewrites")
+
+
 def main():
     if not O.have_ref():
         sys.exit("oracle/_ref/mosref missing: run `make -C oracle ref` first (needs /root/reference)")
@@ -175,6 +202,9 @@ def main():
     run_states(random_frames(rng, 256, 0), "rand_small")
     run_states(random_frames(rng, 256, 1), "rand_mid", phase=7)   # odd frame starts: byte-swap path
     run_states(random_frames(rng, 256, 2), "rand_large")
+    txr = random.Random(0x7C5)
+    tx_fixture(edge_frames() + random_frames(txr, 200, 0) + random_frames(txr, 100, 1), "tx_mixed", phase=2)
+    tx_fixture(random_frames(txr, 120, 2) + random_frames(txr, 60, 0), "tx_odd", phase=7)
     # MSDN Toeplitz vectors (util/rss.c:177-193), Microsoft key (util/rss.c:75-81)
     kat = np.array([
         (0x420995bb, 0xa18e6450, 2794, 1766, 0x51ccc178),

@@ -74,6 +74,8 @@ def lib():
         L.mo_bpf_filter.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_uint32]
         L.mo_bpf_validate.restype = C.c_int
         L.mo_bpf_validate.argtypes = [C.c_void_p, C.c_int]
+        L.mo_tx_csum.restype = C.c_int
+        L.mo_tx_csum.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_int]
         L.mo_bpf_returns.restype = C.c_int
         L.mo_bpf_returns.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_void_p, C.c_uint64, C.c_void_p,
                                      C.c_void_p, C.c_uint32, C.c_void_p]
@@ -117,6 +119,15 @@ def classify_fh(buf, off, ln, p: Params | None = None):
     if rc:
         raise OSError(-rc, "mo_classify_fh failed")
     return out, fh
+
+
+def tx_csum(buf, off, ln, flags: int) -> np.ndarray:
+    """A rewritten copy of `buf` (mo_tx_csum: the MOS_UPDATE_*_CHKSUM rewrite)."""
+    out = np.array(buf, np.uint8, copy=True)
+    off = np.ascontiguousarray(off, np.uint32)
+    ln = np.ascontiguousarray(ln, np.uint16)
+    lib().mo_tx_csum(out.ctypes.data, len(out), off.ctypes.data, ln.ctypes.data, len(off), flags)
+    return out
 
 
 def have_ref() -> bool:

@@ -1,0 +1,100 @@
+"""TX checksum rewrite: mtcp_setlastpkt's MOS_UPDATE_IP_CHKSUM /
+MOS_UPDATE_TCP_CHKSUM (mos_api.c:1177-1193) over a batch, on the GPU.
+
+tests/golden/tx_*.npz hold, per frame, whether each check is rewritten and the
+value mOS's own compiled ip_fast_csum / TCPCalcChecksum give after the check
+fields are zeroed (tests/golden/make_golden.py).  The inputs keep their old
+(valid, corrupted or random) checks, so the zeroing step is exercised too.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import mosrx
+import oracle_py as O
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+FIXTURES = ["tx_mixed", "tx_odd"]
+IP, TCP = mosrx.TX_IP_CSUM, mosrx.TX_TCP_CSUM
+FLAGS = [IP | TCP, IP, TCP]
+
+
+def expected(z, flags):
+    out = z["frames"].copy()
+    for i, (o, n) in enumerate(zip(z["off"].tolist(), z["len"].tolist())):
+        ihl = int(out[o + 14] & 0xF) if n > 14 else 0
+        if (flags & IP) and z["ip_w"][i]:
+            out[o + 24:o + 26] = np.frombuffer(np.uint16(z["ip_check"][i]).tobytes(), np.uint8)
+        if (flags & TCP) and z["tcp_w"][i]:
+            at = o + 30 + 4 * ihl
+            out[at:at + 2] = np.frombuffer(np.uint16(z["tcp_check"][i]).tobytes(), np.uint8)
+    return out
+
+
+@pytest.mark.parametrize("fix", FIXTURES)
+@pytest.mark.parametrize("flags", FLAGS)
+def test_oracle_tx_matches_reference(fix, flags):
+    z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
+    np.testing.assert_array_equal(O.tx_csum(z["frames"], z["off"], z["len"], flags), expected(z, flags))
+
+
+def test_tx_fixture_coverage():
+    z = np.load(os.path.join(GOLDEN, "tx_mixed.npz"))
+    # rewrites, untouched frames, and inputs whose old checks were wrong all occur
+    assert 0 < z["tcp_w"].sum() < z["ip_w"].sum() < len(z["off"])
+    after = O.tx_csum(z["frames"], z["off"], z["len"], IP | TCP)
+    assert (after != z["frames"]).any()
+
+
+def test_tx_rewritten_frames_verify():
+    # property: every rewritten TCP frame then passes mOS's checks (TCP_OK) in the oracle
+    z = np.load(os.path.join(GOLDEN, "tx_mixed.npz"))
+    after = O.tx_csum(z["frames"], z["off"], z["len"], IP | TCP)
+    res = O.classify(after, z["off"], z["len"], O.params(forward=0))
+    ok = z["tcp_w"] & (res["reason"] != mosrx.R["IP_BADVER"]) & (res["reason"] != mosrx.R["IP_SHORT"])
+    assert np.all(res["reason"][ok] == mosrx.R["TCP_OK"])
+
+
+# ---------------------------------------------------------------- GPU parity
+@pytest.mark.gpu
+@pytest.mark.parametrize("fix", FIXTURES)
+@pytest.mark.parametrize("flags", FLAGS)
+def test_tx_golden(gpu_ctx, fix, flags):
+    z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
+    exp = expected(z, flags)
+    np.testing.assert_array_equal(gpu_ctx.tx_csum_host(z["frames"], z["off"], z["len"], flags), exp)
+    db = gpu_ctx.upload(z["frames"], z["off"], z["len"])
+    gpu_ctx.tx_csum_dev(db, flags)
+    np.testing.assert_array_equal(db.frames(len(z["frames"])), exp)
+    db.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [6, 10, 14])
+@pytest.mark.parametrize("fix", FIXTURES)
+def test_tx_forced_shapes(gpu_ctx, variant, fix):
+    z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
+    gpu_ctx.set_variant(variant)
+    try:
+        got = gpu_ctx.tx_csum_host(z["frames"], z["off"], z["len"], IP | TCP)
+    finally:
+        gpu_ctx.set_variant(2)
+    np.testing.assert_array_equal(got, expected(z, IP | TCP))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n", [(mosrx.TRACE_S64, 32_768), (mosrx.TRACE_M1500, 65_536),
+                                    (mosrx.TRACE_IMIX, 262_144)])
+def test_tx_full_size_traces(gpu_ctx, kind, n):
+    t = mosrx.Trace(kind, n)
+    exp = O.tx_csum(t.frames, t.off, t.len, IP | TCP)
+    db = gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len)
+    gpu_ctx.tx_csum_dev(db)
+    got = db.frames(len(t.frames))
+    np.testing.assert_array_equal(got, exp)
+    # size-independent property: the generator's corrupted frames (1/1024 IP, 1/1024 TCP) are repaired
+    gpu_ctx.set_params(mosrx.default_params())
+    gpu_ctx.classify_dev(db)
+    assert np.all(db.results()["reason"] == mosrx.R["TCP_OK"])
+    db.free()

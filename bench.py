@@ -44,7 +44,16 @@ WORKLOADS = {
     "S64_hdr": (mosrx.TRACE_S64, 32_768, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum)"),
     "IMIX": (mosrx.TRACE_IMIX, 262_144, "IMIX 60/590/1514 7:4:1, 1M flows, batch=256K (BASELINE config #4)"),
     "S64_queue": (mosrx.TRACE_S64, 32_768, "config #2, 64 batches of 32K per launch (device batch queue)"),
+    # SURVEY.md §8f rows measured on the same traces
+    "M1500_fh": (mosrx.TRACE_M1500, 65_536, "config #3 classify + flow-table hash (HashFlow of FindStream's tuple)"),
+    "M1500_tx": (mosrx.TRACE_M1500, 65_536, "config #3 TX checksum rewrite (MOS_UPDATE_IP|TCP_CHKSUM), in place"),
+    "IMIX_bpf": (mosrx.TRACE_IMIX, 262_144, "config #4 batched BPF, 8 mOS filter programs (sfbpf_compile output)"),
 }
+OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_tx": mosrx.OP_TX_CSUM, "IMIX_bpf": mosrx.OP_BPF}
+# filter expressions whose compiled programs (tests/golden/bpf.npz, mOS's own compiler) the BPF row runs
+BPF_BENCH = [("tcp", 0), ("tcp port 80", 0), ("tcp[tcpflags] & tcp-syn != 0", 1), ("net 192.168.0.0/16 and tcp", 1),
+             ("host 10.0.0.1 and port 80", 0), ("ip[8] < 64", 1), ("tcp[((tcp[12:1] & 0xf0) >> 2):4] = 0x47455420", 1),
+             ("portrange 1000-2000", 0)]
 QUEUE_DEPTH = 64
 STREAMS = 2   # rx batches in flight per GPU (scripts/tune_streams.py: 2 beats 1 and 4)
 
@@ -84,9 +93,27 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def algo_bytes(tr: mosrx.Trace) -> int:
-    """B_i = caplen_i + 6 (offset+len descriptor) + 16 (result record)."""
-    return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES)
+def algo_bytes(tr: mosrx.Trace, key: str = "") -> int:
+    """B_i = caplen_i + 6 (offset+len descriptor) + 16 (result record).
+    Flow hash: + 4 B per frame.  TX rewrite: caplen + 6 read, 4 B written (no records).
+    BPF: the 6-byte descriptor + 4-byte mask + 64 header bytes per frame (the
+    line a filter reads; deeper loads are extra)."""
+    if key.endswith("_tx"):
+        return tr.caplen_sum + tr.n * (DESC_BYTES + 4)
+    if key.endswith("_bpf"):
+        return tr.n * (DESC_BYTES + 4) + int(np.minimum(tr.len, 64).astype(np.int64).sum())
+    extra = 4 if key.endswith("_fh") else 0
+    return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES + extra)
+
+
+def bpf_bench_programs():
+    z = np.load(os.path.join(ROOT, "tests", "golden", "bpf.npz"))
+    names = [str(x) for x in z["names"]]
+    progs = []
+    for expr, mode in BPF_BENCH:
+        j = names.index(expr)
+        progs.append((z["insns"][z["prog_off"][j]:z["prog_off"][j] + z["prog_len"][j]], mode))
+    return progs
 
 
 def load_pmc(key: str):
@@ -110,8 +137,24 @@ def measure(ctx, dist, key, steps, warmup, rank):
     ncopy = min(ncopy, 256)
     dbs = [ctx.upload(tr.frames, tr.off, tr.len, frames_bytes=tr.frames_bytes, max_len=tr.max_len)
            for _ in range(ncopy)]
-    ab = algo_bytes(tr)
-    if key.endswith("_queue"):
+    ab = algo_bytes(tr, key)
+    if key in OPS:
+        op = OPS[key]
+        arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op == mosrx.OP_TX_CSUM else 0
+        if op == mosrx.OP_BPF:
+            ctx.bpf_set(bpf_bench_programs())
+        if warmup:
+            ctx.time_op(op, dbs, warmup, STREAMS, arg, kernels=False)
+        ctx.device_sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        dev_ms, _ = ctx.time_op(op, dbs, steps, STREAMS, arg, kernels=False)
+        ctx.device_sync()
+        dist.barrier()
+        wall = time.perf_counter() - t0
+        wall_max = dist.max(wall)
+        _, kern_ms = ctx.time_op(op, dbs, min(steps, 200), 1, arg, total=False)
+    elif key.endswith("_queue"):
         # each step = one launch over QUEUE_DEPTH distinct resident 32K batches
         # several queues over disjoint batch copies: the working set exceeds the L3
         qs = [ctx.queue(dbs[i:i + QUEUE_DEPTH]) for i in range(0, len(dbs) - QUEUE_DEPTH + 1, QUEUE_DEPTH)]
@@ -185,9 +228,12 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
     p = O.params(skip_tcp_csum=1 if key == "S64_hdr" else 0)
-    ab = algo_bytes(tr)
+    ab = algo_bytes(tr, key)
     cores_avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     cores_all = max(1, min(16, cores_avail))
+
+    if key in OPS:
+        return cpu_baseline_row(tr, key, min_s, O)
 
     def run(nt):
         reps, t0 = 0, time.perf_counter()
@@ -218,6 +264,28 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0):
     }
 
 
+def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
+    """The oracle for a §8f row (flow hash / TX rewrite / BPF), one thread."""
+    ab = algo_bytes(tr, key)
+    progs = bpf_bench_programs() if key.endswith("_bpf") else None
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        if key.endswith("_fh"):
+            O.classify_fh(tr.frames, tr.off, tr.len, O.params())
+        elif key.endswith("_tx"):
+            O.tx_csum(tr.frames, tr.off, tr.len, mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM)
+        else:
+            O.bpf_eval(progs, tr.frames, tr.off, tr.len)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= min_s:
+            break
+    fn = {"_fh": "mo_classify_fh", "_tx": "mo_tx_csum", "bpf": "mo_bpf_eval"}[key[-3:]]
+    return {"value": round(reps * ab / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "mpkts": round(reps * tr.n / el / 1e6, 3),
+            "sample": f"{reps} passes over one {tr.n}-frame batch ({el:.1f} s), oracle {fn}, 1 thread"}
+
+
 def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
     """End-to-end host->HBM->host rate (pinned staging, 2 slots); recorded in DESIGN.md."""
     ctx.set_params(mosrx.default_params())
@@ -245,14 +313,18 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
 
 
 def main():
+    global STREAMS
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workloads", default="M1500,S64,S64_hdr,S64_queue,IMIX")
+    ap.add_argument("--workloads", default="M1500,S64,S64_hdr,S64_queue,IMIX,M1500_fh,M1500_tx,IMIX_bpf")
+    ap.add_argument("--streams", type=int, default=STREAMS,
+                    help="rx batches in flight (1 = strictly serial launches, as for rocprof summaries)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (PCIe) leg")
     args = ap.parse_args()
+    STREAMS = args.streams
 
     ws, rank, local = dist_env()
     if ws != args.gpus:
@@ -274,7 +346,7 @@ def main():
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
         head = "M1500" if "M1500" in traces else keys[0]
-        cpu = cpu_baseline(traces[head], head)
+        cpu = cpu_baseline(traces[head], head, min_s=10.0)
         for k in keys:
             if k != head:
                 results[k]["cpu_baseline"] = cpu_baseline(traces[k], k, min_s=2.0)
@@ -301,6 +373,7 @@ def main():
         "config": {"workload": h["workload"], "batch": h["batch"],
                    "algo_bytes_per_batch": h["algo_bytes_per_batch"],
                    "parallelism": f"replicas x{ws}: batches round-robin per GPU, no collectives",
+                   "streams_per_gpu": STREAMS,
                    "resident_copies": h["resident_copies"]},
         "roofline": h["roofline"],
         "cpu_baseline": cpu,

@@ -201,6 +201,14 @@ int  mosrx_time_dev_streams(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
  * by its own pair of HIP events on the stream it runs on (the roofline figure). */
 int  mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
                             mosrx_result *const *d_out, uint32_t iters, float *avg_ms);
+/* The same two measurements for any row of the path: `op` over batch i % nb
+ * on stream i % nstreams (total_ms), and the average single-launch duration on
+ * the context stream (avg_kernel_ms); either pointer may be NULL.  out[i]:
+ * records (CLASSIFY, CLASSIFY_FH), match masks (BPF), unused (TX_CSUM, `arg`
+ * = its flags); aux[i]: flow hashes (CLASSIFY_FH). */
+enum { MOSRX_OP_CLASSIFY = 0, MOSRX_OP_CLASSIFY_FH = 1, MOSRX_OP_BPF = 2, MOSRX_OP_TX_CSUM = 3 };
+int  mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
+                   void *const *aux, uint32_t iters, uint32_t nstreams, float *total_ms, float *avg_kernel_ms);
 /* The device's streaming-read ceiling: `iters` coalesced 16-byte-load passes
  * cycling over `nbuf` buffers of `bytes` each (sized past the 256 MiB Infinity
  * Cache), in GB/s.  The roofline figure next to the 8 TB/s spec peak. */

@@ -594,16 +594,60 @@ int mosrx_time_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_resul
 	return 0;
 }
 
-int mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
-                           uint32_t iters, float *avg_ms)
+/* One enqueue of operation `op` on batch b (see mosrx_time_op). */
+static int run_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, void *out, void *aux, hipStream_t s)
+{
+	switch (op) {
+	case MOSRX_OP_CLASSIFY: return mosrx_classify_dev(c, b, (mosrx_result *)out, s);
+	case MOSRX_OP_CLASSIFY_FH: return mosrx_classify_dev_fh(c, b, (mosrx_result *)out, (uint32_t *)aux, s);
+	case MOSRX_OP_BPF: return mosrx_bpf_dev(c, b, (uint32_t *)out, s);
+	case MOSRX_OP_TX_CSUM: return mosrx_tx_csum_dev(c, b, arg, s);
+	default: return -EINVAL;
+	}
+}
+
+static int time_streams(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
+                        void *const *aux, uint32_t iters, uint32_t nstreams, float *ms)
+{
+	hipStream_t st[MOSRX_MAX_STREAMS];
+	hipEvent_t done[MOSRX_MAX_STREAMS];
+	uint32_t i, k, made = 0;
+	int rc = 0;
+	for (k = 0; k < nstreams && !rc; k++, made++)
+		if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess ||
+		    hipEventCreateWithFlags(&done[k], hipEventDisableTiming) != hipSuccess)
+			rc = -EIO;
+	if (!rc && hipEventRecord(c->ev0, c->stream) != hipSuccess)
+		rc = -EIO;
+	for (k = 0; k < nstreams && !rc; k++)
+		if (hipStreamWaitEvent(st[k], c->ev0, 0) != hipSuccess)
+			rc = -EIO;
+	/* batch i on stream i % nstreams: independent batches overlap their
+	 * launch/drain phases the way several rx queues would */
+	for (i = 0; i < iters && !rc; i++)
+		rc = run_op(c, op, arg, &b[i % nb], out ? out[i % nb] : NULL, aux ? aux[i % nb] : NULL,
+		            st[i % nstreams]);
+	for (k = 0; k < nstreams && !rc; k++)
+		if (hipEventRecord(done[k], st[k]) != hipSuccess || hipStreamWaitEvent(c->stream, done[k], 0) != hipSuccess)
+			rc = -EIO;
+	if (!rc && (hipEventRecord(c->ev1, c->stream) != hipSuccess || hipEventSynchronize(c->ev1) != hipSuccess ||
+	            hipEventElapsedTime(ms, c->ev0, c->ev1) != hipSuccess))
+		rc = -EIO;
+	hipDeviceSynchronize();
+	for (k = 0; k < made; k++) {
+		hipStreamDestroy(st[k]);
+		hipEventDestroy(done[k]);
+	}
+	return rc;
+}
+
+static int time_kernels(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
+                        void *const *aux, uint32_t iters, float *avg_ms)
 {
 	hipEvent_t *ev;
 	uint32_t i;
 	int rc = 0;
 	double tot = 0;
-	if (!c || !b || !d_out || !avg_ms || nb == 0 || iters == 0)
-		return -EINVAL;
-	HIPCHK(hipSetDevice(c->device));
 	ev = calloc((size_t)iters * 2, sizeof(*ev));
 	if (!ev)
 		return -ENOMEM;
@@ -612,7 +656,7 @@ int mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosr
 			rc = -EIO;
 	for (i = 0; i < iters && !rc; i++) {
 		if (hipEventRecord(ev[2 * i], c->stream) != hipSuccess) { rc = -EIO; break; }
-		if ((rc = mosrx_classify_dev(c, &b[i % nb], d_out[i % nb], c->stream)))
+		if ((rc = run_op(c, op, arg, &b[i % nb], out ? out[i % nb] : NULL, aux ? aux[i % nb] : NULL, c->stream)))
 			break;
 		if (hipEventRecord(ev[2 * i + 1], c->stream) != hipSuccess) { rc = -EIO; break; }
 	}
@@ -632,41 +676,36 @@ int mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosr
 	return rc;
 }
 
+int mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
+                  void *const *aux, uint32_t iters, uint32_t nstreams, float *total_ms, float *avg_kernel_ms)
+{
+	int rc;
+	if (!c || !b || nb == 0 || iters == 0 || nstreams == 0 || nstreams > MOSRX_MAX_STREAMS ||
+	    op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_TX_CSUM || (op != MOSRX_OP_TX_CSUM && !out) ||
+	    (op == MOSRX_OP_CLASSIFY_FH && !aux))
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	if (total_ms && (rc = time_streams(c, op, arg, b, nb, out, aux, iters, nstreams, total_ms)))
+		return rc;
+	if (avg_kernel_ms && (rc = time_kernels(c, op, arg, b, nb, out, aux, iters, avg_kernel_ms)))
+		return rc;
+	return 0;
+}
+
+int mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
+                           uint32_t iters, float *avg_ms)
+{
+	if (!avg_ms)
+		return -EINVAL;
+	return mosrx_time_op(c, MOSRX_OP_CLASSIFY, 0, b, nb, (void *const *)d_out, NULL, iters, 1, NULL, avg_ms);
+}
+
 int mosrx_time_dev_streams(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
                            uint32_t iters, uint32_t nstreams, float *ms)
 {
-	hipStream_t st[MOSRX_MAX_STREAMS];
-	hipEvent_t done[MOSRX_MAX_STREAMS];
-	uint32_t i, k, made = 0;
-	int rc = 0;
-	if (!c || !b || !d_out || !ms || nb == 0 || nstreams == 0 || nstreams > MOSRX_MAX_STREAMS)
+	if (!ms)
 		return -EINVAL;
-	HIPCHK(hipSetDevice(c->device));
-	for (k = 0; k < nstreams && !rc; k++, made++)
-		if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess ||
-		    hipEventCreateWithFlags(&done[k], hipEventDisableTiming) != hipSuccess)
-			rc = -EIO;
-	if (!rc && hipEventRecord(c->ev0, c->stream) != hipSuccess)
-		rc = -EIO;
-	for (k = 0; k < nstreams && !rc; k++)
-		if (hipStreamWaitEvent(st[k], c->ev0, 0) != hipSuccess)
-			rc = -EIO;
-	/* batch i on stream i % nstreams: independent batches overlap their
-	 * launch/drain phases the way several rx queues would */
-	for (i = 0; i < iters && !rc; i++)
-		rc = mosrx_classify_dev(c, &b[i % nb], d_out[i % nb], st[i % nstreams]);
-	for (k = 0; k < nstreams && !rc; k++)
-		if (hipEventRecord(done[k], st[k]) != hipSuccess || hipStreamWaitEvent(c->stream, done[k], 0) != hipSuccess)
-			rc = -EIO;
-	if (!rc && (hipEventRecord(c->ev1, c->stream) != hipSuccess || hipEventSynchronize(c->ev1) != hipSuccess ||
-	            hipEventElapsedTime(ms, c->ev0, c->ev1) != hipSuccess))
-		rc = -EIO;
-	hipDeviceSynchronize();
-	for (k = 0; k < made; k++) {
-		hipStreamDestroy(st[k]);
-		hipEventDestroy(done[k]);
-	}
-	return rc;
+	return mosrx_time_op(c, MOSRX_OP_CLASSIFY, 0, b, nb, (void *const *)d_out, NULL, iters, nstreams, ms, NULL);
 }
 
 int mosrx_probe_read_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, float *gbps)

@@ -55,6 +55,7 @@ class Batch(C.Structure):
 BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])   # mosrx_bpf_insn
 BPF_LEN_FRAME, BPF_LEN_IP = 0, 1
 TX_IP_CSUM, TX_TCP_CSUM = 1 << 4, 1 << 5   # MOS_UPDATE_IP_CHKSUM / MOS_UPDATE_TCP_CHKSUM
+OP_CLASSIFY, OP_CLASSIFY_FH, OP_BPF, OP_TX_CSUM = 0, 1, 2, 3
 BPF_MAX_PROGS = 32
 
 
@@ -126,6 +127,8 @@ def lib():
             "mosrx_time_dev": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_time_dev_kernels": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_device_sync": (I, [P]),
+            "mosrx_time_op": (I, [P, I, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P), U32, U32,
+                                  C.POINTER(C.c_float), C.POINTER(C.c_float)]),
             "mosrx_time_dev_streams": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, U32, C.POINTER(C.c_float)]),
             "mosrx_probe_read_bw": (I, [P, U64, U32, U32, C.POINTER(C.c_float)]),
             "mosrx_queue_create": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
@@ -410,6 +413,24 @@ class Context:
         ms = C.c_float()
         _chk(lib().mosrx_time_dev(self.handle, bs, len(dbs), outs, iters, C.byref(ms)), "mosrx_time_dev")
         return float(ms.value)
+
+    def time_op(self, op: int, dbs: list[DevBatch], iters: int, nstreams: int = 1, arg: int = 0,
+                total: bool = True, kernels: bool = True):
+        """mosrx_time_op: (total ms over `iters` launches on `nstreams` streams,
+        average single-launch ms); either is None when not requested."""
+        for d in dbs:
+            if op == OP_CLASSIFY_FH and d.d_fhash is None:
+                d.d_fhash = DevBuffer(self, max(d.n * 4, 4))
+            if op == OP_BPF and d.d_match is None:
+                d.d_match = DevBuffer(self, max(d.n * 4, 4))
+        bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
+        outs = (C.c_void_p * len(dbs))(*[(d.d_match.ptr if op == OP_BPF else d.d_out.ptr) for d in dbs])
+        aux = (C.c_void_p * len(dbs))(*[(d.d_fhash.ptr if d.d_fhash else None) for d in dbs])
+        tot, avg = C.c_float(), C.c_float()
+        _chk(lib().mosrx_time_op(self.handle, op, arg, bs, len(dbs), outs, aux, iters, nstreams,
+                                 C.byref(tot) if total else None, C.byref(avg) if kernels else None),
+             "mosrx_time_op")
+        return (float(tot.value) if total else None), (float(avg.value) if kernels else None)
 
     def time_dev_streams(self, dbs: list[DevBatch], iters: int, nstreams: int) -> float:
         """Total ms for `iters` launches spread round-robin over `nstreams` streams."""

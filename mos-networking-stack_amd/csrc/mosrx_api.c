@@ -216,6 +216,11 @@ void mosrx_close(mosrx_ctx *c)
 	}
 	if (c->d_tables) hipFree(c->d_tables);
 	if (c->d_bpf) hipFree(c->d_bpf);
+	for (i = 0; i < (int)c->nxs; i++) {
+		hipStreamSynchronize(c->xs[i]);
+		hipStreamDestroy(c->xs[i]);
+		hipEventDestroy(c->xdone[i]);
+	}
 	if (c->ev0) hipEventDestroy(c->ev0);
 	if (c->ev1) hipEventDestroy(c->ev1);
 	if (c->stream) hipStreamDestroy(c->stream);
@@ -606,39 +611,46 @@ static int run_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, void *out
 	}
 }
 
+/* Streams for the multi-stream timing, kept for the context's life so a timed
+ * call holds launches only (creating streams costs milliseconds). */
+static int ensure_streams(mosrx_ctx *c, uint32_t n)
+{
+	while (c->nxs < n) {
+		if (hipStreamCreateWithFlags(&c->xs[c->nxs], hipStreamNonBlocking) != hipSuccess)
+			return -EIO;
+		if (hipEventCreateWithFlags(&c->xdone[c->nxs], hipEventDisableTiming) != hipSuccess) {
+			hipStreamDestroy(c->xs[c->nxs]);
+			return -EIO;
+		}
+		c->nxs++;
+	}
+	return 0;
+}
+
 static int time_streams(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
                         void *const *aux, uint32_t iters, uint32_t nstreams, float *ms)
 {
-	hipStream_t st[MOSRX_MAX_STREAMS];
-	hipEvent_t done[MOSRX_MAX_STREAMS];
-	uint32_t i, k, made = 0;
-	int rc = 0;
-	for (k = 0; k < nstreams && !rc; k++, made++)
-		if (hipStreamCreateWithFlags(&st[k], hipStreamNonBlocking) != hipSuccess ||
-		    hipEventCreateWithFlags(&done[k], hipEventDisableTiming) != hipSuccess)
-			rc = -EIO;
-	if (!rc && hipEventRecord(c->ev0, c->stream) != hipSuccess)
-		rc = -EIO;
-	for (k = 0; k < nstreams && !rc; k++)
-		if (hipStreamWaitEvent(st[k], c->ev0, 0) != hipSuccess)
-			rc = -EIO;
+	uint32_t i, k;
+	int rc;
+	if ((rc = ensure_streams(c, nstreams)))
+		return rc;
+	HIPCHK(hipEventRecord(c->ev0, c->stream));
+	for (k = 0; k < nstreams; k++)
+		HIPCHK(hipStreamWaitEvent(c->xs[k], c->ev0, 0));
 	/* batch i on stream i % nstreams: independent batches overlap their
 	 * launch/drain phases the way several rx queues would */
-	for (i = 0; i < iters && !rc; i++)
-		rc = run_op(c, op, arg, &b[i % nb], out ? out[i % nb] : NULL, aux ? aux[i % nb] : NULL,
-		            st[i % nstreams]);
-	for (k = 0; k < nstreams && !rc; k++)
-		if (hipEventRecord(done[k], st[k]) != hipSuccess || hipStreamWaitEvent(c->stream, done[k], 0) != hipSuccess)
-			rc = -EIO;
-	if (!rc && (hipEventRecord(c->ev1, c->stream) != hipSuccess || hipEventSynchronize(c->ev1) != hipSuccess ||
-	            hipEventElapsedTime(ms, c->ev0, c->ev1) != hipSuccess))
-		rc = -EIO;
-	hipDeviceSynchronize();
-	for (k = 0; k < made; k++) {
-		hipStreamDestroy(st[k]);
-		hipEventDestroy(done[k]);
+	for (i = 0; i < iters; i++)
+		if ((rc = run_op(c, op, arg, &b[i % nb], out ? out[i % nb] : NULL, aux ? aux[i % nb] : NULL,
+		                 c->xs[i % nstreams])))
+			return rc;
+	for (k = 0; k < nstreams; k++) {
+		HIPCHK(hipEventRecord(c->xdone[k], c->xs[k]));
+		HIPCHK(hipStreamWaitEvent(c->stream, c->xdone[k], 0));
 	}
-	return rc;
+	HIPCHK(hipEventRecord(c->ev1, c->stream));
+	HIPCHK(hipEventSynchronize(c->ev1));
+	HIPCHK(hipEventElapsedTime(ms, c->ev0, c->ev1));
+	return 0;
 }
 
 static int time_kernels(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,

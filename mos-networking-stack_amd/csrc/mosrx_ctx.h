@@ -42,6 +42,9 @@ struct mosrx_ctx {
 	int variant;                     /* kernel cache-policy variant (mosrx_set_variant) */
 	mosrx_bpf_insn *d_bpf;           /* installed BPF programs (MOSRX_BPF_MAX_INSNS), NULL until set */
 	mosrx_bparams bpf;               /* program table of the installed set */
+	hipStream_t xs[MOSRX_MAX_STREAMS];   /* timing streams (mosrx_time_op), created on first use */
+	hipEvent_t xdone[MOSRX_MAX_STREAMS];
+	uint32_t nxs;
 };
 
 int mosrx__check_batch(const mosrx_batch *b, int dev);

@@ -18,7 +18,7 @@
 
 int mosrx_set_variant(mosrx_ctx *c, int variant)
 {
-	if (!c || variant < 0 || variant > 15)
+	if (!c || variant < 0 || variant > 31)
 		return -EINVAL;
 	c->variant = variant;
 	return 0;
@@ -141,6 +141,8 @@ int mosrx_set_params(mosrx_ctx *c, const mosrx_params *p)
 	return 0;
 }
 
+int mosrx__ensure_streams(mosrx_ctx *c, uint32_t n);
+
 int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 {
 	mosrx_ctx *c;
@@ -162,9 +164,13 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 	c->device = device;
 	c->variant = MOSRX_DEFAULT_VARIANT;
 	if (getenv("MOSRX_KVARIANT"))
-		c->variant = atoi(getenv("MOSRX_KVARIANT")) & 15;
+		c->variant = atoi(getenv("MOSRX_KVARIANT")) & 31;
+	/* the timing streams are created right after the context stream: HIP maps
+	 * streams to hardware queues round robin (GPU_MAX_HW_QUEUES, 4 by default),
+	 * so the first three land on queues of their own */
 	if (hipSetDevice(device) != hipSuccess ||
 	    hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+	    mosrx__ensure_streams(c, 3) != 0 ||
 	    hipMalloc((void **)&c->d_tables, MOSRX_TAB_WORDS * 4) != hipSuccess ||
 	    hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
 		mosrx_close(c);
@@ -243,13 +249,14 @@ int mosrx__check_batch(const mosrx_batch *b, int dev)
 /* Kernel shape: SMALL when every frame fits the header window (max_len known
  * and <= 94), else LARGE.  Measured on MI355X (profiles/r01_tune_kinds.log):
  * LARGE beats MID for M1500 (22.7 vs 30.3 us) and for IMIX (43.5 vs 49.0 us);
- * MID stays reachable for tuning.  Variant bits 2-3 force a shape (value - 1). */
+ * MID and the L* shapes stay reachable for tuning: variant bits 2-4 force a
+ * shape (value - 1, MOSRX_KIND_*). */
 static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_t n)
 {
-	const int force = (c->variant >> 2) & 3;
+	const int force = (c->variant >> 2) & 7;
 	(void)bytes;
 	(void)n;
-	if (force)
+	if (force && force <= MOSRX_KIND_COUNT)
 		return force - 1;
 	if (max_len && max_len <= MOSRX_WINDOW_END)
 		return MOSRX_KIND_SMALL;
@@ -613,7 +620,7 @@ static int run_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, void *out
 
 /* Streams for the multi-stream timing, kept for the context's life so a timed
  * call holds launches only (creating streams costs milliseconds). */
-static int ensure_streams(mosrx_ctx *c, uint32_t n)
+int mosrx__ensure_streams(mosrx_ctx *c, uint32_t n)
 {
 	while (c->nxs < n) {
 		if (hipStreamCreateWithFlags(&c->xs[c->nxs], hipStreamNonBlocking) != hipSuccess)
@@ -632,7 +639,7 @@ static int time_streams(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uin
 {
 	uint32_t i, k;
 	int rc;
-	if ((rc = ensure_streams(c, nstreams)))
+	if ((rc = mosrx__ensure_streams(c, nstreams)))
 		return rc;
 	HIPCHK(hipEventRecord(c->ev0, c->stream));
 	for (k = 0; k < nstreams; k++)

@@ -11,11 +11,14 @@
 // through scalar loads, its opcode switch is a scalar branch, and the lanes
 // whose own pc equals i execute it under the exec mask.  Instructions no lane
 // sits on are skipped with one ballot; the walk ends when every lane returned.
-// Scratch memory M[16] lives in LDS (one column per lane, conflict-free).
+// Scratch memory M[16] lives in registers: its index is the instruction's k,
+// uniform, so a load/store is a uniform compare chain of v_cndmask.
 //
-// Packet loads read the frame bytes from HBM/L2 through the batch buffer
-// resource (two dword loads + v_alignbyte for an unaligned word), after the
-// same bounds checks the reference makes against buflen.
+// Packet loads: every lane first stages its frame's first STAGE_B bytes in LDS
+// with one burst of 16-byte loads (one memory latency per frame instead of one
+// per filter load); a load inside that window is two LDS reads + v_alignbyte,
+// a deeper one goes to HBM/L2 through the batch buffer resource.  Bounds are
+// checked against buflen exactly as the reference does first.
 
 #include <errno.h>
 
@@ -23,6 +26,10 @@
 
 #define BPF_TILE 256u
 #define BPF_DONE 0xFFFFFFFFu
+#define STAGE_V  9u                 // 16-byte loads per frame: bytes [o & ~3, +144)
+#define STAGE_DW (4u * STAGE_V)     // staged dwords per frame
+#define STAGE_LD (STAGE_DW + 1u)    // LDS stride per lane (odd: conflict-free columns)
+#define STAGE_B  (4u * STAGE_DW - 3u) // frame bytes guaranteed staged: [0, 141)
 
 // opcode fields (include/bpf/sfbpf.h)
 enum : uint32_t {
@@ -43,12 +50,40 @@ __device__ __forceinline__ uint32_t ld_le32(__amdgpu_buffer_rsrc_t rs, uint32_t 
 	const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, a4 + 4u, 0, 0);
 	return __builtin_amdgcn_alignbyte(hi, lo, a & 3u);
 }
+// Little-endian dword of frame bytes [k, k+4) (k + 4 <= STAGE_B + 3 staged):
+// from the lane's LDS window when inside it, else from memory.
+__device__ __forceinline__ uint32_t fr_le32(const uint32_t *win, uint32_t sh, __amdgpu_buffer_rsrc_t rs,
+                                            uint32_t o, uint32_t k, uint32_t size)
+{
+	if (k + size <= STAGE_B) {
+		const uint32_t a = sh + k;
+		return __builtin_amdgcn_alignbyte(win[(a >> 2) + 1u], win[a >> 2], a & 3u);
+	}
+	return ld_le32(rs, o + k);
+}
+
+// M[k] with k uniform (< 16, checked at set)
+__device__ __forceinline__ uint32_t mem_get(const uint32_t (&M)[16], uint32_t k)
+{
+	uint32_t r = 0;
+#pragma unroll
+	for (uint32_t q = 0; q < 16; q++)
+		r = (k == q) ? M[q] : r;
+	return r;
+}
+__device__ __forceinline__ void mem_put(uint32_t (&M)[16], uint32_t k, uint32_t v)
+{
+#pragma unroll
+	for (uint32_t q = 0; q < 16; q++)
+		M[q] = (k == q) ? v : M[q];
+}
+
 __device__ __forceinline__ uint32_t be32(uint32_t le) { return __builtin_bswap32(le); }
 __device__ __forceinline__ uint32_t be16(uint32_t le) { return ((le & 0xFFu) << 8) | ((le >> 8) & 0xFFu); }
 
 __global__ __launch_bounds__(BPF_TILE) void mosrx_bpf_kernel(const mosrx_bparams bp)
 {
-	__shared__ uint32_t s_mem[16 * BPF_TILE];
+	__shared__ uint32_t s_win[STAGE_LD * BPF_TILE];
 	const uint32_t t = threadIdx.x;
 	const uint32_t p = blockIdx.x * BPF_TILE + t;
 	const bool live = p < bp.n;
@@ -59,10 +94,24 @@ __global__ __launch_bounds__(BPF_TILE) void mosrx_bpf_kernel(const mosrx_bparams
 		o = bp.off[p];
 		cap = eff_caplen(o, bp.len[p], bp.frames_bytes);
 	}
+	// stage bytes [o & ~3, +144) of the frame (out-of-range dwords read 0)
+	uint32_t *win = s_win + STAGE_LD * t;
+	const uint32_t sh = o & 3u;
+	{
+		const uint32_t base = live ? (o & ~3u) : bp.frames_bytes + 16u;
+		u32x4 v[STAGE_V];
+#pragma unroll
+		for (uint32_t m = 0; m < STAGE_V; m++)
+			v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u * m, 0, 0);
+#pragma unroll
+		for (uint32_t m = 0; m < STAGE_V; m++) {
+			win[4 * m + 0] = v[m].x; win[4 * m + 1] = v[m].y; win[4 * m + 2] = v[m].z; win[4 * m + 3] = v[m].w;
+		}
+	}
 	// datagram length for the SYN/orphan call sites: 14 + tot_len of an IPv4
 	// frame whose datagram lies inside the capture
-	if (cap >= 18u && (ld_le32(rs, o + 12u) & 0xFFFFu) == 0x0008u) {
-		lip = 14u + be16(ld_le32(rs, o + 16u));
+	if (cap >= 18u && (fr_le32(win, sh, rs, o, 12u, 2u) & 0xFFFFu) == 0x0008u) {
+		lip = 14u + be16(fr_le32(win, sh, rs, o, 16u, 2u));
 		if (lip > cap)
 			lip = 0;
 	}
@@ -78,7 +127,11 @@ __global__ __launch_bounds__(BPF_TILE) void mosrx_bpf_kernel(const mosrx_bparams
 			continue;
 		}
 		const uint2 *prog = reinterpret_cast<const uint2 *>(bp.insns + bp.prog_off[j]);
-		uint32_t pc = act ? 0u : BPF_DONE, A = 0, X = 0, ret = 0, memw = 0;
+		uint32_t pc = act ? 0u : BPF_DONE, A = 0, X = 0, ret = 0;
+		uint32_t M[16];
+#pragma unroll
+		for (int q = 0; q < 16; q++)
+			M[q] = 0;
 		for (uint32_t i = 0; i < plen; i++) {
 			if (__ballot(pc == i) == 0) {
 				if (__ballot(pc != BPF_DONE) == 0)
@@ -95,46 +148,46 @@ __global__ __launch_bounds__(BPF_TILE) void mosrx_bpf_kernel(const mosrx_bparams
 			case B_RET | B_A: ret = e ? A : ret; npc = BPF_DONE; break;
 			case B_LD | B_W | B_ABS:
 				oob = (uint64_t)k + 4u > L;
-				if (e && !oob) A = be32(ld_le32(rs, o + k));
+				if (e && !oob) A = be32(fr_le32(win, sh, rs, o, k, 4u));
 				break;
 			case B_LD | B_H | B_ABS:
 				oob = (uint64_t)k + 2u > L;
-				if (e && !oob) A = be16(ld_le32(rs, o + k));
+				if (e && !oob) A = be16(fr_le32(win, sh, rs, o, k, 2u));
 				break;
 			case B_LD | B_B | B_ABS:
 				oob = k >= L;
-				if (e && !oob) A = ld_le32(rs, o + k) & 0xFFu;
+				if (e && !oob) A = fr_le32(win, sh, rs, o, k, 1u) & 0xFFu;
 				break;
 			case B_LD | B_W | B_LEN: if (e) A = L; break;
 			case B_LDX | B_W | B_LEN: if (e) X = L; break;
 			case B_LD | B_W | B_IND: {
 				const uint32_t kk = X + k;
 				oob = (uint64_t)kk + 4u > L;
-				if (e && !oob) A = be32(ld_le32(rs, o + kk));
+				if (e && !oob) A = be32(fr_le32(win, sh, rs, o, kk, 4u));
 				break;
 			}
 			case B_LD | B_H | B_IND: {
 				const uint32_t kk = X + k;
 				oob = (uint64_t)kk + 2u > L;
-				if (e && !oob) A = be16(ld_le32(rs, o + kk));
+				if (e && !oob) A = be16(fr_le32(win, sh, rs, o, kk, 2u));
 				break;
 			}
 			case B_LD | B_B | B_IND: {
 				const uint32_t kk = X + k;
 				oob = kk >= L;
-				if (e && !oob) A = ld_le32(rs, o + kk) & 0xFFu;
+				if (e && !oob) A = fr_le32(win, sh, rs, o, kk, 1u) & 0xFFu;
 				break;
 			}
 			case B_LDX | B_MSH | B_B:
 				oob = k >= L;
-				if (e && !oob) X = (ld_le32(rs, o + k) & 0xFu) << 2;
+				if (e && !oob) X = (fr_le32(win, sh, rs, o, k, 1u) & 0xFu) << 2;
 				break;
 			case B_LD | B_IMM: if (e) A = k; break;
 			case B_LDX | B_IMM: if (e) X = k; break;
-			case B_LD | B_MEM: if (e) A = ((memw >> k) & 1u) ? s_mem[k * BPF_TILE + t] : 0u; break;
-			case B_LDX | B_MEM: if (e) X = ((memw >> k) & 1u) ? s_mem[k * BPF_TILE + t] : 0u; break;
-			case B_ST: if (e) { s_mem[k * BPF_TILE + t] = A; memw |= 1u << k; } break;
-			case B_STX: if (e) { s_mem[k * BPF_TILE + t] = X; memw |= 1u << k; } break;
+			case B_LD | B_MEM: if (e) A = mem_get(M, k); break;
+			case B_LDX | B_MEM: if (e) X = mem_get(M, k); break;
+			case B_ST: if (e) mem_put(M, k, A); break;
+			case B_STX: if (e) mem_put(M, k, X); break;
 			case B_JMP | B_JA: npc = i + 1u + k; break;
 			case B_JMP | B_JGT | B_K: npc = i + 1u + ((A > k) ? jt : jf); break;
 			case B_JMP | B_JGE | B_K: npc = i + 1u + ((A >= k) ? jt : jf); break;

@@ -7,6 +7,8 @@
 
 #include "mosrx_internal.h"
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 // The resource range is frames_bytes rounded up to 16: the 16-byte chunk that
 // holds the buffer's last byte is readable whole (it cannot cross a page the
 // buffer does not touch), and every byte past the last frame's end is masked.

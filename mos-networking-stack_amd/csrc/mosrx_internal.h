@@ -44,10 +44,18 @@ typedef struct mosrx_kparams {
 
 /* Kernel shapes ("kinds"):
  *   SMALL  256 frames / 4 waves, every frame fits the header window (64 B configs)
- *   LARGE   64 frames / 1 header wave + 4 streamer waves (large frames)
- *   MID    256 frames / 4 header waves + 4 streamer waves (mixed sizes, IMIX) */
-enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_LARGE = 1, MOSRX_KIND_MID = 2 };
-#define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_LARGE ? 64u : 256u)
+ *   LARGE   64 frames / 1 header wave + 4 streamer waves (the default otherwise)
+ *   MID    256 frames / 4 header waves + 4 streamer waves
+ *   L12     64 frames / 1 header wave + 2 streamers
+ *   L24    128 frames / 2 header waves + 4 streamers
+ *   L28    128 frames / 2 header waves + 8 streamers
+ * (the last four are tuning shapes, reachable through the variant bits) */
+enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_LARGE = 1, MOSRX_KIND_MID = 2, MOSRX_KIND_L12 = 3, MOSRX_KIND_L24 = 4,
+       MOSRX_KIND_L28 = 5, MOSRX_KIND_COUNT = 6 };
+/* header waves / streamer waves of a large-type kind */
+#define MOSRX_KIND_H(k) ((k) == MOSRX_KIND_MID ? 4 : ((k) == MOSRX_KIND_L24 || (k) == MOSRX_KIND_L28) ? 2 : 1)
+#define MOSRX_KIND_S(k) ((k) == MOSRX_KIND_L12 ? 2 : (k) == MOSRX_KIND_L28 ? 8 : 4)
+#define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_SMALL ? 256u : 64u * (unsigned)MOSRX_KIND_H(k))
 /* Frames whose IP datagram ends at or before this frame byte are finished in
  * the per-lane header window; longer ones stream their tail cooperatively. */
 #define MOSRX_WINDOW_END 94

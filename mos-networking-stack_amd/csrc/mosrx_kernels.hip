@@ -41,7 +41,6 @@
 
 #include "mosrx_device.h"
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 #define WIN_RAW 24     // raw dwords per lane window (96 B)
@@ -52,7 +51,7 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 static_assert(2 + 4 * WIN_DW == MOSRX_WINDOW_END, "window end");
 static_assert(sizeof(mosrx_result) == 16, "record size");
 // small: 4 waves, one frame per lane; large: 1 header + 4 streamer waves; mid: 4 + 4
-#define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? 256 : ((kind) == MOSRX_KIND_LARGE ? 320 : 512))
+#define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? 256 : 64 * (MOSRX_KIND_H(kind) + MOSRX_KIND_S(kind)))
 
 
 // 16 bytes at byte offset c (OOB offsets read zero).  No data-dependent branch:
@@ -593,17 +592,15 @@ __device__ __forceinline__ uint32_t range_sum(__amdgpu_buffer_rsrc_t rs, uint32_
 // prefetched measured slower at every grid cap: per-workgroup concurrency, not
 // launch startup, bounds this kernel; profiles/r01_tune_persistent.log.)
 //
-// H = header waves (64 frames each, TILE = 64 H); 4 streamer waves follow them.
-// H = 1 (large frames): the 4 streamers share the subtile's candidates.
-// H = 4 (mixed sizes, e.g. IMIX): streamer s serves subtile s, so a workgroup
-// covers 256 frames and keeps enough bytes in flight when most frames are small.
-template <int H, int VAR>
+// H = header waves (64 frames each, TILE = 64 H); S streamer waves follow them,
+// SP = S / H per 64-frame subtile sharing its candidates.  LARGE is H=1, S=4.
+template <int H, int S, int VAR>
 __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uint32_t tile)
 {
 	constexpr uint32_t TILE = 64u * H;
-	constexpr int SP = 4 / H;                 // streamers per 64-frame subtile
+	constexpr int SP = S / H;                 // streamers per 64-frame subtile
 	constexpr int AUX = TAIL_AUX(VAR);
-	static_assert(H == 1 || H == 4, "header waves");
+	static_assert(SP >= 1 && S % H == 0, "shape");
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
 	__shared__ uint32_t s_spec[TILE];
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
@@ -682,8 +679,8 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 		uint32_t *spec = s_spec + 64u * sub;
 		tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 0, b0, f0);
 		tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 1, b1, f1);
-		if constexpr (H == 1) {
-			// at most 4 groups: straight-line code
+		if constexpr (SP == 4) {
+			// at most 4 groups (64 candidates / 16 per group): straight-line code
 			tail_consume<AUX>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
 			if (ngrp > 2) {
 				tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 2, b0, f0);
@@ -713,10 +710,8 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 {
 	if constexpr (KIND == MOSRX_KIND_SMALL)
 		classify_tile_small<VAR>(kp, tile);
-	else if constexpr (KIND == MOSRX_KIND_LARGE)
-		classify_tile_large<1, VAR>(kp, tile);
 	else
-		classify_tile_large<4, VAR>(kp, tile);
+		classify_tile_large<MOSRX_KIND_H(KIND), MOSRX_KIND_S(KIND), VAR>(kp, tile);
 }
 
 template <int KIND, int VAR>
@@ -809,13 +804,14 @@ extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles,
 {
 	if (!qp || qp->nb == 0 || total_tiles == 0)
 		return qp ? 0 : -EINVAL;
-	if (kind < 0 || kind > MOSRX_KIND_MID)
+	if (kind < 0 || kind >= MOSRX_KIND_COUNT)
 		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-	static void (*const tab[3][2])(const mosrx_qparams *, uint32_t, hipStream_t) = {
-		{launch_queue_v<MOSRX_KIND_SMALL, 0>, launch_queue_v<MOSRX_KIND_SMALL, 2>},
-		{launch_queue_v<MOSRX_KIND_LARGE, 0>, launch_queue_v<MOSRX_KIND_LARGE, 2>},
-		{launch_queue_v<MOSRX_KIND_MID, 0>, launch_queue_v<MOSRX_KIND_MID, 2>}};
+#define QROW(k) {launch_queue_v<k, 0>, launch_queue_v<k, 2>}
+	static void (*const tab[MOSRX_KIND_COUNT][2])(const mosrx_qparams *, uint32_t, hipStream_t) = {
+		QROW(MOSRX_KIND_SMALL), QROW(MOSRX_KIND_LARGE), QROW(MOSRX_KIND_MID),
+		QROW(MOSRX_KIND_L12), QROW(MOSRX_KIND_L24), QROW(MOSRX_KIND_L28)};
+#undef QROW
 	tab[kind][(variant >> 1) & 1](qp, total_tiles, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
@@ -824,13 +820,14 @@ extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int vari
 {
 	if (!kp || kp->n == 0)
 		return kp ? 0 : -EINVAL;
-	if (kind < 0 || kind > MOSRX_KIND_MID)
+	if (kind < 0 || kind >= MOSRX_KIND_COUNT)
 		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-	static void (*const tab[3][3])(const mosrx_kparams *, hipStream_t) = {
-		{launch_v<MOSRX_KIND_SMALL, 0>, launch_v<MOSRX_KIND_SMALL, 2>, launch_v<MOSRX_KIND_SMALL, 2 | VAR_TX>},
-		{launch_v<MOSRX_KIND_LARGE, 0>, launch_v<MOSRX_KIND_LARGE, 2>, launch_v<MOSRX_KIND_LARGE, 2 | VAR_TX>},
-		{launch_v<MOSRX_KIND_MID, 0>, launch_v<MOSRX_KIND_MID, 2>, launch_v<MOSRX_KIND_MID, 2 | VAR_TX>}};
+#define KROW(k) {launch_v<k, 0>, launch_v<k, 2>, launch_v<k, 2 | VAR_TX>}
+	static void (*const tab[MOSRX_KIND_COUNT][3])(const mosrx_kparams *, hipStream_t) = {
+		KROW(MOSRX_KIND_SMALL), KROW(MOSRX_KIND_LARGE), KROW(MOSRX_KIND_MID),
+		KROW(MOSRX_KIND_L12), KROW(MOSRX_KIND_L24), KROW(MOSRX_KIND_L28)};
+#undef KROW
 	tab[kind][(kp->flags & (MOSRX_KF_TX_IP | MOSRX_KF_TX_TCP)) ? 2 : (variant >> 1) & 1](kp, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -238,9 +238,9 @@ def test_batch_queue_one_launch(gpu_ctx, kind, n, nb):
         d.free()
 
 
-# kernel shapes forced through variant bits 2-3 (value - 1: SMALL, LARGE, MID) with both
+# kernel shapes forced through variant bits 2-4 (value - 1: SMALL, LARGE, MID, L12, L24, L28) with both
 # tail-load cache policies; every shape must be exact on every frame mix
-@pytest.mark.parametrize("variant", [2, 6, 10, 14, 0, 8, 12])
+@pytest.mark.parametrize("variant", [2, 6, 10, 14, 18, 22, 26, 0, 8, 12])
 @pytest.mark.parametrize("kind,n", [(mosrx.TRACE_S64, 20_000), (mosrx.TRACE_M1500, 9_000),
                                     (mosrx.TRACE_IMIX, 30_000)])
 def test_forced_kernel_shapes(gpu_ctx, variant, kind, n):

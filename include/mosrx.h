@@ -116,9 +116,9 @@ typedef struct mosrx_ctx mosrx_ctx;
  * the HIP kernels are unavailable: there is no CPU fallback. */
 int  mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out);
 int  mosrx_set_params(mosrx_ctx *c, const mosrx_params *p);
-/* Tuning knob (0..31; results never depend on it): bit 1 = non-temporal tail
+/* Tuning knob (0..127; results never depend on it): bit 1 = non-temporal tail
  * stream (bit 0, non-temporal header windows, measured slower and folded onto
- * bit 1's setting); bits 2-4 = force a kernel shape (value - 1; 0 = automatic).
+ * bit 1's setting); bits 2-6 = force a kernel shape (value - 1; 0 = automatic).
  * Default from measurements; env MOSRX_KVARIANT overrides at open. */
 int  mosrx_set_variant(mosrx_ctx *c, int variant);
 void mosrx_close(mosrx_ctx *c);

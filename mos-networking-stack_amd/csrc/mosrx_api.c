@@ -18,7 +18,7 @@
 
 int mosrx_set_variant(mosrx_ctx *c, int variant)
 {
-	if (!c || variant < 0 || variant > 31)
+	if (!c || variant < 0 || variant > 127)
 		return -EINVAL;
 	c->variant = variant;
 	return 0;
@@ -164,7 +164,7 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 	c->device = device;
 	c->variant = MOSRX_DEFAULT_VARIANT;
 	if (getenv("MOSRX_KVARIANT"))
-		c->variant = atoi(getenv("MOSRX_KVARIANT")) & 31;
+		c->variant = atoi(getenv("MOSRX_KVARIANT")) & 127;
 	/* the timing streams are created right after the context stream: HIP maps
 	 * streams to hardware queues round robin (GPU_MAX_HW_QUEUES, 4 by default),
 	 * so the first three land on queues of their own */
@@ -249,11 +249,11 @@ int mosrx__check_batch(const mosrx_batch *b, int dev)
 /* Kernel shape: SMALL when every frame fits the header window (max_len known
  * and <= 94), else LARGE.  Measured on MI355X (profiles/r01_tune_kinds.log):
  * LARGE beats MID for M1500 (22.7 vs 30.3 us) and for IMIX (43.5 vs 49.0 us);
- * MID and the L* shapes stay reachable for tuning: variant bits 2-4 force a
+ * MID, the L* and S* shapes stay reachable for tuning: variant bits 2-6 force a
  * shape (value - 1, MOSRX_KIND_*). */
 static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_t n)
 {
-	const int force = (c->variant >> 2) & 7;
+	const int force = (c->variant >> 2) & 31;
 	(void)bytes;
 	(void)n;
 	if (force && force <= MOSRX_KIND_COUNT)

@@ -1,0 +1,9 @@
+# stream v2 (scalar ownership): parity, then time shares
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout=120 --timeout-method thread -p no:cacheprovider -k "stream or forced or flow_hash_device or tx_forced" > gpurun_out/pytest_i.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_i.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 100 ./scripts/probe_classify 2 65536 > gpurun_out/probe_classify4.log 2>&1 && timeout -k 10 100 ./scripts/probe_classify 3 262144 >> gpurun_out/probe_classify4.log 2>&1; rc=$?
+cat gpurun_out/probe_classify4.log
+exit $rc

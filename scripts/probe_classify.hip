@@ -1,0 +1,125 @@
+// probe_classify.hip — time shares of the LARGE classify tile (diagnostic only).
+// Builds the library's kernel source with the DBG knob of classify_tile_large
+// (1: no header parse/records, 2: no header window loads, 4: no streamer sums)
+// and times each build on the BASELINE config #3 trace, back-to-back and one
+// launch at a time.  Results are meaningless for DBG != 0; only time counts.
+#include "../mos-networking-stack_amd/csrc/mosrx_kernels.hip"
+#include "../include/mosrx_trace.h"
+#include <stdio.h>
+#include <stdlib.h>
+
+#define CHK(x) do { if ((x) != hipSuccess) { printf("HIP error %s line %d\n", #x, __LINE__); return 1; } } while (0)
+
+template <int DBG, int MINB = 1>
+__global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(MINB > 1 ? 8 : 1))) void k_dbg(mosrx_kparams kp)
+{
+	classify_tile_large<1, 4, 2, DBG>(kp, blockIdx.x);
+}
+
+template <int H, int S, int DBG>
+__global__ __launch_bounds__(64 * (H + S)) void k_sdbg(mosrx_kparams kp)
+{
+	classify_tile_stream<H, S, 2, DBG>(kp, blockIdx.x);
+}
+
+typedef void (*lfn)(const mosrx_kparams *, hipStream_t);
+template <int DBG, int MINB = 1>
+static void launch_dbg(const mosrx_kparams *kp, hipStream_t s)
+{
+	hipLaunchKernelGGL((k_dbg<DBG, MINB>), dim3((kp->n + 63) / 64), dim3(320), 0, s, *kp);
+}
+template <int H, int S, int DBG>
+static void launch_sdbg(const mosrx_kparams *kp, hipStream_t s)
+{
+	hipLaunchKernelGGL((k_sdbg<H, S, DBG>), dim3((kp->n + 64 * H - 1) / (64 * H)), dim3(64 * (H + S)), 0, s, *kp);
+}
+static void launch_product(const mosrx_kparams *kp, hipStream_t s)
+{
+	mosrx_launch_classify(kp, MOSRX_KIND_LARGE, 2, s);
+}
+static void launch_stream(const mosrx_kparams *kp, hipStream_t s)
+{
+	mosrx_launch_classify(kp, MOSRX_KIND_S14, 2, s);
+}
+
+static int run(const char *name, lfn f, mosrx_kparams *kps, int nb, double bytes)
+{
+	hipEvent_t a, b;
+	CHK(hipEventCreate(&a));
+	CHK(hipEventCreate(&b));
+	for (int i = 0; i < nb; i++)
+		f(&kps[i], 0);
+	const int iters = 60;
+	float best_bb = 1e9, best_one = 1e9;
+	for (int rep = 0; rep < 3; rep++) {
+		float ms, one = 0;
+		CHK(hipEventRecord(a, 0));
+		for (int i = 0; i < iters; i++)
+			f(&kps[i % nb], 0);
+		CHK(hipEventRecord(b, 0));
+		CHK(hipEventSynchronize(b));
+		CHK(hipEventElapsedTime(&ms, a, b));
+		for (int i = 0; i < iters; i++) {
+			float t;
+			CHK(hipEventRecord(a, 0));
+			f(&kps[i % nb], 0);
+			CHK(hipEventRecord(b, 0));
+			CHK(hipEventSynchronize(b));
+			CHK(hipEventElapsedTime(&t, a, b));
+			one += t;
+		}
+		if (ms / iters < best_bb) best_bb = ms / iters;
+		if (one / iters < best_one) best_one = one / iters;
+	}
+	printf("%-40s back-to-back %6.2f us (%5.0f GB/s) | single %6.2f us (%5.0f GB/s)\n", name, best_bb * 1e3,
+	       bytes / (best_bb * 1e-3) / 1e9, best_one * 1e3, bytes / (best_one * 1e-3) / 1e9);
+	return 0;
+}
+
+int main(int argc, char **argv)
+{
+	int kind = argc > 1 ? atoi(argv[1]) : MOSRX_TRACE_M1500;
+	uint32_t n = argc > 2 ? (uint32_t)atoi(argv[2]) : 65536;
+	mosrx_trace t;
+	if (mosrx_trace_gen(kind, n, 1000000, 0, &t)) {
+		printf("trace_gen failed\n");
+		return 1;
+	}
+	const int nb = 6;
+	mosrx_kparams kps[nb];
+	uint32_t *tables;
+	CHK(hipMalloc((void **)&tables, MOSRX_TAB_WORDS * 4));
+	CHK(hipMemset(tables, 0, MOSRX_TAB_WORDS * 4));
+	for (int i = 0; i < nb; i++) {
+		uint8_t *f; uint32_t *o; uint16_t *l; mosrx_result *r;
+		CHK(hipMalloc((void **)&f, t.frames_bytes + 64));
+		CHK(hipMemcpy(f, t.frames, t.frames_bytes + 64, hipMemcpyHostToDevice));
+		CHK(hipMalloc((void **)&o, n * 4));
+		CHK(hipMemcpy(o, t.off, n * 4, hipMemcpyHostToDevice));
+		CHK(hipMalloc((void **)&l, n * 2));
+		CHK(hipMemcpy(l, t.len, n * 2, hipMemcpyHostToDevice));
+		CHK(hipMalloc((void **)&r, n * 16));
+		kps[i] = (mosrx_kparams){f, o, l, r, tables, NULL, NULL, (uint32_t)t.frames_bytes, n, MOSRX_KF_VERIFY, 0};
+	}
+	const double bytes = (double)t.caplen_sum + 22.0 * n;
+	printf("trace kind %d n %u: %.2f MB algorithmic\n", kind, n, bytes / 1e6);
+	run("product LARGE", launch_product, kps, nb, bytes);
+	run("product S14", launch_stream, kps, nb, bytes);
+	run("DBG 0 (same as product)", launch_dbg<0>, kps, nb, bytes);
+	run("DBG 3 no header work at all", launch_dbg<3>, kps, nb, bytes);
+	run("DBG 4 no streamer sums", launch_dbg<4>, kps, nb, bytes);
+	run("DBG 5 no parse + no sums", launch_dbg<5>, kps, nb, bytes);
+	run("DBG 7 loads only", launch_dbg<7>, kps, nb, bytes);
+	run("S14 DBG 0", launch_sdbg<1, 4, 0>, kps, nb, bytes);
+	run("S14 DBG 4 streamer loads only", launch_sdbg<1, 4, 4>, kps, nb, bytes);
+	run("S14 DBG 7 loads only", launch_sdbg<1, 4, 7>, kps, nb, bytes);
+	run("S14 DBG 3 no header work", launch_sdbg<1, 4, 3>, kps, nb, bytes);
+	run("S44 DBG 0", launch_sdbg<4, 4, 0>, kps, nb, bytes);
+	run("S44 DBG 4", launch_sdbg<4, 4, 4>, kps, nb, bytes);
+	run("S44 DBG 7", launch_sdbg<4, 4, 7>, kps, nb, bytes);
+	run("S24 DBG 0", launch_sdbg<2, 4, 0>, kps, nb, bytes);
+	run("S22 DBG 0", launch_sdbg<2, 2, 0>, kps, nb, bytes);
+	run("S42 DBG 0", launch_sdbg<4, 2, 0>, kps, nb, bytes);
+	run("S12 DBG 0", launch_sdbg<1, 2, 0>, kps, nb, bytes);
+	return 0;
+}

@@ -238,9 +238,12 @@ def test_batch_queue_one_launch(gpu_ctx, kind, n, nb):
         d.free()
 
 
-# kernel shapes forced through variant bits 2-4 (value - 1: SMALL, LARGE, MID, L12, L24, L28) with both
-# tail-load cache policies; every shape must be exact on every frame mix
-@pytest.mark.parametrize("variant", [2, 6, 10, 14, 18, 22, 26, 0, 8, 12])
+# kernel shapes forced through variant bits 2-6 (value - 1: SMALL, LARGE, MID, L12, L24, L28, S14, S12,
+# S24, S22, S42, S44) with both tail-load cache policies; every shape must be exact on every frame mix
+STREAM_VARIANTS = [((k + 1) << 2) | 2 for k in range(6, 12)]
+
+
+@pytest.mark.parametrize("variant", [2, 6, 10, 14, 18, 22, 26, 0, 8, 12] + STREAM_VARIANTS + [28])
 @pytest.mark.parametrize("kind,n", [(mosrx.TRACE_S64, 20_000), (mosrx.TRACE_M1500, 9_000),
                                     (mosrx.TRACE_IMIX, 30_000)])
 def test_forced_kernel_shapes(gpu_ctx, variant, kind, n):
@@ -269,7 +272,7 @@ def test_flow_hash_golden(gpu_ctx, fix):
     np.testing.assert_array_equal(fh, ofh)
 
 
-@pytest.mark.parametrize("variant", [2, 6, 10, 14])
+@pytest.mark.parametrize("variant", [2, 6, 10, 14, 30, 46])
 @pytest.mark.parametrize("kind,n", [(mosrx.TRACE_S64, 32_768), (mosrx.TRACE_M1500, 16_384),
                                     (mosrx.TRACE_IMIX, 65_536)])
 def test_flow_hash_device(gpu_ctx, variant, kind, n):
@@ -289,3 +292,37 @@ def test_flow_hash_device(gpu_ctx, variant, kind, n):
     np.testing.assert_array_equal(fh, ofh)
     # size-independent property: frames of one flow share a bucket; 5000 flows -> <= 5000 buckets
     assert len(np.unique(fh[ora["payload_off"] != 0] & 0x1FFFF)) <= 5000
+
+
+# Stream shapes on the layouts that stress the span walk: tight packing at any
+# alignment (owners change inside a wave load), jumbo frames longer than a
+# streamer's run (one frame flushed by several streamers), frames out of buffer
+# order (the per-frame fallback), the last frame ending at the buffer end.
+@pytest.mark.parametrize("variant", STREAM_VARIANTS)
+def test_stream_shapes_layouts(gpu_ctx, variant):
+    gpu_ctx.set_variant(variant)
+    try:
+        rng = random.Random(variant)
+        from golden.make_golden import random_frames
+        for phase in (0, 1, 2, 7):
+            frames = random_frames(rng, 300, 0) + random_frames(rng, 150, 2) + random_frames(rng, 150, 1)
+            rng.shuffle(frames)
+            buf, off, ln = pack_frames(frames, align=rng.choice([1, 2, 16]), phase=phase, gap=rng.randint(0, 3))
+            run_both(gpu_ctx, buf, off, ln, mosrx.default_params(forward=0))
+            # same frames, descriptors in reverse buffer order: unsorted tiles
+            run_both(gpu_ctx, buf, off[::-1].copy(), ln[::-1].copy(), mosrx.default_params(forward=0))
+        big = [tcp_frame(payload=bytes(rng.getrandbits(8) for _ in range(k)), doff=5)
+               for k in (65535 - 54, 30000, 9000, 3000, 1500, 600, 10)]
+        buf, off, ln = pack_frames(big * 3, phase=3)
+        run_both(gpu_ctx, buf, off, ln, mosrx.default_params())
+        for plen in (0, 1, 15, 16, 17, 1000, 1447):
+            f = tcp_frame(payload=bytes(range(256)) * (plen // 256) + bytes(plen % 256), doff=8)
+            buf, off, ln = pack_frames([tcp_frame(payload=b"x" * 1400), f], phase=plen % 16)
+            run_both(gpu_ctx, buf, off, ln, mosrx.default_params(), frames_bytes=int(off[-1]) + int(ln[-1]))
+        rb = np.random.default_rng(variant)
+        buf = rb.integers(0, 256, 200_000, dtype=np.uint8)
+        off = np.sort(rb.integers(0, len(buf) - 2000, 3000)).astype(np.uint32)
+        ln = rb.integers(0, 2000, 3000).astype(np.uint16)          # sorted offsets, overlapping captures
+        run_both(gpu_ctx, buf, off, ln, mosrx.default_params())
+    finally:
+        gpu_ctx.set_variant(2)

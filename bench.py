@@ -153,7 +153,9 @@ def measure(ctx, dist, key, steps, warmup, rank):
         dist.barrier()
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
-        _, kern_ms = ctx.time_op(op, dbs, min(steps, 200), 1, arg, total=False)
+        kk = min(steps, 200)
+        kern_ms = ctx.time_op(op, dbs, kk, 1, arg, kernels=False)[0] / kk
+        _, kern_iso = ctx.time_op(op, dbs, kk, 1, arg, total=False)
     elif key.endswith("_queue"):
         # each step = one launch over QUEUE_DEPTH distinct resident 32K batches
         # several queues over disjoint batch copies: the working set exceeds the L3
@@ -171,6 +173,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         _, kern_ms = qs[0].time(min(steps, 64), qs[1:])
+        kern_iso = kern_ms
         for q in qs:
             q.destroy()
     else:
@@ -187,9 +190,13 @@ def measure(ctx, dist, key, steps, warmup, rank):
         dist.barrier()
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
-        # roofline: average duration of ONE launch alone on its stream, HIP
-        # events around each launch (the rocprofv3 kernel-trace figure)
-        kern_ms = ctx.time_dev_kernels(dbs, min(steps, 200))
+        # roofline: average launch duration on ONE stream, HIP events around
+        # K back-to-back launches on the launch stream (the figure rocprofv3's
+        # kernel trace reports); the isolated figure (events around each single
+        # launch, dispatch included) is kept beside it
+        kk = min(steps, 200)
+        kern_ms = ctx.time_dev_streams(dbs, kk, 1) / kk
+        kern_iso = ctx.time_dev_kernels(dbs, kk)
     for d in dbs:
         d.free()
     n = dist.ws
@@ -205,6 +212,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         "mpkts": n * batch * steps / wall_max / 1e6,
         "device_ms_per_batch": dev_ms / steps,
         "kernel_ms": kern_ms,
+        "kernel_ms_isolated": kern_iso,
     }
     achieved = ab / (kern_ms * 1e-3) / 1e9
     pmc = load_pmc(key)

@@ -247,20 +247,19 @@ int mosrx__check_batch(const mosrx_batch *b, int dev)
 }
 
 /* Kernel shape: SMALL when every frame fits the header window (max_len known
- * and <= 94), else LARGE.  Measured on MI355X (profiles/r01_tune_kinds.log):
- * LARGE beats MID for M1500 (22.7 vs 30.3 us) and for IMIX (43.5 vs 49.0 us);
- * MID, the L* and S* shapes stay reachable for tuning: variant bits 2-6 force a
- * shape (value - 1, MOSRX_KIND_*). */
+ * and <= 94); otherwise a stream shape, S14 for MTU-sized frames and S13 below
+ * a 1 KiB mean frame footprint.  Measured on MI355X
+ * (profiles/r01_probe_stream_scan.log): 1500 B config S14 19.4 us, S13 19.6,
+ * LARGE 20.7; IMIX S13 20.4 us, S14 21.9, LARGE 41.8.  Every other shape stays
+ * reachable for tuning: variant bits 2-6 force one (value - 1, MOSRX_KIND_*). */
 static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_t n)
 {
 	const int force = (c->variant >> 2) & 31;
-	(void)bytes;
-	(void)n;
 	if (force && force <= MOSRX_KIND_COUNT)
 		return force - 1;
 	if (max_len && max_len <= MOSRX_WINDOW_END)
 		return MOSRX_KIND_SMALL;
-	return MOSRX_KIND_LARGE;
+	return (n && bytes / n < 1024u) ? MOSRX_KIND_S13 : MOSRX_KIND_S14;
 }
 
 static int tile_for(const mosrx_ctx *c, const mosrx_batch *b)

@@ -44,26 +44,24 @@ typedef struct mosrx_kparams {
 
 /* Kernel shapes ("kinds"):
  *   SMALL  256 frames / 4 waves, every frame fits the header window (64 B configs)
- *   LARGE   64 frames / 1 header wave + 4 streamer waves (the default otherwise)
+ *   LARGE   64 frames / 1 header wave + 4 streamer waves that stream whole tails
  *   MID    256 frames / 4 header waves + 4 streamer waves
  *   L12     64 frames / 1 header wave + 2 streamers
  *   L24    128 frames / 2 header waves + 4 streamers
  *   L28    128 frames / 2 header waves + 8 streamers
- * (the last four are tuning shapes, reachable through the variant bits)
- *   Shh    64*H frames / H header waves + S streamer waves that read the tile's
- *          tail span in buffer order (frames sorted and disjoint, checked per
- *          tile; unsorted tiles stream frame by frame): S14, S12, S24, S22, S42, S44 */
+ *   S1s     64 frames / 1 header wave + s streamer waves that read the tile's
+ *          tail span in buffer order with a prefix scan (frames sorted and
+ *          disjoint, checked per tile; unsorted tiles stream whole tails like
+ *          LARGE): S13 and S14 are the defaults (measured), S12 and S16 tune */
 enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_LARGE = 1, MOSRX_KIND_MID = 2, MOSRX_KIND_L12 = 3, MOSRX_KIND_L24 = 4,
-       MOSRX_KIND_L28 = 5, MOSRX_KIND_S14 = 6, MOSRX_KIND_S12 = 7, MOSRX_KIND_S24 = 8, MOSRX_KIND_S22 = 9,
-       MOSRX_KIND_S42 = 10, MOSRX_KIND_S44 = 11, MOSRX_KIND_COUNT = 12 };
+       MOSRX_KIND_L28 = 5, MOSRX_KIND_S14 = 6, MOSRX_KIND_S12 = 7, MOSRX_KIND_S13 = 8, MOSRX_KIND_S16 = 9,
+       MOSRX_KIND_COUNT = 10 };
 #define MOSRX_KIND_IS_STREAM(k) ((k) >= MOSRX_KIND_S14)
 /* header waves / streamer waves of a large-type or stream kind */
-#define MOSRX_KIND_H(k)                                                                                           \
-	(((k) == MOSRX_KIND_MID || (k) == MOSRX_KIND_S42 || (k) == MOSRX_KIND_S44) ? 4                                \
-	 : ((k) == MOSRX_KIND_L24 || (k) == MOSRX_KIND_L28 || (k) == MOSRX_KIND_S24 || (k) == MOSRX_KIND_S22) ? 2 : 1)
+#define MOSRX_KIND_H(k) ((k) == MOSRX_KIND_MID ? 4 : ((k) == MOSRX_KIND_L24 || (k) == MOSRX_KIND_L28) ? 2 : 1)
 #define MOSRX_KIND_S(k)                                                                                           \
-	(((k) == MOSRX_KIND_L12 || (k) == MOSRX_KIND_S12 || (k) == MOSRX_KIND_S22 || (k) == MOSRX_KIND_S42) ? 2       \
-	 : (k) == MOSRX_KIND_L28 ? 8 : 4)
+	(((k) == MOSRX_KIND_L12 || (k) == MOSRX_KIND_S12) ? 2 : (k) == MOSRX_KIND_S13 ? 3                            \
+	 : (k) == MOSRX_KIND_S16 ? 6 : (k) == MOSRX_KIND_L28 ? 8 : 4)
 #define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_SMALL ? 256u : 64u * (unsigned)MOSRX_KIND_H(k))
 /* Frames whose IP datagram ends at or before this frame byte are finished in
  * the per-lane header window; longer ones stream their tail cooperatively. */

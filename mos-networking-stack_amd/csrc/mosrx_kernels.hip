@@ -576,6 +576,44 @@ __device__ __forceinline__ void tail_consume(__amdgpu_buffer_rsrc_t rs, uint32_t
 	}
 }
 
+// Streamer q of SP sharing a 64-frame subtile: candidates [SP*4g + 4q, +4) of
+// group g, sums into spec[frame].  Groups come in pairs (double buffered);
+// slots past the count are issued anyway (out-of-range loads, no traffic) so
+// the load counts stay static and every wait is a counted vmcnt(N), never a
+// drain.
+template <int SP, int AUX, int DBG = 0>
+__device__ __forceinline__ void tail_streamers(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
+                                               uint32_t hi_l, bool cand, uint64_t cmask, uint32_t rank_l,
+                                               uint32_t q, uint32_t lane, uint32_t *spec)
+{
+	const uint32_t ngrp = (__builtin_popcountll(cmask) + SP * TAIL_G - 1u) / (SP * TAIL_G);
+	tail_grp_t b0, b1;
+	uint32_t f0[TAIL_G], f1[TAIL_G];
+	tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 0, b0, f0);
+	tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 1, b1, f1);
+	if constexpr (SP == 4) {
+		// at most 4 groups (64 candidates / 16 per group): straight-line code
+		tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
+		if (ngrp > 2) {
+			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 2, b0, f0);
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 3, b1, f1);
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+		} else {
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+		}
+	} else {
+#pragma unroll 1
+		for (uint32_t g = 0; g < ngrp; g += 2) {
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
+			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 2, b0, f0);
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 3, b1, f1);
+		}
+	}
+}
+
 // Absolute-grid word sum of the bytes [a, b) (any alignment), whole wave.
 __device__ __forceinline__ uint32_t range_sum(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t a, uint32_t b,
                                               uint32_t lane)
@@ -706,119 +744,45 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 			              lane, s_cnt);
 		}
 	} else {
-		// ---- streamer waves: streamer q of its subtile takes candidates
-		// [SP*4g + 4q, +4) of group g.  Groups come in pairs (double buffered);
-		// slots past the count are issued anyway (out-of-range loads, no traffic)
-		// so the load counts stay static and every wait is a counted vmcnt(N),
-		// never a drain.
-		const uint32_t q = (wave - H) % SP;
-		const uint32_t ngrp = (__builtin_popcountll(cmask) + SP * TAIL_G - 1u) / (SP * TAIL_G);
-		tail_grp_t b0, b1;
-		uint32_t f0[TAIL_G], f1[TAIL_G];
-		uint32_t *spec = s_spec + 64u * sub;
-		tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 0, b0, f0);
-		tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 1, b1, f1);
-		if constexpr (SP == 4) {
-			// at most 4 groups (64 candidates / 16 per group): straight-line code
-			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
-			if (ngrp > 2) {
-				tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 2, b0, f0);
-				tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
-				tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 3, b1, f1);
-				tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
-				tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
-			} else {
-				tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
-			}
-		} else {
-#pragma unroll 1
-			for (uint32_t g = 0; g < ngrp; g += 2) {
-				tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
-				tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 2, b0, f0);
-				tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
-				tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 3, b1, f1);
-			}
-		}
+		// ---- streamer waves ----
+		tail_streamers<SP, AUX, DBG>(rs, nbytes, lo_l, hi_l, cand, cmask, rank_l, (wave - H) % SP, lane,
+		                             s_spec + 64u * sub);
 		__syncthreads();   // B
 	}
 	flush_counters(kp, s_cnt, t);
 }
 
 // ---------------------------------------------------------------------------
-// stream tile: H header waves + S streamers over the tile's tail span
+// stream tile: 64 frames, one header wave + S streamers over the tile's tail span
 // ---------------------------------------------------------------------------
 // Frames of a received batch sit in buffer order (an rx ring, a pcap file, the
 // loopback source): frame j+1 starts at or after the capture end of frame j.
 // Then the speculative tails [split_j, off_j + caplen_j) of a tile are
-// disjoint, sorted and start on 16-byte boundaries, so the tile's bytes from
-// the first split to the last capture end (the "span") can be read as plain
-// contiguous 1 KiB wave loads: streamer s of S takes the s-th contiguous run of
-// the span's 1 KiB blocks with STREAM_U loads in flight per lane, every lane
-// busy (chunks outside all tails are header windows, read again from L2, and
-// masked).  Ownership is wave-uniform: the tails that overlap a block are a
-// run of consecutive candidates, walked with scalar code; a lane picks its
-// tail with two compares per candidate, the chunk is summed once and one
-// masked DPP reduction per (block, tail) lands in the streamer's own LDS row
-// (no cross-wave atomics, no barrier before streaming).  The header waves add
-// the S rows.  Tiles not in buffer order stream frame by frame (same sums).
+// disjoint, sorted and start on 16-byte boundaries, and every 16-byte chunk
+// holds bytes of at most one tail (the next tail starts >= 79 bytes past this
+// capture's end).  The tile's bytes from the first split to the last capture
+// end (the "span") are read as plain contiguous 1 KiB wave loads: streamer s
+// of S takes the s-th run of the span's 1 KiB blocks with STREAM_U loads in
+// flight per lane, every lane busy (chunks outside all tails are header
+// windows and short frames, read again from L2, and never counted).  A tail
+// [lo, hi) covers the chunks lo .. ec = (hi - 1) & ~15 with only ec partial,
+// so its sum over a run is E(ec) + partial(ec) - E(lo), E being the run's
+// exclusive prefix of whole-chunk sums: per block one wave scan gives E for
+// its 64 chunks; the frame lanes (lane = frame) whose lo or ec falls in the
+// block fetch E there with ds_bpermute, and an ending frame sums its last
+// chunk's bytes below hi from an LDS copy of the block.  A tail entering the
+// run counts from 0, one leaving it ends at the run total.  No ownership
+// walk, no per-tail reduction; the header wave adds the S rows.  Tiles not in
+// buffer order stream frame by frame with the LARGE tile's streamers.
 #define STREAM_U 8
 #define ZERO_OFF 0xFFFFFFF0u   // buffer offset past any batch (loads there are never consumed)
 
-// Sum of [lo, hi) (lo 16-aligned) by one wave; the fallback of unsorted tiles.
-template <int AUX>
-__device__ __forceinline__ uint32_t span_sum(__amdgpu_buffer_rsrc_t rs, uint32_t lo, uint32_t hi, uint32_t lane)
-{
-	uint32_t acc = 0;
-#pragma unroll 1
-	for (uint32_t base = lo; base < hi; base += 2048u) {
-		const uint32_t c0 = base + 16u * lane, c1 = c0 + 1024u;
-		const u32x4 v0 = load16<AUX>(rs, c0 < hi ? c0 : ZERO_OFF, 0);
-		const u32x4 v1 = load16<AUX>(rs, c1 < hi ? c1 : ZERO_OFF, 0);
-		acc = chunk_sum(v0, c0, hi, acc);
-		acc = chunk_sum(v1, c1, hi, acc);
-	}
-	return wave_sum(acc);
-}
-
-// Wave-uniform value: readfirstlane tells the compiler it lives in an SGPR
-// (otherwise a readlane index it cannot prove uniform becomes a waterfall loop).
+// Wave-uniform value: readfirstlane tells the compiler it lives in an SGPR.
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Candidate set of a tile: bit l of word 2g (+1 for lanes 32..63) = frame 64g + l
-// has a tail.  Scalar.
-template <int H>
-struct cand_set {
-	uint32_t m[2 * H];
-	// first candidate at or after frame f (64 H when none)
-	__device__ __forceinline__ uint32_t from(uint32_t f) const
-	{
-		uint32_t r = 64u * H;
-#pragma unroll
-		for (int w = 2 * H - 1; w >= 0; w--) {
-			const uint32_t base = 32u * w;
-			const uint32_t x = f <= base ? m[w] : (f < base + 32u ? m[w] & (~0u << (f - base)) : 0u);
-			r = x ? base + (uint32_t)__builtin_ctz(x) : r;
-		}
-		return uni(r);
-	}
-};
-
-// readlane of frame f's value (f uniform) from the per-group registers v[g] (lane = frame % 64)
-template <int H>
-__device__ __forceinline__ uint32_t frame_val(const uint32_t (&v)[H], uint32_t f)
-{
-	uint32_t r = 0;
-#pragma unroll
-	for (int g = 0; g < H; g++) {
-		const uint32_t x = __builtin_amdgcn_readlane(v[g], f & 63u);
-		r = (f >> 6) == (uint32_t)g ? x : r;
-	}
-	return uni(r);
-}
-
-// Wave total in VALU: row scans (4 DPP row shifts), then row_bcast:15 and
-// row_bcast:31 carry the row totals up; lane 63 holds the sum (one readlane).
-__device__ __forceinline__ uint32_t wave_total(uint32_t v)
+// Inclusive prefix sum over the 64 lanes: row scans (4 DPP row shifts), then
+// row_bcast:15 and row_bcast:31 carry the row totals up.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v)
 {
 	int x = (int)v;
 	x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);   // row_shr:1
@@ -827,45 +791,21 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t v)
 	x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);   // row_shr:8
 	x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
 	x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
-	return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+	return (uint32_t)x;
 }
 
-// Streamer sidx over its run of the span; sums go to row[] (this wave's LDS row).
-// Per 1 KiB block the overlapping tails (at most STREAM_NT on the fast path)
-// are a run of consecutive candidates, fetched with scalar code and cached in
-// SGPRs; each lane takes the last of them starting at or before its chunk
-// (3 VALU per tail), sums its chunk once with that tail's end mask, and one
-// VALU wave total per (block, tail) accumulates into the tail's scalar sum.
-// Blocks with more tail starts (frames of ~100-250 B) finish the rest one
-// masked reduction at a time.
-#define STREAM_NT 4
-template <int H, int S, int AUX>
-__device__ __forceinline__ void stream_span(__amdgpu_buffer_rsrc_t rs, const uint32_t (&lo)[H],
-                                            const uint32_t (&hi)[H], const cand_set<H> &cs, uint32_t nact,
-                                            uint32_t A, uint32_t Z, uint32_t sidx, uint32_t lane, uint32_t *row)
+// Streamer sidx of S over its run of the span [A, Z); the frame lanes' sums go
+// to row[lane].  DBG 4 (probe builds): loads only.
+template <int S, int AUX, int DBG = 0>
+__device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t lo_l, uint32_t hi_l, uint32_t A,
+                                            uint32_t Z, uint32_t sidx, uint32_t lane, uint32_t *row, u32x4 *s_raw)
 {
-	constexpr uint32_t END = 64u * H;
 	const uint32_t nblk = (Z - A + 1023u) >> 10;
 	const uint32_t b0 = uni((nblk * sidx) / S), b1 = uni((nblk * (sidx + 1u)) / S);
-	if (b0 >= b1)
-		return;
-	// first candidate whose tail ends past the run start (hi is non-decreasing
-	// over the active frames of a tile in buffer order): binary search
-	uint32_t t;
-	{
-		const uint32_t c0 = A + (b0 << 10);
-		uint32_t l = 0, r = nact;
-		while (l < r) {
-			const uint32_t mid = uni((l + r) >> 1);
-			if (frame_val<H>(hi, mid) <= c0)
-				l = mid + 1u;
-			else
-				r = mid;
-		}
-		t = cs.from(l);
-	}
-	uint32_t tlo = t < END ? frame_val<H>(lo, t) : ~0u, thi = t < END ? frame_val<H>(hi, t) : 0u;
-	uint32_t acc = 0;   // this run's sum of tail t so far (scalar)
+	const bool cand = hi_l > lo_l;
+	const uint32_t ec_l = (hi_l - 1u) & ~15u;
+	const uint32_t R1 = A + (b1 << 10);
+	uint32_t acc = 0, carry = 0;
 
 	u32x4 v[STREAM_U];
 #pragma unroll
@@ -878,133 +818,74 @@ __device__ __forceinline__ void stream_span(__amdgpu_buffer_rsrc_t rs, const uin
 #pragma unroll
 		for (int i = 0; i < STREAM_U; i++) {
 			const uint32_t b = k + (uint32_t)i;
-			const uint32_t c0 = A + (b << 10), c1 = c0 + 1024u, c = c0 + 16u * lane;
-			if (b < b1 && tlo < c1) {          // t < END is implied (tlo = ~0 past the end)
-				// tails overlapping [c0, c1): ju[0] = t, then while the previous one ends here
-				uint32_t ju[STREAM_NT], jlo[STREAM_NT], jhi[STREAM_NT];
-				ju[0] = t; jlo[0] = tlo; jhi[0] = thi;
-				uint32_t m = 1;
-#pragma unroll
-				for (int j = 1; j < STREAM_NT; j++) {
-					ju[j] = END; jlo[j] = ~0u; jhi[j] = 0u;
-					if (m == (uint32_t)j && jhi[j - 1] <= c1) {
-						const uint32_t u = cs.from(ju[j - 1] + 1u);
-						const uint32_t ulo = u < END ? frame_val<H>(lo, u) : ~0u;
-						if (ulo < c1) {
-							ju[j] = u; jlo[j] = ulo; jhi[j] = frame_val<H>(hi, u);
-							m = j + 1;
-						}
-					}
-				}
-				uint32_t my_hi = 0, my_j = STREAM_NT;
-#pragma unroll
-				for (int j = 0; j < STREAM_NT; j++) {
-					const bool sel = (uint32_t)j < m && c >= jlo[j];
-					my_hi = sel ? jhi[j] : my_hi;
-					my_j = sel ? (uint32_t)j : my_j;
-				}
-				const uint32_t sv = chunk_sum(v[i], c, my_hi, 0u);
-				bool open = false;                              // the last tail continues past c1
-#pragma unroll
-				for (int j = 0; j < STREAM_NT; j++) {
-					if ((uint32_t)j < m) {
-						acc += wave_total(my_j == (uint32_t)j ? sv : 0u);
-						if (jhi[j] > c1) {
-							open = true;
-							t = ju[j]; tlo = jlo[j]; thi = jhi[j];   // continues in the next block
-						} else {
-							if (lane == 0)
-								row[ju[j]] = acc;
-							acc = 0;
-							t = END; tlo = ~0u; thi = 0u;
-							if ((uint32_t)j + 1u == m) {             // next candidate after the last
-								t = cs.from(ju[j] + 1u);
-								tlo = t < END ? frame_val<H>(lo, t) : ~0u;
-								thi = t < END ? frame_val<H>(hi, t) : 0u;
-							}
-						}
-					}
-				}
-				// more tails start in this block than the fast path holds (the last
-				// fast-path tail ended here and the next candidate starts here too)
-				while (!open && tlo < c1) {
-					const bool in = c >= tlo && c < thi;
-					acc += wave_total(in ? chunk_sum(v[i], c, thi, 0u) : 0u);
-					if (thi > c1) {
-						open = true;
-						break;
-					}
-					if (lane == 0)
-						row[t] = acc;
-					acc = 0;
-					t = cs.from(t + 1u);
-					tlo = t < END ? frame_val<H>(lo, t) : ~0u;
-					thi = t < END ? frame_val<H>(hi, t) : 0u;
+			if constexpr (DBG & 4) {
+				acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+			} else if (b < b1) {
+				const uint32_t c0 = A + (b << 10);
+				uint32_t s = add16x2(0u, v[i].x);
+				s = add16x2(s, v[i].y);
+				s = add16x2(s, v[i].z);
+				s = add16x2(s, v[i].w);
+				const uint32_t x = wave_scan(s);
+				const uint32_t E = carry + x - s;
+				carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+				const uint32_t rl = lo_l - c0, re = ec_l - c0;
+				const bool es = cand && rl < 1024u, ee = cand && re < 1024u;
+				const uint64_t me = __ballot(ee);
+				if (__ballot(es) | me) {
+					if (me)
+						s_raw[lane] = v[i];
+					const uint32_t Es = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rl >> 2) & 0xFCu), (int)E);
+					const uint32_t Ee = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((re >> 2) & 0xFCu), (int)E);
+					acc = es ? acc - Es : acc;
+					if (ee)
+						acc += Ee + chunk_sum(s_raw[(re >> 4) & 63u], ec_l, hi_l, 0u);
 				}
 			}
 			const uint32_t bn = b + STREAM_U;
 			v[i] = load16<AUX>(rs, bn < b1 ? A + (bn << 10) + 16u * lane : ZERO_OFF, 0);
 		}
 	}
-	if (t < END && acc && lane == 0)
-		row[t] = acc;                        // tail continuing into the next run
-}
-
-// Streamer loads of its run with no ownership work (DBG 4 of classify_tile_stream).
-template <int S, int AUX>
-__device__ __forceinline__ void stream_span_loads(__amdgpu_buffer_rsrc_t rs, uint32_t A, uint32_t Z, uint32_t sidx,
-                                                  uint32_t lane, uint32_t *row)
-{
-	const uint32_t nblk = (Z - A + 1023u) >> 10;
-	const uint32_t b0 = (nblk * sidx) / S, b1 = (nblk * (sidx + 1u)) / S;
-	uint32_t x = 0;
-	u32x4 v[STREAM_U];
-#pragma unroll
-	for (int i = 0; i < STREAM_U; i++) {
-		const uint32_t b = b0 + i;
-		v[i] = load16<AUX>(rs, b < b1 ? A + (b << 10) + 16u * lane : ZERO_OFF, 0);
+	if constexpr (DBG & 4) {
+		if (acc == 0x9E3779B9u)
+			row[lane] = acc;
+		return;
 	}
-#pragma unroll 1
-	for (uint32_t k = b0; k < b1; k += STREAM_U) {
-#pragma unroll
-		for (int i = 0; i < STREAM_U; i++) {
-			x ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
-			const uint32_t b = k + i + STREAM_U;
-			v[i] = load16<AUX>(rs, b < b1 ? A + (b << 10) + 16u * lane : ZERO_OFF, 0);
-		}
-	}
-	if (x == 0x9E3779B9u)
-		row[lane] = x;
+	if (cand && lo_l < R1 && ec_l >= R1)
+		acc += carry;                        // tail continuing past the run
+	row[lane] = acc;
 }
 
 // DBG (probe builds only, the library uses 0): 1 no parse/records, 2 no header
 // window loads, 4 streamer loads only.
-template <int H, int S, int VAR, int DBG = 0>
+template <int S, int VAR, int DBG = 0>
 __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, uint32_t tile)
 {
-	constexpr uint32_t TILE = 64u * H;
 	constexpr int AUX = TAIL_AUX(VAR);
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
-	__shared__ uint32_t s_part[S][TILE];   // streamer s's tail sums
+	__shared__ uint32_t s_part[S][64];   // streamer s's tail sums
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
+	__shared__ __attribute__((aligned(16))) u32x4 s_raw[S][64];   // stream_scan's block copies
 
 	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
 	const uint32_t nbytes = kp.frames_bytes;
-	const uint32_t nact = min(TILE, kp.n - tile * TILE);
+	const uint32_t nact = min(64u, kp.n - tile * 64u);
 
-	if (wave < (uint32_t)H) {
-		// ---- header wave h: frames 64h .. 64h+63 of the tile.  Every header
-		// wave fills s_tab with the same words (a wave's own LDS accesses are
-		// ordered, so each reads tables it wrote itself) ----
-		const uint32_t j = 64u * wave + lane;
-		const uint32_t p = tile * TILE + j;
-		const bool active = j < nact;
-		uint32_t o = 0, cap = 0;
-		if (active) {
-			o = kp.off[p];
-			cap = eff_caplen(o, kp.len[p], nbytes);
-		}
+	// every wave reads the tile's descriptors (lane = frame)
+	const uint32_t p = tile * 64u + lane;
+	const bool active = lane < nact;
+	uint32_t o = 0, cap = 0;
+	if (active) {
+		o = kp.off[p];
+		cap = eff_caplen(o, kp.len[p], nbytes);
+	}
+	// speculative tail bounds from the capture length: [split, off + caplen)
+	const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
+	const uint32_t hi_l = active ? o + cap : 0u;
+
+	if (wave == 0) {
+		// ---- header wave (fills s_tab itself: a wave's LDS accesses are ordered) ----
 		hdr_win_t win;
 		if constexpr (DBG & 2) {
 #pragma unroll
@@ -1018,18 +899,16 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 			const u32x4 a = tg[lane], b = tg[lane + 64];
 			reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
 			reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
-			if (wave == 0 && lane <= MOSRX_R_COUNT)
+			if (lane <= MOSRX_R_COUNT)
 				s_cnt[lane] = 0;
 		}
-		const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
-		const uint32_t hi_l = active ? o + cap : 0u;
 		if constexpr (DBG & 1) {
 			uint32_t x = 0;
 #pragma unroll
 			for (int i = 0; i < WIN_RAW; i++)
 				x ^= win.raw[i];
 			__syncthreads();   // B
-			if (active && (x ^ s_part[0][j]) == 0x9E3779B9u)
+			if (active && (x ^ s_part[0][lane]) == 0x9E3779B9u)
 				kp.out[p].rss = x;
 		} else {
 			const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab);
@@ -1038,60 +917,29 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 			if (h.has_tail) {
 #pragma unroll
 				for (int s = 0; s < S; s++)
-					tail += s_part[s][j];
+					tail += s_part[s][lane];
 			}
 			hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, tail, p, active, lane, s_cnt);
 		}
 	} else {
-		// ---- streamer: every frame's descriptor of the tile, group g in lo[g]/hi[g] ----
-		const uint32_t sidx = wave - H;
+		// ---- streamer sidx ----
+		const uint32_t sidx = wave - 1u;
 		uint32_t *row = s_part[sidx];
-#pragma unroll
-		for (int g = 0; g < H; g++)
-			row[64u * g + lane] = 0;
-		uint32_t lo[H], hi[H], o[H];
-		cand_set<H> cs;
-		bool sorted = true;
-#pragma unroll
-		for (int g = 0; g < H; g++) {
-			const uint32_t j = 64u * g + lane;
-			o[g] = 0;
-			uint32_t cap = 0;
-			if (j < nact) {
-				o[g] = kp.off[tile * TILE + j];
-				cap = eff_caplen(o[g], kp.len[tile * TILE + j], nbytes);
-			}
-			lo[g] = (o[g] + (uint32_t)MOSRX_WINDOW_END) & ~15u;
-			hi[g] = j < nact ? o[g] + cap : 0u;
-			const uint64_t cm = __ballot(hi[g] > lo[g]);
-			cs.m[2 * g] = uni((uint32_t)cm);
-			cs.m[2 * g + 1] = uni((uint32_t)(cm >> 32));
-		}
+		row[lane] = 0;
 		// buffer order: the next frame starts at or after this capture's end
-#pragma unroll
-		for (int g = 0; g < H; g++) {
-			const uint32_t j = 64u * g + lane;
-			uint32_t onext = (uint32_t)__shfl_down((int)o[g], 1);
-			if (g + 1 < H)
-				onext = lane == 63u ? __builtin_amdgcn_readlane(o[g + 1 < H ? g + 1 : g], 0) : onext;
-			sorted = sorted && __ballot(j + 1u < nact && onext < hi[g]) == 0;
-		}
-		if constexpr (DBG & 4) {
-			stream_span_loads<S, AUX>(rs, __builtin_amdgcn_readlane(lo[0], 0),
-			                          frame_val<H>(hi, nact - 1u), sidx, lane, row);
-		} else if (sorted) {
-			const uint32_t A = __builtin_amdgcn_readlane(lo[0], 0);
-			const uint32_t Z = frame_val<H>(hi, nact - 1u);   // hi is non-decreasing in buffer order
+		const uint32_t onext = (uint32_t)__shfl_down((int)o, 1);
+		const bool sorted = __ballot(lane + 1u < nact && onext < hi_l) == 0;
+		if (sorted) {
+			const uint32_t A = uni(__builtin_amdgcn_readlane(lo_l, 0));
+			const uint32_t Z = uni(__builtin_amdgcn_readlane(hi_l, nact - 1u));   // non-decreasing in buffer order
 			if (Z > A)
-				stream_span<H, S, AUX>(rs, lo, hi, cs, nact, A, Z, sidx, lane, row);
+				stream_scan<S, AUX, DBG>(rs, lo_l, hi_l, A, Z, sidx, lane, row, s_raw[sidx]);
 		} else {
-			for (uint32_t f = cs.from(0); f < TILE; f = cs.from(f + 1)) {
-				if (f % S == sidx) {
-					const uint32_t x = span_sum<AUX>(rs, frame_val<H>(lo, f), frame_val<H>(hi, f), lane);
-					if (lane == 0)
-						row[f] = x;
-				}
-			}
+			const bool cand = hi_l > lo_l;
+			const uint64_t cmask = __ballot(cand);
+			const uint32_t rank_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(cmask >> 32),
+			                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)cmask, 0u));
+			tail_streamers<S, AUX>(rs, nbytes, lo_l, hi_l, cand, cmask, rank_l, sidx, lane, row);
 		}
 		__syncthreads();   // B
 	}
@@ -1104,13 +952,18 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 	if constexpr (KIND == MOSRX_KIND_SMALL)
 		classify_tile_small<VAR>(kp, tile);
 	else if constexpr (MOSRX_KIND_IS_STREAM(KIND))
-		classify_tile_stream<MOSRX_KIND_H(KIND), MOSRX_KIND_S(KIND), VAR>(kp, tile);
+		classify_tile_stream<MOSRX_KIND_S(KIND), VAR>(kp, tile);
 	else
 		classify_tile_large<MOSRX_KIND_H(KIND), MOSRX_KIND_S(KIND), VAR>(kp, tile);
 }
 
+// Stream shapes are held to 80 VGPRs (6 waves per SIMD): the unsorted-tile
+// fallback would otherwise push them to 81-82 and 5 waves.
+#define MIN_WAVES(kind) (MOSRX_KIND_IS_STREAM(kind) ? 6 : 1)
+
 template <int KIND, int VAR>
-__global__ __launch_bounds__(WG_THREADS(KIND)) void mosrx_classify_kernel(mosrx_kparams kp)
+__global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))
+void mosrx_classify_kernel(mosrx_kparams kp)
 {
 	classify_tile<KIND, VAR>(kp, blockIdx.x);
 }
@@ -1118,7 +971,8 @@ __global__ __launch_bounds__(WG_THREADS(KIND)) void mosrx_classify_kernel(mosrx_
 // Batch queue: one launch over nb resident batches (descriptor table in HBM).
 // Workgroup b finds its batch by a binary search of tile_base[] (scalar loads).
 template <int KIND, int VAR>
-__global__ __launch_bounds__(WG_THREADS(KIND)) void mosrx_classify_queue_kernel(mosrx_qparams qp)
+__global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))
+void mosrx_classify_queue_kernel(mosrx_qparams qp)
 {
 	const uint32_t b = blockIdx.x;
 	uint32_t lo = 0, hi = qp.nb;               // find k: tile_base[k] <= b < tile_base[k+1]
@@ -1206,8 +1060,7 @@ extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles,
 	static void (*const tab[MOSRX_KIND_COUNT][2])(const mosrx_qparams *, uint32_t, hipStream_t) = {
 		QROW(MOSRX_KIND_SMALL), QROW(MOSRX_KIND_LARGE), QROW(MOSRX_KIND_MID),
 		QROW(MOSRX_KIND_L12), QROW(MOSRX_KIND_L24), QROW(MOSRX_KIND_L28),
-		QROW(MOSRX_KIND_S14), QROW(MOSRX_KIND_S12), QROW(MOSRX_KIND_S24),
-		QROW(MOSRX_KIND_S22), QROW(MOSRX_KIND_S42), QROW(MOSRX_KIND_S44)};
+		QROW(MOSRX_KIND_S14), QROW(MOSRX_KIND_S12), QROW(MOSRX_KIND_S13), QROW(MOSRX_KIND_S16)};
 #undef QROW
 	tab[kind][(variant >> 1) & 1](qp, total_tiles, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
@@ -1224,8 +1077,7 @@ extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int vari
 	static void (*const tab[MOSRX_KIND_COUNT][3])(const mosrx_kparams *, hipStream_t) = {
 		KROW(MOSRX_KIND_SMALL), KROW(MOSRX_KIND_LARGE), KROW(MOSRX_KIND_MID),
 		KROW(MOSRX_KIND_L12), KROW(MOSRX_KIND_L24), KROW(MOSRX_KIND_L28),
-		KROW(MOSRX_KIND_S14), KROW(MOSRX_KIND_S12), KROW(MOSRX_KIND_S24),
-		KROW(MOSRX_KIND_S22), KROW(MOSRX_KIND_S42), KROW(MOSRX_KIND_S44)};
+		KROW(MOSRX_KIND_S14), KROW(MOSRX_KIND_S12), KROW(MOSRX_KIND_S13), KROW(MOSRX_KIND_S16)};
 #undef KROW
 	tab[kind][(kp->flags & (MOSRX_KF_TX_IP | MOSRX_KF_TX_TCP)) ? 2 : (variant >> 1) & 1](kp, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;

@@ -1,4 +1,4 @@
-// probe_classify.hip — time shares of the LARGE classify tile (diagnostic only).
+// probe_classify.hip — time shares of the LARGE and stream classify tiles (diagnostic only).
 // Builds the library's kernel source with the DBG knob of classify_tile_large
 // (1: no header parse/records, 2: no header window loads, 4: no streamer sums)
 // and times each build on the BASELINE config #3 trace, back-to-back and one
@@ -16,10 +16,10 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(MINB > 1 ? 
 	classify_tile_large<1, 4, 2, DBG>(kp, blockIdx.x);
 }
 
-template <int H, int S, int DBG>
-__global__ __launch_bounds__(64 * (H + S)) void k_sdbg(mosrx_kparams kp)
+template <int S, int DBG, int W = 6>
+__global__ __launch_bounds__(64 * (1 + S)) __attribute__((amdgpu_waves_per_eu(W))) void k_sdbg(mosrx_kparams kp)
 {
-	classify_tile_stream<H, S, 2, DBG>(kp, blockIdx.x);
+	classify_tile_stream<S, 2, DBG>(kp, blockIdx.x);
 }
 
 typedef void (*lfn)(const mosrx_kparams *, hipStream_t);
@@ -28,10 +28,10 @@ static void launch_dbg(const mosrx_kparams *kp, hipStream_t s)
 {
 	hipLaunchKernelGGL((k_dbg<DBG, MINB>), dim3((kp->n + 63) / 64), dim3(320), 0, s, *kp);
 }
-template <int H, int S, int DBG>
+template <int S, int DBG, int W = 6>
 static void launch_sdbg(const mosrx_kparams *kp, hipStream_t s)
 {
-	hipLaunchKernelGGL((k_sdbg<H, S, DBG>), dim3((kp->n + 64 * H - 1) / (64 * H)), dim3(64 * (H + S)), 0, s, *kp);
+	hipLaunchKernelGGL((k_sdbg<S, DBG, W>), dim3((kp->n + 63) / 64), dim3(64 * (1 + S)), 0, s, *kp);
 }
 static void launch_product(const mosrx_kparams *kp, hipStream_t s)
 {
@@ -105,21 +105,15 @@ int main(int argc, char **argv)
 	printf("trace kind %d n %u: %.2f MB algorithmic\n", kind, n, bytes / 1e6);
 	run("product LARGE", launch_product, kps, nb, bytes);
 	run("product S14", launch_stream, kps, nb, bytes);
-	run("DBG 0 (same as product)", launch_dbg<0>, kps, nb, bytes);
-	run("DBG 3 no header work at all", launch_dbg<3>, kps, nb, bytes);
-	run("DBG 4 no streamer sums", launch_dbg<4>, kps, nb, bytes);
-	run("DBG 5 no parse + no sums", launch_dbg<5>, kps, nb, bytes);
-	run("DBG 7 loads only", launch_dbg<7>, kps, nb, bytes);
-	run("S14 DBG 0", launch_sdbg<1, 4, 0>, kps, nb, bytes);
-	run("S14 DBG 4 streamer loads only", launch_sdbg<1, 4, 4>, kps, nb, bytes);
-	run("S14 DBG 7 loads only", launch_sdbg<1, 4, 7>, kps, nb, bytes);
-	run("S14 DBG 3 no header work", launch_sdbg<1, 4, 3>, kps, nb, bytes);
-	run("S44 DBG 0", launch_sdbg<4, 4, 0>, kps, nb, bytes);
-	run("S44 DBG 4", launch_sdbg<4, 4, 4>, kps, nb, bytes);
-	run("S44 DBG 7", launch_sdbg<4, 4, 7>, kps, nb, bytes);
-	run("S24 DBG 0", launch_sdbg<2, 4, 0>, kps, nb, bytes);
-	run("S22 DBG 0", launch_sdbg<2, 2, 0>, kps, nb, bytes);
-	run("S42 DBG 0", launch_sdbg<4, 2, 0>, kps, nb, bytes);
-	run("S12 DBG 0", launch_sdbg<1, 2, 0>, kps, nb, bytes);
+	run("S13 w6", launch_sdbg<3, 0, 6>, kps, nb, bytes);
+	run("S13 w7", launch_sdbg<3, 0, 7>, kps, nb, bytes);
+	run("S13 w8", launch_sdbg<3, 0, 8>, kps, nb, bytes);
+	run("S14 w7", launch_sdbg<4, 0, 7>, kps, nb, bytes);
+	run("S14 w8", launch_sdbg<4, 0, 8>, kps, nb, bytes);
+	run("S12 w6", launch_sdbg<2, 0, 6>, kps, nb, bytes);
+	run("S12 w8", launch_sdbg<2, 0, 8>, kps, nb, bytes);
+	run("S13 DBG 4 streamer loads only", launch_sdbg<3, 4>, kps, nb, bytes);
+	run("S13 DBG 3 no header work", launch_sdbg<3, 3>, kps, nb, bytes);
+	run("S13 DBG 7 loads only", launch_sdbg<3, 7>, kps, nb, bytes);
 	return 0;
 }

@@ -239,8 +239,8 @@ def test_batch_queue_one_launch(gpu_ctx, kind, n, nb):
 
 
 # kernel shapes forced through variant bits 2-6 (value - 1: SMALL, LARGE, MID, L12, L24, L28, S14, S12,
-# S24, S22, S42, S44) with both tail-load cache policies; every shape must be exact on every frame mix
-STREAM_VARIANTS = [((k + 1) << 2) | 2 for k in range(6, 12)]
+# S13, S16) with both tail-load cache policies; every shape must be exact on every frame mix
+STREAM_VARIANTS = [((k + 1) << 2) | 2 for k in range(6, 10)]
 
 
 @pytest.mark.parametrize("variant", [2, 6, 10, 14, 18, 22, 26, 0, 8, 12] + STREAM_VARIANTS + [28])
@@ -272,7 +272,7 @@ def test_flow_hash_golden(gpu_ctx, fix):
     np.testing.assert_array_equal(fh, ofh)
 
 
-@pytest.mark.parametrize("variant", [2, 6, 10, 14, 30, 46])
+@pytest.mark.parametrize("variant", [2, 6, 10, 14, 30, 38])
 @pytest.mark.parametrize("kind,n", [(mosrx.TRACE_S64, 32_768), (mosrx.TRACE_M1500, 16_384),
                                     (mosrx.TRACE_IMIX, 65_536)])
 def test_flow_hash_device(gpu_ctx, variant, kind, n):

@@ -55,6 +55,7 @@ BPF_BENCH = [("tcp", 0), ("tcp port 80", 0), ("tcp[tcpflags] & tcp-syn != 0", 1)
              ("host 10.0.0.1 and port 80", 0), ("ip[8] < 64", 1), ("tcp[((tcp[12:1] & 0xf0) >> 2):4] = 0x47455420", 1),
              ("portrange 1000-2000", 0)]
 QUEUE_DEPTH = 64
+PREWARM_S = 0.3
 STREAMS = 2   # rx batches in flight per GPU (scripts/tune_streams.py: 2 beats 1 and 4)
 
 
@@ -126,6 +127,15 @@ def load_pmc(key: str):
         return None
 
 
+def prewarm(fn, seconds: float = PREWARM_S):
+    """Untimed GPU work before a workload's warmup steps: the MI355X's clocks
+    ramp over the first ~100 ms of load, and a few ms of steps alone measured
+    ~9 % slow (gpurun_out r01: 22.4 us per 1500 B launch after 2 ms, 20.5 after 20 ms)."""
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        fn()
+
+
 def measure(ctx, dist, key, steps, warmup, rank):
     kind, batch, label = WORKLOADS[key]
     params = mosrx.default_params(skip_tcp_csum=1 if key == "S64_hdr" else 0)
@@ -143,6 +153,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op == mosrx.OP_TX_CSUM else 0
         if op == mosrx.OP_BPF:
             ctx.bpf_set(bpf_bench_programs())
+        prewarm(lambda: ctx.time_op(op, dbs, 200, STREAMS, arg, kernels=False))
         if warmup:
             ctx.time_op(op, dbs, warmup, STREAMS, arg, kernels=False)
         ctx.device_sync()
@@ -153,7 +164,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         dist.barrier()
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
-        kk = min(steps, 200)
+        kk = 500
         kern_ms = ctx.time_op(op, dbs, kk, 1, arg, kernels=False)[0] / kk
         _, kern_iso = ctx.time_op(op, dbs, kk, 1, arg, total=False)
     elif key.endswith("_queue"):
@@ -162,22 +173,25 @@ def measure(ctx, dist, key, steps, warmup, rank):
         qs = [ctx.queue(dbs[i:i + QUEUE_DEPTH]) for i in range(0, len(dbs) - QUEUE_DEPTH + 1, QUEUE_DEPTH)]
         ab *= QUEUE_DEPTH
         batch *= QUEUE_DEPTH
+        prewarm(lambda: qs[0].time(20, qs[1:], kernels=False))
         if warmup:
-            qs[0].time(warmup, qs[1:])
+            qs[0].time(warmup, qs[1:], kernels=False)
         ctx.device_sync()
         dist.barrier()
         t0 = time.perf_counter()
-        dev_ms, _ = qs[0].time(steps, qs[1:])
+        dev_ms, _ = qs[0].time(steps, qs[1:], kernels=False)
         ctx.device_sync()
         dist.barrier()
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
-        _, kern_ms = qs[0].time(min(steps, 64), qs[1:])
-        kern_iso = kern_ms
+        kk = min(steps, 64)
+        tot_ms, kern_iso = qs[0].time(kk, qs[1:])
+        kern_ms = tot_ms / kk
         for q in qs:
             q.destroy()
     else:
         # warmup (untimed)
+        prewarm(lambda: ctx.time_dev_streams(dbs, 200, STREAMS))
         if warmup:
             ctx.time_dev_streams(dbs, warmup, STREAMS)
         ctx.device_sync()
@@ -194,7 +208,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         # K back-to-back launches on the launch stream (the figure rocprofv3's
         # kernel trace reports); the isolated figure (events around each single
         # launch, dispatch included) is kept beside it
-        kk = min(steps, 200)
+        kk = 500
         kern_ms = ctx.time_dev_streams(dbs, kk, 1) / kk
         kern_iso = ctx.time_dev_kernels(dbs, kk)
     for d in dbs:
@@ -324,8 +338,8 @@ def main():
     global STREAMS
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workloads", default="M1500,S64,S64_hdr,S64_queue,IMIX,M1500_fh,M1500_tx,IMIX_bpf")
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="rx batches in flight (1 = strictly serial launches, as for rocprof summaries)")

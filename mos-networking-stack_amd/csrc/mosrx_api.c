@@ -247,13 +247,17 @@ int mosrx__check_batch(const mosrx_batch *b, int dev)
 }
 
 /* Kernel shape: SMALL when every frame fits the header window (max_len known
- * and <= 94); otherwise a stream shape, S14 for MTU-sized frames and S13 below
- * a 1 KiB mean frame footprint.  Measured on MI355X
- * (profiles/r01_probe_stream_scan.log): 1500 B config S14 19.4 us, S13 19.6,
- * LARGE 20.7; IMIX S13 20.4 us, S14 21.9, LARGE 41.8.  Every other shape stays
- * reachable for tuning: variant bits 2-6 force one (value - 1, MOSRX_KIND_*). */
+ * and <= 94); otherwise S13 (one header wave + three span streamers, 54 VGPRs,
+ * 8 waves per SIMD).  Measured on MI355X (profiles/r01_probe_w8.log,
+ * back-to-back launches): 1500 B config S13 18.75 us, S14 18.73, S12 18.73,
+ * LARGE 20.84; IMIX S13 20.5 us, S14 21.6, S12 21.7, LARGE 41.8; IMIX with
+ * descriptors in reverse buffer order (unsorted tiles) S13 43.5, LARGE 41.6.
+ * Every other shape stays reachable for tuning: variant bits 2-6 force one
+ * (value - 1, MOSRX_KIND_*). */
 static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_t n)
 {
+	(void)bytes;
+	(void)n;
 	const int force = (c->variant >> 2) & 31;
 	if (force && force <= MOSRX_KIND_COUNT)
 		return force - 1;

@@ -773,8 +773,8 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 // chunk's bytes below hi from an LDS copy of the block.  A tail entering the
 // run counts from 0, one leaving it ends at the run total.  No ownership
 // walk, no per-tail reduction; the header wave adds the S rows.  Tiles not in
-// buffer order stream frame by frame with the LARGE tile's streamers.
-#define STREAM_U 8
+// buffer order stream tail by tail (stream_frames).
+#define STREAM_U 4
 #define ZERO_OFF 0xFFFFFFF0u   // buffer offset past any batch (loads there are never consumed)
 
 // Wave-uniform value: readfirstlane tells the compiler it lives in an SGPR.
@@ -796,7 +796,7 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v)
 
 // Streamer sidx of S over its run of the span [A, Z); the frame lanes' sums go
 // to row[lane].  DBG 4 (probe builds): loads only.
-template <int S, int AUX, int DBG = 0>
+template <int S, int AUX, int DBG = 0, int U = STREAM_U>
 __device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t lo_l, uint32_t hi_l, uint32_t A,
                                             uint32_t Z, uint32_t sidx, uint32_t lane, uint32_t *row, u32x4 *s_raw)
 {
@@ -807,16 +807,16 @@ __device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t 
 	const uint32_t R1 = A + (b1 << 10);
 	uint32_t acc = 0, carry = 0;
 
-	u32x4 v[STREAM_U];
+	u32x4 v[U];
 #pragma unroll
-	for (int i = 0; i < STREAM_U; i++) {
+	for (int i = 0; i < U; i++) {
 		const uint32_t b = b0 + (uint32_t)i;
 		v[i] = load16<AUX>(rs, b < b1 ? A + (b << 10) + 16u * lane : ZERO_OFF, 0);
 	}
 #pragma unroll 1
-	for (uint32_t k = b0; k < b1; k += STREAM_U) {
+	for (uint32_t k = b0; k < b1; k += U) {
 #pragma unroll
-		for (int i = 0; i < STREAM_U; i++) {
+		for (int i = 0; i < U; i++) {
 			const uint32_t b = k + (uint32_t)i;
 			if constexpr (DBG & 4) {
 				acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
@@ -842,7 +842,7 @@ __device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t 
 						acc += Ee + chunk_sum(s_raw[(re >> 4) & 63u], ec_l, hi_l, 0u);
 				}
 			}
-			const uint32_t bn = b + STREAM_U;
+			const uint32_t bn = b + U;
 			v[i] = load16<AUX>(rs, bn < b1 ? A + (bn << 10) + 16u * lane : ZERO_OFF, 0);
 		}
 	}
@@ -856,9 +856,43 @@ __device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t 
 	row[lane] = acc;
 }
 
+// Tiles not in buffer order: streamer sidx sums the candidates of rank
+// sidx, sidx + S, ... one tail at a time, 4 KiB per pass.  Lean on registers
+// on purpose (the tile's VGPR count sets its occupancy, and the span path
+// needs 54): such tiles are rare (descriptors reordered after capture).
+template <int S, int AUX>
+__device__ __forceinline__ void stream_frames(__amdgpu_buffer_rsrc_t rs, uint32_t lo_l, uint32_t hi_l,
+                                              uint32_t sidx, uint32_t lane, uint32_t *row)
+{
+	uint64_t m = __ballot(hi_l > lo_l);
+	for (uint32_t r = 0; m; r++, m &= m - 1) {
+		if (r % S != sidx)
+			continue;
+		const uint32_t f = (uint32_t)__builtin_ctzll(m);
+		const uint32_t lo = uni(__builtin_amdgcn_readlane(lo_l, f)), hi = uni(__builtin_amdgcn_readlane(hi_l, f));
+		uint32_t acc = 0;
+#pragma unroll 1
+		for (uint32_t base = lo; base < hi; base += 4096u) {
+			u32x4 v[4];
+#pragma unroll
+			for (int i = 0; i < 4; i++) {
+				const uint32_t c = base + 1024u * i + 16u * lane;
+				v[i] = load16<AUX>(rs, c < hi ? c : ZERO_OFF, 0);
+			}
+#pragma unroll
+			for (int i = 0; i < 4; i++)
+				acc = chunk_sum(v[i], base + 1024u * i + 16u * lane, hi, acc);
+		}
+		const uint32_t x = wave_sum(acc);
+		if (lane == 0)
+			row[f] = x;
+	}
+}
+
 // DBG (probe builds only, the library uses 0): 1 no parse/records, 2 no header
-// window loads, 4 streamer loads only.
-template <int S, int VAR, int DBG = 0>
+// window loads, 4 streamer loads only, 16 no unsorted-tile path, 32 header wave
+// at raised issue priority.
+template <int S, int VAR, int DBG = 0, int U = STREAM_U>
 __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, uint32_t tile)
 {
 	constexpr int AUX = TAIL_AUX(VAR);
@@ -886,6 +920,8 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 
 	if (wave == 0) {
 		// ---- header wave (fills s_tab itself: a wave's LDS accesses are ordered) ----
+		if constexpr (DBG & 32)
+			__builtin_amdgcn_s_setprio(2);
 		hdr_win_t win;
 		if constexpr (DBG & 2) {
 #pragma unroll
@@ -933,13 +969,9 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 			const uint32_t A = uni(__builtin_amdgcn_readlane(lo_l, 0));
 			const uint32_t Z = uni(__builtin_amdgcn_readlane(hi_l, nact - 1u));   // non-decreasing in buffer order
 			if (Z > A)
-				stream_scan<S, AUX, DBG>(rs, lo_l, hi_l, A, Z, sidx, lane, row, s_raw[sidx]);
-		} else {
-			const bool cand = hi_l > lo_l;
-			const uint64_t cmask = __ballot(cand);
-			const uint32_t rank_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(cmask >> 32),
-			                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)cmask, 0u));
-			tail_streamers<S, AUX>(rs, nbytes, lo_l, hi_l, cand, cmask, rank_l, sidx, lane, row);
+				stream_scan<S, AUX, DBG, U>(rs, lo_l, hi_l, A, Z, sidx, lane, row, s_raw[sidx]);
+		} else if constexpr (!(DBG & 16)) {
+			stream_frames<S, AUX>(rs, lo_l, hi_l, sidx, lane, row);
 		}
 		__syncthreads();   // B
 	}
@@ -957,9 +989,9 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 		classify_tile_large<MOSRX_KIND_H(KIND), MOSRX_KIND_S(KIND), VAR>(kp, tile);
 }
 
-// Stream shapes are held to 80 VGPRs (6 waves per SIMD): the unsorted-tile
-// fallback would otherwise push them to 81-82 and 5 waves.
-#define MIN_WAVES(kind) (MOSRX_KIND_IS_STREAM(kind) ? 6 : 1)
+// Stream shapes are held to 64 VGPRs: 8 waves per SIMD (7 for S16, whose
+// 7-wave workgroups fit 4 per CU).
+#define MIN_WAVES(kind) (!MOSRX_KIND_IS_STREAM(kind) ? 1 : (kind) == MOSRX_KIND_S16 ? 7 : 8)
 
 template <int KIND, int VAR>
 __global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))

@@ -495,14 +495,15 @@ class Queue:
         if sync:
             _chk(lib().mosrx_sync(self.ctx.handle), "mosrx_sync")
 
-    def time(self, iters: int, others: list["Queue"] = ()) -> tuple[float, float]:
-        """(total ms, average kernel ms) of `iters` launches cycling over self + others."""
+    def time(self, iters: int, others: list["Queue"] = (), kernels: bool = True) -> tuple[float, float]:
+        """(total ms of `iters` back-to-back launches cycling over self + others,
+        average isolated-launch ms or None when `kernels` is False)."""
         qs = [self] + list(others)
         arr = (C.c_void_p * len(qs))(*[q.handle for q in qs])
         tot, kern = C.c_float(), C.c_float()
-        _chk(lib().mosrx_time_queue(self.ctx.handle, arr, len(qs), iters, C.byref(tot), C.byref(kern)),
-             "mosrx_time_queue")
-        return float(tot.value), float(kern.value)
+        _chk(lib().mosrx_time_queue(self.ctx.handle, arr, len(qs), iters, C.byref(tot),
+                                    C.byref(kern) if kernels else None), "mosrx_time_queue")
+        return float(tot.value), (float(kern.value) if kernels else None)
 
     def destroy(self):
         if self.handle:

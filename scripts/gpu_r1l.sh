@@ -1,6 +1,6 @@
 # occupancy variants of the stream tile
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 100 ./scripts/probe_classify 2 65536 > gpurun_out/probe_occ.log 2>&1 && timeout -k 10 100 ./scripts/probe_classify 3 262144 >> gpurun_out/probe_occ.log 2>&1; rc=$?
-cat gpurun_out/probe_occ.log
+timeout -k 10 100 ./scripts/probe_classify 2 65536 > gpurun_out/probe_u.log 2>&1 && timeout -k 10 100 ./scripts/probe_classify 3 262144 >> gpurun_out/probe_u.log 2>&1; rc=$?
+cat gpurun_out/probe_u.log
 exit $rc

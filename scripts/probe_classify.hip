@@ -16,10 +16,10 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(MINB > 1 ? 
 	classify_tile_large<1, 4, 2, DBG>(kp, blockIdx.x);
 }
 
-template <int S, int DBG, int W = 6>
+template <int S, int DBG, int W = 6, int U = 8>
 __global__ __launch_bounds__(64 * (1 + S)) __attribute__((amdgpu_waves_per_eu(W))) void k_sdbg(mosrx_kparams kp)
 {
-	classify_tile_stream<S, 2, DBG>(kp, blockIdx.x);
+	classify_tile_stream<S, 2, DBG, U>(kp, blockIdx.x);
 }
 
 typedef void (*lfn)(const mosrx_kparams *, hipStream_t);
@@ -28,10 +28,10 @@ static void launch_dbg(const mosrx_kparams *kp, hipStream_t s)
 {
 	hipLaunchKernelGGL((k_dbg<DBG, MINB>), dim3((kp->n + 63) / 64), dim3(320), 0, s, *kp);
 }
-template <int S, int DBG, int W = 6>
+template <int S, int DBG, int W = 6, int U = 8>
 static void launch_sdbg(const mosrx_kparams *kp, hipStream_t s)
 {
-	hipLaunchKernelGGL((k_sdbg<S, DBG, W>), dim3((kp->n + 63) / 64), dim3(64 * (1 + S)), 0, s, *kp);
+	hipLaunchKernelGGL((k_sdbg<S, DBG, W, U>), dim3((kp->n + 63) / 64), dim3(64 * (1 + S)), 0, s, *kp);
 }
 static void launch_product(const mosrx_kparams *kp, hipStream_t s)
 {
@@ -39,7 +39,7 @@ static void launch_product(const mosrx_kparams *kp, hipStream_t s)
 }
 static void launch_stream(const mosrx_kparams *kp, hipStream_t s)
 {
-	mosrx_launch_classify(kp, MOSRX_KIND_S14, 2, s);
+	mosrx_launch_classify(kp, MOSRX_KIND_S13, 2, s);
 }
 
 static int run(const char *name, lfn f, mosrx_kparams *kps, int nb, double bytes)
@@ -85,6 +85,13 @@ int main(int argc, char **argv)
 		printf("trace_gen failed\n");
 		return 1;
 	}
+	if (argc > 3 && argv[3][0] == 'r') {   // descriptors in reverse buffer order: unsorted tiles
+		for (uint32_t i = 0; i < n / 2; i++) {
+			uint32_t to = t.off[i]; t.off[i] = t.off[n - 1 - i]; t.off[n - 1 - i] = to;
+			uint16_t tl = t.len[i]; t.len[i] = t.len[n - 1 - i]; t.len[n - 1 - i] = tl;
+		}
+		printf("descriptors reversed\n");
+	}
 	const int nb = 6;
 	mosrx_kparams kps[nb];
 	uint32_t *tables;
@@ -104,16 +111,15 @@ int main(int argc, char **argv)
 	const double bytes = (double)t.caplen_sum + 22.0 * n;
 	printf("trace kind %d n %u: %.2f MB algorithmic\n", kind, n, bytes / 1e6);
 	run("product LARGE", launch_product, kps, nb, bytes);
-	run("product S14", launch_stream, kps, nb, bytes);
-	run("S13 w6", launch_sdbg<3, 0, 6>, kps, nb, bytes);
-	run("S13 w7", launch_sdbg<3, 0, 7>, kps, nb, bytes);
-	run("S13 w8", launch_sdbg<3, 0, 8>, kps, nb, bytes);
-	run("S14 w7", launch_sdbg<4, 0, 7>, kps, nb, bytes);
-	run("S14 w8", launch_sdbg<4, 0, 8>, kps, nb, bytes);
-	run("S12 w6", launch_sdbg<2, 0, 6>, kps, nb, bytes);
-	run("S12 w8", launch_sdbg<2, 0, 8>, kps, nb, bytes);
-	run("S13 DBG 4 streamer loads only", launch_sdbg<3, 4>, kps, nb, bytes);
-	run("S13 DBG 3 no header work", launch_sdbg<3, 3>, kps, nb, bytes);
-	run("S13 DBG 7 loads only", launch_sdbg<3, 7>, kps, nb, bytes);
+	run("product S13", launch_stream, kps, nb, bytes);
+	run("S13 prio", launch_sdbg<3, 32, 8, 4>, kps, nb, bytes);
+	run("S14 prio", launch_sdbg<4, 32, 8, 4>, kps, nb, bytes);
+	run("S12 prio", launch_sdbg<2, 32, 8, 4>, kps, nb, bytes);
+	run("S13 U2", launch_sdbg<3, 0, 8, 2>, kps, nb, bytes);
+	run("S13 U3", launch_sdbg<3, 0, 8, 3>, kps, nb, bytes);
+	run("S13 U4 DBG 4", launch_sdbg<3, 4, 8, 4>, kps, nb, bytes);
+	run("S13 U4 DBG 1 no parse", launch_sdbg<3, 1, 8, 4>, kps, nb, bytes);
+	run("S13 U4 DBG 2 no window loads", launch_sdbg<3, 2, 8, 4>, kps, nb, bytes);
+	run("S13 U4 DBG 7", launch_sdbg<3, 7, 8, 4>, kps, nb, bytes);
 	return 0;
 }

@@ -10,27 +10,30 @@
 // of its frame (6 x buffer_load_dwordx4 from frame byte 2, realigned with
 // v_alignbyte so the IP header sits dword-aligned in registers), parses every
 // field, runs the ip_fast_csum carry chain, the Toeplitz hash (24 nibble-table
-// lookups in LDS) and the TCP one's-complement sum of the segment bytes before
-// the frame's "split": the first 16-byte-aligned buffer offset at or below
-// frame byte 94.  64-byte frames finish there.
+// lookups in LDS) and the TCP one's-complement sum of the segment bytes in the
+// window: all of them when the datagram ends by frame byte 94 (64-byte frames
+// finish there), else those before the frame's "split", the first
+// 16-byte-aligned buffer offset at or below frame byte 94.
 //
-// Bytes past the split (the "tail") are streamed wave-per-frame with
+// Bytes past the split (the "tail") are streamed by whole waves with
 // coalesced 16-byte-aligned loads, 1 KiB per wave instruction, summed as
 // 16-bit words on the absolute even address grid with v_dot2_u32_u16 and
 // reduced with DPP row steps + 4 readlanes.  The segment-grid sum is the
 // absolute-grid sum, byte-swapped when the frame starts at an odd address
 // (256 * x == bswap16(x) mod 0xFFFF).
 //
-// Two tile shapes (256-thread workgroups):
-//   small (TILE 256): every lane owns a frame; frames that do have a tail are
-//     compacted into an LDS list and streamed by the four waves.  Used when
-//     every frame fits the header window (64-byte configs).
-//   large (TILE 64): every wave loads the tile's 64 descriptors; wave w owns
-//     the tails of frames w, w+4, ... and issues their loads SPECULATIVELY from
-//     the capture length (hi = off + caplen) right after the descriptor load,
-//     so HBM streams while wave 0 parses the headers.  After one barrier the
-//     exact end (off + 14 + tot_len) masks the sums; the next group of four
-//     tails is in flight while the current one is reduced (double buffered).
+// Tile shapes ("kinds", mosrx_internal.h):
+//   small (TILE 256): every lane owns a frame and finishes it in registers when
+//     the datagram ends inside the window (the 64-byte configs); longer frames
+//     are summed by their wave.
+//   large (TILE 64): every wave loads the tile's 64 descriptors; wave 0 parses
+//     the headers while the streamer waves sum whole tails, loads issued
+//     SPECULATIVELY from the capture length (hi = off + caplen) right after
+//     the descriptor load; after one barrier the exact end (off + 14 + tot_len)
+//     corrects the sums.
+//   stream (TILE 64, the default for frames past the window): the streamers
+//     read the tile's tail span in buffer order as plain contiguous 1 KiB wave
+//     loads and attribute the bytes to tails with one prefix scan per block.
 //
 // All frame loads go through a buffer resource whose range is the batch
 // buffer: a bad offset can never fault, out-of-range dwords read as zero.
@@ -135,7 +138,7 @@ __device__ __forceinline__ uint32_t tail_rest(__amdgpu_buffer_rsrc_t rs, uint32_
 // ---------------------------------------------------------------------------
 struct hdr_t {
 	uint32_t o, fend, split_abs;
-	uint32_t wsum;                 // segment-grid sum of the segment bytes before the split
+	uint32_t wsum;                 // segment-grid sum of the segment bytes in the window (before the split)
 	uint32_t saddr, daddr, ip_len, ihl, doff, th0, th3;
 	uint32_t rss, queue, ipc, reason;
 	uint32_t tcw, ipc_tx;          // TX: segment-grid TCP check word, IP checksum with check = 0
@@ -223,11 +226,14 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	// TX: iph->check = 0 first (mos_api.c:1180-1181): the check is frame bytes 24,25 = w[5] bytes 2,3
 	const uint32_t ipc_tx = IS_TX(VAR) ? ip_chain(w, ihl, w[5] & 0xFFFFu) : 0u;
 
-	// TCP segment sum over frame bytes [14+4*ihl, min(fend, split)); the
-	// realigned grid (dword j = frame bytes [4j+2, 4j+6)) is the segment grid.
+	// TCP segment sum over frame bytes [14+4*ihl, wend): the whole segment when
+	// the datagram ends inside the window, else up to the split (the tail
+	// streamers take over there).  The realigned grid (dword j = frame bytes
+	// [4j+2, 4j+6)) is the segment grid.
+	const bool in_win = fend <= (uint32_t)MOSRX_WINDOW_END;
 	uint32_t wsum = 0;
 	{
-		const int wend = (int)min(fend, split);
+		const int wend = (int)(in_win ? fend : split);
 #pragma unroll
 		for (int j = 8; j < WIN_DW; j++) {
 			uint32_t m = keep_lo(wend - (4 * j + 2));
@@ -299,7 +305,7 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	h.saddr = saddr; h.daddr = daddr; h.ip_len = ip_len; h.ihl = ihl; h.doff = doff; h.th0 = th0; h.th3 = th3;
 	h.rss = rss; h.queue = queue; h.ipc = ipc; h.reason = reason; h.verdict = verdict;
 	h.tcw = tcw; h.ipc_tx = ipc_tx; h.tx_ip = tx_ip;
-	h.fields = fields; h.need_tcp = need_tcp; h.has_tail = need_tcp && fend > split; h.is_tcp = is_tcp;
+	h.fields = fields; h.need_tcp = need_tcp; h.has_tail = need_tcp && !in_win; h.is_tcp = is_tcp;
 	return h;
 }
 
@@ -397,16 +403,10 @@ __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffe
 	}
 }
 
-__device__ __forceinline__ void tables_to_lds(const mosrx_kparams &kp, uint32_t *s_tab, uint32_t *s_cnt, uint32_t t)
-{
-	if (t < 256) {                            // RSS nibble tables + queue LUT (2 KiB, L2-resident)
-		s_tab[t] = kp.tables[t];
-		s_tab[t + 256] = kp.tables[t + 256];
-	}
-	if (t <= MOSRX_R_COUNT)
-		s_cnt[t] = 0;
-}
+#define ZERO_OFF 0xFFFFFFF0u   // buffer offset past any batch (loads there are never consumed)
 
+// Wave-uniform value: readfirstlane tells the compiler it lives in an SGPR.
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 __device__ __forceinline__ void store_record(const mosrx_kparams &kp, uint32_t p, u32x4 rec, uint32_t *s_cnt)
 {
@@ -425,22 +425,24 @@ __device__ __forceinline__ void flush_counters(const mosrx_kparams &kp, const ui
 }
 
 // ---------------------------------------------------------------------------
-// small tile: 256 frames, lane per frame, compacted tails
+// small tile: 256 frames, lane per frame
 // ---------------------------------------------------------------------------
+// Every frame whose datagram ends inside the header window (all frames of a
+// batch with max_len <= 94) finishes in its lane: no cross-wave work, no
+// barrier (each wave fills the LDS tables itself; a wave's LDS accesses are
+// ordered).  Longer frames (only when the shape is forced onto them) are
+// summed by their wave tail by tail, 4 KiB per pass.
 template <int VAR>
 __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uint32_t tile)
 {
 	constexpr uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL);
 	constexpr int AUX = TAIL_AUX(VAR);
-	__shared__ uint32_t s_tab[MOSRX_TAB_WORDS];
-	__shared__ uint32_t s_tail_lo[TILE], s_tail_hi[TILE], s_tail_sum[TILE], s_tail_pkt[TILE];
-	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];   // [MOSRX_R_COUNT] = number of tails
+	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
+	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
 
-	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+	const uint32_t t = threadIdx.x, lane = t & 63u;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
 	const uint32_t nbytes = kp.frames_bytes;
-	tables_to_lds(kp, s_tab, s_cnt, t);
-
 	const uint32_t p = tile * TILE + t;
 	const bool active = p < kp.n;
 	uint32_t o = 0, cap = 0;
@@ -450,50 +452,45 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	}
 	hdr_win_t win;
 	hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
-	__syncthreads();   // s_tab, s_cnt ready
+	{
+		const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
+		const u32x4 a = tg[lane], b = tg[lane + 64];
+		reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
+		reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
+	}
+	if (kp.counters) {                        // uniform: the whole workgroup takes this barrier or none
+		if (t <= MOSRX_R_COUNT)
+			s_cnt[t] = 0;
+		__syncthreads();
+	}
 	const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab);
-	if (h.has_tail) {
-		const uint32_t k = atomicAdd(&s_cnt[MOSRX_R_COUNT], 1u);
-		s_tail_pkt[k] = t;
-		s_tail_lo[k] = h.split_abs;
-		s_tail_hi[k] = o + h.fend;
-	}
-	__syncthreads();
-
-	const uint32_t ntail = __builtin_amdgcn_readfirstlane(s_cnt[MOSRX_R_COUNT]);
+	uint32_t tail = 0;
+	for (uint64_t m = __ballot(h.has_tail); m; m &= m - 1) {
+		const uint32_t f = (uint32_t)__builtin_ctzll(m);
+		const uint32_t lo = uni(__builtin_amdgcn_readlane(h.split_abs, f));
+		const uint32_t hi = uni(__builtin_amdgcn_readlane(o + h.fend, f));
+		uint32_t acc = 0;
 #pragma unroll 1
-	for (uint32_t k0 = wave * TAIL_G; k0 < ntail; k0 += 4u * TAIL_G) {
-		uint32_t lo[TAIL_G], hi[TAIL_G];
-		u32x4 v[TAIL_G][TAIL_U];
+		for (uint32_t base = lo; base < hi; base += 4096u) {
+			u32x4 v[4];
 #pragma unroll
-		for (int u = 0; u < TAIL_G; u++) {
-			const bool ok = k0 + u < ntail;
-			lo[u] = ok ? __builtin_amdgcn_readfirstlane(s_tail_lo[k0 + u]) : 0u;
-			hi[u] = ok ? __builtin_amdgcn_readfirstlane(s_tail_hi[k0 + u]) : 0u;
-#pragma unroll
-			for (int q = 0; q < TAIL_U; q++) {
-				const uint32_t c = lo[u] + 1024u * q + 16u * lane;
-				v[u][q] = load16<AUX>(rs, c < hi[u] ? c : nbytes, nbytes);
+			for (int i = 0; i < 4; i++) {
+				const uint32_t c = base + 1024u * i + 16u * lane;
+				v[i] = load16<AUX>(rs, c < hi ? c : ZERO_OFF, 0);
 			}
-		}
 #pragma unroll
-		for (int u = 0; u < TAIL_G; u++) {
-			uint32_t acc = 0;
-#pragma unroll
-			for (int q = 0; q < TAIL_U; q++)
-				acc = chunk_sum(v[u][q], lo[u] + 1024u * q + 16u * lane, hi[u], acc);
-			acc = tail_rest<AUX>(rs, nbytes, lo[u], hi[u], lane, acc);
-			const uint32_t s = wave_sum(acc);
-			if (k0 + u < ntail && lane == 0)
-				s_tail_sum[__builtin_amdgcn_readfirstlane(s_tail_pkt[k0 + u])] = s;
+			for (int i = 0; i < 4; i++)
+				acc = chunk_sum(v[i], base + 1024u * i + 16u * lane, hi, acc);
 		}
+		const uint32_t x = wave_sum(acc);
+		if (lane == f)
+			tail = x;
 	}
-	__syncthreads();
 	if constexpr (IS_TX(VAR)) {
-		tx_store(kp, rs, h, h.has_tail ? s_tail_sum[t] : 0u);
+		tx_store(kp, rs, h, tail);
 	} else {
 		if (active)
-			store_record(kp, p, hdr_finish(h, h.has_tail ? s_tail_sum[t] : 0u, kp.flags), s_cnt);
+			store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (active && kp.fhash)
 			kp.fhash[p] = flow_hash(h);
 	}
@@ -775,10 +772,6 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 // walk, no per-tail reduction; the header wave adds the S rows.  Tiles not in
 // buffer order stream tail by tail (stream_frames).
 #define STREAM_U 4
-#define ZERO_OFF 0xFFFFFFF0u   // buffer offset past any batch (loads there are never consumed)
-
-// Wave-uniform value: readfirstlane tells the compiler it lives in an SGPR.
-__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // Inclusive prefix sum over the 64 lanes: row scans (4 DPP row shifts), then
 // row_bcast:15 and row_bcast:31 carry the row totals up.

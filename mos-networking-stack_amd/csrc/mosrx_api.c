@@ -263,7 +263,7 @@ static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_
 		return force - 1;
 	if (max_len && max_len <= MOSRX_WINDOW_END)
 		return MOSRX_KIND_SMALL;
-	return (n && bytes / n < 1024u) ? MOSRX_KIND_S13 : MOSRX_KIND_S14;
+	return MOSRX_KIND_S13;
 }
 
 static int tile_for(const mosrx_ctx *c, const mosrx_batch *b)

@@ -885,7 +885,7 @@ __device__ __forceinline__ void stream_frames(__amdgpu_buffer_rsrc_t rs, uint32_
 // DBG (probe builds only, the library uses 0): 1 no parse/records, 2 no header
 // window loads, 4 streamer loads only, 16 no unsorted-tile path, 32 header wave
 // at raised issue priority.
-template <int S, int VAR, int DBG = 0, int U = STREAM_U>
+template <int S, int VAR, int DBG = 0, int U = STREAM_U, uint32_t T = 64>
 __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, uint32_t tile)
 {
 	constexpr int AUX = TAIL_AUX(VAR);
@@ -897,10 +897,10 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
 	const uint32_t nbytes = kp.frames_bytes;
-	const uint32_t nact = min(64u, kp.n - tile * 64u);
+	const uint32_t nact = min(T, kp.n - tile * T);
 
 	// every wave reads the tile's descriptors (lane = frame)
-	const uint32_t p = tile * 64u + lane;
+	const uint32_t p = tile * T + lane;
 	const bool active = lane < nact;
 	uint32_t o = 0, cap = 0;
 	if (active) {

@@ -16,10 +16,10 @@ __global__ __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(MINB > 1 ? 
 	classify_tile_large<1, 4, 2, DBG>(kp, blockIdx.x);
 }
 
-template <int S, int DBG, int W = 6, int U = 8>
+template <int S, int DBG, int W = 6, int U = 8, uint32_t T = 64>
 __global__ __launch_bounds__(64 * (1 + S)) __attribute__((amdgpu_waves_per_eu(W))) void k_sdbg(mosrx_kparams kp)
 {
-	classify_tile_stream<S, 2, DBG, U>(kp, blockIdx.x);
+	classify_tile_stream<S, 2, DBG, U, T>(kp, blockIdx.x);
 }
 
 typedef void (*lfn)(const mosrx_kparams *, hipStream_t);
@@ -28,10 +28,10 @@ static void launch_dbg(const mosrx_kparams *kp, hipStream_t s)
 {
 	hipLaunchKernelGGL((k_dbg<DBG, MINB>), dim3((kp->n + 63) / 64), dim3(320), 0, s, *kp);
 }
-template <int S, int DBG, int W = 6, int U = 8>
+template <int S, int DBG, int W = 6, int U = 8, uint32_t T = 64>
 static void launch_sdbg(const mosrx_kparams *kp, hipStream_t s)
 {
-	hipLaunchKernelGGL((k_sdbg<S, DBG, W, U>), dim3((kp->n + 63) / 64), dim3(64 * (1 + S)), 0, s, *kp);
+	hipLaunchKernelGGL((k_sdbg<S, DBG, W, U, T>), dim3((kp->n + T - 1) / T), dim3(64 * (1 + S)), 0, s, *kp);
 }
 static void launch_product(const mosrx_kparams *kp, hipStream_t s)
 {
@@ -112,14 +112,13 @@ int main(int argc, char **argv)
 	printf("trace kind %d n %u: %.2f MB algorithmic\n", kind, n, bytes / 1e6);
 	run("product LARGE", launch_product, kps, nb, bytes);
 	run("product S13", launch_stream, kps, nb, bytes);
-	run("S13 prio", launch_sdbg<3, 32, 8, 4>, kps, nb, bytes);
-	run("S14 prio", launch_sdbg<4, 32, 8, 4>, kps, nb, bytes);
-	run("S12 prio", launch_sdbg<2, 32, 8, 4>, kps, nb, bytes);
-	run("S13 U2", launch_sdbg<3, 0, 8, 2>, kps, nb, bytes);
-	run("S13 U3", launch_sdbg<3, 0, 8, 3>, kps, nb, bytes);
-	run("S13 U4 DBG 4", launch_sdbg<3, 4, 8, 4>, kps, nb, bytes);
-	run("S13 U4 DBG 1 no parse", launch_sdbg<3, 1, 8, 4>, kps, nb, bytes);
-	run("S13 U4 DBG 2 no window loads", launch_sdbg<3, 2, 8, 4>, kps, nb, bytes);
-	run("S13 U4 DBG 7", launch_sdbg<3, 7, 8, 4>, kps, nb, bytes);
+	run("S13 T32", launch_sdbg<3, 0, 8, 4, 32>, kps, nb, bytes);
+	run("S12 T32", launch_sdbg<2, 0, 8, 4, 32>, kps, nb, bytes);
+	run("S11 T32", launch_sdbg<1, 0, 8, 4, 32>, kps, nb, bytes);
+	run("S11 T32 U8", launch_sdbg<1, 0, 8, 8, 32>, kps, nb, bytes);
+	run("S12 T32 U8", launch_sdbg<2, 0, 8, 8, 32>, kps, nb, bytes);
+	run("S13 T48", launch_sdbg<3, 0, 8, 4, 48>, kps, nb, bytes);
+	run("S13 T32 DBG 7", launch_sdbg<3, 7, 8, 4, 32>, kps, nb, bytes);
+	run("S13 DBG 7", launch_sdbg<3, 7, 8, 4>, kps, nb, bytes);
 	return 0;
 }

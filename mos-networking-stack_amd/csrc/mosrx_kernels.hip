@@ -185,6 +185,41 @@ __device__ __forceinline__ uint32_t ip_chain(const uint32_t *w, uint32_t ihl, ui
 	return (~rr) & 0xFFFFu;
 }
 
+// The ihl-dependent header pieces: TCP header dwords 0 and 3 at iph + ihl*4
+// (and the check word for TX), ip_fast_csum (and its TX variant with the check
+// zeroed) and the segment sum over frame bytes [14+4*ihl, wend) on the
+// realigned grid (dword j = frame bytes [4j+2, 4j+6), the segment grid).  F5:
+// every active lane of the wave has ihl == 5 (no IP options, nearly all
+// traffic), so every position is a constant and the selects fold away.
+template <int VAR, bool F5>
+__device__ __forceinline__ void hdr_ihl(const uint32_t (&w)[WIN_DW], uint32_t ihl_l, int wend, uint32_t &th0,
+                                        uint32_t &th3, uint32_t &tcw, uint32_t &ipc, uint32_t &ipc_tx,
+                                        uint32_t &wsum)
+{
+	const uint32_t ihl = F5 ? 5u : ihl_l;
+	th0 = 0; th3 = 0; tcw = 0;
+#pragma unroll
+	for (int k = 0; k < 16; k++) {
+		if (ihl == (uint32_t)k) {
+			th0 = w[3 + k];
+			th3 = w[6 + k];
+			if (IS_TX(VAR))
+				tcw = w[7 + k] & 0xFFFFu;                  // tcph->check (frame bytes 30+4ihl, +1)
+		}
+	}
+	ipc = ip_chain(w, ihl, w[5]);
+	// TX: iph->check = 0 first (mos_api.c:1180-1181): the check is frame bytes 24,25 = w[5] bytes 2,3
+	ipc_tx = IS_TX(VAR) ? ip_chain(w, ihl, w[5] & 0xFFFFu) : 0u;
+	wsum = 0;
+#pragma unroll
+	for (int j = 8; j < WIN_DW; j++) {
+		uint32_t m = keep_lo(wend - (4 * j + 2));
+		if ((uint32_t)j < 3u + ihl)
+			m = 0;
+		wsum = add16x2(wsum, w[j] & m);
+	}
+}
+
 // Parse + checks + IP checksum + RSS + in-window TCP sum.  Mirrors
 // ProcessPacket (eth_in.c:27) -> ProcessInIPv4Packet (ip_in.c:30) ->
 // ProcessInTCPPacket prefix (tcp.c:408-445); see oracle/mosrx_oracle.c.
@@ -206,42 +241,21 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	const uint32_t ip_len = be16hi(w[3]);             // frame bytes 16,17  (ip_in.c:39)
 	const uint32_t proto = (w[5] >> 8) & 0xFFu;       // frame byte 23
 	const uint32_t saddr = w[6], daddr = w[7];        // raw network-order words
-	uint32_t th0 = 0, th3 = 0, tcw = 0;                // TCP header dwords 0 and 3 at iph + ihl*4
-#pragma unroll
-	for (int k = 0; k < 16; k++) {
-		if (ihl == (uint32_t)k) {
-			th0 = w[3 + k];
-			th3 = w[6 + k];
-			if (IS_TX(VAR))
-				tcw = w[7 + k] & 0xFFFFu;                  // tcph->check (frame bytes 30+4ihl, +1)
-		}
-	}
 	const bool is_tcp = (proto == 6u);
-	const uint32_t doff = is_tcp ? ((th3 >> 4) & 0xFu) : 0u;
 	const uint32_t fend = 14u + ip_len;                // frame byte after the IP datagram
 	const uint32_t split_abs = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
 	const uint32_t split = split_abs - o;              // frame byte 79..94
-
-	const uint32_t ipc = ip_chain(w, ihl, w[5]);
-	// TX: iph->check = 0 first (mos_api.c:1180-1181): the check is frame bytes 24,25 = w[5] bytes 2,3
-	const uint32_t ipc_tx = IS_TX(VAR) ? ip_chain(w, ihl, w[5] & 0xFFFFu) : 0u;
-
 	// TCP segment sum over frame bytes [14+4*ihl, wend): the whole segment when
 	// the datagram ends inside the window, else up to the split (the tail
-	// streamers take over there).  The realigned grid (dword j = frame bytes
-	// [4j+2, 4j+6)) is the segment grid.
+	// streamers take over there).
 	const bool in_win = fend <= (uint32_t)MOSRX_WINDOW_END;
-	uint32_t wsum = 0;
-	{
-		const int wend = (int)(in_win ? fend : split);
-#pragma unroll
-		for (int j = 8; j < WIN_DW; j++) {
-			uint32_t m = keep_lo(wend - (4 * j + 2));
-			if ((uint32_t)j < 3u + ihl)
-				m = 0;
-			wsum = add16x2(wsum, w[j] & m);
-		}
-	}
+	const int wend = (int)(in_win ? fend : split);
+	uint32_t th0, th3, tcw, ipc, ipc_tx, wsum;
+	if (__ballot(active && ihl != 5u) == 0)            // no IP options in the wave: constant positions
+		hdr_ihl<VAR, true>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum);
+	else
+		hdr_ihl<VAR, false>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum);
+	const uint32_t doff = is_tcp ? ((th3 >> 4) & 0xFu) : 0u;
 
 	// Toeplitz over saddr|daddr|sport|dport in wire order (util.c:61-99, host-order args)
 	uint32_t rss = 0;

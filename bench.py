@@ -22,6 +22,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -286,6 +287,34 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0):
     }
 
 
+def cpu_reference(tr: mosrx.Trace, key: str, seconds: float):
+    """mOS's own compiled functions (oracle/_ref/mosref --time: the header checks,
+    ip_fast_csum, TCPCalcChecksum, GetRSSHash, GetRSSCPUCore per frame) on one
+    host core, when the reference build travelled with the tree; else None.
+    A reported baseline beside the port, never the measured path."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "mosref")
+    if not os.access(exe, os.X_OK):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import tempfile
+    import pktlib
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "trace.mrxt")
+        pktlib.write_ref_trace(path, tr.frames[:tr.frames_bytes], tr.off, tr.len)
+        try:
+            out = subprocess.run([exe, "--time", path, str(seconds)], capture_output=True, text=True,
+                                 timeout=seconds + 60)
+            r = json.loads(out.stdout.strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+            return None
+    el = r["seconds"]
+    return {"value": round(algo_bytes(tr, key) * r["passes"] / el / 1e9, 3), "unit": "GB/s", "cores": 1,
+            "kind": "reference", "mpkts": round(r["mpkts"], 3),
+            "sample": f"{r['passes']} passes over one {tr.n}-frame batch ({el:.1f} s), mOS core/src "
+                      f"ip_fast_csum + TCPCalcChecksum + GetRSSHash + GetRSSCPUCore + header checks "
+                      f"(oracle/_ref/mosref --time), 1 thread"}
+
+
 def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
     """The oracle for a §8f row (flow hash / TX rewrite / BPF), one thread."""
     ab = algo_bytes(tr, key)
@@ -369,9 +398,16 @@ def main():
     if rank == 0 and ws == 1 and not args.no_cpu:
         head = "M1500" if "M1500" in traces else keys[0]
         cpu = cpu_baseline(traces[head], head, min_s=10.0)
+        ref = cpu_reference(traces[head], head, 10.0)
+        if ref:
+            cpu["reference"] = ref
         for k in keys:
             if k != head:
                 results[k]["cpu_baseline"] = cpu_baseline(traces[k], k, min_s=2.0)
+                if k in ("S64", "IMIX"):
+                    ref = cpu_reference(traces[k], k, 2.0)
+                    if ref:
+                        results[k]["cpu_baseline"]["reference"] = ref
     ctx.close()
     dist.close()
     if rank != 0:

@@ -21,12 +21,21 @@
  *
  * forward must be 0: ForwardIPPacket/ForwardEthernetFrame need route/ARP
  * tables and TX buffers.
+ *
+ * Usage: mosref --time <trace.in> <seconds>
+ *   CPU baseline of the reference's own per-frame arithmetic on this host, one
+ *   thread: the header checks of eth_in.c / ip_in.c / tcp.c, ip_fast_csum,
+ *   TCPCalcChecksum, GetRSSHash and GetRSSCPUCore
+ *   over every frame, passes repeated for at least <seconds>.  Prints one JSON
+ *   line.  ProcessPacket itself is not timed: past the checksum it runs
+ *   FindStream and the stateful flow engine (out of scope).
  */
 #include <arpa/inet.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "mtcp.h"
 #include "config.h"
@@ -58,6 +67,67 @@ unsigned int HashFlow(const tcp_stream *flow);
 
 static int rd(FILE *f, void *p, size_t n) { return fread(p, 1, n, f) == n ? 0 : -1; }
 
+/* The scope of the GPU transform, computed by the reference's own functions. */
+static uint32_t ref_frame(const uint8_t *f, uint32_t cap, int nq)
+{
+	struct iphdr *iph;
+	struct tcphdr *th;
+	unsigned ihl, ip_len, proto;
+	uint32_t acc;
+	uint16_t sp = 0, dp = 0;
+	if (cap < 34 || f[12] != 0x08 || f[13] != 0x00)
+		return 0;
+	iph = (struct iphdr *)(f + 14);
+	ihl = iph->ihl;
+	ip_len = ntohs(iph->tot_len);
+	proto = iph->protocol;
+	if (ip_len < 20 || iph->version != 4 || 14 + ihl * 4 > cap || 14 + ip_len > cap ||
+	    (proto == 6 && 14 + ihl * 4 + 20 > cap))
+		return 1;
+	acc = ip_fast_csum(iph, ihl);
+	th = (struct tcphdr *)((uint8_t *)iph + ihl * 4);
+	if (proto == 6) {
+		sp = ntohs(th->source);
+		dp = ntohs(th->dest);
+		if (ip_len >= (ihl + th->doff) * 4) {
+			uint16_t payloadlen = ip_len - (ihl * 4 + th->doff * 4);
+			acc += TCPCalcChecksum((uint16_t *)th, (th->doff << 2) + payloadlen, iph->saddr, iph->daddr);
+		}
+	}
+	acc += GetRSSHash(ntohl(iph->saddr), ntohl(iph->daddr), sp, dp);
+	acc += (uint32_t)GetRSSCPUCore(ntohl(iph->saddr), ntohl(iph->daddr), sp, dp, nq);
+	return acc;
+}
+
+static double now_s(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static int time_mode(uint32_t n, const uint32_t *off, const uint16_t *len, const uint8_t *frames, int nq,
+                     double seconds)
+{
+	uint64_t passes = 0, bytes = 0;
+	uint32_t i, sink = 0;
+	double t0, el;
+	for (i = 0; i < n; i++)
+		bytes += len[i];
+	t0 = now_s();
+	do {
+		for (i = 0; i < n; i++)
+			sink += ref_frame(frames + off[i], len[i], nq);
+		passes++;
+		el = now_s() - t0;
+	} while (el < seconds);
+	printf("{\"frames\": %u, \"passes\": %llu, \"seconds\": %.3f, \"mpkts\": %.4f, "
+	       "\"caplen_gbps\": %.4f, \"sink\": %u}\n",
+	       n, (unsigned long long)passes, el, (double)n * passes / el / 1e6, (double)bytes * passes / el / 1e9,
+	       sink);
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	FILE *in, *out;
@@ -76,10 +146,13 @@ int main(int argc, char **argv)
 	static io_module_func null_iom;
 	static log_thread_context lg;
 
-	if (argc != 3) {
-		fprintf(stderr, "usage: %s trace.in results.out\n", argv[0]);
+	int timing = argc == 4 && !strcmp(argv[1], "--time");
+	if (argc != 3 && !timing) {
+		fprintf(stderr, "usage: %s trace.in results.out | %s --time trace.in seconds\n", argv[0], argv[0]);
 		return 2;
 	}
+	if (timing)
+		argv++;
 	in = fopen(argv[1], "rb");
 	if (!in || rd(in, magic, 4) || memcmp(magic, "MRXT", 4) || rd(in, &ver, 4) || ver != 1 ||
 	    rd(in, &n, 4) || rd(in, &fb, 8) || rd(in, &num_msp, 4) || rd(in, &num_esp, 4) ||
@@ -101,6 +174,8 @@ int main(int argc, char **argv)
 	}
 	fclose(in);
 	g_qmode = qmode;
+	if (timing)
+		return time_mode(n, off, len, frames, nq, atof(argv[2]));
 
 	/* stack state: core.c:1079-1110 InitializeMTCPManager, reduced */
 	nd.num = 0;

@@ -45,6 +45,7 @@ WORKLOADS = {
     "S64_hdr": (mosrx.TRACE_S64, 32_768, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum)"),
     "IMIX": (mosrx.TRACE_IMIX, 262_144, "IMIX 60/590/1514 7:4:1, 1M flows, batch=256K (BASELINE config #4)"),
     "S64_queue": (mosrx.TRACE_S64, 32_768, "config #2, 64 batches of 32K per launch (device batch queue)"),
+    "M1500_queue": (mosrx.TRACE_M1500, 65_536, "config #3, 4 batches of 64K per launch (device batch queue)"),
     # SURVEY.md §8f rows measured on the same traces
     "M1500_fh": (mosrx.TRACE_M1500, 65_536, "config #3 classify + flow-table hash (HashFlow of FindStream's tuple)"),
     "M1500_tx": (mosrx.TRACE_M1500, 65_536, "config #3 TX checksum rewrite (MOS_UPDATE_IP|TCP_CHKSUM), in place"),
@@ -55,7 +56,7 @@ OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_tx": mosrx.OP_TX_CSUM, "IMIX_bpf
 BPF_BENCH = [("tcp", 0), ("tcp port 80", 0), ("tcp[tcpflags] & tcp-syn != 0", 1), ("net 192.168.0.0/16 and tcp", 1),
              ("host 10.0.0.1 and port 80", 0), ("ip[8] < 64", 1), ("tcp[((tcp[12:1] & 0xf0) >> 2):4] = 0x47455420", 1),
              ("portrange 1000-2000", 0)]
-QUEUE_DEPTH = 64
+QUEUE_DEPTH = {"S64_queue": 64, "M1500_queue": 4}   # resident batches per queue launch
 PREWARM_S = 0.3
 STREAMS = 2   # rx batches in flight per GPU (scripts/tune_streams.py: 2 beats 1 and 4)
 
@@ -145,7 +146,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
     # synthetic content differs per rank (seed), the shape does not.
     tr = mosrx.Trace(kind, batch, seed=0 if rank == 0 else 0x6D4F5321 + kind + 1000 * rank)
     ncopy = max(2, -(-2 * L3_BYTES // max(tr.frames_bytes, 1)))
-    ncopy = min(ncopy, 256)
+    ncopy = min(max(ncopy, 2 * QUEUE_DEPTH.get(key, 1)), 256)
     dbs = [ctx.upload(tr.frames, tr.off, tr.len, frames_bytes=tr.frames_bytes, max_len=tr.max_len)
            for _ in range(ncopy)]
     ab = algo_bytes(tr, key)
@@ -169,11 +170,12 @@ def measure(ctx, dist, key, steps, warmup, rank):
         kern_ms = ctx.time_op(op, dbs, kk, 1, arg, kernels=False)[0] / kk
         _, kern_iso = ctx.time_op(op, dbs, kk, 1, arg, total=False)
     elif key.endswith("_queue"):
-        # each step = one launch over QUEUE_DEPTH distinct resident 32K batches
+        # each step = one launch over `depth` distinct resident batches
+        depth = QUEUE_DEPTH[key]
         # several queues over disjoint batch copies: the working set exceeds the L3
-        qs = [ctx.queue(dbs[i:i + QUEUE_DEPTH]) for i in range(0, len(dbs) - QUEUE_DEPTH + 1, QUEUE_DEPTH)]
-        ab *= QUEUE_DEPTH
-        batch *= QUEUE_DEPTH
+        qs = [ctx.queue(dbs[i:i + depth]) for i in range(0, len(dbs) - depth + 1, depth)]
+        ab *= depth
+        batch *= depth
         prewarm(lambda: qs[0].time(20, qs[1:], kernels=False))
         if warmup:
             qs[0].time(warmup, qs[1:], kernels=False)
@@ -369,7 +371,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--workloads", default="M1500,S64,S64_hdr,S64_queue,IMIX,M1500_fh,M1500_tx,IMIX_bpf")
+    ap.add_argument("--workloads",
+                    default="M1500,S64,S64_hdr,S64_queue,M1500_queue,IMIX,M1500_fh,M1500_tx,IMIX_bpf")
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="rx batches in flight (1 = strictly serial launches, as for rocprof summaries)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")

@@ -224,7 +224,8 @@ def test_gpu_io_module_batches_and_ioctl():
         be.close()
 
 
-@pytest.mark.parametrize("kind,n,nb", [(mosrx.TRACE_S64, 32_768, 8), (mosrx.TRACE_IMIX, 9_000, 5)])
+@pytest.mark.parametrize("kind,n,nb", [(mosrx.TRACE_S64, 32_768, 8), (mosrx.TRACE_IMIX, 9_000, 5),
+                                       (mosrx.TRACE_M1500, 9_000, 4)])
 def test_batch_queue_one_launch(gpu_ctx, kind, n, nb):
     gpu_ctx.set_params(mosrx.default_params())
     trs = [mosrx.Trace(kind, n - 7 * i, nflows=4000, seed=100 + i) for i in range(nb)]

@@ -12,7 +12,7 @@ for W in M1500 IMIX S64; do
   python3 scripts/pmc_parse.py $W gpurun_out/prof/pmcf_$W gpurun_out/prof/pmcw_$W mosrx_classify_kernel gpurun_out/pmc_traffic.json
 done
 cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json
-for W in M1500 IMIX S64 S64_queue M1500_fh M1500_tx IMIX_bpf; do
+for W in M1500 IMIX S64 S64_queue M1500_queue M1500_fh M1500_tx IMIX_bpf; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/kt_$W -o kt --output-format csv -- python3 bench.py --workloads $W --streams 1 --no-cpu --no-e2e > gpurun_out/prof/kt_$W.log 2>&1; rc=$?
   echo "kt $W rc=$rc"; grep "^\[bench\]" gpurun_out/prof/kt_$W.log
   [ $rc -ne 0 ] && exit $rc

@@ -260,6 +260,22 @@ int  mosrx_bpf_check(const mosrx_bpf_insn *insns, uint32_t len);
  * SET_BPFFILTER failing makes mtcp_bind_monitor_filter return EINVAL
  * (mos_api.c:127-155).  nprog = 0 clears the set. */
 int  mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog);
+/* Evaluation engine of the next mosrx_bpf_set.  JIT (default): the set is
+ * translated to one straight-line gfx950 kernel and compiled with hipRTC at
+ * set time (cached per context); INTERP: the uniform-pc interpreter kernel.
+ * Both run on the GPU with the same results; env MOSRX_BPF_ENGINE=0 selects
+ * INTERP at open.  mosrx_bpf_engine() reports the engine of the installed set
+ * (INTERP when the JIT could not compile; mosrx_bpf_jit_log() says why). */
+enum { MOSRX_BPF_ENGINE_INTERP = 0, MOSRX_BPF_ENGINE_JIT = 1 };
+int  mosrx_bpf_set_engine(mosrx_ctx *c, int engine);
+int  mosrx_bpf_engine(const mosrx_ctx *c);
+const char *mosrx_bpf_jit_log(const mosrx_ctx *c);
+/* The generated kernel source of a program set (no GPU needed; free() it). */
+int  mosrx_bpf_jit_source(const mosrx_bpf_prog *progs, uint32_t nprog, char **src);
+/* Generate and compile a program set with hipRTC for gfx950 without loading
+ * it (no GPU needed): 0 and the code-object size, or -errno and the log. */
+int  mosrx_bpf_jit_compile(const mosrx_bpf_prog *progs, uint32_t nprog, char *log, size_t logsz,
+                           size_t *code_size);
 /* Device-resident evaluation: d_match[i] bit j = (sfbpf_filter(prog j, frame i) != 0). */
 int  mosrx_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t *d_match, void *stream);
 /* End-to-end from host memory (blocking). */

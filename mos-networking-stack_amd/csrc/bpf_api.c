@@ -7,6 +7,7 @@
  * programs sfbpf_filter (bpf/sf_bpf_filter.c:214-536) runs to a defined result.
  */
 #include <errno.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "mosrx_ctx.h"
@@ -68,13 +69,14 @@ int mosrx_bpf_check(const mosrx_bpf_insn *f, uint32_t len)
 	return (f[len - 1].code & 7) == RET ? 0 : -EINVAL;
 }
 
-int mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
+/* Program table + staged instructions of an admitted set. */
+static int stage_set(const mosrx_bpf_prog *progs, uint32_t nprog, mosrx_bparams *tp, mosrx_bpf_insn *staged,
+                     uint32_t *totalp)
 {
 	mosrx_bparams t;
-	mosrx_bpf_insn staged[MOSRX_BPF_MAX_INSNS];
 	uint32_t j, total = 0;
 	int rc;
-	if (!c || nprog > MOSRX_BPF_MAX_PROGS || (nprog && !progs))
+	if (nprog > MOSRX_BPF_MAX_PROGS || (nprog && !progs))
 		return -EINVAL;
 	memset(&t, 0, sizeof(t));
 	for (j = 0; j < nprog; j++) {
@@ -94,6 +96,69 @@ int mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
 		total += len;
 	}
 	t.nprog = nprog;
+	*tp = t;
+	*totalp = total;
+	return 0;
+}
+
+int mosrx_bpf_jit_source(const mosrx_bpf_prog *progs, uint32_t nprog, char **src)
+{
+	mosrx_bpf_insn *staged;
+	mosrx_bparams t;
+	uint32_t total;
+	int rc;
+	if (!src)
+		return -EINVAL;
+	*src = NULL;
+	if (!(staged = malloc(MOSRX_BPF_MAX_INSNS * sizeof(*staged))))
+		return -ENOMEM;
+	if (!(rc = stage_set(progs, nprog, &t, staged, &total)))
+		rc = mosrx__bpf_jit_source(staged, &t, src);
+	free(staged);
+	return rc;
+}
+
+int mosrx_bpf_jit_compile(const mosrx_bpf_prog *progs, uint32_t nprog, char *log, size_t logsz,
+                          size_t *code_size)
+{
+	char *src = NULL;
+	int rc = mosrx_bpf_jit_source(progs, nprog, &src);
+	if (!rc)
+		rc = mosrx__bpf_jit_compile(src, log, logsz, code_size);
+	free(src);
+	return rc;
+}
+
+int mosrx_bpf_set_engine(mosrx_ctx *c, int engine)
+{
+	if (!c || (engine != MOSRX_BPF_ENGINE_INTERP && engine != MOSRX_BPF_ENGINE_JIT))
+		return -EINVAL;
+	c->bpf_engine_req = engine;
+	return 0;
+}
+
+int mosrx_bpf_engine(const mosrx_ctx *c)
+{
+	if (!c)
+		return -EINVAL;
+	return c->bpf_fn ? MOSRX_BPF_ENGINE_JIT : MOSRX_BPF_ENGINE_INTERP;
+}
+
+const char *mosrx_bpf_jit_log(const mosrx_ctx *c)
+{
+	return c ? c->bpf_jit_log : "";
+}
+
+int mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
+{
+	mosrx_bparams t;
+	mosrx_bpf_insn staged[MOSRX_BPF_MAX_INSNS];
+	uint32_t total = 0;
+	int rc;
+	if (!c)
+		return -EINVAL;
+	if ((rc = stage_set(progs, nprog, &t, staged, &total)))
+		return rc;
 	HIPCHK(hipSetDevice(c->device));
 	if (!c->d_bpf)
 		HIPCHK(hipMalloc((void **)&c->d_bpf, MOSRX_BPF_MAX_INSNS * sizeof(mosrx_bpf_insn)));
@@ -103,6 +168,9 @@ int mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
 	if (total)
 		HIPCHK(hipMemcpy(c->d_bpf, staged, (size_t)total * sizeof(mosrx_bpf_insn), hipMemcpyHostToDevice));
 	c->bpf = t;
+	c->bpf_fn = NULL;
+	if (c->bpf_engine_req == MOSRX_BPF_ENGINE_JIT && nprog)
+		mosrx__bpf_jit_build(c, staged);   /* on failure the interpreter runs the set */
 	return 0;
 }
 
@@ -117,6 +185,8 @@ static int bpf_launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames,
 	bp.insns = c->d_bpf;
 	bp.frames_bytes = (uint32_t)b->frames_bytes;
 	bp.n = b->n;
+	if (c->bpf_fn)
+		return mosrx__bpf_jit_launch(c, &bp, s);
 	return mosrx_launch_bpf(&bp, (void *)s);
 }
 

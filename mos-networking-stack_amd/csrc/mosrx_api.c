@@ -165,6 +165,9 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 	c->variant = MOSRX_DEFAULT_VARIANT;
 	if (getenv("MOSRX_KVARIANT"))
 		c->variant = atoi(getenv("MOSRX_KVARIANT")) & 127;
+	c->bpf_engine_req = MOSRX_BPF_ENGINE_JIT;
+	if (getenv("MOSRX_BPF_ENGINE") && atoi(getenv("MOSRX_BPF_ENGINE")) == 0)
+		c->bpf_engine_req = MOSRX_BPF_ENGINE_INTERP;
 	/* the timing streams are created right after the context stream: HIP maps
 	 * streams to hardware queues round robin (GPU_MAX_HW_QUEUES, 4 by default),
 	 * so the first three land on queues of their own */
@@ -222,6 +225,7 @@ void mosrx_close(mosrx_ctx *c)
 	}
 	if (c->d_tables) hipFree(c->d_tables);
 	if (c->d_bpf) hipFree(c->d_bpf);
+	mosrx__bpf_jit_free(c);
 	for (i = 0; i < (int)c->nxs; i++) {
 		hipStreamSynchronize(c->xs[i]);
 		hipStreamDestroy(c->xs[i]);

@@ -12,6 +12,8 @@
 
 #define HIPCHK(x) do { if ((x) != hipSuccess) return -EIO; } while (0)
 
+#define MOSRX_BPF_JIT_CACHE 16   /* compiled program sets kept per context */
+
 /* pipeline slots for the end-to-end path (double-buffered H2D | kernel | D2H) */
 #define NSLOT MOSRX_NSLOT
 
@@ -42,12 +44,22 @@ struct mosrx_ctx {
 	int variant;                     /* kernel cache-policy variant (mosrx_set_variant) */
 	mosrx_bpf_insn *d_bpf;           /* installed BPF programs (MOSRX_BPF_MAX_INSNS), NULL until set */
 	mosrx_bparams bpf;               /* program table of the installed set */
+	hipFunction_t bpf_fn;            /* compiled form of the installed set (bpf_jit.c), NULL: interpreter */
+	int bpf_engine_req;              /* MOSRX_BPF_ENGINE_* for the next mosrx_bpf_set */
+	char bpf_jit_log[512];           /* hipRTC log of the last failed compile */
+	struct { uint64_t key; hipModule_t mod; hipFunction_t fn; } jit[MOSRX_BPF_JIT_CACHE];
+	uint32_t njit;
 	hipStream_t xs[MOSRX_MAX_STREAMS];   /* timing streams (mosrx_time_op), created on first use */
 	hipEvent_t xdone[MOSRX_MAX_STREAMS];
 	uint32_t nxs;
 };
 
 int mosrx__check_batch(const mosrx_batch *b, int dev);
+int mosrx__bpf_jit_build(mosrx_ctx *c, const mosrx_bpf_insn *insns);
+int mosrx__bpf_jit_launch(mosrx_ctx *c, const mosrx_bparams *bp, hipStream_t s);
+int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out);
+void mosrx__bpf_jit_free(mosrx_ctx *c);
+int mosrx__bpf_jit_compile(const char *src, char *log, size_t logsz, size_t *code_size);
 int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uint32_t n);
 
 #endif

@@ -143,6 +143,11 @@ def lib():
             "mosrx_bpf_set": (I, [P, C.POINTER(BpfProg), U32]),
             "mosrx_bpf_dev": (I, [P, C.POINTER(Batch), P, P]),
             "mosrx_bpf_host": (I, [P, C.POINTER(Batch), P]),
+            "mosrx_bpf_set_engine": (I, [P, I]),
+            "mosrx_bpf_engine": (I, [P]),
+            "mosrx_bpf_jit_log": (C.c_char_p, [P]),
+            "mosrx_bpf_jit_source": (I, [C.POINTER(BpfProg), U32, C.POINTER(P)]),
+            "mosrx_bpf_jit_compile": (I, [C.POINTER(BpfProg), U32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
             "mosrx_trace_gen": (I, [I, U32, U32, U64, C.POINTER(TraceC)]),
             "mosrx_trace_free": (None, [C.POINTER(TraceC)]),
             "mosrx_source_mem": (P, [P, P, P, U32, U32]),
@@ -181,6 +186,39 @@ def default_params(**kw) -> Params:
             p.rss_key[i] = key[i] if i < len(key) else 0
         p.rss_key_len = len(key)
     return p
+
+
+BPF_ENGINE_INTERP, BPF_ENGINE_JIT = 0, 1
+
+
+def _bpf_progs(progs):
+    keep = [np.ascontiguousarray(i if i is not None else [], BPF_INSN) for i, _ in progs]
+    arr = (BpfProg * max(1, len(progs)))()
+    for j, ((_, mode), ins) in enumerate(zip(progs, keep)):
+        arr[j].insns = ins.ctypes.data if len(ins) else None
+        arr[j].len = len(ins)
+        arr[j].len_mode = mode
+    return arr, keep
+
+
+def bpf_jit_source(progs) -> str:
+    """mosrx_bpf_jit_source: the gfx950 kernel source generated for a program set."""
+    arr, _keep = _bpf_progs(progs)
+    out = C.c_void_p()
+    _chk(lib().mosrx_bpf_jit_source(arr, len(progs), C.byref(out)), "mosrx_bpf_jit_source")
+    try:
+        return C.string_at(out.value).decode()
+    finally:
+        C.CDLL(None).free(out)
+
+
+def bpf_jit_compile(progs):
+    """mosrx_bpf_jit_compile: (rc, code-object bytes, hipRTC log); no GPU needed."""
+    arr, _keep = _bpf_progs(progs)
+    log = C.create_string_buffer(4096)
+    sz = C.c_size_t(0)
+    rc = lib().mosrx_bpf_jit_compile(arr, len(progs), log, len(log), C.byref(sz))
+    return rc, int(sz.value), log.value.decode(errors="replace")
 
 
 def bpf_check(insns) -> int:
@@ -360,13 +398,19 @@ class Context:
     # ---- batched BPF (mosrx_bpf_*) ----
     def bpf_set(self, progs) -> None:
         """progs: list of (insns, len_mode); insns None/empty = no filter (matches)."""
-        keep = [np.ascontiguousarray(i if i is not None else [], BPF_INSN) for i, _ in progs]
-        arr = (BpfProg * max(1, len(progs)))()
-        for j, ((_, mode), ins) in enumerate(zip(progs, keep)):
-            arr[j].insns = ins.ctypes.data if len(ins) else None
-            arr[j].len = len(ins)
-            arr[j].len_mode = mode
+        arr, _keep = _bpf_progs(progs)
         _chk(lib().mosrx_bpf_set(self.handle, arr, len(progs)), "mosrx_bpf_set")
+
+    def bpf_set_engine(self, engine: int) -> None:
+        """Engine of the next bpf_set: BPF_ENGINE_JIT (hipRTC-compiled set) or BPF_ENGINE_INTERP."""
+        _chk(lib().mosrx_bpf_set_engine(self.handle, engine), "mosrx_bpf_set_engine")
+
+    def bpf_engine(self) -> int:
+        """Engine of the installed set."""
+        return lib().mosrx_bpf_engine(self.handle)
+
+    def bpf_jit_log(self) -> str:
+        return (lib().mosrx_bpf_jit_log(self.handle) or b"").decode(errors="replace")
 
     def bpf_host(self, frames, off, ln, frames_bytes=None) -> np.ndarray:
         frames = np.ascontiguousarray(frames, np.uint8)

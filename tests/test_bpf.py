@@ -144,12 +144,40 @@ def test_bpf_check_admits_every_reference_runnable_program():
             assert mosrx.bpf_check(progs[j]) != 0, z["names"][j]
 
 
+def test_bpf_jit_compiles_every_golden_set():
+    """Every admitted program becomes gfx950 code through hipRTC (compile only, no GPU)."""
+    z, progs = load()
+    sets = [ps for ps, _ in program_sets(z, progs)]
+    sets.append([(p, m) for p, m in ((prog(I_(0x81), I_(0x40, 0xFFFFFFFC), I_(0x16)), 0),
+                                     (prog(I_(0x81), I_(0x50, 0xFFFFFFFF), I_(0x44, 0x100), I_(0x16)), 1),
+                                     (None, 0))])
+    for ps in sets:
+        rc, size, log = mosrx.bpf_jit_compile(ps)
+        assert rc == 0 and size > 0, log
+        src = mosrx.bpf_jit_source(ps)
+        assert src.count("/* program ") == len(ps)
+
+
 # ---------------------------------------------------------------- GPU parity
+@pytest.fixture(params=[mosrx.BPF_ENGINE_JIT, mosrx.BPF_ENGINE_INTERP], ids=["jit", "interp"])
+def engine(gpu_ctx, request):
+    """Both GPU engines: the hipRTC-compiled set and the interpreter kernel."""
+    gpu_ctx.bpf_set_engine(request.param)
+    yield request.param
+    gpu_ctx.bpf_set_engine(mosrx.BPF_ENGINE_JIT)
+
+
+def bpf_set(ctx, engine, ps):
+    ctx.bpf_set(ps)
+    if any(p is not None and len(p) for p, _ in ps):
+        assert ctx.bpf_engine() == engine, ctx.bpf_jit_log()
+
+
 @pytest.mark.gpu
-def test_bpf_golden_sets(gpu_ctx):
+def test_bpf_golden_sets(gpu_ctx, engine):
     z, progs = load()
     for ps, exp in program_sets(z, progs):
-        gpu_ctx.bpf_set(ps)
+        bpf_set(gpu_ctx, engine, ps)
         got = gpu_ctx.bpf_host(z["frames"], z["off"], z["len"])
         np.testing.assert_array_equal(got, exp)
         db = gpu_ctx.upload(z["frames"], z["off"], z["len"])
@@ -160,22 +188,22 @@ def test_bpf_golden_sets(gpu_ctx):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("phase,align", [(0, 1), (1, 1), (3, 4), (7, 16), (13, 2)])
-def test_bpf_misaligned_layouts(gpu_ctx, phase, align):
+def test_bpf_misaligned_layouts(gpu_ctx, engine, phase, align):
     z, progs = load()
     frames = [bytes(z["frames"][o:o + n]) for o, n in zip(z["off"], z["len"])]
     buf, off, ln = pack_frames(frames, align=align, phase=phase)
     ps = program_sets(z, progs)[0][0]
-    gpu_ctx.bpf_set(ps)
+    bpf_set(gpu_ctx, engine, ps)
     np.testing.assert_array_equal(gpu_ctx.bpf_host(buf, off, ln), O.bpf_eval(ps, buf, off, ln))
 
 
 @pytest.mark.gpu
-def test_bpf_buffer_end_and_truncation(gpu_ctx):
+def test_bpf_buffer_end_and_truncation(gpu_ctx, engine):
     # loads of the very last frame bytes, with frames_bytes ending mid-dword
     last = prog(I_(0x81), I_(0x40, 0xFFFFFFFC), I_(0x16))
     lastb = prog(I_(0x81), I_(0x50, 0xFFFFFFFF), I_(0x44, 0x100), I_(0x16))
     ps = [(last, 0), (lastb, 0), (last, 1), (lastb, 1)]
-    gpu_ctx.bpf_set(ps)
+    bpf_set(gpu_ctx, engine, ps)
     for plen in range(0, 24):
         f = tcp_frame(payload=bytes(range(1, plen + 1)))
         buf, off, ln = pack_frames([tcp_frame(payload=b"x" * 50), f], phase=plen % 16)
@@ -185,9 +213,9 @@ def test_bpf_buffer_end_and_truncation(gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_bpf_empty_and_nofilter(gpu_ctx):
+def test_bpf_empty_and_nofilter(gpu_ctx, engine):
     buf, off, ln = pack_frames([tcp_frame(payload=b"a"), tcp_frame(ethertype=0x86DD, pad_to=60)])
-    gpu_ctx.bpf_set([(None, 0), (None, 1), (prog(I_(0x06, 0)), 0)])
+    bpf_set(gpu_ctx, engine, [(None, 0), (None, 1), (prog(I_(0x06, 0)), 0)])
     assert gpu_ctx.bpf_host(buf, off, ln).tolist() == [0b011, 0b001]   # LEN_IP only on IPv4
     gpu_ctx.bpf_set([])
     assert gpu_ctx.bpf_host(buf, off, ln).tolist() == [0, 0]
@@ -198,11 +226,11 @@ def test_bpf_empty_and_nofilter(gpu_ctx):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,n", [(mosrx.TRACE_IMIX, 262_144), (mosrx.TRACE_M1500, 65_536),
                                     (mosrx.TRACE_S64, 32_768)])
-def test_bpf_full_size_traces(gpu_ctx, kind, n):
+def test_bpf_full_size_traces(gpu_ctx, engine, kind, n):
     z, progs = load()
     t = mosrx.Trace(kind, n, nflows=3000)
     ps = program_sets(z, progs)[0][0]
-    gpu_ctx.bpf_set(ps)
+    bpf_set(gpu_ctx, engine, ps)
     db = gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len)
     gpu_ctx.bpf_dev(db)
     got = db.matches()

@@ -6,7 +6,8 @@
  * gotos (forward only, so the control flow is a DAG the compiler structurizes
  * for divergent lanes), A / X / the used scratch slots as registers, packet
  * loads at constant offsets resolved at generation time to the frame's LDS
- * stage or to memory — and the whole set is one kernel, compiled with hipRTC
+ * stage (sized to what the set reads) or to memory — and the whole set is one
+ * kernel, compiled with hipRTC
  * for gfx950 and loaded as a module.  Same semantics as the interpreter in
  * mosrx_bpf.hip (itself pinned to mOS's sfbpf_filter, bpf/sf_bpf_filter.c:
  * 214-536): the staging, bounds checks and return conventions are generated
@@ -32,8 +33,6 @@ enum {
 	ADD = 0, SUB = 0x10, MUL = 0x20, DIV = 0x30, OR = 0x40, AND = 0x50, LSH = 0x60, RSH = 0x70, NEG = 0x80,
 	JA = 0, JEQ = 0x10, JGT = 0x20, JGE = 0x30, JSET = 0x40, K = 0, X = 8, A = 0x10, TAX = 0, TXA = 0x80,
 };
-
-#define STAGE_B 141u   /* frame bytes staged in LDS, as in mosrx_bpf.hip */
 
 /* ---- growable text buffer ---- */
 struct sbuf {
@@ -80,9 +79,6 @@ static const char k_preamble[] =
 	"typedef unsigned short u16;\n"
 	"typedef unsigned char u8;\n"
 	"typedef u32 u32x4 __attribute__((ext_vector_type(4)));\n"
-	"#define STAGE_V 9u\n"
-	"#define STAGE_LD 37u\n"
-	"#define STAGE_B 141u\n"
 	"static __device__ __attribute__((always_inline)) inline u32 ld_le32(__amdgpu_buffer_rsrc_t rs, u32 a) {\n"
 	"  const u32 a4 = a & ~3u;\n"
 	"  const u32 lo = __builtin_amdgcn_raw_buffer_load_b32(rs, a4, 0, 0);\n"
@@ -275,12 +271,38 @@ static uint64_t set_hash(const mosrx_bpf_insn *insns, const mosrx_bparams *t)
 	return h;
 }
 
+/* 16-byte pieces of each frame to stage in LDS: enough for every constant
+ * offset the set loads, and 96 bytes (Ethernet + IP + TCP headers with
+ * options) when a program loads at X + k; loads past the stage read memory. */
+static uint32_t stage_pieces(const mosrx_bpf_insn *insns, const mosrx_bparams *t)
+{
+	uint64_t need = 18;   /* the datagram-length probe reads frame bytes 12..17 */
+	uint32_t j, i;
+	for (j = 0; j < t->nprog; j++)
+		for (i = 0; i < t->prog_len[j]; i++) {
+			const mosrx_bpf_insn *f = &insns[t->prog_off[j] + i];
+			const uint16_t c = f->code;
+			uint64_t end = 0;
+			if (c == (LD | W | ABS)) end = (uint64_t)f->k + 4;
+			else if (c == (LD | H | ABS)) end = (uint64_t)f->k + 2;
+			else if (c == (LD | B | ABS) || c == (LDX | MSH | B)) end = (uint64_t)f->k + 1;
+			else if (c == (LD | W | IND) || c == (LD | H | IND) || c == (LD | B | IND)) end = 96;
+			if (end > need)
+				need = end;
+		}
+	/* frame bytes [0, 16 V - 3) are staged whatever the start alignment */
+	need = (need + 3 + 15) / 16;
+	return need > 9 ? 9 : (uint32_t)need;
+}
+
 int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out)
 {
 	struct sbuf s = {0};
+	const uint32_t v = stage_pieces(insns, t);
 	uint32_t j;
 	int rc;
 	*out = NULL;
+	sb_printf(&s, "#define STAGE_V %uu\n#define STAGE_LD %uu\n#define STAGE_B %uu\n", v, 4 * v + 1, 16 * v - 3);
 	sb_printf(&s, "%s", k_preamble);
 	for (j = 0; j < t->nprog; j++)
 		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u))) {

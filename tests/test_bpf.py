@@ -7,6 +7,7 @@ CPU tests pin the oracle restatement to them; GPU tests compare the kernel
 (through the C ABI) with both, bit-exact on every match bit.
 """
 import os
+import random
 import struct
 
 import numpy as np
@@ -158,6 +159,66 @@ def test_bpf_jit_compiles_every_golden_set():
         assert src.count("/* program ") == len(ps)
 
 
+# random admitted programs: every opcode sfbpf_filter runs, forward jumps to
+# anywhere later, loads in / past the LDS stage / past the frame, scratch slots
+_LOADS = [0x20, 0x28, 0x30, 0x40, 0x48, 0x50, 0xb1, 0x80, 0x81]
+_ALU = [0x04, 0x14, 0x24, 0x34, 0x44, 0x54, 0x64, 0x74, 0x0c, 0x1c, 0x2c, 0x3c, 0x4c, 0x5c, 0x6c, 0x7c, 0x84]
+_JMP = [0x15, 0x25, 0x35, 0x45, 0x1d, 0x2d, 0x3d, 0x4d]
+_MISC = [0x00, 0x01, 0x60, 0x61, 0x02, 0x03, 0x07, 0x87]
+
+
+def random_program(rng, n):
+    ins = []
+    for i in range(n - 1):
+        left = n - 2 - i                       # last valid jump offset
+        r = rng.random()
+        if r < 0.30:
+            code = rng.choice(_LOADS)
+            mode = code & 0xe0
+            k = (rng.randint(0, 80) if rng.random() < 0.8 else rng.choice([rng.randint(80, 2000), 0xFFFFFFF0]))
+            if mode == 0x40:
+                k = rng.randint(0, 60)
+            elif code == 0xb1:
+                k = rng.choice([14, rng.randint(0, 100)])
+            ins.append(I_(code, k))
+        elif r < 0.55:
+            code = rng.choice(_ALU)
+            k = rng.getrandbits(32)
+            if code in (0x64, 0x74):
+                k = rng.randint(0, 40)
+            if code == 0x34 and k == 0:
+                k = 3
+            ins.append(I_(code, k))
+        elif r < 0.80:
+            code = rng.choice(_JMP + [0x05])
+            if code == 0x05:
+                ins.append(I_(code, rng.randint(0, left)))
+            else:
+                k = rng.choice([0, 0x800, 6, rng.getrandbits(8), rng.getrandbits(32)])
+                ins.append(I_(code, k, rng.randint(0, left), rng.randint(0, left)))
+        elif r < 0.95:
+            code = rng.choice(_MISC)
+            k = rng.randint(0, 15) if code in (0x60, 0x61, 0x02, 0x03) else rng.getrandbits(32)
+            ins.append(I_(code, k))
+        else:
+            ins.append(I_(rng.choice([0x06, 0x16]), rng.choice([0, 1, rng.getrandbits(32)])))
+    ins.append(I_(rng.choice([0x06, 0x16]), rng.choice([1, 0xFFFF, rng.getrandbits(32)])))
+    return prog(*ins)
+
+
+def random_sets(seed, nsets=2):
+    rng = random.Random(seed)
+    return [[(random_program(rng, rng.randint(2, 48)), b % 2) for b in range(32)] for _ in range(nsets)]
+
+
+def test_random_programs_admitted_and_compiled():
+    for ps in random_sets(7):
+        for p, _ in ps:
+            assert mosrx.bpf_check(p) == 0, p
+        rc, size, log = mosrx.bpf_jit_compile(ps)
+        assert rc == 0 and size > 0, log
+
+
 # ---------------------------------------------------------------- GPU parity
 @pytest.fixture(params=[mosrx.BPF_ENGINE_JIT, mosrx.BPF_ENGINE_INTERP], ids=["jit", "interp"])
 def engine(gpu_ctx, request):
@@ -236,3 +297,16 @@ def test_bpf_full_size_traces(gpu_ctx, engine, kind, n):
     got = db.matches()
     db.free()
     np.testing.assert_array_equal(got, O.bpf_eval(ps, t.frames[:t.frames_bytes], t.off, t.len))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_bpf_random_programs(gpu_ctx, engine, seed):
+    """Random admitted programs on both engines against the oracle (itself pinned to
+    mOS's sfbpf_filter by the golden returns): every opcode, jump shape and bound."""
+    z, _ = load()
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 4096, nflows=500, seed=seed)
+    for buf, off, ln in ((z["frames"], z["off"], z["len"]), (t.frames[:t.frames_bytes], t.off, t.len)):
+        for ps in random_sets(seed):
+            bpf_set(gpu_ctx, engine, ps)
+            np.testing.assert_array_equal(gpu_ctx.bpf_host(buf, off, ln), O.bpf_eval(ps, buf, off, ln))

@@ -446,10 +446,9 @@ __device__ __forceinline__ void flush_counters(const mosrx_kparams &kp, const ui
 // barrier (each wave fills the LDS tables itself; a wave's LDS accesses are
 // ordered).  Longer frames (only when the shape is forced onto them) are
 // summed by their wave tail by tail, 4 KiB per pass.
-template <int VAR>
+template <int VAR, uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL)>
 __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uint32_t tile)
 {
-	constexpr uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL);
 	constexpr int AUX = TAIL_AUX(VAR);
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
@@ -972,13 +971,18 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		// buffer order: the next frame starts at or after this capture's end
 		const uint32_t onext = (uint32_t)__shfl_down((int)o, 1);
 		const bool sorted = __ballot(lane + 1u < nact && onext < hi_l) == 0;
-		if (sorted) {
-			const uint32_t A = uni(__builtin_amdgcn_readlane(lo_l, 0));
-			const uint32_t Z = uni(__builtin_amdgcn_readlane(hi_l, nact - 1u));   // non-decreasing in buffer order
-			if (Z > A)
-				stream_scan<S, AUX, DBG, U>(rs, lo_l, hi_l, A, Z, sidx, lane, row, s_raw[sidx]);
-		} else if constexpr (!(DBG & 16)) {
-			stream_frames<S, AUX>(rs, lo_l, hi_l, sidx, lane, row);
+		const uint64_t cmask = __ballot(hi_l > lo_l);
+		if (sorted && cmask) {
+			// the span runs from the first candidate's split to the last
+			// candidate's capture end (in buffer order both are monotone, and a
+			// candidate's capture is clipped to the buffer, so a bogus offset on a
+			// frame without a tail can never stretch the span)
+			const uint32_t A = uni(__builtin_amdgcn_readlane(lo_l, (int)__builtin_ctzll(cmask)));
+			const uint32_t Z = uni(__builtin_amdgcn_readlane(hi_l, 63 - (int)__builtin_clzll(cmask)));
+			stream_scan<S, AUX, DBG, U>(rs, lo_l, hi_l, A, Z, sidx, lane, row, s_raw[sidx]);
+		} else if (!sorted) {
+			if constexpr (!(DBG & 16))
+				stream_frames<S, AUX>(rs, lo_l, hi_l, sidx, lane, row);
 		}
 		__syncthreads();   // B
 	}

@@ -22,7 +22,18 @@ __global__ __launch_bounds__(64 * (1 + S)) __attribute__((amdgpu_waves_per_eu(W)
 	classify_tile_stream<S, 2, DBG, U, T>(kp, blockIdx.x);
 }
 
+template <uint32_t T>
+__global__ __launch_bounds__(T) void k_small(mosrx_kparams kp)
+{
+	classify_tile_small<2, T>(kp, blockIdx.x);
+}
+
 typedef void (*lfn)(const mosrx_kparams *, hipStream_t);
+template <uint32_t T>
+static void launch_small(const mosrx_kparams *kp, hipStream_t s)
+{
+	hipLaunchKernelGGL((k_small<T>), dim3((kp->n + T - 1) / T), dim3(T), 0, s, *kp);
+}
 template <int DBG, int MINB = 1>
 static void launch_dbg(const mosrx_kparams *kp, hipStream_t s)
 {
@@ -110,15 +121,13 @@ int main(int argc, char **argv)
 	}
 	const double bytes = (double)t.caplen_sum + 22.0 * n;
 	printf("trace kind %d n %u: %.2f MB algorithmic\n", kind, n, bytes / 1e6);
+	if (kind == MOSRX_TRACE_S64 || kind == MOSRX_TRACE_FW64) {
+		run("SMALL 256", launch_small<256>, kps, nb, bytes);
+		run("SMALL 128", launch_small<128>, kps, nb, bytes);
+		run("SMALL 64", launch_small<64>, kps, nb, bytes);
+		return 0;
+	}
 	run("product LARGE", launch_product, kps, nb, bytes);
 	run("product S13", launch_stream, kps, nb, bytes);
-	run("S13 T32", launch_sdbg<3, 0, 8, 4, 32>, kps, nb, bytes);
-	run("S12 T32", launch_sdbg<2, 0, 8, 4, 32>, kps, nb, bytes);
-	run("S11 T32", launch_sdbg<1, 0, 8, 4, 32>, kps, nb, bytes);
-	run("S11 T32 U8", launch_sdbg<1, 0, 8, 8, 32>, kps, nb, bytes);
-	run("S12 T32 U8", launch_sdbg<2, 0, 8, 8, 32>, kps, nb, bytes);
-	run("S13 T48", launch_sdbg<3, 0, 8, 4, 48>, kps, nb, bytes);
-	run("S13 T32 DBG 7", launch_sdbg<3, 7, 8, 4, 32>, kps, nb, bytes);
-	run("S13 DBG 7", launch_sdbg<3, 7, 8, 4>, kps, nb, bytes);
 	return 0;
 }

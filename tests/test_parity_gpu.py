@@ -327,3 +327,18 @@ def test_stream_shapes_layouts(gpu_ctx, variant):
         run_both(gpu_ctx, buf, off, ln, mosrx.default_params())
     finally:
         gpu_ctx.set_variant(2)
+
+
+def test_bogus_offsets_after_sorted_frames(gpu_ctx):
+    """Descriptors in buffer order whose last entries point past the buffer (or
+    carry zero length): the tail span stops at the last frame with a tail."""
+    frames = [tcp_frame(payload=bytes(range(200)) * 7) for _ in range(70)]
+    buf, off, ln = pack_frames(frames)
+    off = np.concatenate([off, np.array([len(buf) + 5, 0xFFFF0000, 0xFFFFFFF0], np.uint32)])
+    ln = np.concatenate([ln, np.array([1500, 1500, 0], np.uint16)])
+    for variant in STREAM_VARIANTS + [2]:
+        gpu_ctx.set_variant(variant)
+        try:
+            run_both(gpu_ctx, buf, off, ln, mosrx.default_params())
+        finally:
+            gpu_ctx.set_variant(2)

@@ -384,7 +384,9 @@ def main():
     if ws != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {ws}", file=sys.stderr)
     dist = Dist(ws, rank)
-    ctx = mosrx.Context(local)
+    # MOSRX_BENCH_DEVICE pins every rank to one device: a rehearsal of the
+    # multi-rank path on a one-GPU box (scripts/gpu_r1_dist.sh), never a result
+    ctx = mosrx.Context(int(os.environ.get("MOSRX_BENCH_DEVICE", local)))
     keys = [k for k in args.workloads.split(",") if k]
     results, traces = {}, {}
     for k in keys:

@@ -5,9 +5,10 @@
  * straight-line gfx950 code — one labelled block per instruction, jumps as
  * gotos (forward only, so the control flow is a DAG the compiler structurizes
  * for divergent lanes), A / X / the used scratch slots as registers, packet
- * loads at constant offsets resolved at generation time to the frame's LDS
- * stage (sized to what the set reads) or to memory — and the whole set is one
- * kernel, compiled with hipRTC
+ * loads at constant offsets resolved at generation time to registers (the
+ * staged bytes realigned once per frame), to the LDS stage (sized to what the
+ * set reads; loads at X + k) or to memory — and the whole set is one kernel,
+ * compiled with hipRTC
  * for gfx950 and loaded as a module.  Same semantics as the interpreter in
  * mosrx_bpf.hip (itself pinned to mOS's sfbpf_filter, bpf/sf_bpf_filter.c:
  * 214-536): the staging, bounds checks and return conventions are generated
@@ -93,6 +94,9 @@ static const char k_preamble[] =
 	"  }\n"
 	"  return ld_le32(rs, o + k);\n"
 	"}\n"
+	"#define STAGE_W (4u * STAGE_V - 1u)\n"
+	"/* little-endian dword of frame bytes [k, k+4), k constant, from the registers */\n"
+	"#define W32(k) ((k) % 4u == 0u ? w[(k) / 4u] : __builtin_amdgcn_alignbyte(w[(k) / 4u + 1u], w[(k) / 4u], (k) % 4u))\n"
 	"static __device__ __attribute__((always_inline)) inline u32 be32(u32 v) { return __builtin_bswap32(v); }\n"
 	"static __device__ __attribute__((always_inline)) inline u32 be16(u32 v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }\n"
 	"extern \"C\" __global__ __launch_bounds__(256) void mosrx_bpf_jit(const u8 *frames, const u32 *offs,\n"
@@ -111,18 +115,23 @@ static const char k_preamble[] =
 	"  }\n"
 	"  u32 *win = s_win + STAGE_LD * t;\n"
 	"  const u32 sh = o & 3u;\n"
+	"  u32 w[STAGE_W];   /* frame bytes [4i, 4i + 4) in w[i]: constant-offset loads read registers */\n"
 	"  {\n"
 	"    const u32 base = live ? (o & ~3u) : nbytes + 16u;\n"
 	"    u32x4 v[STAGE_V];\n"
 	"#pragma unroll\n"
 	"    for (u32 m = 0; m < STAGE_V; m++) v[m] = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u * m, 0, 0);\n"
+	"    u32 r[4 * STAGE_V];\n"
 	"#pragma unroll\n"
 	"    for (u32 m = 0; m < STAGE_V; m++) {\n"
+	"      r[4 * m + 0] = v[m].x; r[4 * m + 1] = v[m].y; r[4 * m + 2] = v[m].z; r[4 * m + 3] = v[m].w;\n"
 	"      win[4 * m + 0] = v[m].x; win[4 * m + 1] = v[m].y; win[4 * m + 2] = v[m].z; win[4 * m + 3] = v[m].w;\n"
 	"    }\n"
+	"#pragma unroll\n"
+	"    for (u32 i = 0; i < STAGE_W; i++) w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);\n"
 	"  }\n"
-	"  if (cap >= 18u && (fr_le32(win, sh, rs, o, 12u, 2u) & 0xFFFFu) == 0x0008u) {\n"
-	"    lip = 14u + be16(fr_le32(win, sh, rs, o, 16u, 2u));\n"
+	"  if (cap >= 18u && (w[3] & 0xFFFFu) == 0x0008u) {\n"
+	"    lip = 14u + be16(w[4]);\n"
 	"    if (lip > cap) lip = 0;\n"
 	"  }\n"
 	"  u32 match = 0;\n";
@@ -136,7 +145,18 @@ static void gen_abs_check(struct sbuf *s, unsigned j, uint32_t k, uint32_t size)
 		sb_printf(s, "if (%uu > L) goto P%u_R0; ", (unsigned)(k + size), j);
 }
 
-static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_t len, int ipm)
+/* Constant-offset load expression: registers when frame bytes [k, k + 8) are
+ * in w[], else the LDS stage / memory (fr_le32). */
+static void gen_ld(struct sbuf *s, uint32_t k, uint32_t size, uint32_t stage_w)
+{
+	if ((uint64_t)k + 8 <= 4ull * stage_w)
+		sb_printf(s, "W32(%uu)", k);
+	else
+		sb_printf(s, "fr_le32(win, sh, rs, o, %uu, %uu)", k, size);
+}
+
+static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_t len, int ipm,
+                       uint32_t stage_w)
 {
 	uint8_t *tgt, mem_used[16];
 	uint32_t i, q;
@@ -184,9 +204,15 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 		switch (c) {
 		case RET | K: sb_printf(s, "ret = %uu; goto P%u_E;", k, j); break;
 		case RET | A: sb_printf(s, "ret = A; goto P%u_E;", j); break;
-		case LD | W | ABS: gen_abs_check(s, j, k, 4); sb_printf(s, "A = be32(fr_le32(win, sh, rs, o, %uu, 4u));", k); break;
-		case LD | H | ABS: gen_abs_check(s, j, k, 2); sb_printf(s, "A = be16(fr_le32(win, sh, rs, o, %uu, 2u));", k); break;
-		case LD | B | ABS: gen_abs_check(s, j, k, 1); sb_printf(s, "A = fr_le32(win, sh, rs, o, %uu, 1u) & 0xFFu;", k); break;
+		case LD | W | ABS:
+			gen_abs_check(s, j, k, 4); sb_printf(s, "A = be32("); gen_ld(s, k, 4, stage_w); sb_printf(s, ");");
+			break;
+		case LD | H | ABS:
+			gen_abs_check(s, j, k, 2); sb_printf(s, "A = be16("); gen_ld(s, k, 2, stage_w); sb_printf(s, ");");
+			break;
+		case LD | B | ABS:
+			gen_abs_check(s, j, k, 1); sb_printf(s, "A = "); gen_ld(s, k, 1, stage_w); sb_printf(s, " & 0xFFu;");
+			break;
 		case LD | W | LEN: sb_printf(s, "A = L;"); break;
 		case LDX | W | LEN: sb_printf(s, "X = L;"); break;
 		case LD | W | IND:
@@ -203,7 +229,7 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 			break;
 		case LDX | MSH | B:
 			gen_abs_check(s, j, k, 1);
-			sb_printf(s, "X = (fr_le32(win, sh, rs, o, %uu, 1u) & 0xFu) << 2;", k);
+			sb_printf(s, "X = ("); gen_ld(s, k, 1, stage_w); sb_printf(s, " & 0xFu) << 2;");
 			break;
 		case LD | IMM: sb_printf(s, "A = %uu;", k); break;
 		case LDX | IMM: sb_printf(s, "X = %uu;", k); break;
@@ -305,7 +331,7 @@ int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, c
 	sb_printf(&s, "#define STAGE_V %uu\n#define STAGE_LD %uu\n#define STAGE_B %uu\n", v, 4 * v + 1, 16 * v - 3);
 	sb_printf(&s, "%s", k_preamble);
 	for (j = 0; j < t->nprog; j++)
-		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u))) {
+		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u, 4 * v - 1))) {
 			free(s.p);
 			return rc;
 		}

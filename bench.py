@@ -50,8 +50,10 @@ WORKLOADS = {
     "M1500_fh": (mosrx.TRACE_M1500, 65_536, "config #3 classify + flow-table hash (HashFlow of FindStream's tuple)"),
     "M1500_tx": (mosrx.TRACE_M1500, 65_536, "config #3 TX checksum rewrite (MOS_UPDATE_IP|TCP_CHKSUM), in place"),
     "IMIX_bpf": (mosrx.TRACE_IMIX, 262_144, "config #4 batched BPF, 8 mOS filter programs (sfbpf_compile output)"),
+    "IMIX_cls_bpf": (mosrx.TRACE_IMIX, 262_144, "config #4 classify + the 8 BPF programs fused in one pass"),
 }
-OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_tx": mosrx.OP_TX_CSUM, "IMIX_bpf": mosrx.OP_BPF}
+OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_tx": mosrx.OP_TX_CSUM, "IMIX_bpf": mosrx.OP_BPF,
+       "IMIX_cls_bpf": mosrx.OP_CLASSIFY_BPF}
 # filter expressions whose compiled programs (tests/golden/bpf.npz, mOS's own compiler) the BPF row runs
 BPF_BENCH = [("tcp", 0), ("tcp port 80", 0), ("tcp[tcpflags] & tcp-syn != 0", 1), ("net 192.168.0.0/16 and tcp", 1),
              ("host 10.0.0.1 and port 80", 0), ("ip[8] < 64", 1), ("tcp[((tcp[12:1] & 0xf0) >> 2):4] = 0x47455420", 1),
@@ -103,6 +105,8 @@ def algo_bytes(tr: mosrx.Trace, key: str = "") -> int:
     line a filter reads; deeper loads are extra)."""
     if key.endswith("_tx"):
         return tr.caplen_sum + tr.n * (DESC_BYTES + 4)
+    if key.endswith("_cls_bpf"):   # the classify bytes + the 4-byte match mask
+        return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES + 4)
     if key.endswith("_bpf"):
         return tr.n * (DESC_BYTES + 4) + int(np.minimum(tr.len, 64).astype(np.int64).sum())
     extra = 4 if key.endswith("_fh") else 0
@@ -153,7 +157,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
     if key in OPS:
         op = OPS[key]
         arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op == mosrx.OP_TX_CSUM else 0
-        if op == mosrx.OP_BPF:
+        if op in (mosrx.OP_BPF, mosrx.OP_CLASSIFY_BPF):
             ctx.bpf_set(bpf_bench_programs())
         prewarm(lambda: ctx.time_op(op, dbs, 200, STREAMS, arg, kernels=False))
         if warmup:
@@ -327,13 +331,17 @@ def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
             O.classify_fh(tr.frames, tr.off, tr.len, O.params())
         elif key.endswith("_tx"):
             O.tx_csum(tr.frames, tr.off, tr.len, mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM)
+        elif key.endswith("_cls_bpf"):
+            O.classify(tr.frames, tr.off, tr.len, O.params())
+            O.bpf_eval(progs, tr.frames, tr.off, tr.len)
         else:
             O.bpf_eval(progs, tr.frames, tr.off, tr.len)
         reps += 1
         el = time.perf_counter() - t0
         if el >= min_s:
             break
-    fn = {"_fh": "mo_classify_fh", "_tx": "mo_tx_csum", "bpf": "mo_bpf_eval"}[key[-3:]]
+    fn = ("mo_classify + mo_bpf_eval" if key.endswith("_cls_bpf") else
+          {"_fh": "mo_classify_fh", "_tx": "mo_tx_csum", "bpf": "mo_bpf_eval"}[key[-3:]])
     return {"value": round(reps * ab / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "mpkts": round(reps * tr.n / el / 1e6, 3),
             "sample": f"{reps} passes over one {tr.n}-frame batch ({el:.1f} s), oracle {fn}, 1 thread"}
@@ -372,7 +380,7 @@ def main():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workloads",
-                    default="M1500,S64,S64_hdr,S64_queue,M1500_queue,IMIX,M1500_fh,M1500_tx,IMIX_bpf")
+                    default="M1500,S64,S64_hdr,S64_queue,M1500_queue,IMIX,M1500_fh,M1500_tx,IMIX_bpf,IMIX_cls_bpf")
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="rx batches in flight (1 = strictly serial launches, as for rocprof summaries)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")

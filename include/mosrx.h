@@ -31,8 +31,19 @@
 #ifndef MOSRX_H
 #define MOSRX_H
 
+#ifndef __HIPCC_RTC__
 #include <stddef.h>
 #include <stdint.h>
+#else   /* compiled by hipRTC for a fused BPF kernel (csrc/bpf_jit.c): no libc headers there */
+typedef unsigned char uint8_t;
+typedef signed char int8_t;
+typedef unsigned short uint16_t;
+typedef unsigned int uint32_t;
+typedef int int32_t;
+typedef unsigned long long uint64_t;
+typedef long long int64_t;
+typedef unsigned long size_t;
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -205,9 +216,11 @@ int  mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
 /* The same two measurements for any row of the path: `op` over batch i % nb
  * on stream i % nstreams (total_ms), and the average single-launch duration on
  * the context stream (avg_kernel_ms); either pointer may be NULL.  out[i]:
- * records (CLASSIFY, CLASSIFY_FH), match masks (BPF), unused (TX_CSUM, `arg`
- * = its flags); aux[i]: flow hashes (CLASSIFY_FH). */
-enum { MOSRX_OP_CLASSIFY = 0, MOSRX_OP_CLASSIFY_FH = 1, MOSRX_OP_BPF = 2, MOSRX_OP_TX_CSUM = 3 };
+ * records (CLASSIFY, CLASSIFY_FH, CLASSIFY_BPF), match masks (BPF), unused
+ * (TX_CSUM, `arg` = its flags); aux[i]: flow hashes (CLASSIFY_FH), match masks
+ * (CLASSIFY_BPF). */
+enum { MOSRX_OP_CLASSIFY = 0, MOSRX_OP_CLASSIFY_FH = 1, MOSRX_OP_BPF = 2, MOSRX_OP_TX_CSUM = 3,
+       MOSRX_OP_CLASSIFY_BPF = 4 };
 int  mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
                    void *const *aux, uint32_t iters, uint32_t nstreams, float *total_ms, float *avg_kernel_ms);
 /* The device's streaming-read ceiling: `iters` coalesced 16-byte-load passes
@@ -276,6 +289,18 @@ int  mosrx_bpf_jit_source(const mosrx_bpf_prog *progs, uint32_t nprog, char **sr
  * it (no GPU needed): 0 and the code-object size, or -errno and the log. */
 int  mosrx_bpf_jit_compile(const mosrx_bpf_prog *progs, uint32_t nprog, char *log, size_t logsz,
                            size_t *code_size);
+/* Same for the fused classify + BPF kernel (the set inlined into the
+ * classification kernel's header wave). */
+int  mosrx_bpf_jit_compile_fused(const mosrx_bpf_prog *progs, uint32_t nprog, char *log, size_t logsz,
+                                 size_t *code_size);
+/* Classification (as mosrx_classify_dev) and the installed BPF set (as
+ * mosrx_bpf_dev) in ONE pass over the frames: with the JIT engine the set is
+ * compiled into the classify kernel, whose header wave evaluates it on the
+ * bytes it already holds; otherwise two launches, same results.
+ * mosrx_bpf_fused() = 1 when the installed set has the fused kernel. */
+int  mosrx_classify_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_match,
+                            void *stream);
+int  mosrx_bpf_fused(const mosrx_ctx *c);
 /* Device-resident evaluation: d_match[i] bit j = (sfbpf_filter(prog j, frame i) != 0). */
 int  mosrx_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t *d_match, void *stream);
 /* End-to-end from host memory (blocking). */

@@ -129,6 +129,26 @@ int mosrx_bpf_jit_compile(const mosrx_bpf_prog *progs, uint32_t nprog, char *log
 	return rc;
 }
 
+int mosrx_bpf_jit_compile_fused(const mosrx_bpf_prog *progs, uint32_t nprog, char *log, size_t logsz,
+                                size_t *code_size)
+{
+	mosrx_bpf_insn *staged;
+	mosrx_bparams t;
+	uint32_t total;
+	int rc;
+	if (!(staged = malloc(MOSRX_BPF_MAX_INSNS * sizeof(*staged))))
+		return -ENOMEM;
+	if (!(rc = stage_set(progs, nprog, &t, staged, &total)))
+		rc = mosrx__bpf_jit_compile_fused(staged, &t, log, logsz, code_size);
+	free(staged);
+	return rc;
+}
+
+int mosrx_bpf_fused(const mosrx_ctx *c)
+{
+	return c && c->bpf_fs && c->bpf_fm ? 1 : 0;
+}
+
 int mosrx_bpf_set_engine(mosrx_ctx *c, int engine)
 {
 	if (!c || (engine != MOSRX_BPF_ENGINE_INTERP && engine != MOSRX_BPF_ENGINE_JIT))
@@ -168,7 +188,9 @@ int mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
 	if (total)
 		HIPCHK(hipMemcpy(c->d_bpf, staged, (size_t)total * sizeof(mosrx_bpf_insn), hipMemcpyHostToDevice));
 	c->bpf = t;
-	c->bpf_fn = NULL;
+	c->bpf_fn = NULL;   /* the compiled kernels of the previous set no longer apply */
+	c->bpf_fs = NULL;
+	c->bpf_fm = NULL;
 	if (c->bpf_engine_req == MOSRX_BPF_ENGINE_JIT && nprog)
 		mosrx__bpf_jit_build(c, staged);   /* on failure the interpreter runs the set */
 	return 0;

@@ -145,18 +145,40 @@ static void gen_abs_check(struct sbuf *s, unsigned j, uint32_t k, uint32_t size)
 		sb_printf(s, "if (%uu > L) goto P%u_R0; ", (unsigned)(k + size), j);
 }
 
-/* Constant-offset load expression: registers when frame bytes [k, k + 8) are
- * in w[], else the LDS stage / memory (fr_le32). */
-static void gen_ld(struct sbuf *s, uint32_t k, uint32_t size, uint32_t stage_w)
+/* How the generated program code reads frame bytes. */
+struct genopt {
+	int fused;          /* 0: standalone kernel (staged bytes); 1: classify header wave (its window) */
+	uint32_t stage_w;   /* standalone: realigned staged dwords in w[] */
+};
+
+/* Constant-offset load expression.  Standalone: registers when frame bytes
+ * [k, k + 8) are in w[], else the LDS stage / memory (fr_le32).  Fused: the
+ * header window's realigned registers (frame bytes [2, 94)), else memory. */
+static void gen_ld(struct sbuf *s, uint32_t k, uint32_t size, const struct genopt *g)
 {
-	if ((uint64_t)k + 8 <= 4ull * stage_w)
+	if (g->fused) {
+		if (k >= 2 && (uint64_t)k + 8 <= 94)
+			sb_printf(s, "RW32(%uu)", k);
+		else
+			sb_printf(s, "hk_ld_le32(rs, o + %uu)", k);
+	} else if ((uint64_t)k + 8 <= 4ull * g->stage_w) {
 		sb_printf(s, "W32(%uu)", k);
-	else
+	} else {
 		sb_printf(s, "fr_le32(win, sh, rs, o, %uu, %uu)", k, size);
+	}
+}
+
+/* Load at the run-time offset kk (X + k). */
+static const char *ind_ld(const struct genopt *g, uint32_t size)
+{
+	if (g->fused)
+		return size == 4 ? "hk_ind(kk, 4u)" : size == 2 ? "hk_ind(kk, 2u)" : "hk_ind(kk, 1u)";
+	return size == 4 ? "fr_le32(win, sh, rs, o, kk, 4u)" : size == 2 ? "fr_le32(win, sh, rs, o, kk, 2u)"
+	                                                          : "fr_le32(win, sh, rs, o, kk, 1u)";
 }
 
 static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_t len, int ipm,
-                       uint32_t stage_w)
+                       const struct genopt *g)
 {
 	uint8_t *tgt, mem_used[16];
 	uint32_t i, q;
@@ -205,31 +227,31 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 		case RET | K: sb_printf(s, "ret = %uu; goto P%u_E;", k, j); break;
 		case RET | A: sb_printf(s, "ret = A; goto P%u_E;", j); break;
 		case LD | W | ABS:
-			gen_abs_check(s, j, k, 4); sb_printf(s, "A = be32("); gen_ld(s, k, 4, stage_w); sb_printf(s, ");");
+			gen_abs_check(s, j, k, 4); sb_printf(s, "A = be32("); gen_ld(s, k, 4, g); sb_printf(s, ");");
 			break;
 		case LD | H | ABS:
-			gen_abs_check(s, j, k, 2); sb_printf(s, "A = be16("); gen_ld(s, k, 2, stage_w); sb_printf(s, ");");
+			gen_abs_check(s, j, k, 2); sb_printf(s, "A = be16("); gen_ld(s, k, 2, g); sb_printf(s, ");");
 			break;
 		case LD | B | ABS:
-			gen_abs_check(s, j, k, 1); sb_printf(s, "A = "); gen_ld(s, k, 1, stage_w); sb_printf(s, " & 0xFFu;");
+			gen_abs_check(s, j, k, 1); sb_printf(s, "A = "); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFFu;");
 			break;
 		case LD | W | LEN: sb_printf(s, "A = L;"); break;
 		case LDX | W | LEN: sb_printf(s, "X = L;"); break;
 		case LD | W | IND:
-			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 4u > L) goto P%u_R0; "
-			             "A = be32(fr_le32(win, sh, rs, o, kk, 4u)); }", k, j);
+			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 4u > L) goto P%u_R0; A = be32(%s); }",
+			          k, j, ind_ld(g, 4));
 			break;
 		case LD | H | IND:
-			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 2u > L) goto P%u_R0; "
-			             "A = be16(fr_le32(win, sh, rs, o, kk, 2u)); }", k, j);
+			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 2u > L) goto P%u_R0; A = be16(%s); }",
+			          k, j, ind_ld(g, 2));
 			break;
 		case LD | B | IND:
-			sb_printf(s, "{ const u32 kk = X + %uu; if (kk >= L) goto P%u_R0; "
-			             "A = fr_le32(win, sh, rs, o, kk, 1u) & 0xFFu; }", k, j);
+			sb_printf(s, "{ const u32 kk = X + %uu; if (kk >= L) goto P%u_R0; A = %s & 0xFFu; }",
+			          k, j, ind_ld(g, 1));
 			break;
 		case LDX | MSH | B:
 			gen_abs_check(s, j, k, 1);
-			sb_printf(s, "X = ("); gen_ld(s, k, 1, stage_w); sb_printf(s, " & 0xFu) << 2;");
+			sb_printf(s, "X = ("); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFu) << 2;");
 			break;
 		case LD | IMM: sb_printf(s, "A = %uu;", k); break;
 		case LDX | IMM: sb_printf(s, "X = %uu;", k); break;
@@ -325,13 +347,14 @@ int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, c
 {
 	struct sbuf s = {0};
 	const uint32_t v = stage_pieces(insns, t);
+	const struct genopt g = {0, 4 * v - 1};
 	uint32_t j;
 	int rc;
 	*out = NULL;
 	sb_printf(&s, "#define STAGE_V %uu\n#define STAGE_LD %uu\n#define STAGE_B %uu\n", v, 4 * v + 1, 16 * v - 3);
 	sb_printf(&s, "%s", k_preamble);
 	for (j = 0; j < t->nprog; j++)
-		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u, 4 * v - 1))) {
+		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u, &g))) {
 			free(s.p);
 			return rc;
 		}
@@ -344,15 +367,84 @@ int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, c
 	return 0;
 }
 
+/* The fused hook: the program set as a device function the classify header
+ * wave calls with its 96-byte window (mosrx_kernels.hip, VAR_BPF), plus the
+ * kernel entry points that instantiate the S13 and SMALL tiles with it. */
+static const char k_hook_pre[] =
+	"typedef unsigned int u32;\n"
+	"typedef unsigned long long u64;\n"
+	"static __device__ __attribute__((always_inline)) inline u32 be32(u32 v) { return __builtin_bswap32(v); }\n"
+	"static __device__ __attribute__((always_inline)) inline u32 be16(u32 v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }\n"
+	"static __device__ __attribute__((always_inline)) inline u32 hk_ld_le32(__amdgpu_buffer_rsrc_t rs, u32 a) {\n"
+	"  const u32 a4 = a & ~3u;\n"
+	"  const u32 lo = __builtin_amdgcn_raw_buffer_load_b32(rs, a4, 0, 0);\n"
+	"  const u32 hi = __builtin_amdgcn_raw_buffer_load_b32(rs, a4 + 4u, 0, 0);\n"
+	"  return __builtin_amdgcn_alignbyte(hi, lo, a & 3u);\n"
+	"}\n"
+	"/* frame bytes [k, k+4), k constant in [2, 86]: the realigned window registers */\n"
+	"#define RW32(k) (((k) - 2u) % 4u == 0u ? w[((k) - 2u) / 4u] \\\n"
+	"                 : __builtin_amdgcn_alignbyte(w[((k) - 2u) / 4u + 1u], w[((k) - 2u) / 4u], ((k) - 2u) % 4u))\n"
+	"/* frame bytes [kk, kk+4) at a run-time offset: the lane's LDS copy of the window, else memory */\n"
+	"#define hk_ind(kk, size) (((kk) >= 2u && (kk) + (size) <= 94u) \\\n"
+	"  ? __builtin_amdgcn_alignbyte(lw[(((kk) - 2u) >> 2) + 1u], lw[((kk) - 2u) >> 2], ((kk) - 2u) & 3u) \\\n"
+	"  : hk_ld_le32(rs, o + (kk)))\n"
+	"static __device__ __attribute__((always_inline)) inline u32 mosrx_bpf_hook(const hdr_win_t &win, u32 o, u32 cap,\n"
+	"    bool live, __amdgpu_buffer_rsrc_t rs, u32 *lw) {\n"
+	"  u32 w[WIN_DW];\n"
+	"  const u32 rsh = (o + 2u) & 3u;\n"
+	"#pragma unroll\n"
+	"  for (int j = 0; j < WIN_DW; j++) w[j] = __builtin_amdgcn_alignbyte(win.raw[j + 1], win.raw[j], rsh);\n"
+	"#pragma unroll\n"
+	"  for (int j = 0; j < WIN_DW; j++) lw[j] = w[j];\n"
+	"  lw[WIN_DW] = 0u;\n"
+	"  u32 lip = 0;\n"
+	"  if (cap >= 18u && be16hi(w[2]) == 0x0800u) {\n"
+	"    lip = 14u + be16hi(w[3]);\n"
+	"    if (lip > cap) lip = 0;\n"
+	"  }\n"
+	"  u32 match = 0;\n";
+
+static const char k_fused_main[] =
+	"#define MOSRX_RTC_BPF 1\n"
+	"#include \"mosrx_kernels.hip\"\n"
+	"extern \"C\" __global__ __launch_bounds__(WG_THREADS(MOSRX_KIND_S13)) void mosrx_classify_bpf_stream(mosrx_kparams kp)\n"
+	"{ classify_tile<MOSRX_KIND_S13, 2 | VAR_BPF>(kp, blockIdx.x); }\n"
+	"extern \"C\" __global__ __launch_bounds__(WG_THREADS(MOSRX_KIND_SMALL)) void mosrx_classify_bpf_small(mosrx_kparams kp)\n"
+	"{ classify_tile<MOSRX_KIND_SMALL, 2 | VAR_BPF>(kp, blockIdx.x); }\n";
+
+int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out)
+{
+	struct sbuf s = {0};
+	const struct genopt g = {1, 0};
+	uint32_t j;
+	int rc;
+	*out = NULL;
+	sb_printf(&s, "/* generated by bpf_jit.c */\n%s", k_hook_pre);
+	for (j = 0; j < t->nprog; j++)
+		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u, &g))) {
+			free(s.p);
+			return rc;
+		}
+	sb_printf(&s, "  return match;\n}\n#undef RW32\n#undef hk_ind\n");
+	if (s.err) {
+		free(s.p);
+		return -ENOMEM;
+	}
+	*out = s.p;
+	return 0;
+}
+
 /* hipRTC: source -> gfx950 code object (malloc'd into *code). */
-static int compile_code(const char *src, char **code, size_t *size, char *log, size_t logsz)
+static int compile_code_h(const char *src, int nh, const char *const *htexts, const char *const *hnames,
+                          char **code, size_t *size, char *log, size_t logsz)
 {
 	hiprtcProgram prog;
 	const char *opts[] = {"--offload-arch=gfx950", "-O3"};
 	size_t sz = 0;
 	int rc = 0;
 	*code = NULL;
-	if (hiprtcCreateProgram(&prog, src, "mosrx_bpf_jit.hip", 0, NULL, NULL) != HIPRTC_SUCCESS)
+	if (hiprtcCreateProgram(&prog, src, "mosrx_bpf_jit.hip", nh, (const char **)htexts, (const char **)hnames) !=
+	    HIPRTC_SUCCESS)
 		return -EIO;
 	if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
 		size_t ls = 0;
@@ -380,6 +472,44 @@ static int compile_code(const char *src, char **code, size_t *size, char *log, s
 	return rc;
 }
 
+static int compile_code(const char *src, char **code, size_t *size, char *log, size_t logsz)
+{
+	return compile_code_h(src, 0, NULL, NULL, code, size, log, logsz);
+}
+
+extern const int mosrx__src_count;
+extern const char *const mosrx__src_names[];
+extern const char *const mosrx__src_texts[];
+
+/* The fused classify + BPF module: the embedded kernel sources + the hook. */
+static int compile_fused(const char *hook, hipModule_t *mod, hipFunction_t *fs, hipFunction_t *fm, char *log,
+                         size_t logsz, size_t *code_size)
+{
+	const char *names[8], *texts[8];
+	char *code;
+	size_t sz = 0;
+	int i, n = mosrx__src_count, rc;
+	for (i = 0; i < n && i < 7; i++) {
+		names[i] = mosrx__src_names[i];
+		texts[i] = mosrx__src_texts[i];
+	}
+	names[n] = "mosrx_bpf_hook.h";
+	texts[n] = hook;
+	rc = compile_code_h(k_fused_main, n + 1, texts, names, &code, &sz, log, logsz);
+	if (code_size)
+		*code_size = rc ? 0 : sz;
+	if (rc || !mod) {
+		free(code);
+		return rc;
+	}
+	if (hipModuleLoadData(mod, code) != hipSuccess ||
+	    hipModuleGetFunction(fs, *mod, "mosrx_classify_bpf_stream") != hipSuccess ||
+	    hipModuleGetFunction(fm, *mod, "mosrx_classify_bpf_small") != hipSuccess)
+		rc = -EIO;
+	free(code);
+	return rc;
+}
+
 static int compile_module(const char *src, hipModule_t *mod, hipFunction_t *fn, char *log, size_t logsz)
 {
 	char *code;
@@ -390,6 +520,17 @@ static int compile_module(const char *src, hipModule_t *mod, hipFunction_t *fn, 
 	if (hipModuleLoadData(mod, code) != hipSuccess || hipModuleGetFunction(fn, *mod, "mosrx_bpf_jit") != hipSuccess)
 		rc = -EIO;
 	free(code);
+	return rc;
+}
+
+int mosrx__bpf_jit_compile_fused(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char *log, size_t logsz,
+                                 size_t *code_size)
+{
+	char *hook = NULL;
+	int rc = mosrx__bpf_jit_hook_source(insns, t, &hook);
+	if (!rc)
+		rc = compile_fused(hook, NULL, NULL, NULL, log, logsz, code_size);
+	free(hook);
 	return rc;
 }
 
@@ -414,10 +555,14 @@ int mosrx__bpf_jit_build(mosrx_ctx *c, const mosrx_bpf_insn *insns)
 	uint32_t i;
 	int rc;
 	c->bpf_fn = NULL;
+	c->bpf_fs = NULL;
+	c->bpf_fm = NULL;
 	c->bpf_jit_log[0] = 0;
 	for (i = 0; i < c->njit; i++)
 		if (c->jit[i].key == key) {
 			c->bpf_fn = c->jit[i].fn;
+			c->bpf_fs = c->jit[i].fs;
+			c->bpf_fm = c->jit[i].fm;
 			return 0;
 		}
 	if ((rc = mosrx__bpf_jit_source(insns, t, &src)))
@@ -429,17 +574,48 @@ int mosrx__bpf_jit_build(mosrx_ctx *c, const mosrx_bpf_insn *insns)
 		free(src);
 		if (rc)
 			return rc;
+		hipModule_t fmod = NULL;
+		hipFunction_t fs = NULL, fm = NULL;
+		char *hook = NULL;
+		if (mosrx__bpf_jit_hook_source(insns, t, &hook) ||
+		    compile_fused(hook, &fmod, &fs, &fm, c->bpf_jit_log, sizeof(c->bpf_jit_log), NULL)) {
+			fmod = NULL;   /* no fused kernel: mosrx_classify_bpf_dev runs two launches */
+			fs = fm = NULL;
+		}
+		free(hook);
 		if (c->njit == MOSRX_BPF_JIT_CACHE) {   /* evict the oldest */
 			hipModuleUnload(c->jit[0].mod);
+			if (c->jit[0].fmod)
+				hipModuleUnload(c->jit[0].fmod);
 			memmove(&c->jit[0], &c->jit[1], sizeof(c->jit[0]) * (MOSRX_BPF_JIT_CACHE - 1));
 			c->njit--;
 		}
 		c->jit[c->njit].key = key;
 		c->jit[c->njit].mod = mod;
 		c->jit[c->njit].fn = fn;
+		c->jit[c->njit].fmod = fmod;
+		c->jit[c->njit].fs = fs;
+		c->jit[c->njit].fm = fm;
 		c->njit++;
 		c->bpf_fn = fn;
+		c->bpf_fs = fs;
+		c->bpf_fm = fm;
 	}
+	return 0;
+}
+
+/* Fused classify + BPF launch (kp carries bmatch). */
+int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hipStream_t s)
+{
+	hipFunction_t f = small ? c->bpf_fm : c->bpf_fs;
+	const unsigned tile = small ? MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL) : MOSRX_KIND_FRAMES(MOSRX_KIND_S13);
+	const unsigned threads = small ? 256u : 64u * (MOSRX_KIND_H(MOSRX_KIND_S13) + MOSRX_KIND_S(MOSRX_KIND_S13));
+	mosrx_kparams k = *kp;
+	void *args[] = {&k};
+	if (!f)
+		return -EINVAL;
+	if (hipModuleLaunchKernel(f, (kp->n + tile - 1) / tile, 1, 1, threads, 1, 1, 0, s, args, NULL) != hipSuccess)
+		return -EIO;
 	return 0;
 }
 
@@ -462,8 +638,13 @@ int mosrx__bpf_jit_launch(mosrx_ctx *c, const mosrx_bparams *bp, hipStream_t s)
 void mosrx__bpf_jit_free(mosrx_ctx *c)
 {
 	uint32_t i;
-	for (i = 0; i < c->njit; i++)
+	for (i = 0; i < c->njit; i++) {
 		hipModuleUnload(c->jit[i].mod);
+		if (c->jit[i].fmod)
+			hipModuleUnload(c->jit[i].fmod);
+	}
 	c->njit = 0;
 	c->bpf_fn = NULL;
+	c->bpf_fs = NULL;
+	c->bpf_fm = NULL;
 }

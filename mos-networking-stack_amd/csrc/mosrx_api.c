@@ -287,6 +287,7 @@ static int launch_flags(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frame
 	kp.tables = c->d_tables;
 	kp.counters = cnt;
 	kp.fhash = fhash;
+	kp.bmatch = NULL;
 	kp.frames_bytes = (uint32_t)b->frames_bytes;
 	kp.n = b->n;
 	kp.flags = kflags;
@@ -361,6 +362,40 @@ int mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_ou
 int mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, void *stream)
 {
 	return mosrx_classify_dev_fh(c, b, d_out, NULL, stream);
+}
+
+int mosrx_classify_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_match,
+                           void *stream)
+{
+	const hipStream_t s = stream ? (hipStream_t)stream : (c ? c->stream : NULL);
+	mosrx_kparams kp;
+	int rc, kind;
+	if (!c || (rc = mosrx__check_batch(b, 1)))
+		return c ? rc : -EINVAL;
+	if (b->n == 0)
+		return 0;
+	if (!d_out || !d_match || ((uintptr_t)d_out & 15) || ((uintptr_t)d_match & 3))
+		return -EINVAL;
+	kind = tile_for(c, b);
+	if (!mosrx_bpf_fused(c) || (kind != MOSRX_KIND_SMALL && kind != MOSRX_KIND_S13)) {
+		if ((rc = mosrx_classify_dev(c, b, d_out, stream)))
+			return rc;
+		return mosrx_bpf_dev(c, b, d_match, stream);
+	}
+	kp.frames = b->frames;
+	kp.off = b->off;
+	kp.len = b->len;
+	kp.out = d_out;
+	kp.tables = c->d_tables;
+	kp.counters = NULL;
+	kp.fhash = NULL;
+	kp.bmatch = d_match;
+	kp.frames_bytes = (uint32_t)b->frames_bytes;
+	kp.n = b->n;
+	kp.flags = c->kflags;
+	kp.grid_cap = 0;
+	HIPCHK(hipSetDevice(c->device));
+	return mosrx__bpf_fused_launch(c, &kp, kind == MOSRX_KIND_SMALL, s);
 }
 
 int mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
@@ -621,6 +656,7 @@ static int run_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, void *out
 	case MOSRX_OP_CLASSIFY_FH: return mosrx_classify_dev_fh(c, b, (mosrx_result *)out, (uint32_t *)aux, s);
 	case MOSRX_OP_BPF: return mosrx_bpf_dev(c, b, (uint32_t *)out, s);
 	case MOSRX_OP_TX_CSUM: return mosrx_tx_csum_dev(c, b, arg, s);
+	case MOSRX_OP_CLASSIFY_BPF: return mosrx_classify_bpf_dev(c, b, (mosrx_result *)out, (uint32_t *)aux, s);
 	default: return -EINVAL;
 	}
 }
@@ -707,8 +743,8 @@ int mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t 
 {
 	int rc;
 	if (!c || !b || nb == 0 || iters == 0 || nstreams == 0 || nstreams > MOSRX_MAX_STREAMS ||
-	    op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_TX_CSUM || (op != MOSRX_OP_TX_CSUM && !out) ||
-	    (op == MOSRX_OP_CLASSIFY_FH && !aux))
+	    op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_CLASSIFY_BPF || (op != MOSRX_OP_TX_CSUM && !out) ||
+	    ((op == MOSRX_OP_CLASSIFY_FH || op == MOSRX_OP_CLASSIFY_BPF) && !aux))
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
 	if (total_ms && (rc = time_streams(c, op, arg, b, nb, out, aux, iters, nstreams, total_ms)))

@@ -47,7 +47,8 @@ struct mosrx_ctx {
 	hipFunction_t bpf_fn;            /* compiled form of the installed set (bpf_jit.c), NULL: interpreter */
 	int bpf_engine_req;              /* MOSRX_BPF_ENGINE_* for the next mosrx_bpf_set */
 	char bpf_jit_log[512];           /* hipRTC log of the last failed compile */
-	struct { uint64_t key; hipModule_t mod; hipFunction_t fn; } jit[MOSRX_BPF_JIT_CACHE];
+	hipFunction_t bpf_fs, bpf_fm;    /* fused classify + BPF kernels (S13 / SMALL tiles), NULL: none */
+	struct { uint64_t key; hipModule_t mod, fmod; hipFunction_t fn, fs, fm; } jit[MOSRX_BPF_JIT_CACHE];
 	uint32_t njit;
 	hipStream_t xs[MOSRX_MAX_STREAMS];   /* timing streams (mosrx_time_op), created on first use */
 	hipEvent_t xdone[MOSRX_MAX_STREAMS];
@@ -60,6 +61,10 @@ int mosrx__bpf_jit_launch(mosrx_ctx *c, const mosrx_bparams *bp, hipStream_t s);
 int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out);
 void mosrx__bpf_jit_free(mosrx_ctx *c);
 int mosrx__bpf_jit_compile(const char *src, char *log, size_t logsz, size_t *code_size);
+int mosrx__bpf_jit_compile_fused(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char *log, size_t logsz,
+                                 size_t *code_size);
+int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out);
+int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hipStream_t s);
 int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uint32_t n);
 
 #endif

@@ -2,8 +2,9 @@
 #ifndef MOSRX_DEVICE_H
 #define MOSRX_DEVICE_H
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
-#include <stdint.h>
+#endif
 
 #include "mosrx_internal.h"
 

@@ -6,7 +6,6 @@
 #ifndef MOSRX_INTERNAL_H
 #define MOSRX_INTERNAL_H
 
-#include <stdint.h>
 #include "../../include/mosrx.h"
 
 #ifdef __cplusplus
@@ -36,6 +35,7 @@ typedef struct mosrx_kparams {
 	const uint32_t *tables;     /* MOSRX_TAB_WORDS */
 	uint32_t       *counters;   /* MOSRX_R_COUNT u32, accumulated with atomics; may be NULL */
 	uint32_t       *fhash;      /* n flow hashes (HashFlow before the NUM_BINS mask); may be NULL */
+	uint32_t       *bmatch;     /* fused BPF match masks (hipRTC-built kernels only); else NULL */
 	uint32_t        frames_bytes;
 	uint32_t        n;
 	uint32_t        flags;      /* MOSRX_KF_* */

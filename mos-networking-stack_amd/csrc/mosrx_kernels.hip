@@ -38,9 +38,10 @@
 // All frame loads go through a buffer resource whose range is the batch
 // buffer: a bad offset can never fault, out-of-range dwords read as zero.
 
+#ifndef __HIPCC_RTC__   // hipRTC compiles this file too, for the fused classify + BPF kernel (bpf_jit.c)
 #include <hip/hip_runtime.h>
 #include <errno.h>
-#include <stdint.h>
+#endif
 
 #include "mosrx_device.h"
 
@@ -72,6 +73,8 @@ __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t c, ui
 // Variant bit 4: TX checksum fill (mosrx_tx_csum_dev) instead of classification.
 #define VAR_TX 16
 #define IS_TX(v) (((v) & VAR_TX) != 0)
+// Variant bit 5: BPF program set fused into the header wave (hipRTC builds only, bpf_jit.c).
+#define VAR_BPF 32
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 __device__ __forceinline__ uint32_t be16hi(uint32_t w) { return ((w >> 8) & 0xFF00u) | (w >> 24); } // bytes 2,3
@@ -161,6 +164,10 @@ __device__ __forceinline__ void hdr_load(__amdgpu_buffer_rsrc_t rs, uint32_t nby
 		win.raw[4 * m + 0] = v.x; win.raw[4 * m + 1] = v.y; win.raw[4 * m + 2] = v.z; win.raw[4 * m + 3] = v.w;
 	}
 }
+
+#ifdef MOSRX_RTC_BPF
+#include "mosrx_bpf_hook.h"   // generated by bpf_jit.c: mosrx_bpf_hook(win, o, cap, live, rs, lds)
+#endif
 
 // ip_fast_csum (ip_in.h:10-38) over the realigned header (w[3] = IP dword 0):
 // 32-bit adc chain, the final carry added once (its own carry lost), fold, not.
@@ -507,6 +514,14 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 		if (active && kp.fhash)
 			kp.fhash[p] = flow_hash(h);
 	}
+#ifdef MOSRX_RTC_BPF
+	if constexpr ((VAR & VAR_BPF) != 0) {
+		__shared__ uint32_t s_bw[25u * TILE];
+		const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * t);
+		if (active)
+			kp.bmatch[p] = m;
+	}
+#endif
 	flush_counters(kp, s_cnt, t);
 }
 
@@ -962,6 +977,14 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 					tail += s_part[s][lane];
 			}
 			hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, tail, p, active, lane, s_cnt);
+#ifdef MOSRX_RTC_BPF
+			if constexpr ((VAR & VAR_BPF) != 0) {
+				__shared__ uint32_t s_bw[25u * 64u];
+				const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * lane);
+				if (active)
+					kp.bmatch[p] = m;
+			}
+#endif
 		}
 	} else {
 		// ---- streamer sidx ----
@@ -1035,6 +1058,7 @@ void mosrx_classify_queue_kernel(mosrx_qparams qp)
 	kp.tables = qp.tables;
 	kp.counters = qp.counters;
 	kp.fhash = nullptr;
+	kp.bmatch = nullptr;
 	kp.frames_bytes = d->frames_bytes;
 	kp.n = d->n;
 	kp.flags = qp.flags;
@@ -1042,6 +1066,7 @@ void mosrx_classify_queue_kernel(mosrx_qparams qp)
 	classify_tile<KIND, VAR>(kp, b - d->tile_base);
 }
 
+#ifndef __HIPCC_RTC__
 // Streaming-read ceiling of the box: each workgroup streams one contiguous slab
 // with coalesced non-temporal 16-byte loads, 4 in flight per lane; a
 // data-dependent sink keeps them live.  The fastest shape found by
@@ -1125,3 +1150,4 @@ extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int vari
 	tab[kind][(kp->flags & (MOSRX_KF_TX_IP | MOSRX_KF_TX_TCP)) ? 2 : (variant >> 1) & 1](kp, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
+#endif   // __HIPCC_RTC__

@@ -55,7 +55,7 @@ class Batch(C.Structure):
 BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])   # mosrx_bpf_insn
 BPF_LEN_FRAME, BPF_LEN_IP = 0, 1
 TX_IP_CSUM, TX_TCP_CSUM = 1 << 4, 1 << 5   # MOS_UPDATE_IP_CHKSUM / MOS_UPDATE_TCP_CHKSUM
-OP_CLASSIFY, OP_CLASSIFY_FH, OP_BPF, OP_TX_CSUM = 0, 1, 2, 3
+OP_CLASSIFY, OP_CLASSIFY_FH, OP_BPF, OP_TX_CSUM, OP_CLASSIFY_BPF = 0, 1, 2, 3, 4
 BPF_MAX_PROGS = 32
 
 
@@ -148,6 +148,10 @@ def lib():
             "mosrx_bpf_jit_log": (C.c_char_p, [P]),
             "mosrx_bpf_jit_source": (I, [C.POINTER(BpfProg), U32, C.POINTER(P)]),
             "mosrx_bpf_jit_compile": (I, [C.POINTER(BpfProg), U32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+            "mosrx_bpf_jit_compile_fused": (I, [C.POINTER(BpfProg), U32, C.c_char_p, C.c_size_t,
+                                                C.POINTER(C.c_size_t)]),
+            "mosrx_classify_bpf_dev": (I, [P, C.POINTER(Batch), P, P, P]),
+            "mosrx_bpf_fused": (I, [P]),
             "mosrx_trace_gen": (I, [I, U32, U32, U64, C.POINTER(TraceC)]),
             "mosrx_trace_free": (None, [C.POINTER(TraceC)]),
             "mosrx_source_mem": (P, [P, P, P, U32, U32]),
@@ -218,6 +222,16 @@ def bpf_jit_compile(progs):
     log = C.create_string_buffer(4096)
     sz = C.c_size_t(0)
     rc = lib().mosrx_bpf_jit_compile(arr, len(progs), log, len(log), C.byref(sz))
+    return rc, int(sz.value), log.value.decode(errors="replace")
+
+
+def bpf_jit_compile_fused(progs):
+    """mosrx_bpf_jit_compile_fused: (rc, code-object bytes, hipRTC log) of the fused
+    classify + BPF kernel; no GPU needed."""
+    arr, _keep = _bpf_progs(progs)
+    log = C.create_string_buffer(8192)
+    sz = C.c_size_t(0)
+    rc = lib().mosrx_bpf_jit_compile_fused(arr, len(progs), log, len(log), C.byref(sz))
     return rc, int(sz.value), log.value.decode(errors="replace")
 
 
@@ -409,6 +423,20 @@ class Context:
         """Engine of the installed set."""
         return lib().mosrx_bpf_engine(self.handle)
 
+    def bpf_fused(self) -> bool:
+        """The installed set has a fused classify + BPF kernel."""
+        return lib().mosrx_bpf_fused(self.handle) == 1
+
+    def classify_bpf_dev(self, db: "DevBatch", sync: bool = True) -> None:
+        """Records into db.d_out and match masks into db.d_match in one pass."""
+        if db.d_match is None:
+            db.d_match = DevBuffer(self, max(db.n * 4, 4))
+        b = db.batch()
+        _chk(lib().mosrx_classify_bpf_dev(self.handle, C.byref(b), db.d_out.ptr, db.d_match.ptr, None),
+             "mosrx_classify_bpf_dev")
+        if sync:
+            _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
+
     def bpf_jit_log(self) -> str:
         return (lib().mosrx_bpf_jit_log(self.handle) or b"").decode(errors="replace")
 
@@ -465,11 +493,12 @@ class Context:
         for d in dbs:
             if op == OP_CLASSIFY_FH and d.d_fhash is None:
                 d.d_fhash = DevBuffer(self, max(d.n * 4, 4))
-            if op == OP_BPF and d.d_match is None:
+            if op in (OP_BPF, OP_CLASSIFY_BPF) and d.d_match is None:
                 d.d_match = DevBuffer(self, max(d.n * 4, 4))
         bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
         outs = (C.c_void_p * len(dbs))(*[(d.d_match.ptr if op == OP_BPF else d.d_out.ptr) for d in dbs])
-        aux = (C.c_void_p * len(dbs))(*[(d.d_fhash.ptr if d.d_fhash else None) for d in dbs])
+        aux = (C.c_void_p * len(dbs))(*[(d.d_match.ptr if op == OP_CLASSIFY_BPF else
+                                         (d.d_fhash.ptr if d.d_fhash else None)) for d in dbs])
         tot, avg = C.c_float(), C.c_float()
         _chk(lib().mosrx_time_op(self.handle, op, arg, bs, len(dbs), outs, aux, iters, nstreams,
                                  C.byref(tot) if total else None, C.byref(avg) if kernels else None),

@@ -117,7 +117,7 @@ int main(int argc, char **argv)
 		CHK(hipMalloc((void **)&l, n * 2));
 		CHK(hipMemcpy(l, t.len, n * 2, hipMemcpyHostToDevice));
 		CHK(hipMalloc((void **)&r, n * 16));
-		kps[i] = (mosrx_kparams){f, o, l, r, tables, NULL, NULL, (uint32_t)t.frames_bytes, n, MOSRX_KF_VERIFY, 0};
+		kps[i] = (mosrx_kparams){f, o, l, r, tables, NULL, NULL, NULL, (uint32_t)t.frames_bytes, n, MOSRX_KF_VERIFY, 0};
 	}
 	const double bytes = (double)t.caplen_sum + 22.0 * n;
 	printf("trace kind %d n %u: %.2f MB algorithmic\n", kind, n, bytes / 1e6);

@@ -219,6 +219,15 @@ def test_random_programs_admitted_and_compiled():
         assert rc == 0 and size > 0, log
 
 
+def test_fused_classify_bpf_compiles():
+    """The classify kernel source embedded in libmosrx.so + each set's hook
+    compile with hipRTC (no GPU needed)."""
+    z, progs = load()
+    for ps in [ps for ps, _ in program_sets(z, progs)] + random_sets(11, 1):
+        rc, size, log = mosrx.bpf_jit_compile_fused(ps)
+        assert rc == 0 and size > 0, log
+
+
 # ---------------------------------------------------------------- GPU parity
 @pytest.fixture(params=[mosrx.BPF_ENGINE_JIT, mosrx.BPF_ENGINE_INTERP], ids=["jit", "interp"])
 def engine(gpu_ctx, request):
@@ -310,3 +319,58 @@ def test_bpf_random_programs(gpu_ctx, engine, seed):
         for ps in random_sets(seed):
             bpf_set(gpu_ctx, engine, ps)
             np.testing.assert_array_equal(gpu_ctx.bpf_host(buf, off, ln), O.bpf_eval(ps, buf, off, ln))
+
+
+# ---------------------------------------------------------------- fused classify + BPF
+def fused_check(ctx, buf, off, ln, ps, frames_bytes=None, max_len=None):
+    fb = len(buf) if frames_bytes is None else frames_bytes
+    db = ctx.upload(buf, off, ln, frames_bytes=fb, max_len=max_len)
+    ctx.classify_bpf_dev(db)
+    rec, got = db.results(), db.matches()
+    db.free()
+    np.testing.assert_array_equal(got, O.bpf_eval(ps, buf[:fb], off, ln))
+    ora = O.classify(buf[:fb], off, ln, O.params())
+    assert np.array_equal(rec.view(np.uint8), ora.view(np.uint8)), "records differ from the oracle"
+
+
+@pytest.mark.gpu
+def test_classify_bpf_fused_golden(gpu_ctx, engine):
+    """One pass: records bit-exact with the oracle, match masks with mOS's returns."""
+    z, progs = load()
+    gpu_ctx.set_params(mosrx.default_params())
+    for ps, exp in program_sets(z, progs):
+        bpf_set(gpu_ctx, engine, ps)
+        assert gpu_ctx.bpf_fused() == (engine == mosrx.BPF_ENGINE_JIT), gpu_ctx.bpf_jit_log()
+        db = gpu_ctx.upload(z["frames"], z["off"], z["len"])
+        gpu_ctx.classify_bpf_dev(db)
+        np.testing.assert_array_equal(db.matches(), exp)
+        ora = O.classify(z["frames"], z["off"], z["len"], O.params())
+        assert np.array_equal(db.results().view(np.uint8), ora.view(np.uint8))
+        db.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n", [(mosrx.TRACE_IMIX, 100_000), (mosrx.TRACE_M1500, 20_000),
+                                    (mosrx.TRACE_S64, 32_768)])
+def test_classify_bpf_fused_traces(gpu_ctx, engine, kind, n):
+    z, progs = load()
+    gpu_ctx.set_params(mosrx.default_params())
+    t = mosrx.Trace(kind, n, nflows=3000)
+    for ps in (program_sets(z, progs)[0][0], random_sets(5, 1)[0]):
+        bpf_set(gpu_ctx, engine, ps)
+        fused_check(gpu_ctx, t.frames, t.off, t.len, ps, frames_bytes=t.frames_bytes, max_len=t.max_len)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("phase,align", [(1, 1), (3, 4), (13, 2)])
+def test_classify_bpf_fused_layouts(gpu_ctx, phase, align):
+    """Misaligned frames (window realignment inside the hook) and reversed
+    descriptors (the unsorted-tile path of the stream kernel)."""
+    z, progs = load()
+    gpu_ctx.set_params(mosrx.default_params())
+    frames = [bytes(z["frames"][o:o + n]) for o, n in zip(z["off"], z["len"])]
+    buf, off, ln = pack_frames(frames, align=align, phase=phase)
+    for ps in (program_sets(z, progs)[1][0], random_sets(phase, 1)[0]):
+        bpf_set(gpu_ctx, mosrx.BPF_ENGINE_JIT, ps)
+        fused_check(gpu_ctx, buf, off, ln, ps)
+        fused_check(gpu_ctx, buf, off[::-1].copy(), ln[::-1].copy(), ps)

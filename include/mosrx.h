@@ -301,6 +301,11 @@ int  mosrx_bpf_jit_compile_fused(const mosrx_bpf_prog *progs, uint32_t nprog, ch
 int  mosrx_classify_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_match,
                             void *stream);
 int  mosrx_bpf_fused(const mosrx_ctx *c);
+/* The same from host memory: H2D, the one-pass kernel, D2H of records and
+ * masks (blocking, or submit/wait on a pipeline slot like mosrx_classify_host). */
+int  mosrx_classify_bpf_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_match);
+int  mosrx_classify_bpf_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out,
+                                    uint32_t *h_match);
 /* Device-resident evaluation: d_match[i] bit j = (sfbpf_filter(prog j, frame i) != 0). */
 int  mosrx_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t *d_match, void *stream);
 /* End-to-end from host memory (blocking). */

@@ -17,7 +17,9 @@
  *     (io_module.h:81-84, dpdk_module.c:568-571); -1 for unsupported commands;
  *   - NULL members are "not provided" (select, link_devices, set_wptr).
  * New: dev_ioctl(MOSRX_PKT_RX_RESULTS) returns the batch's mosrx_result array,
- * whose verdicts the rx loop consumes instead of re-running ProcessPacket's checks.
+ * whose verdicts the rx loop consumes instead of re-running ProcessPacket's checks;
+ * with monitor filters configured, dev_ioctl(MOSRX_PKT_RX_MATCH) returns their
+ * per-frame match masks, computed in the same pass (EVAL_BPFFILTER, ip_in.c:56-63).
  */
 #ifndef MOSRX_IO_MODULE_H
 #define MOSRX_IO_MODULE_H
@@ -65,6 +67,7 @@ typedef struct {
 #endif
 
 #define MOSRX_PKT_RX_RESULTS 0x10   /* argp: const mosrx_result ** (whole batch) */
+#define MOSRX_PKT_RX_MATCH   0x11   /* argp: const uint32_t ** (whole batch's BPF match masks, bit j = program j) */
 #define MOSRX_MAX_DEVICES    16     /* MAX_DEVICES, io_module.h:87 */
 
 extern io_module_func gpu_module_func;
@@ -95,6 +98,8 @@ typedef struct mosrx_gpu_module_cfg {
 	int32_t       ngpu;                             /* 0 = all visible */
 	int32_t       pipeline;                         /* 1: classify batch k+1 while k is consumed */
 	mosrx_params  params;                           /* stack state (num_msp, forward, key, ...) */
+	const mosrx_bpf_prog *bpf_progs;                /* monitor filters (SET_BPFFILTER output), evaluated in the */
+	uint32_t      bpf_nprog;                        /*   classify pass; kept by the caller until init_handle */
 } mosrx_gpu_module_cfg;
 
 void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg);

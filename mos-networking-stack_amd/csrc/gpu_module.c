@@ -34,6 +34,7 @@ struct stage {
 	uint32_t *off;            /* pinned */
 	uint16_t *len;            /* pinned */
 	mosrx_result *res;        /* pinned */
+	uint32_t *match;          /* pinned, BPF match masks (monitor filters configured) */
 	uint64_t cap_bytes;
 	uint32_t n;
 	uint64_t bytes;
@@ -122,6 +123,7 @@ static void stage_free(mosrx_ctx *mc, struct stage *s)
 	if (s->off) mosrx_host_free(mc, s->off);
 	if (s->len) mosrx_host_free(mc, s->len);
 	if (s->res) mosrx_host_free(mc, s->res);
+	if (s->match) mosrx_host_free(mc, s->match);
 	memset(s, 0, sizeof(*s));
 }
 
@@ -160,13 +162,18 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 			exit(EXIT_FAILURE);
 		}
 		is->cur = is->inflight = -1;
+		if (g_cfg.bpf_nprog && (rc = mosrx_bpf_set(is->mc, g_cfg.bpf_progs, g_cfg.bpf_nprog))) {
+			fprintf(stderr, "[mosrx] gpu_module: mosrx_bpf_set: %s\n", mosrx_strerror(rc));
+			exit(EXIT_FAILURE);
+		}
 		for (k = 0; k < MOSRX_NSLOT; k++) {
 			struct stage *s = &is->st[k];
 			s->cap_bytes = (uint64_t)g_cfg.batch * ((g_cfg.max_frame + 15u + 16u) & ~15u) + 64;
 			if (mosrx_host_alloc(is->mc, s->cap_bytes, (void **)&s->frames) ||
 			    mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * 4, (void **)&s->off) ||
 			    mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * 2, (void **)&s->len) ||
-			    mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * sizeof(mosrx_result), (void **)&s->res)) {
+			    mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * sizeof(mosrx_result), (void **)&s->res) ||
+			    (g_cfg.bpf_nprog && mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * 4, (void **)&s->match))) {
 				fprintf(stderr, "[mosrx] gpu_module: pinned staging allocation failed\n");
 				exit(EXIT_FAILURE);
 			}
@@ -204,6 +211,8 @@ static int stage_submit(struct if_state *is, int k)
 	b.len = s->len;
 	b.n = s->n;
 	b.max_len = g_cfg.max_frame;
+	if (g_cfg.bpf_nprog)
+		return mosrx_classify_bpf_host_submit(is->mc, k, &b, s->res, s->match);
 	return mosrx_classify_host_submit(is->mc, k, &b, s->res);
 }
 
@@ -313,6 +322,11 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
 		if (pv->ifs[nif].cur < 0)
 			return -1;
 		*(const mosrx_result **)argp = pv->ifs[nif].st[pv->ifs[nif].cur].res;
+		return 0;
+	case MOSRX_PKT_RX_MATCH:
+		if (pv->ifs[nif].cur < 0 || !g_cfg.bpf_nprog)
+			return -1;
+		*(const uint32_t **)argp = pv->ifs[nif].st[pv->ifs[nif].cur].match;
 		return 0;
 	case DRV_NAME:
 		*(const char **)argp = "mosrx_gpu";

@@ -364,38 +364,47 @@ int mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, 
 	return mosrx_classify_dev_fh(c, b, d_out, NULL, stream);
 }
 
+/* Classification + the installed BPF set over a device-resident batch: the
+ * fused kernel when the set has one and the shape is a stream or SMALL tile,
+ * else the two kernels back to back on the same stream. */
+static int cls_bpf_launch(mosrx_ctx *c, const mosrx_batch *db, mosrx_result *out, uint32_t *cnt, uint32_t *match,
+                          hipStream_t s)
+{
+	mosrx_kparams kp;
+	int rc;
+	const int kind = tile_for(c, db);
+	if (!mosrx_bpf_fused(c) || (kind != MOSRX_KIND_SMALL && kind != MOSRX_KIND_S13)) {
+		if ((rc = launch(c, db, db->frames, db->off, db->len, out, cnt, NULL, s)))
+			return rc;
+		return mosrx_bpf_dev(c, db, match, (void *)s);
+	}
+	kp.frames = db->frames;
+	kp.off = db->off;
+	kp.len = db->len;
+	kp.out = out;
+	kp.tables = c->d_tables;
+	kp.counters = cnt;
+	kp.fhash = NULL;
+	kp.bmatch = match;
+	kp.frames_bytes = (uint32_t)db->frames_bytes;
+	kp.n = db->n;
+	kp.flags = c->kflags;
+	kp.grid_cap = 0;
+	return mosrx__bpf_fused_launch(c, &kp, kind == MOSRX_KIND_SMALL, s);
+}
+
 int mosrx_classify_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_match,
                            void *stream)
 {
-	const hipStream_t s = stream ? (hipStream_t)stream : (c ? c->stream : NULL);
-	mosrx_kparams kp;
-	int rc, kind;
+	int rc;
 	if (!c || (rc = mosrx__check_batch(b, 1)))
 		return c ? rc : -EINVAL;
 	if (b->n == 0)
 		return 0;
 	if (!d_out || !d_match || ((uintptr_t)d_out & 15) || ((uintptr_t)d_match & 3))
 		return -EINVAL;
-	kind = tile_for(c, b);
-	if (!mosrx_bpf_fused(c) || (kind != MOSRX_KIND_SMALL && kind != MOSRX_KIND_S13)) {
-		if ((rc = mosrx_classify_dev(c, b, d_out, stream)))
-			return rc;
-		return mosrx_bpf_dev(c, b, d_match, stream);
-	}
-	kp.frames = b->frames;
-	kp.off = b->off;
-	kp.len = b->len;
-	kp.out = d_out;
-	kp.tables = c->d_tables;
-	kp.counters = NULL;
-	kp.fhash = NULL;
-	kp.bmatch = d_match;
-	kp.frames_bytes = (uint32_t)b->frames_bytes;
-	kp.n = b->n;
-	kp.flags = c->kflags;
-	kp.grid_cap = 0;
 	HIPCHK(hipSetDevice(c->device));
-	return mosrx__bpf_fused_launch(c, &kp, kind == MOSRX_KIND_SMALL, s);
+	return cls_bpf_launch(c, b, d_out, NULL, d_match, stream ? (hipStream_t)stream : c->stream);
 }
 
 int mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
@@ -435,8 +444,10 @@ int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uin
 }
 
 /* Enqueue one end-to-end batch on slot s: H2D frames+descriptors, kernel, D2H results. */
+/* h_fhash: flow hashes; h_match: the installed BPF set's match masks (one of
+ * the two at most; both use the slot's per-frame u32 buffer). */
 static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosrx_result *h_out,
-                        uint32_t *h_fhash)
+                        uint32_t *h_fhash, uint32_t *h_match)
 {
 	int rc;
 	if ((rc = mosrx__slot_reserve(c, s, b->frames_bytes, b->n)))
@@ -445,13 +456,22 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 	HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
 	HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
 	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_R_COUNT * 4, s->stream));
-	if ((rc = launch(c, b, s->d_frames, s->d_off, s->d_len, s->d_res, s->d_cnt, h_fhash ? s->d_fh : NULL,
-	                 s->stream)))
+	if (h_match) {
+		mosrx_batch db = *b;
+		db.frames = s->d_frames;
+		db.off = s->d_off;
+		db.len = s->d_len;
+		rc = cls_bpf_launch(c, &db, s->d_res, s->d_cnt, s->d_fh, s->stream);
+	} else {
+		rc = launch(c, b, s->d_frames, s->d_off, s->d_len, s->d_res, s->d_cnt, h_fhash ? s->d_fh : NULL, s->stream);
+	}
+	if (rc)
 		return rc;
 	HIPCHK(hipMemcpyAsync(h_out, s->d_res, (size_t)b->n * sizeof(mosrx_result), hipMemcpyDeviceToHost,
 	                      s->stream));
-	if (h_fhash)
-		HIPCHK(hipMemcpyAsync(h_fhash, s->d_fh, (size_t)b->n * 4, hipMemcpyDeviceToHost, s->stream));
+	if (h_fhash || h_match)
+		HIPCHK(hipMemcpyAsync(h_fhash ? h_fhash : h_match, s->d_fh, (size_t)b->n * 4, hipMemcpyDeviceToHost,
+		                      s->stream));
 	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_R_COUNT * 4, hipMemcpyDeviceToHost, s->stream));
 	HIPCHK(hipEventRecord(s->done, s->stream));
 	s->busy = 1;
@@ -482,7 +502,7 @@ int mosrx_classify_host_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_o
 	if (!h_out)
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
-	if ((rc = host_enqueue(c, &c->slot[0], b, h_out, h_fhash)))
+	if ((rc = host_enqueue(c, &c->slot[0], b, h_out, h_fhash, NULL)))
 		return rc;
 	return mosrx_classify_host_wait(c, 0);
 }
@@ -504,7 +524,36 @@ int mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mos
 	if (!h_out)
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
-	return host_enqueue(c, &c->slot[slot], b, h_out, NULL);
+	return host_enqueue(c, &c->slot[slot], b, h_out, NULL, NULL);
+}
+
+int mosrx_classify_bpf_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out,
+                                   uint32_t *h_match)
+{
+	int rc;
+	if (!c || slot < 0 || slot >= NSLOT)
+		return -EINVAL;
+	if ((rc = mosrx__check_batch(b, 0)))
+		return rc;
+	if (c->slot[slot].busy)
+		return -EBUSY;
+	if (b->n == 0) {
+		memset(c->slot[slot].h_cnt, 0, sizeof(c->slot[slot].h_cnt));
+		c->slot[slot].busy = 2;   /* nothing enqueued */
+		return 0;
+	}
+	if (!h_out || !h_match)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	return host_enqueue(c, &c->slot[slot], b, h_out, NULL, h_match);
+}
+
+int mosrx_classify_bpf_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_match)
+{
+	int rc;
+	if ((rc = mosrx_classify_bpf_host_submit(c, 0, b, h_out, h_match)))
+		return rc;
+	return mosrx_classify_host_wait(c, 0);
 }
 
 int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
@@ -634,7 +683,7 @@ int mosrx_time_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_resul
 			return -EBUSY;
 	for (i = 0; i < iters; i++) {
 		struct slot *s = &c->slot[i % NSLOT];
-		if ((rc = host_enqueue(c, s, &b[i % nb], h_out[i % nb], NULL)))
+		if ((rc = host_enqueue(c, s, &b[i % nb], h_out[i % nb], NULL, NULL)))
 			return rc;
 	}
 	for (k = 0; k < NSLOT; k++) {

@@ -78,7 +78,7 @@ class ModuleCfg(C.Structure):
     _fields_ = [("num_ifs", C.c_uint32), ("if_names", (C.c_char * 16) * 16),
                 ("src", C.c_void_p * 16), ("batch", C.c_uint32), ("max_frame", C.c_uint32),
                 ("gpu_base", C.c_int32), ("ngpu", C.c_int32), ("pipeline", C.c_int32),
-                ("params", Params)]
+                ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32)]
 
 
 class MosrxError(OSError):
@@ -152,6 +152,8 @@ def lib():
                                                 C.POINTER(C.c_size_t)]),
             "mosrx_classify_bpf_dev": (I, [P, C.POINTER(Batch), P, P, P]),
             "mosrx_bpf_fused": (I, [P]),
+            "mosrx_classify_bpf_host": (I, [P, C.POINTER(Batch), P, P]),
+            "mosrx_classify_bpf_host_submit": (I, [P, I, C.POINTER(Batch), P, P]),
             "mosrx_trace_gen": (I, [I, U32, U32, U64, C.POINTER(TraceC)]),
             "mosrx_trace_free": (None, [C.POINTER(TraceC)]),
             "mosrx_source_mem": (P, [P, P, P, U32, U32]),
@@ -437,6 +439,19 @@ class Context:
         if sync:
             _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
 
+    def classify_bpf_host(self, frames, off, ln, frames_bytes=None):
+        """(records, match masks) of a host batch in one GPU pass."""
+        frames = np.ascontiguousarray(frames, np.uint8)
+        off = np.ascontiguousarray(off, np.uint32)
+        ln = np.ascontiguousarray(ln, np.uint16)
+        out = np.zeros(len(off), RESULT_DTYPE)
+        match = np.zeros(len(off), np.uint32)
+        b = Batch(frames.ctypes.data, int(frames_bytes if frames_bytes is not None else len(frames)),
+                  off.ctypes.data, ln.ctypes.data, len(off), 0)
+        _chk(lib().mosrx_classify_bpf_host(self.handle, C.byref(b), out.ctypes.data, match.ctypes.data),
+             "mosrx_classify_bpf_host")
+        return out, match
+
     def bpf_jit_log(self) -> str:
         return (lib().mosrx_bpf_jit_log(self.handle) or b"").decode(errors="replace")
 
@@ -599,7 +614,7 @@ _CTXFN = C.CFUNCTYPE(None, C.c_void_p)
 _IOCTLFN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int, C.c_int, C.c_void_p)
 _RECVFN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int)
 _RPTRFN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint16))
-PKT_RX_RSS, DRV_NAME, PKT_RX_RESULTS = 0x03, 0x08, 0x10
+PKT_RX_RSS, DRV_NAME, PKT_RX_RESULTS, PKT_RX_MATCH = 0x03, 0x08, 0x10, 0x11
 
 
 class IoModuleFunc(C.Structure):
@@ -623,7 +638,7 @@ class GpuBackend:
 
     def __init__(self, sources: list[int], params: Params | None = None, batch: int = 32768,
                  max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
-                 ngpu: int = 1):
+                 ngpu: int = 1, bpf=None):
         cfg = ModuleCfg()
         lib().mosrx_gpu_module_cfg_default(C.byref(cfg))
         cfg.num_ifs = len(sources)
@@ -634,6 +649,11 @@ class GpuBackend:
         cfg.gpu_base, cfg.ngpu = gpu_base, ngpu
         if params is not None:
             cfg.params = params
+        self._bpf = None
+        if bpf:
+            self._bpf = _bpf_progs(bpf)          # kept alive until init_handle has installed them
+            cfg.bpf_progs = C.addressof(self._bpf[0])
+            cfg.bpf_nprog = len(bpf)
         _chk(lib().mosrx_gpu_module_configure(C.byref(cfg)), "mosrx_gpu_module_configure")
         self.nif = len(sources)
         self.sources = list(sources)
@@ -660,6 +680,13 @@ class GpuBackend:
         if self._ioctl(self.ctx, ifidx, PKT_RX_RESULTS, C.byref(p)):
             raise MosrxError(5, "dev_ioctl(MOSRX_PKT_RX_RESULTS)")
         return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), (n * 16,)).view(RESULT_DTYPE).copy()
+
+    def matches(self, ifidx: int, n: int) -> np.ndarray:
+        """dev_ioctl(MOSRX_PKT_RX_MATCH): the batch's BPF match masks."""
+        p = C.c_void_p()
+        if self._ioctl(self.ctx, ifidx, PKT_RX_MATCH, C.byref(p)):
+            raise MosrxError(5, "dev_ioctl(MOSRX_PKT_RX_MATCH)")
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint32)), (n,)).copy()
 
     def rss_of(self, ifidx: int, pktidx: int) -> int | None:
         ri = RssInfo(pktidx, 0)

@@ -374,3 +374,30 @@ def test_classify_bpf_fused_layouts(gpu_ctx, phase, align):
         bpf_set(gpu_ctx, mosrx.BPF_ENGINE_JIT, ps)
         fused_check(gpu_ctx, buf, off, ln, ps)
         fused_check(gpu_ctx, buf, off[::-1].copy(), ln[::-1].copy(), ps)
+
+
+@pytest.mark.gpu
+def test_classify_bpf_host_and_backend(gpu_ctx):
+    """Host path (H2D, one pass, D2H) and the io_module backend with monitor
+    filters: records and match masks per batch, through dev_ioctl."""
+    z, progs = load()
+    ps = program_sets(z, progs)[0][0]
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 20_000, nflows=800)
+    ora = O.classify(t.frames, t.off, t.len, O.params())
+    om = O.bpf_eval(ps, t.frames[:t.frames_bytes], t.off, t.len)
+    gpu_ctx.set_params(mosrx.default_params())
+    bpf_set(gpu_ctx, mosrx.BPF_ENGINE_JIT, ps)
+    rec, m = gpu_ctx.classify_bpf_host(t.frames, t.off, t.len, frames_bytes=t.frames_bytes)
+    np.testing.assert_array_equal(m, om)
+    assert np.array_equal(rec.view(np.uint8), ora.view(np.uint8))
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=1)
+    be = mosrx.GpuBackend([src], batch=3000, pipeline=True, cpu=4, bpf=ps)
+    try:
+        seen = 0
+        while (n := be.recv_pkts(0)) > 0:
+            assert np.array_equal(be.results(0, n).view(np.uint8), ora[seen:seen + n].view(np.uint8))
+            np.testing.assert_array_equal(be.matches(0, n), om[seen:seen + n])
+            seen += n
+        assert seen == t.n
+    finally:
+        be.close()

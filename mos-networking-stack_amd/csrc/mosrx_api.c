@@ -874,6 +874,7 @@ struct mosrx_queue {
 	mosrx_qdesc *d_desc;
 	uint32_t nb;
 	uint32_t total_tiles;
+	uint32_t tpb;   /* tiles per batch if uniform, else 0 */
 	int tile;
 };
 
@@ -931,6 +932,10 @@ int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_re
 	free(h);
 	qq->nb = nb;
 	qq->total_tiles = tiles;
+	qq->tpb = tiles % nb == 0 ? tiles / nb : 0u;
+	for (i = 0; i < nb && qq->tpb; i++)
+		if ((b[i].n + (uint32_t)tile - 1) / (uint32_t)tile != qq->tpb)
+			qq->tpb = 0;
 	qq->tile = kind;
 	*q = qq;
 	return 0;
@@ -946,6 +951,7 @@ int mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream)
 	qp.counters = NULL;
 	qp.nb = q->nb;
 	qp.flags = c->kflags;
+	qp.tpb = q->tpb;
 	return mosrx_launch_queue(&qp, q->total_tiles, q->tile, c->variant, stream ? stream : (void *)c->stream);
 }
 

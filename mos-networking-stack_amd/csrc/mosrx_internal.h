@@ -85,6 +85,7 @@ typedef struct mosrx_qparams {
 	uint32_t          *counters;
 	uint32_t           nb;
 	uint32_t           flags;
+	uint32_t           tpb;      /* tiles per batch when every batch has the same tile count, else 0 */
 } mosrx_qparams;
 
 /* Batched BPF launch: the program table rides in the kernel arguments, the

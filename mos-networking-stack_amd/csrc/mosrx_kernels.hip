@@ -83,11 +83,14 @@ __device__ __forceinline__ uint32_t add16x2(uint32_t acc, uint32_t d)
 {
 	return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, d), (u16x2){1, 1}, acc, false);
 }
-// mask keeping bytes [0, nb) of a little-endian dword, nb clamped to [0, 4]
-__device__ __forceinline__ uint32_t keep_lo(int nb)
+// mask keeping the low 32 - sh bits, sh clamped to [0, 32]: v_med3 + one 64-bit
+// shift (sh == 32 gives 0), no compares, no lane-mask hazards
+__device__ __forceinline__ uint32_t keep_bits(int sh)
 {
-	return nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : ((1u << (8 * nb)) - 1u));
+	return (uint32_t)(0xFFFFFFFFull >> min(max(sh, 0), 32));
 }
+// mask keeping bytes [0, nb) of a little-endian dword, nb clamped to [0, 4]
+__device__ __forceinline__ uint32_t keep_lo(int nb) { return keep_bits(32 - 8 * nb); }
 __device__ __forceinline__ uint32_t fold16(uint32_t s)
 {
 	s = (s & 0xFFFFu) + (s >> 16);
@@ -177,14 +180,15 @@ __device__ __forceinline__ uint32_t ip_chain(const uint32_t *w, uint32_t ihl, ui
 	uint32_t s = w[3];
 	if (ihl <= 4u)
 		return s & 0xFFFFu;
-	uint64_t tt = (uint64_t)s + w[4];
-	s = (uint32_t)tt; uint32_t c = (uint32_t)(tt >> 32);
-	tt = (uint64_t)s + w5 + c; s = (uint32_t)tt; c = (uint32_t)(tt >> 32);
-	tt = (uint64_t)s + w[6] + c; s = (uint32_t)tt; c = (uint32_t)(tt >> 32);
+	unsigned int c;   // v_add_co / v_addc_co chain, carry in VCC
+	s = __builtin_addc(s, w[4], 0u, &c);
+	s = __builtin_addc(s, w5, c, &c);
+	s = __builtin_addc(s, w[6], c, &c);
 #pragma unroll
 	for (int k = 4; k < 15; k++) {
-		tt = (uint64_t)s + w[3 + k] + c;
-		if ((uint32_t)k < ihl) { s = (uint32_t)tt; c = (uint32_t)(tt >> 32); }
+		unsigned int c2;
+		const uint32_t t = __builtin_addc(s, w[3 + k], c, &c2);
+		if ((uint32_t)k < ihl) { s = t; c = c2; }
 	}
 	s += c;
 	const uint32_t a = (s >> 16) + (s & 0xFFFFu);
@@ -218,14 +222,23 @@ __device__ __forceinline__ void hdr_ihl(const uint32_t (&w)[WIN_DW], uint32_t ih
 	// TX: iph->check = 0 first (mos_api.c:1180-1181): the check is frame bytes 24,25 = w[5] bytes 2,3
 	ipc_tx = IS_TX(VAR) ? ip_chain(w, ihl, w[5] & 0xFFFFu) : 0u;
 	wsum = 0;
+	const int u = 8 * wend;
 #pragma unroll
 	for (int j = 8; j < WIN_DW; j++) {
-		uint32_t m = keep_lo(wend - (4 * j + 2));
+		uint32_t m = keep_bits(32 * j + 48 - u);       // keep_lo(wend - (4j + 2))
 		if ((uint32_t)j < 3u + ihl)
 			m = 0;
 		wsum = add16x2(wsum, w[j] & m);
 	}
 }
+
+// verdict + 1 of every reason code, 2 bits per code (eth_in.c:27-87, ip_in.c:30-101, tcp.c:408-445)
+#define VT(r, v) ((uint32_t)((v) + 1) << (2 * (r)))
+#define VERDICT_TAB                                                                                                    \
+	(VT(MOSRX_R_TCP_OK, 1) | VT(MOSRX_R_ARP, 1) | VT(MOSRX_R_NON_IPV4, -1) | VT(MOSRX_R_IP_SHORT, -1) |                \
+	 VT(MOSRX_R_IP_BADVER, 0) | VT(MOSRX_R_NOVERIFY_PASS, 1) | VT(MOSRX_R_IP_BADCSUM, -1) | VT(MOSRX_R_NOT_TCP, 0) |   \
+	 VT(MOSRX_R_TCP_SHORT, -1) | VT(MOSRX_R_TCP_BADCSUM, -1) | VT(MOSRX_R_TRUNCATED, -1) | VT(MOSRX_R_TCP_LEN_OK, 1))
+static_assert(MOSRX_R_COUNT <= 16, "verdict table holds 16 codes");
 
 // Parse + checks + IP checksum + RSS + in-window TCP sum.  Mirrors
 // ProcessPacket (eth_in.c:27) -> ProcessInIPv4Packet (ip_in.c:30) ->
@@ -268,46 +281,46 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	uint32_t rss = 0;
 	{
 		const uint32_t tup[3] = {saddr, daddr, is_tcp ? th0 : 0u};
+		const char *tb = reinterpret_cast<const char *>(s_tab);
 #pragma unroll
-		for (int k = 0; k < 12; k++) {
-			const uint32_t b = (tup[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-			rss ^= s_tab[(2 * k) * 16 + (b >> 4)] ^ s_tab[(2 * k + 1) * 16 + (b & 0xFu)];
+		for (int d = 0; d < 3; d++) {
+			// every byte's nibbles as LDS byte offsets (nibble * 4) in two ops
+			uint32_t H = (tup[d] >> 2) & 0x3C3C3C3Cu, L = (tup[d] << 2) & 0x3C3C3C3Cu;
+			asm("" : "+v"(H), "+v"(L));   // keep the packed form (else it is re-split into shift + and per nibble)
+#pragma unroll
+			for (int b = 0; b < 4; b++) {
+				const int k = 4 * d + b;
+				rss ^= *reinterpret_cast<const uint32_t *>(tb + (2 * k) * 64 + ((H >> (8 * b)) & 0xFFu)) ^
+				       *reinterpret_cast<const uint32_t *>(tb + (2 * k + 1) * 64 + ((L >> (8 * b)) & 0xFFu));
+			}
 		}
 	}
 	const uint32_t queue = (s_tab[MOSRX_TAB_RSS_WORDS + ((rss & 0x1FFu) >> 2)] >> (8 * (rss & 3u))) & 0xFFu;
 
-	// verdict chain (eth_in.c:27 -> ip_in.c:30 -> tcp.c:408)
+	// verdict chain (eth_in.c:27 -> ip_in.c:30 -> tcp.c:408), evaluated without
+	// branches: the reason is a select chain applied from the last check back to
+	// the first (so the first failing check wins, as in the reference's early
+	// returns), the verdict a 2-bit field of a per-launch table indexed by it.
 	const bool verify = kflags & MOSRX_KF_VERIFY;
-	int verdict = -1;
-	uint32_t reason = MOSRX_R_TRUNCATED;
-	bool fields = false, need_tcp = false;
-	if (cap < 14u) {
-		verdict = -1; reason = MOSRX_R_TRUNCATED;
-	} else if (h_proto != 0x0800u) {
-		reason = (h_proto == 0x0806u) ? MOSRX_R_ARP : MOSRX_R_NON_IPV4;
-		verdict = ((kflags & MOSRX_KF_FWD_NONIP) || h_proto == 0x0806u) ? 1 : -1;
-	} else if (cap < 34u || 14u + ihl * 4u > cap || fend > cap || (is_tcp && 14u + ihl * 4u + 20u > cap)) {
-		verdict = -1; reason = MOSRX_R_TRUNCATED;
-	} else if (ip_len < 20u) {
-		verdict = -1; reason = MOSRX_R_IP_SHORT;
-	} else if (ver != 4u) {
-		verdict = 0; reason = MOSRX_R_IP_BADVER;
-	} else {
-		fields = true;
-		if (!verify) {
-			verdict = 1; reason = MOSRX_R_NOVERIFY_PASS;
-		} else if (ipc != 0u) {
-			verdict = -1; reason = MOSRX_R_IP_BADCSUM;
-		} else if (!is_tcp) {
-			verdict = 0; reason = MOSRX_R_NOT_TCP;
-		} else if (ip_len < (ihl + doff) * 4u) {
-			verdict = -1; reason = MOSRX_R_TCP_SHORT;
-		} else if (kflags & MOSRX_KF_SKIP_TCP) {
-			verdict = 1; reason = MOSRX_R_TCP_LEN_OK;
-		} else {
-			need_tcp = true;   // verdict decided after the tail sum
-		}
-	}
+	const uint32_t l_ip = 14u + ihl * 4u;
+	const bool c_nonip = h_proto != 0x0800u;
+	const bool c_trunc = cap < 34u || l_ip > cap || fend > cap || (is_tcp && l_ip + 20u > cap);
+	const bool c_tshort = ip_len < (ihl + doff) * 4u;
+	const bool fields = cap >= 14u && !c_nonip && !c_trunc && ip_len >= 20u && ver == 4u;
+	uint32_t reason = (kflags & MOSRX_KF_SKIP_TCP) ? MOSRX_R_TCP_LEN_OK : MOSRX_R_TRUNCATED;   // TRUNCATED: pending TCP sum
+	reason = c_tshort ? MOSRX_R_TCP_SHORT : reason;                     // tcp.c:429-430
+	reason = !is_tcp ? MOSRX_R_NOT_TCP : reason;                        // ip_in.c:82-93
+	reason = ipc != 0u ? MOSRX_R_IP_BADCSUM : reason;                   // ip_in.c:74-77
+	reason = !verify ? MOSRX_R_NOVERIFY_PASS : reason;                  // ip_in.c:67-72
+	reason = ver != 4u ? MOSRX_R_IP_BADVER : reason;                    // ip_in.c:47-51
+	reason = ip_len < 20u ? MOSRX_R_IP_SHORT : reason;                  // ip_in.c:42-45
+	reason = c_trunc ? MOSRX_R_TRUNCATED : reason;
+	reason = c_nonip ? (h_proto == 0x0806u ? MOSRX_R_ARP : MOSRX_R_NON_IPV4) : reason;   // eth_in.c:62-77
+	reason = cap < 14u ? MOSRX_R_TRUNCATED : reason;
+	bool need_tcp = fields && verify && ipc == 0u && is_tcp && !c_tshort && !(kflags & MOSRX_KF_SKIP_TCP);
+	// verdict + 1 per reason, 2 bits each (NON_IPV4 -> 1 when forwarding non-IP frames)
+	const uint32_t vtab = VERDICT_TAB | ((kflags & MOSRX_KF_FWD_NONIP) ? (2u << (2 * MOSRX_R_NON_IPV4)) : 0u);
+	const int verdict = (int)((vtab >> (2u * reason)) & 3u) - 1;
 	// TX (mtcp_setlastpkt's MOS_UPDATE_*_CHKSUM, mos_api.c:1177-1193): every
 	// untruncated IPv4 frame with a full header gets the IP check; TCP frames
 	// whose length covers the header also get the TCP check.
@@ -1035,13 +1048,17 @@ void mosrx_classify_kernel(mosrx_kparams kp)
 }
 
 // Batch queue: one launch over nb resident batches (descriptor table in HBM).
-// Workgroup b finds its batch by a binary search of tile_base[] (scalar loads).
+// Workgroup b finds its batch by one scalar division when every batch has the
+// same tile count (the usual rx ring of equal batches), else by a binary
+// search of tile_base[] (a chain of dependent scalar loads).
 template <int KIND, int VAR>
 __global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))
 void mosrx_classify_queue_kernel(mosrx_qparams qp)
 {
 	const uint32_t b = blockIdx.x;
 	uint32_t lo = 0, hi = qp.nb;               // find k: tile_base[k] <= b < tile_base[k+1]
+	if (qp.tpb)
+		lo = hi = min(b / qp.tpb, qp.nb - 1u);
 	while (hi - lo > 1) {
 		const uint32_t mid = (lo + hi) >> 1;
 		if (__builtin_amdgcn_readfirstlane(qp.desc[mid].tile_base) <= b)

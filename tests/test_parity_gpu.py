@@ -224,6 +224,23 @@ def test_gpu_io_module_batches_and_ioctl():
         be.close()
 
 
+@pytest.mark.parametrize("kind,sizes", [(mosrx.TRACE_S64, [5_000, 300, 70_001, 256, 1]),
+                                        (mosrx.TRACE_IMIX, [3_000, 64, 9_100, 65])])
+def test_batch_queue_unequal_batches(gpu_ctx, kind, sizes):
+    """Batches of different tile counts: workgroups find their batch by the
+    binary search of tile_base[] (equal batches take the division path)."""
+    gpu_ctx.set_params(mosrx.default_params())
+    trs = [mosrx.Trace(kind, n, nflows=2000, seed=300 + i) for i, n in enumerate(sizes)]
+    dbs = [gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len) for t in trs]
+    q = gpu_ctx.queue(dbs)
+    q.run()
+    for t, d in zip(trs, dbs):
+        assert_records_equal(d.results(), O.classify(t.frames, t.off, t.len, O.params()), "queue (unequal)")
+    q.destroy()
+    for d in dbs:
+        d.free()
+
+
 @pytest.mark.parametrize("kind,n,nb", [(mosrx.TRACE_S64, 32_768, 8), (mosrx.TRACE_IMIX, 9_000, 5),
                                        (mosrx.TRACE_M1500, 9_000, 4)])
 def test_batch_queue_one_launch(gpu_ctx, kind, n, nb):

@@ -829,10 +829,14 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v)
 }
 
 // Streamer sidx of S over its run of the span [A, Z); the frame lanes' sums go
-// to row[lane].  DBG 4 (probe builds): loads only.
+// to row[lane].  A tail is summed in whole 16-byte chunks, from its split to the
+// end of the chunk holding its last captured byte: the header wave subtracts
+// the few bytes past the capture end (chunk_overshoot), so a block costs one
+// scan and two ds_bpermute reads whatever its frames.  DBG 4 (probe builds):
+// loads only.
 template <int S, int AUX, int DBG = 0, int U = STREAM_U>
 __device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t lo_l, uint32_t hi_l, uint32_t A,
-                                            uint32_t Z, uint32_t sidx, uint32_t lane, uint32_t *row, u32x4 *s_raw)
+                                            uint32_t Z, uint32_t sidx, uint32_t lane, uint32_t *row)
 {
 	const uint32_t nblk = (Z - A + 1023u) >> 10;
 	const uint32_t b0 = uni((nblk * sidx) / S), b1 = uni((nblk * (sidx + 1u)) / S);
@@ -860,20 +864,16 @@ __device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t 
 				s = add16x2(s, v[i].y);
 				s = add16x2(s, v[i].z);
 				s = add16x2(s, v[i].w);
-				const uint32_t x = wave_scan(s);
-				const uint32_t E = carry + x - s;
-				carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+				const uint32_t X = carry + wave_scan(s);   // inclusive prefix of the run
+				carry = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
 				const uint32_t rl = lo_l - c0, re = ec_l - c0;
 				const bool es = cand && rl < 1024u, ee = cand && re < 1024u;
-				const uint64_t me = __ballot(ee);
-				if (__ballot(es) | me) {
-					if (me)
-						s_raw[lane] = v[i];
-					const uint32_t Es = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rl >> 2) & 0xFCu), (int)E);
-					const uint32_t Ee = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((re >> 2) & 0xFCu), (int)E);
+				if (__ballot(es || ee)) {
+					// tail = X(end chunk) - E(start chunk), E = X - s the exclusive prefix
+					const uint32_t Es = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rl >> 2) & 0xFCu), (int)(X - s));
+					const uint32_t Xe = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((re >> 2) & 0xFCu), (int)X);
 					acc = es ? acc - Es : acc;
-					if (ee)
-						acc += Ee + chunk_sum(s_raw[(re >> 4) & 63u], ec_l, hi_l, 0u);
+					acc = ee ? acc + Xe : acc;
 				}
 			}
 			const uint32_t bn = b + U;
@@ -888,6 +888,21 @@ __device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t 
 	if (cand && lo_l < R1 && ec_l >= R1)
 		acc += carry;                        // tail continuing past the run
 	row[lane] = acc;
+}
+
+// Absolute-grid word sum of the bytes of the 16-byte chunk at c (the chunk
+// holding byte hi - 1) at or past hi: what stream_scan summed beyond a capture.
+__device__ __forceinline__ uint32_t chunk_overshoot(u32x4 v, uint32_t c, uint32_t hi)
+{
+	const int h = (int)(hi - c);   // bytes of the capture in the chunk, 1..16
+	v.x &= ~keep_lo(h);
+	v.y &= ~keep_lo(h - 4);
+	v.z &= ~keep_lo(h - 8);
+	v.w &= ~keep_lo(h - 12);
+	uint32_t acc = add16x2(0u, v.x);
+	acc = add16x2(acc, v.y);
+	acc = add16x2(acc, v.z);
+	return add16x2(acc, v.w);
 }
 
 // Tiles not in buffer order: streamer sidx sums the candidates of rank
@@ -933,7 +948,6 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
 	__shared__ uint32_t s_part[S][64];   // streamer s's tail sums
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
-	__shared__ __attribute__((aligned(16))) u32x4 s_raw[S][64];   // stream_scan's block copies
 
 	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
@@ -951,6 +965,9 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 	// speculative tail bounds from the capture length: [split, off + caplen)
 	const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
 	const uint32_t hi_l = active ? o + cap : 0u;
+	// buffer order: the next frame starts at or after this capture's end
+	const uint32_t onext = (uint32_t)__shfl_down((int)o, 1);
+	const bool sorted = __ballot(lane + 1u < nact && onext < hi_l) == 0;
 
 	if (wave == 0) {
 		// ---- header wave (fills s_tab itself: a wave's LDS accesses are ordered) ----
@@ -964,6 +981,9 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		} else {
 			hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
 		}
+		// the chunk holding the capture's last byte (stream_scan sums it whole)
+		const bool cand = hi_l > lo_l;
+		const u32x4 ov = load16<WIN_AUX(VAR)>(rs, sorted && cand ? (hi_l - 1u) & ~15u : ZERO_OFF, 0);
 		{
 			const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
 			const u32x4 a = tg[lane], b = tg[lane + 64];
@@ -988,6 +1008,8 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 #pragma unroll
 				for (int s = 0; s < S; s++)
 					tail += s_part[s][lane];
+				if (sorted)
+					tail -= chunk_overshoot(ov, (hi_l - 1u) & ~15u, hi_l);
 			}
 			hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, tail, p, active, lane, s_cnt);
 #ifdef MOSRX_RTC_BPF
@@ -1004,9 +1026,6 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		const uint32_t sidx = wave - 1u;
 		uint32_t *row = s_part[sidx];
 		row[lane] = 0;
-		// buffer order: the next frame starts at or after this capture's end
-		const uint32_t onext = (uint32_t)__shfl_down((int)o, 1);
-		const bool sorted = __ballot(lane + 1u < nact && onext < hi_l) == 0;
 		const uint64_t cmask = __ballot(hi_l > lo_l);
 		if (sorted && cmask) {
 			// the span runs from the first candidate's split to the last
@@ -1015,7 +1034,7 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 			// frame without a tail can never stretch the span)
 			const uint32_t A = uni(__builtin_amdgcn_readlane(lo_l, (int)__builtin_ctzll(cmask)));
 			const uint32_t Z = uni(__builtin_amdgcn_readlane(hi_l, 63 - (int)__builtin_clzll(cmask)));
-			stream_scan<S, AUX, DBG, U>(rs, lo_l, hi_l, A, Z, sidx, lane, row, s_raw[sidx]);
+			stream_scan<S, AUX, DBG, U>(rs, lo_l, hi_l, A, Z, sidx, lane, row);
 		} else if (!sorted) {
 			if constexpr (!(DBG & 16))
 				stream_frames<S, AUX>(rs, lo_l, hi_l, sidx, lane, row);

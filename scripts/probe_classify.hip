@@ -129,5 +129,19 @@ int main(int argc, char **argv)
 	}
 	run("product LARGE", launch_product, kps, nb, bytes);
 	run("product S13", launch_stream, kps, nb, bytes);
+	// S13 as the library builds it (8 waves/SIMD, 4 blocks in flight) with pieces removed
+	run("S13 full", launch_sdbg<3, 0, 8, 4>, kps, nb, bytes);
+	run("S13 streamers: loads only", launch_sdbg<3, 4, 8, 4>, kps, nb, bytes);
+	run("S13 header: no parse", launch_sdbg<3, 1, 8, 4>, kps, nb, bytes);
+	run("S13 header: no window loads", launch_sdbg<3, 2, 8, 4>, kps, nb, bytes);
+	run("S13 no parse + streamer loads only", launch_sdbg<3, 5, 8, 4>, kps, nb, bytes);
+	// blocks in flight per streamer (U) vs waves per SIMD (W, sets the VGPR budget)
+	run("S13 W4 U6", launch_sdbg<3, 0, 4, 6>, kps, nb, bytes);
+	run("S13 W4 U8", launch_sdbg<3, 0, 4, 8>, kps, nb, bytes);
+	run("S13 W4 U12", launch_sdbg<3, 0, 4, 12>, kps, nb, bytes);
+	run("S13 W5 U6", launch_sdbg<3, 0, 5, 6>, kps, nb, bytes);
+	run("S13 W6 U6", launch_sdbg<3, 0, 6, 6>, kps, nb, bytes);
+	run("S13 W4 U8 loads only", launch_sdbg<3, 4, 4, 8>, kps, nb, bytes);
+	run("S16 W4 U8", launch_sdbg<6, 0, 4, 8>, kps, nb, bytes);
 	return 0;
 }

@@ -135,13 +135,10 @@ int main(int argc, char **argv)
 	run("S13 header: no parse", launch_sdbg<3, 1, 8, 4>, kps, nb, bytes);
 	run("S13 header: no window loads", launch_sdbg<3, 2, 8, 4>, kps, nb, bytes);
 	run("S13 no parse + streamer loads only", launch_sdbg<3, 5, 8, 4>, kps, nb, bytes);
-	// blocks in flight per streamer (U) vs waves per SIMD (W, sets the VGPR budget)
-	run("S13 W4 U6", launch_sdbg<3, 0, 4, 6>, kps, nb, bytes);
-	run("S13 W4 U8", launch_sdbg<3, 0, 4, 8>, kps, nb, bytes);
-	run("S13 W4 U12", launch_sdbg<3, 0, 4, 12>, kps, nb, bytes);
-	run("S13 W5 U6", launch_sdbg<3, 0, 5, 6>, kps, nb, bytes);
-	run("S13 W6 U6", launch_sdbg<3, 0, 6, 6>, kps, nb, bytes);
-	run("S13 W4 U8 loads only", launch_sdbg<3, 4, 4, 8>, kps, nb, bytes);
-	run("S16 W4 U8", launch_sdbg<6, 0, 4, 8>, kps, nb, bytes);
+	// streamer waves per 64-frame tile (S11 .. S14), library occupancy and depth
+	run("S11 W8 U4", launch_sdbg<1, 0, 8, 4>, kps, nb, bytes);
+	run("S12 W8 U4", launch_sdbg<2, 0, 8, 4>, kps, nb, bytes);
+	run("S14 W8 U4", launch_sdbg<4, 0, 8, 4>, kps, nb, bytes);
+	run("S12 W8 U6", launch_sdbg<2, 0, 8, 6>, kps, nb, bytes);
 	return 0;
 }

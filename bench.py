@@ -142,6 +142,11 @@ def prewarm(fn, seconds: float = PREWARM_S):
         fn()
 
 
+def median_of(fn, reps: int = 5) -> float:
+    """Median of `reps` repetitions of a per-launch timing."""
+    return float(np.median([fn() for _ in range(reps)]))
+
+
 def measure(ctx, dist, key, steps, warmup, rank):
     kind, batch, label = WORKLOADS[key]
     params = mosrx.default_params(skip_tcp_csum=1 if key == "S64_hdr" else 0)
@@ -171,7 +176,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         kk = 500
-        kern_ms = ctx.time_op(op, dbs, kk, 1, arg, kernels=False)[0] / kk
+        kern_ms = median_of(lambda: ctx.time_op(op, dbs, kk, 1, arg, kernels=False)[0] / kk)
         _, kern_iso = ctx.time_op(op, dbs, kk, 1, arg, total=False)
     elif key.endswith("_queue"):
         # each step = one launch over `depth` distinct resident batches
@@ -192,8 +197,8 @@ def measure(ctx, dist, key, steps, warmup, rank):
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         kk = min(steps, 64)
-        tot_ms, kern_iso = qs[0].time(kk, qs[1:])
-        kern_ms = tot_ms / kk
+        kern_ms = median_of(lambda: qs[0].time(kk, qs[1:], kernels=False)[0] / kk)
+        _, kern_iso = qs[0].time(kk, qs[1:])
         for q in qs:
             q.destroy()
     else:
@@ -212,11 +217,11 @@ def measure(ctx, dist, key, steps, warmup, rank):
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         # roofline: average launch duration on ONE stream, HIP events around
-        # K back-to-back launches on the launch stream (the figure rocprofv3's
-        # kernel trace reports); the isolated figure (events around each single
-        # launch, dispatch included) is kept beside it
+        # 500 back-to-back launches on the launch stream (the figure rocprofv3's
+        # kernel trace reports), median of 5 such runs; the isolated figure
+        # (events around each single launch, dispatch included) is kept beside it
         kk = 500
-        kern_ms = ctx.time_dev_streams(dbs, kk, 1) / kk
+        kern_ms = median_of(lambda: ctx.time_dev_streams(dbs, kk, 1) / kk)
         kern_iso = ctx.time_dev_kernels(dbs, kk)
     for d in dbs:
         d.free()

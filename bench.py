@@ -378,6 +378,30 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
             "method": "pinned hipHostMalloc staging, H2D frames+descriptors, kernel, D2H records; 2 streams"}
 
 
+def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int):
+    """The drop-in boundary's own rate: mosrx_rx_loop (RunMainLoop's rx section,
+    core.c:897-909) over gpu_module_func (io_module.h:63-78) fed by an in-memory
+    source replaying the trace — per batch: source -> pinned staging, H2D,
+    classify, D2H records, then the per-frame get_rptr + NETSTAT walk on the
+    host, with batch k+1 in flight while k is consumed.  Recorded in DESIGN.md;
+    never the bench value."""
+    ctx_batch = {"S64": 32_768, "M1500": 65_536, "IMIX": 262_144}[key]
+    loops = max(1, frames_target // tr.n)
+    src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
+    be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu)
+    try:
+        be.run_loop(max_pkts=2 * ctx_batch)            # warm-up: staging sized, module loaded
+        t0 = time.perf_counter()
+        st = be.run_loop()
+        dt = time.perf_counter() - t0
+    finally:
+        be.close()
+    n = int(st.rx_packets)
+    nb = n / tr.n
+    return {"mpkts": n / dt / 1e6, "gbps": nb * algo_bytes(tr) / dt / 1e9, "frames": n, "seconds": round(dt, 3),
+            "method": "mosrx_rx_loop over gpu_module_func (pipelined), in-memory source replaying the trace"}
+
+
 def main():
     global STREAMS
     ap = argparse.ArgumentParser()
@@ -399,7 +423,8 @@ def main():
     dist = Dist(ws, rank)
     # MOSRX_BENCH_DEVICE pins every rank to one device: a rehearsal of the
     # multi-rank path on a one-GPU box (scripts/gpu_r1_dist.sh), never a result
-    ctx = mosrx.Context(int(os.environ.get("MOSRX_BENCH_DEVICE", local)))
+    device = int(os.environ.get("MOSRX_BENCH_DEVICE", local))
+    ctx = mosrx.Context(device)
     keys = [k for k in args.workloads.split(",") if k]
     results, traces = {}, {}
     for k in keys:
@@ -412,6 +437,9 @@ def main():
     e2e = None
     if not args.no_e2e and "M1500" in traces:
         e2e = {k: measure_e2e(ctx, traces[k], 20) for k in ("M1500", "S64") if k in traces}
+        # the gpu_module_func backend itself (host thread = this rank)
+        e2e["backend"] = {k: measure_backend(traces[k], k, 4_000_000 if k == "S64" else 1_500_000, device)
+                          for k in ("M1500", "S64", "IMIX") if k in traces}
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
         head = "M1500" if "M1500" in traces else keys[0]

@@ -438,7 +438,7 @@ def main():
     if not args.no_e2e and "M1500" in traces:
         e2e = {k: measure_e2e(ctx, traces[k], 20) for k in ("M1500", "S64") if k in traces}
         # the gpu_module_func backend itself (host thread = this rank)
-        e2e["backend"] = {k: measure_backend(traces[k], k, 4_000_000 if k == "S64" else 1_500_000, device)
+        e2e["backend"] = {k: measure_backend(traces[k], k, {"S64": 16_000_000, "M1500": 2_000_000}.get(k, 4_000_000), device)
                           for k in ("M1500", "S64", "IMIX") if k in traces}
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:

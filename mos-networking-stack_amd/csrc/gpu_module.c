@@ -29,10 +29,14 @@
 #define MAX_THREADS 64
 #define TX_FRAME_LEN 2048    /* ETHERNET_FRAME_LEN (mtcp.h:64-68) */
 
+/* One pinned block per stage, descriptors first: off[batch] | len[batch] | frames.
+ * A full batch is then one contiguous span and crosses PCIe in one copy
+ * (mosrx_api.c batch_span). */
 struct stage {
-	uint8_t *frames;          /* pinned */
-	uint32_t *off;            /* pinned */
-	uint16_t *len;            /* pinned */
+	uint8_t *blk;             /* pinned block holding off, len and frames */
+	uint8_t *frames;
+	uint32_t *off;
+	uint16_t *len;
 	mosrx_result *res;        /* pinned */
 	uint32_t *match;          /* pinned, BPF match masks (monitor filters configured) */
 	uint64_t cap_bytes;
@@ -119,9 +123,7 @@ static void gpu_load_module_upper_half(void)
 
 static void stage_free(mosrx_ctx *mc, struct stage *s)
 {
-	if (s->frames) mosrx_host_free(mc, s->frames);
-	if (s->off) mosrx_host_free(mc, s->off);
-	if (s->len) mosrx_host_free(mc, s->len);
+	if (s->blk) mosrx_host_free(mc, s->blk);
 	if (s->res) mosrx_host_free(mc, s->res);
 	if (s->match) mosrx_host_free(mc, s->match);
 	memset(s, 0, sizeof(*s));
@@ -168,15 +170,17 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 		}
 		for (k = 0; k < MOSRX_NSLOT; k++) {
 			struct stage *s = &is->st[k];
+			const uint64_t dsc = ((uint64_t)g_cfg.batch * 6 + 15) & ~15ull;
 			s->cap_bytes = (uint64_t)g_cfg.batch * ((g_cfg.max_frame + 15u + 16u) & ~15u) + 64;
-			if (mosrx_host_alloc(is->mc, s->cap_bytes, (void **)&s->frames) ||
-			    mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * 4, (void **)&s->off) ||
-			    mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * 2, (void **)&s->len) ||
+			if (mosrx_host_alloc(is->mc, dsc + s->cap_bytes, (void **)&s->blk) ||
 			    mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * sizeof(mosrx_result), (void **)&s->res) ||
 			    (g_cfg.bpf_nprog && mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * 4, (void **)&s->match))) {
 				fprintf(stderr, "[mosrx] gpu_module: pinned staging allocation failed\n");
 				exit(EXIT_FAILURE);
 			}
+			s->off = (uint32_t *)s->blk;
+			s->len = (uint16_t *)(s->blk + (size_t)g_cfg.batch * 4);
+			s->frames = s->blk + dsc;
 		}
 	}
 	g_tab[slot].priv = pv;

@@ -28,7 +28,7 @@ struct slot {
 	uint32_t cap_n;
 	hipStream_t stream;
 	hipEvent_t done;
-	uint32_t h_cnt[MOSRX_R_COUNT];
+	uint32_t *h_cnt;   /* MOSRX_R_COUNT, pinned: a D2H copy into pageable memory blocks the host */
 	int busy;
 };
 

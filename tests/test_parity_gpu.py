@@ -359,3 +359,39 @@ def test_bogus_offsets_after_sorted_frames(gpu_ctx):
             run_both(gpu_ctx, buf, off, ln, mosrx.default_params())
         finally:
             gpu_ctx.set_variant(2)
+
+
+@pytest.mark.parametrize("layout", ["frames_off_len", "off_len_frames", "gaps", "too_sparse", "overlap"])
+def test_host_one_block_layouts(gpu_ctx, layout):
+    """classify_host with frames and descriptors in one block (the gpu_module
+    staging layout): one H2D copy of the span (mosrx_api.c batch_span), device
+    pointers at the same relative offsets.  Sparse blocks, and descriptors lying
+    inside frames_bytes, take the three-copy path; every layout gives the
+    oracle's records and counters."""
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 5000, nflows=500)
+    n, fb = t.n, int(t.frames_bytes)
+    fa = (fb + 15) & ~15
+    off, ln = np.asarray(t.off, np.uint32), np.asarray(t.len, np.uint16)
+    gap = {"gaps": 4000, "too_sparse": 10 * fb}.get(layout, 0)
+    if layout == "off_len_frames":
+        d = (n * 6 + 15) & ~15
+        blk = np.zeros(d + fb, np.uint8)
+        o_at, l_at, f_at = 0, n * 4, d
+    else:
+        blk = np.zeros(fa + gap + n * 6 + 16, np.uint8)
+        o_at, l_at, f_at = fa + gap, fa + gap + n * 4 + (16 if gap else 0), 0
+    blk[f_at:f_at + fb] = np.asarray(t.frames[:fb], np.uint8)
+    ov = blk[o_at:o_at + n * 4].view(np.uint32)
+    lv = blk[l_at:l_at + n * 2].view(np.uint16)
+    ov[:] = off
+    lv[:] = ln
+    if layout == "overlap":           # frames_bytes covers the descriptors too
+        fb = len(blk) - f_at
+    frames = blk[f_at:f_at + fb]
+    p = mosrx.default_params()
+    gpu_ctx.set_params(p)
+    ora = O.classify(frames.copy(), off, ln, oparams(p))
+    got = gpu_ctx.classify_host(frames, ov, lv, frames_bytes=fb, max_len=int(ln.max()))
+    assert_records_equal(got, ora, layout)
+    cnt = np.asarray(gpu_ctx.last_counters())
+    assert cnt.sum() == n and np.array_equal(cnt, np.bincount(ora["reason"], minlength=len(cnt)))

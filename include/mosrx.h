@@ -166,7 +166,10 @@ int  mosrx_time_queue(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq, uint32_t
                       float *total_ms, float *avg_kernel_ms);
 
 /* End-to-end: host frames -> pinned staging -> H2D -> kernel -> D2H -> h_out.
- * Blocks until h_out is filled. */
+ * Blocks until h_out is filled.  When frames, off and len lie in ONE host
+ * block (any order, not overlapping frames_bytes, frames 16-byte aligned
+ * within it, gaps under an eighth of the payload + 4 KiB) the batch crosses
+ * PCIe in a single copy of that span; otherwise in three (one per array). */
 int  mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out);
 /* Same, plus the flow hashes into h_fhash[n] (see mosrx_classify_dev_fh). */
 int  mosrx_classify_host_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_fhash);

@@ -369,7 +369,7 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
         bufs += [pb, pr]
         outs.append(pr)
         batches.append(mosrx.Batch(pb, fb, pb + fa, pb + fa + tr.n * 4, tr.n, tr.max_len))
-    ctx.time_host(batches, outs, 2)
+    ctx.time_host(batches, outs, 8)             # warm: both slots, pinned pages mapped
     ms = ctx.time_host(batches, outs, iters)
     for p in bufs:
         ctx.host_free(p)
@@ -437,7 +437,7 @@ def main():
                   file=sys.stderr, flush=True)
     e2e = None
     if not args.no_e2e and "M1500" in traces:
-        e2e = {k: measure_e2e(ctx, traces[k], 20) for k in ("M1500", "S64") if k in traces}
+        e2e = {k: measure_e2e(ctx, traces[k], {"M1500": 60, "S64": 800}[k]) for k in ("M1500", "S64") if k in traces}
         # the gpu_module_func backend itself (host thread = this rank)
         e2e["backend"] = {k: measure_backend(traces[k], k, {"S64": 16_000_000, "M1500": 2_000_000}.get(k, 4_000_000), device)
                           for k in ("M1500", "S64", "IMIX") if k in traces}

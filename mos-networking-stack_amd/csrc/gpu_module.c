@@ -34,7 +34,8 @@
  * (mosrx_api.c batch_span). */
 struct stage {
 	uint8_t *blk;             /* pinned block holding off, len and frames */
-	uint8_t *frames;
+	uint8_t *own;             /* the block's frame area */
+	uint8_t *frames;          /* this batch's frames: own, or a run borrowed from the source */
 	uint32_t *off;
 	uint16_t *len;
 	mosrx_result *res;        /* pinned */
@@ -180,7 +181,7 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 			}
 			s->off = (uint32_t *)s->blk;
 			s->len = (uint16_t *)(s->blk + (size_t)g_cfg.batch * 4);
-			s->frames = s->blk + dsc;
+			s->own = s->frames = s->blk + dsc;
 		}
 	}
 	g_tab[slot].priv = pv;
@@ -192,6 +193,23 @@ static void stage_fill(struct stage *s, mosrx_source *src)
 	uint64_t pos = 2;
 	uint32_t i = 0;
 	const uint32_t mf = g_cfg.max_frame;
+	s->frames = s->own;
+	if (src && src->borrow) {     /* zero-copy: the source's pinned run is the batch */
+		const uint8_t *f = NULL;
+		uint64_t fb = 0;
+		s->n = src->borrow(src, g_cfg.batch, mf, &f, &fb, s->off, s->len);
+		if (s->n) {
+			s->frames = (uint8_t *)f;
+			s->bytes = fb;
+		} else {
+			s->bytes = 2;
+		}
+		return;
+	}
+	if (src && src->fill) {
+		s->n = src->fill(src, s->frames, s->cap_bytes, s->off, s->len, g_cfg.batch, mf, &s->bytes);
+		return;
+	}
 	while (i < g_cfg.batch && src && pos + mf + 16 <= s->cap_bytes) {
 		int l = src->next(src, s->frames + pos, mf);
 		if (l <= 0)

@@ -24,15 +24,22 @@
 #include <unistd.h>
 
 #include "../../include/mosrx_io_module.h"
+#define __HIP_PLATFORM_AMD__ 1   /* host-only C over the HIP runtime API */
+#include <hip/hip_runtime_api.h>
+
 #include "mosrx_source.h"
 
 /* ---------------- in-memory replay ---------------- */
+/* The replay buffer is kept in the staging layout (frame i at a 16-byte
+ * boundary + 2, packed), so a batch is one memcpy per contiguous run with the
+ * offsets rebased (mem_fill), as a NIC ring hands a DMA'd run of slots. */
 struct src_mem {
 	struct mosrx_source base;
 	uint8_t *frames;
 	uint32_t *off;
 	uint16_t *len;
-	uint32_t n, i, loops, done_loops;
+	uint32_t n, i, loops, done_loops, max_len;
+	int pinned;   /* frames in hipHostMalloc'd memory: batches are borrowed, not copied */
 };
 
 static int mem_next(struct mosrx_source *s_, uint8_t *dst, uint32_t cap)
@@ -55,10 +62,88 @@ static int mem_next(struct mosrx_source *s_, uint8_t *dst, uint32_t cap)
 	return (int)l;
 }
 
+static uint32_t mem_fill(struct mosrx_source *s_, uint8_t *dst, uint64_t cap, uint32_t *off, uint16_t *len,
+                         uint32_t max_n, uint32_t max_frame, uint64_t *end)
+{
+	struct src_mem *s = (struct src_mem *)s_;
+	uint64_t pos = 2;
+	uint32_t k = 0;
+	if (s->max_len > max_frame) {   /* frames to truncate: the per-frame path */
+		int l;
+		while (k < max_n && pos + max_frame + 16 <= cap && (l = mem_next(s_, dst + pos, max_frame)) > 0) {
+			off[k] = (uint32_t)pos;
+			len[k] = (uint16_t)l;
+			k++;
+			pos = ((pos + (uint64_t)l - 2 + 15) & ~15ull) + 2;
+		}
+		*end = pos;
+		return k;
+	}
+	while (k < max_n && s->n) {
+		uint32_t a, b, j;
+		uint64_t base, room;
+		if (s->i == s->n) {
+			s->done_loops++;
+			if (s->loops && s->done_loops >= s->loops)
+				break;
+			s->i = 0;
+		}
+		/* the run [a, b) of source frames that fits the count and the space left */
+		a = s->i;
+		base = s->off[a];
+		room = cap - pos;
+		b = a;
+		while (b < s->n && k + (b - a) < max_n && (uint64_t)(s->off[b] - base) + max_frame + 16 <= room)
+			b++;
+		if (b == a)
+			break;
+		memcpy(dst + pos, s->frames + base, (size_t)(s->off[b - 1] - base) + s->len[b - 1]);
+		for (j = a; j < b; j++, k++) {
+			off[k] = (uint32_t)(pos + (s->off[j] - base));
+			len[k] = s->len[j];
+		}
+		pos = ((pos + (s->off[b - 1] - base) + s->len[b - 1] - 2 + 15) & ~15ull) + 2;
+		s->i = b;
+	}
+	*end = pos;
+	return k;
+}
+
+/* Zero-copy: the next run of the pinned replay buffer is the batch itself (as
+ * a NIC's DMA ring slots are); only the rebased descriptors are written. */
+static uint32_t mem_borrow(struct mosrx_source *s_, uint32_t max_n, uint32_t max_frame, const uint8_t **frames,
+                           uint64_t *frames_bytes, uint32_t *off, uint16_t *len)
+{
+	struct src_mem *s = (struct src_mem *)s_;
+	uint32_t a, b, k, base;
+	if (!s->n || !max_n)
+		return 0;
+	if (s->i == s->n) {
+		s->done_loops++;
+		if (s->loops && s->done_loops >= s->loops)
+			return 0;
+		s->i = 0;
+	}
+	a = s->i;
+	b = s->n - a > max_n ? a + max_n : s->n;
+	base = s->off[a] - 2;
+	for (k = 0; a + k < b; k++) {
+		off[k] = s->off[a + k] - base;
+		len[k] = s->len[a + k] < max_frame ? s->len[a + k] : (uint16_t)max_frame;
+	}
+	*frames = s->frames + base;
+	*frames_bytes = (uint64_t)off[k - 1] + len[k - 1];
+	s->i = b;
+	return k;
+}
+
 static void mem_close(struct mosrx_source *s_)
 {
 	struct src_mem *s = (struct src_mem *)s_;
-	free(s->frames);
+	if (s->pinned)
+		hipHostFree(s->frames);
+	else
+		free(s->frames);
 	free(s->off);
 	free(s->len);
 	free(s);
@@ -73,23 +158,34 @@ mosrx_source *mosrx_source_mem(const uint8_t *frames, const uint32_t *off, const
 	if (!s)
 		return NULL;
 	for (i = 0; i < n; i++)
-		total += len[i];
-	s->frames = malloc(total ? total : 1);
+		total += ((uint64_t)len[i] + 15) & ~15ull;
+	total += 16;
+	/* pinned when a HIP device is present (zero-copy batches), else plain */
+	if (hipHostMalloc((void **)&s->frames, total, hipHostMallocPortable) == hipSuccess)
+		s->pinned = 1;
+	else
+		s->frames = malloc(total);
 	s->off = malloc((size_t)(n ? n : 1) * 4);
 	s->len = malloc((size_t)(n ? n : 1) * 2);
 	if (!s->frames || !s->off || !s->len || total >= (1ull << 32)) {
 		mem_close(&s->base);
 		return NULL;
 	}
+	pos = 2;
 	for (i = 0; i < n; i++) {
 		memcpy(s->frames + pos, frames + off[i], len[i]);
 		s->off[i] = (uint32_t)pos;
 		s->len[i] = len[i];
-		pos += len[i];
+		if (len[i] > s->max_len)
+			s->max_len = len[i];
+		pos = ((pos + len[i] - 2 + 15) & ~15ull) + 2;
 	}
 	s->n = n;
 	s->loops = loops;
 	s->base.next = mem_next;
+	s->base.fill = mem_fill;
+	if (s->pinned)
+		s->base.borrow = mem_borrow;
 	s->base.close = mem_close;
 	return &s->base;
 }

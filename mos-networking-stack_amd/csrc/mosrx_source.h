@@ -8,6 +8,20 @@ struct mosrx_source {
 	/* write the next frame into dst (at most cap bytes); returns its caplen, 0 when none */
 	int  (*next)(struct mosrx_source *s, uint8_t *dst, uint32_t cap);
 	void (*close)(struct mosrx_source *s);
+	/* optional batch form (NULL: the backend calls next per frame): receive up
+	 * to max_n frames of at most max_frame bytes into frames[] in the staging
+	 * layout (first frame at byte 2, each next one at the following 16-byte
+	 * boundary + 2, never past cap), writing off[]/len[]; returns the count
+	 * and the staging bytes used in *end */
+	uint32_t (*fill)(struct mosrx_source *s, uint8_t *frames, uint64_t cap, uint32_t *off, uint16_t *len,
+	                 uint32_t max_n, uint32_t max_frame, uint64_t *end);
+	/* optional zero-copy form (NULL: none): hand out up to max_n frames that
+	 * already sit in pinned memory the source owns, as one run starting at
+	 * *frames (first frame at byte 2), writing off[]/len[] (len clamped to
+	 * max_frame) and the run's length in *frames_bytes; the bytes stay valid
+	 * and unmodified until the source is closed */
+	uint32_t (*borrow)(struct mosrx_source *s, uint32_t max_n, uint32_t max_frame, const uint8_t **frames,
+	                   uint64_t *frames_bytes, uint32_t *off, uint16_t *len);
 };
 
 #endif

@@ -199,6 +199,36 @@ def test_gpu_io_module_rx_loop(pipeline):
     assert st.batches == (t.n + 4095) // 4096
 
 
+@pytest.mark.parametrize("max_frame", [2048, 600])
+def test_gpu_io_module_replay_runs(max_frame):
+    """The in-memory source's batch fill (loopback.c mem_fill): runs of the
+    replay buffer copied whole into the staging block and rebased, wrapping
+    inside a batch across replay loops; with max_frame below the longest frame
+    the per-frame truncating path runs instead.  Records match the oracle over
+    the replayed (truncated) stream."""
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 7000, nflows=300)
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=3)
+    be = mosrx.GpuBackend([src], batch=4096, max_frame=max_frame, pipeline=True, cpu=4)
+    ln = np.minimum(t.len, max_frame).astype(np.uint16)
+    ora = O.classify(t.frames, t.off, ln, O.params())
+    try:
+        seen = 0
+        while True:
+            n = be.recv_pkts(0)
+            assert n >= 0
+            if n == 0:
+                break
+            idx = (seen + np.arange(n)) % t.n
+            assert_records_equal(be.results(0, n), ora[idx], f"batch@{seen}")
+            for i in (0, n // 2, n - 1):
+                j = int(idx[i])
+                assert be.get_rptr(0, i) == bytes(t.frames[t.off[j]:t.off[j] + ln[j]])
+            seen += n
+        assert seen == 3 * t.n
+    finally:
+        be.close()
+
+
 def test_gpu_io_module_batches_and_ioctl():
     t = mosrx.Trace(mosrx.TRACE_IMIX, 10_000, nflows=500)
     src = mosrx.mem_source(t.frames, t.off, t.len, loops=1)

@@ -10,6 +10,9 @@
  * through dev_ioctl(PKT_RX_RSS) (dpdk_module.c:568-571).  With `pipeline` set,
  * batch k+1 is received and classified while the application consumes batch
  * k, keeping the reference's pointer lifetime (valid until the next recv_pkts).
+ * A source that holds its frames in pinned memory lends a run of them as the
+ * batch (mosrx_source.h `borrow`, no host copy); one that can copy a run at
+ * once fills the stage in runs (`fill`); any other is read frame by frame.
  *
  * Threading follows mOS: one context per mTCP thread, every call for a context
  * from that thread (core.c:1282-1349), so the module takes no locks on the fast

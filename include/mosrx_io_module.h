@@ -85,6 +85,11 @@ mosrx_source *mosrx_source_pcap(const char *path, uint32_t loops);
 mosrx_source *mosrx_source_afpacket(const char *ifname);
 /* Pull the next frame into dst (at most cap bytes); returns its caplen, 0 when none. */
 int           mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap);
+/* How gpu_module_func takes batches from an in-memory source: 0 = best (the
+ * replay buffer lent zero-copy when it is pinned, else copied in runs), 1 =
+ * copied in runs, 2 = copied frame by frame (what a recvfrom-style source
+ * does).  Results never depend on it.  0 or -EINVAL (not a memory source). */
+int           mosrx_source_mem_set_mode(mosrx_source *s, int mode);
 void          mosrx_source_close(mosrx_source *s);
 
 /* ---- backend configuration (before load_module_upper_half) ---- */

@@ -9,7 +9,8 @@
  *             pcap_module.c:140-156, without libpcap)
  *
  * Each source writes one frame straight into the caller's staging slot, so a
- * backend can receive directly into pinned memory.
+ * backend can receive directly into pinned memory; the memory source also
+ * copies whole runs (fill) or lends its pinned replay buffer (borrow).
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -188,6 +189,16 @@ mosrx_source *mosrx_source_mem(const uint8_t *frames, const uint32_t *off, const
 		s->base.borrow = mem_borrow;
 	s->base.close = mem_close;
 	return &s->base;
+}
+
+int mosrx_source_mem_set_mode(mosrx_source *s_, int mode)
+{
+	struct src_mem *s = (struct src_mem *)s_;
+	if (!s_ || s_->next != mem_next || mode < 0 || mode > 2)
+		return -EINVAL;
+	s->base.borrow = mode == 0 && s->pinned ? mem_borrow : NULL;
+	s->base.fill = mode <= 1 ? mem_fill : NULL;
+	return 0;
 }
 
 /* ---------------- classic pcap file ---------------- */

@@ -161,6 +161,7 @@ def lib():
             "mosrx_source_afpacket": (P, [C.c_char_p]),
             "mosrx_source_close": (None, [P]),
             "mosrx_source_next": (I, [P, P, U32]),
+            "mosrx_source_mem_set_mode": (I, [P, I]),
             "mosrx_gpu_module_cfg_default": (None, [C.POINTER(ModuleCfg)]),
             "mosrx_gpu_module_configure": (I, [C.POINTER(ModuleCfg)]),
             "mosrx_gpu_module_bind": (I, [P, I]),
@@ -707,13 +708,18 @@ class GpuBackend:
             self.sources = []
 
 
-def mem_source(frames: np.ndarray, off: np.ndarray, ln: np.ndarray, loops: int = 1) -> int:
+SRC_BEST, SRC_FILL, SRC_PER_FRAME = 0, 1, 2
+
+
+def mem_source(frames: np.ndarray, off: np.ndarray, ln: np.ndarray, loops: int = 1, mode: int = SRC_BEST) -> int:
     frames = np.ascontiguousarray(frames, np.uint8)
     off = np.ascontiguousarray(off, np.uint32)
     ln = np.ascontiguousarray(ln, np.uint16)
     s = lib().mosrx_source_mem(frames.ctypes.data, off.ctypes.data, ln.ctypes.data, len(off), loops)
     if not s:
         raise MosrxError(12, "mosrx_source_mem")
+    if mode != SRC_BEST:
+        _chk(lib().mosrx_source_mem_set_mode(s, mode), "mosrx_source_mem_set_mode")
     return s
 
 

@@ -199,15 +199,17 @@ def test_gpu_io_module_rx_loop(pipeline):
     assert st.batches == (t.n + 4095) // 4096
 
 
+@pytest.mark.parametrize("mode", [mosrx.SRC_BEST, mosrx.SRC_FILL, mosrx.SRC_PER_FRAME])
 @pytest.mark.parametrize("max_frame", [2048, 600])
-def test_gpu_io_module_replay_runs(max_frame):
+def test_gpu_io_module_replay_runs(max_frame, mode):
     """The in-memory source's batch fill (loopback.c mem_fill): runs of the
     replay buffer copied whole into the staging block and rebased, wrapping
     inside a batch across replay loops; with max_frame below the longest frame
     the per-frame truncating path runs instead.  Records match the oracle over
-    the replayed (truncated) stream."""
+    the replayed (truncated) stream.  Every way a batch reaches the stage: the
+    pinned replay buffer lent zero-copy, copied in runs, copied per frame."""
     t = mosrx.Trace(mosrx.TRACE_IMIX, 7000, nflows=300)
-    src = mosrx.mem_source(t.frames, t.off, t.len, loops=3)
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=3, mode=mode)
     be = mosrx.GpuBackend([src], batch=4096, max_frame=max_frame, pipeline=True, cpu=4)
     ln = np.minimum(t.len, max_frame).astype(np.uint16)
     ora = O.classify(t.frames, t.off, ln, O.params())

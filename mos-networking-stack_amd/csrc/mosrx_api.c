@@ -293,7 +293,6 @@ static int launch_flags(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frame
 	kp.frames_bytes = (uint32_t)b->frames_bytes;
 	kp.n = b->n;
 	kp.flags = kflags;
-	kp.grid_cap = 0;
 	return mosrx_launch_classify(&kp, tile_for(c, b), c->variant, (void *)s);
 }
 
@@ -391,7 +390,6 @@ static int cls_bpf_launch(mosrx_ctx *c, const mosrx_batch *db, mosrx_result *out
 	kp.frames_bytes = (uint32_t)db->frames_bytes;
 	kp.n = db->n;
 	kp.flags = c->kflags;
-	kp.grid_cap = 0;
 	return mosrx__bpf_fused_launch(c, &kp, kind == MOSRX_KIND_SMALL, s);
 }
 

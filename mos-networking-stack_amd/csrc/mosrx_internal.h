@@ -39,7 +39,6 @@ typedef struct mosrx_kparams {
 	uint32_t        frames_bytes;
 	uint32_t        n;
 	uint32_t        flags;      /* MOSRX_KF_* */
-	uint32_t        grid_cap;   /* large tiles: max workgroups (persistent walk), 0 = one per tile */
 } mosrx_kparams;
 
 /* Kernel shapes ("kinds"):

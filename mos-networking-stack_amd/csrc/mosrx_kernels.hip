@@ -1098,7 +1098,6 @@ void mosrx_classify_queue_kernel(mosrx_qparams qp)
 	kp.frames_bytes = d->frames_bytes;
 	kp.n = d->n;
 	kp.flags = qp.flags;
-	kp.grid_cap = 0;
 	classify_tile<KIND, VAR>(kp, b - d->tile_base);
 }
 

@@ -389,7 +389,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int):
     ctx_batch = {"S64": 32_768, "M1500": 65_536, "IMIX": 262_144}[key]
     loops = max(1, frames_target // tr.n)
     src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
-    be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu)
+    be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu)
     try:
         be.run_loop(max_pkts=2 * ctx_batch)            # warm-up: staging sized, module loaded
         t0 = time.perf_counter()

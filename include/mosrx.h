@@ -49,7 +49,7 @@ typedef unsigned long size_t;
 extern "C" {
 #endif
 
-#define MOSRX_ABI_VERSION 1
+#define MOSRX_ABI_VERSION 2
 
 /* ---- per-frame result record (16 bytes) -------------------- */
 
@@ -67,7 +67,8 @@ enum {
 	MOSRX_R_TCP_BADCSUM   = 9,  /* TCPCalcChecksum != 0                  -> -1 (tcp.c:432-444)  */
 	MOSRX_R_TRUNCATED     = 10, /* build-only: a byte the reference reads lies past caplen -> -1 */
 	MOSRX_R_TCP_LEN_OK    = 11, /* skip_tcp_csum mode: length check passed -> 1                 */
-	MOSRX_R_COUNT         = 12
+	MOSRX_R_ICMP_LOCAL    = 12, /* ICMP to a local address: ProcessICMPPacket -> 1 (ip_in.c:83-85, icmp.c:193-227) */
+	MOSRX_R_COUNT         = 13
 };
 
 typedef struct mosrx_result {
@@ -83,11 +84,23 @@ typedef struct mosrx_result {
 	uint8_t  ihl_doff;    /* (ihl << 4) | doff; doff 0 if not TCP */
 } mosrx_result;
 
+/* pkt_info's TCP fields (mos_api.h:122-152) as FillPacketContextTCPInfo
+ * (tcp.c:258-270) fills them, for FindStream and the flow engine after it
+ * (tcp.c:448): host order.  12 bytes per frame, an optional side array of the
+ * classify calls (_ex); all zero where the record's payload_off is 0. */
+typedef struct mosrx_tcpinfo {
+	uint32_t seq;         /* ntohl(tcph->seq) */
+	uint32_t ack_seq;     /* ntohl(tcph->ack_seq) */
+	uint16_t window;      /* ntohs(tcph->window) */
+	uint16_t ip_len;      /* pkt_info.ip_len = ntohs(iph->tot_len) (ip_in.c:36, :53) */
+} mosrx_tcpinfo;
+
 /* ---- parameters: the reference stack state the verdict depends on --------- */
 
 enum { MOSRX_QMAP_I40E = 1, MOSRX_QMAP_IXGBE = 0 };  /* FetchEndianType() values, config.c:1261-1278 */
 
 #define MOSRX_RSS_KEY_MAX 52   /* the DPDK backend programs a 52-byte key (dpdk_module.c:652-662) */
+#define MOSRX_MAX_LOCAL   16   /* netdev entries, MAX_ETH_ENTRY = MAX_DEVICES (config.h:15, io_module.h:87) */
 
 typedef struct mosrx_params {
 	uint32_t num_msp;        /* # MOS_SOCK_MONITOR_STREAM sockets (mtcp.h:243); simple_firewall: 1 */
@@ -98,6 +111,11 @@ typedef struct mosrx_params {
 	int32_t  skip_tcp_csum;  /* 1: header parse + IP checksum + RSS only (BASELINE config #2) */
 	uint32_t rss_key_len;    /* >= 16; only key bytes 0..15 affect a 12-byte input (util.c:47-57) */
 	uint8_t  rss_key[MOSRX_RSS_KEY_MAX];
+	/* the netdevs' IPv4 addresses (netdev_table->ent[i]->ip_addr, network order as
+	 * stored, config.h:54-60): ProcessICMPPacket takes ICMP frames to one of them
+	 * (icmp.c:193-200) and ProcessPacket then returns 1 instead of 0 */
+	uint32_t num_local;      /* 0..MOSRX_MAX_LOCAL */
+	uint32_t local_ip[MOSRX_MAX_LOCAL];
 } mosrx_params;
 
 /* simple_firewall's state: num_msp=1, num_esp=0, forward=1, num_queues=1,
@@ -112,9 +130,13 @@ void mosrx_params_set_ms_key(mosrx_params *p);
  * frame at a 16-byte boundary + 2 (IP header 16-byte aligned); any offset is
  * accepted.  Offsets are relative to `frames`; frames_bytes bounds every read
  * (the kernel never touches memory outside [frames, frames+frames_bytes)). */
+/* Largest batch buffer: its 16-byte-rounded range stays below the offset the
+ * kernels use for "no load" (0xFFFFFFF0), so no rounding can wrap. */
+#define MOSRX_MAX_FRAMES_BYTES 0xFFFFFFE0ull
+
 typedef struct mosrx_batch {
 	const uint8_t  *frames;       /* device pointer (classify_dev) or host pointer (classify_host) */
-	uint64_t        frames_bytes; /* < 4 GiB */
+	uint64_t        frames_bytes; /* <= MOSRX_MAX_FRAMES_BYTES, else -E2BIG */
 	const uint32_t *off;          /* n frame offsets */
 	const uint16_t *len;          /* n capture lengths (pcap caplen / get_rptr *len, core.c:903-905) */
 	uint32_t        n;            /* frames in the batch */
@@ -147,6 +169,12 @@ int  mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out,
 int  mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,
                            void *stream);
 
+/* Same, with every optional per-frame side array: d_fhash[n] (NULL: none, as
+ * above) and d_tcpinfo[n] (NULL: none), the pkt_info TCP fields, computed in the
+ * same pass from the header bytes the kernel already holds. */
+int  mosrx_classify_dev_ex(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,
+                           mosrx_tcpinfo *d_tcpinfo, void *stream);
+
 /* Device-resident classification of `nb` batches in one launch sequence. */
 int  mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
                              mosrx_result *const *d_out, void *stream);
@@ -173,6 +201,9 @@ int  mosrx_time_queue(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq, uint32_t
 int  mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out);
 /* Same, plus the flow hashes into h_fhash[n] (see mosrx_classify_dev_fh). */
 int  mosrx_classify_host_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_fhash);
+/* Same, with the optional side arrays of mosrx_classify_dev_ex (either may be NULL). */
+int  mosrx_classify_host_ex(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_fhash,
+                            mosrx_tcpinfo *h_tcpinfo);
 
 /* Asynchronous end-to-end form for pipelining: two slots per context, each
  * with its own stream.  submit enqueues H2D -> kernel -> D2H and returns; wait

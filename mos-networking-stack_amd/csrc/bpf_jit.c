@@ -609,7 +609,7 @@ int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hi
 {
 	hipFunction_t f = small ? c->bpf_fm : c->bpf_fs;
 	const unsigned tile = small ? MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL) : MOSRX_KIND_FRAMES(MOSRX_KIND_S13);
-	const unsigned threads = small ? 256u : 64u * (MOSRX_KIND_H(MOSRX_KIND_S13) + MOSRX_KIND_S(MOSRX_KIND_S13));
+	const unsigned threads = small ? 256u : 64u * (1u + MOSRX_STREAMERS);
 	mosrx_kparams k = *kp;
 	void *args[] = {&k};
 	if (!f)

@@ -98,6 +98,8 @@ static int check_params(const mosrx_params *p)
 		return -EINVAL;
 	if (p->queue_mode != MOSRX_QMAP_I40E && p->queue_mode != MOSRX_QMAP_IXGBE)
 		return -EINVAL;
+	if (p->num_local > MOSRX_MAX_LOCAL)
+		return -EINVAL;
 	return 0;
 }
 
@@ -120,7 +122,7 @@ static void build_qlut(const mosrx_params *p, uint8_t lut[512])
 
 int mosrx_set_params(mosrx_ctx *c, const mosrx_params *p)
 {
-	uint32_t tab[MOSRX_TAB_WORDS];
+	uint32_t tab[MOSRX_TAB_ALLOC_WORDS];
 	int rc;
 
 	if (!c)
@@ -131,6 +133,8 @@ int mosrx_set_params(mosrx_ctx *c, const mosrx_params *p)
 	if ((rc = mosrx_rss_tables(p->rss_key, p->rss_key_len, tab)))
 		return rc;
 	build_qlut(p, (uint8_t *)(tab + MOSRX_TAB_RSS_WORDS));
+	tab[MOSRX_TAB_LOCAL] = p->num_local;
+	memcpy(tab + MOSRX_TAB_LOCAL + 1, p->local_ip, sizeof(p->local_ip));
 	HIPCHK(hipSetDevice(c->device));
 	HIPCHK(hipMemcpyAsync(c->d_tables, tab, sizeof(tab), hipMemcpyHostToDevice, c->stream));
 	HIPCHK(hipStreamSynchronize(c->stream));
@@ -174,7 +178,7 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 	if (hipSetDevice(device) != hipSuccess ||
 	    hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
 	    mosrx__ensure_streams(c, 3) != 0 ||
-	    hipMalloc((void **)&c->d_tables, MOSRX_TAB_WORDS * 4) != hipSuccess ||
+	    hipMalloc((void **)&c->d_tables, MOSRX_TAB_ALLOC_WORDS * 4) != hipSuccess ||
 	    hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
 		mosrx_close(c);
 		return -ENODEV;
@@ -203,7 +207,8 @@ static void slot_free(struct slot *s)
 	if (s->d_len) hipFree(s->d_len);
 	if (s->d_res) hipFree(s->d_res);
 	if (s->d_fh) hipFree(s->d_fh);
-	s->d_frames = NULL; s->d_off = NULL; s->d_len = NULL; s->d_res = NULL; s->d_fh = NULL;
+	if (s->d_ti) hipFree(s->d_ti);
+	s->d_frames = NULL; s->d_off = NULL; s->d_len = NULL; s->d_res = NULL; s->d_fh = NULL; s->d_ti = NULL;
 	s->cap_frames = 0; s->cap_n = 0;
 }
 
@@ -247,19 +252,19 @@ int mosrx__check_batch(const mosrx_batch *b, int dev)
 		return 0;
 	if (!b->frames || !b->off || !b->len || (dev && ((uintptr_t)b->frames & 15)))
 		return -EINVAL;
-	if (b->frames_bytes >= (1ull << 32))
+	if (b->frames_bytes > MOSRX_MAX_FRAMES_BYTES)
 		return -E2BIG;
 	return 0;
 }
 
 /* Kernel shape: SMALL when every frame fits the header window (max_len known
- * and <= 94); otherwise S13 (one header wave + three span streamers, 54 VGPRs,
+ * and <= 94); otherwise S13 (one header wave + three span streamers, 50 VGPRs,
  * 8 waves per SIMD).  Measured on MI355X (profiles/r01_probe_w8.log,
  * back-to-back launches): 1500 B config S13 18.75 us, S14 18.73, S12 18.73,
  * LARGE 20.84; IMIX S13 20.5 us, S14 21.6, S12 21.7, LARGE 41.8; IMIX with
  * descriptors in reverse buffer order (unsorted tiles) S13 43.5, LARGE 41.6.
- * Every other shape stays reachable for tuning: variant bits 2-6 force one
- * (value - 1, MOSRX_KIND_*). */
+ * The tuning shapes are built by scripts/probe_classify.hip only; variant
+ * bits 2-6 force one of the library's two (value - 1, MOSRX_KIND_*). */
 static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_t n)
 {
 	(void)bytes;
@@ -278,8 +283,8 @@ static int tile_for(const mosrx_ctx *c, const mosrx_batch *b)
 }
 
 static int launch_flags(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
-                        const uint16_t *len, mosrx_result *out, uint32_t *cnt, uint32_t *fhash, uint32_t kflags,
-                        hipStream_t s)
+                        const uint16_t *len, mosrx_result *out, uint32_t *cnt, uint32_t *fhash,
+                        mosrx_tcpinfo *tinfo, uint32_t kflags, hipStream_t s)
 {
 	mosrx_kparams kp;
 	kp.frames = frames;
@@ -290,6 +295,7 @@ static int launch_flags(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frame
 	kp.counters = cnt;
 	kp.fhash = fhash;
 	kp.bmatch = NULL;
+	kp.tinfo = tinfo;
 	kp.frames_bytes = (uint32_t)b->frames_bytes;
 	kp.n = b->n;
 	kp.flags = kflags;
@@ -297,9 +303,10 @@ static int launch_flags(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frame
 }
 
 static int launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
-                  const uint16_t *len, mosrx_result *out, uint32_t *cnt, uint32_t *fhash, hipStream_t s)
+                  const uint16_t *len, mosrx_result *out, uint32_t *cnt, uint32_t *fhash, mosrx_tcpinfo *tinfo,
+                  hipStream_t s)
 {
-	return launch_flags(c, b, frames, off, len, out, cnt, fhash, c->kflags, s);
+	return launch_flags(c, b, frames, off, len, out, cnt, fhash, tinfo, c->kflags, s);
 }
 
 static uint32_t tx_kflags(int flags)
@@ -316,7 +323,7 @@ int mosrx_tx_csum_dev(mosrx_ctx *c, const mosrx_batch *b, int flags, void *strea
 		return -EINVAL;
 	if (b->n == 0 || !flags)
 		return 0;
-	return launch_flags(c, b, b->frames, b->off, b->len, NULL, NULL, NULL, tx_kflags(flags),
+	return launch_flags(c, b, b->frames, b->off, b->len, NULL, NULL, NULL, NULL, tx_kflags(flags),
 	                    stream ? (hipStream_t)stream : c->stream);
 }
 
@@ -339,25 +346,32 @@ int mosrx_tx_csum_host(mosrx_ctx *c, const mosrx_batch *b, int flags)
 	HIPCHK(hipMemcpyAsync(s->d_frames, b->frames, b->frames_bytes, hipMemcpyHostToDevice, s->stream));
 	HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
 	HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
-	if ((rc = launch_flags(c, b, s->d_frames, s->d_off, s->d_len, NULL, NULL, NULL, tx_kflags(flags), s->stream)))
+	if ((rc = launch_flags(c, b, s->d_frames, s->d_off, s->d_len, NULL, NULL, NULL, NULL, tx_kflags(flags),
+	                       s->stream)))
 		return rc;
 	HIPCHK(hipMemcpyAsync((void *)b->frames, s->d_frames, b->frames_bytes, hipMemcpyDeviceToHost, s->stream));
 	HIPCHK(hipStreamSynchronize(s->stream));
 	return 0;
 }
 
-int mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,
-                          void *stream)
+int mosrx_classify_dev_ex(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,
+                          mosrx_tcpinfo *d_tcpinfo, void *stream)
 {
 	int rc;
 	if (!c || (rc = mosrx__check_batch(b, 1)))
 		return c ? rc : -EINVAL;
 	if (b->n == 0)
 		return 0;
-	if (!d_out || ((uintptr_t)d_out & 15) || ((uintptr_t)d_fhash & 3))
+	if (!d_out || ((uintptr_t)d_out & 15) || ((uintptr_t)d_fhash & 3) || ((uintptr_t)d_tcpinfo & 3))
 		return -EINVAL;
-	return launch(c, b, b->frames, b->off, b->len, d_out, NULL, d_fhash,
+	return launch(c, b, b->frames, b->off, b->len, d_out, NULL, d_fhash, d_tcpinfo,
 	              stream ? (hipStream_t)stream : c->stream);
+}
+
+int mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,
+                          void *stream)
+{
+	return mosrx_classify_dev_ex(c, b, d_out, d_fhash, NULL, stream);
 }
 
 int mosrx_classify_dev(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, void *stream)
@@ -375,7 +389,7 @@ static int cls_bpf_launch(mosrx_ctx *c, const mosrx_batch *db, mosrx_result *out
 	int rc;
 	const int kind = tile_for(c, db);
 	if (!mosrx_bpf_fused(c) || (kind != MOSRX_KIND_SMALL && kind != MOSRX_KIND_S13)) {
-		if ((rc = launch(c, db, db->frames, db->off, db->len, out, cnt, NULL, s)))
+		if ((rc = launch(c, db, db->frames, db->off, db->len, out, cnt, NULL, NULL, s)))
 			return rc;
 		return mosrx_bpf_dev(c, db, match, (void *)s);
 	}
@@ -387,6 +401,7 @@ static int cls_bpf_launch(mosrx_ctx *c, const mosrx_batch *db, mosrx_result *out
 	kp.counters = cnt;
 	kp.fhash = NULL;
 	kp.bmatch = match;
+	kp.tinfo = NULL;
 	kp.frames_bytes = (uint32_t)db->frames_bytes;
 	kp.n = db->n;
 	kp.flags = c->kflags;
@@ -470,7 +485,8 @@ int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uin
 		    hipMalloc((void **)&s->d_off, (size_t)nn * 4) != hipSuccess ||
 		    hipMalloc((void **)&s->d_len, (size_t)nn * 2) != hipSuccess ||
 		    hipMalloc((void **)&s->d_res, (size_t)nn * sizeof(mosrx_result)) != hipSuccess ||
-		    hipMalloc((void **)&s->d_fh, (size_t)nn * 4) != hipSuccess) {
+		    hipMalloc((void **)&s->d_fh, (size_t)nn * 4) != hipSuccess ||
+		    hipMalloc((void **)&s->d_ti, (size_t)nn * sizeof(mosrx_tcpinfo)) != hipSuccess) {
 			slot_free(s);
 			return -ENOMEM;
 		}
@@ -483,9 +499,10 @@ int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uin
 
 /* Enqueue one end-to-end batch on slot s: H2D frames+descriptors, kernel, D2H results. */
 /* h_fhash: flow hashes; h_match: the installed BPF set's match masks (one of
- * the two at most; both use the slot's per-frame u32 buffer). */
+ * the two at most; both use the slot's per-frame u32 buffer); h_ti: pkt_info
+ * TCP fields (not with h_match). */
 static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosrx_result *h_out,
-                        uint32_t *h_fhash, uint32_t *h_match)
+                        uint32_t *h_fhash, uint32_t *h_match, mosrx_tcpinfo *h_ti)
 {
 	int rc;
 	if ((rc = mosrx__slot_reserve(c, s, b->frames_bytes, b->n)))
@@ -513,7 +530,8 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 		db.len = dlen;
 		rc = cls_bpf_launch(c, &db, s->d_res, s->d_cnt, s->d_fh, s->stream);
 	} else {
-		rc = launch(c, b, dframes, doff, dlen, s->d_res, s->d_cnt, h_fhash ? s->d_fh : NULL, s->stream);
+		rc = launch(c, b, dframes, doff, dlen, s->d_res, s->d_cnt, h_fhash ? s->d_fh : NULL,
+		            h_ti ? s->d_ti : NULL, s->stream);
 	}
 	if (rc)
 		return rc;
@@ -521,6 +539,9 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 	                      s->stream));
 	if (h_fhash || h_match)
 		HIPCHK(hipMemcpyAsync(h_fhash ? h_fhash : h_match, s->d_fh, (size_t)b->n * 4, hipMemcpyDeviceToHost,
+		                      s->stream));
+	if (h_ti)
+		HIPCHK(hipMemcpyAsync(h_ti, s->d_ti, (size_t)b->n * sizeof(mosrx_tcpinfo), hipMemcpyDeviceToHost,
 		                      s->stream));
 	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_R_COUNT * 4, hipMemcpyDeviceToHost, s->stream));
 	HIPCHK(hipEventRecord(s->done, s->stream));
@@ -538,12 +559,13 @@ int mosrx_classify_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out)
 	return mosrx_classify_host_wait(c, 0);
 }
 
-int mosrx_classify_host_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_fhash)
+int mosrx_classify_host_ex(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_fhash,
+                           mosrx_tcpinfo *h_tcpinfo)
 {
 	int rc;
 	if (!c || (rc = mosrx__check_batch(b, 0)))
 		return c ? rc : -EINVAL;
-	if (!h_fhash)
+	if (!h_fhash && !h_tcpinfo)
 		return mosrx_classify_host(c, b, h_out);
 	if (c->slot[0].busy)
 		return -EBUSY;
@@ -552,9 +574,14 @@ int mosrx_classify_host_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_o
 	if (!h_out)
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
-	if ((rc = host_enqueue(c, &c->slot[0], b, h_out, h_fhash, NULL)))
+	if ((rc = host_enqueue(c, &c->slot[0], b, h_out, h_fhash, NULL, h_tcpinfo)))
 		return rc;
 	return mosrx_classify_host_wait(c, 0);
+}
+
+int mosrx_classify_host_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_fhash)
+{
+	return mosrx_classify_host_ex(c, b, h_out, h_fhash, NULL);
 }
 
 int mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out)
@@ -574,7 +601,7 @@ int mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mos
 	if (!h_out)
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
-	return host_enqueue(c, &c->slot[slot], b, h_out, NULL, NULL);
+	return host_enqueue(c, &c->slot[slot], b, h_out, NULL, NULL, NULL);
 }
 
 int mosrx_classify_bpf_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out,
@@ -595,7 +622,7 @@ int mosrx_classify_bpf_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b,
 	if (!h_out || !h_match)
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
-	return host_enqueue(c, &c->slot[slot], b, h_out, NULL, h_match);
+	return host_enqueue(c, &c->slot[slot], b, h_out, NULL, h_match, NULL);
 }
 
 int mosrx_classify_bpf_host(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_out, uint32_t *h_match)
@@ -733,7 +760,7 @@ int mosrx_time_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_resul
 			return -EBUSY;
 	for (i = 0; i < iters; i++) {
 		struct slot *s = &c->slot[i % NSLOT];
-		if ((rc = host_enqueue(c, s, &b[i % nb], h_out[i % nb], NULL, NULL)))
+		if ((rc = host_enqueue(c, s, &b[i % nb], h_out[i % nb], NULL, NULL, NULL)))
 			return rc;
 	}
 	for (k = 0; k < NSLOT; k++) {

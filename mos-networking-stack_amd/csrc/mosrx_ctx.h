@@ -23,6 +23,7 @@ struct slot {
 	uint16_t *d_len;
 	mosrx_result *d_res;
 	uint32_t *d_fh;
+	mosrx_tcpinfo *d_ti;
 	uint32_t *d_cnt;
 	uint64_t cap_frames;
 	uint32_t cap_n;

@@ -12,12 +12,17 @@
 extern "C" {
 #endif
 
-/* Device-side lookup tables, one 2 KiB block per context:
+/* Device-side lookup tables, one block per context:
  *   [0, 384)   Toeplitz nibble tables, 24 x 16 u32 (mosrx_rss_tables)
- *   [384, 512) GetRSSCPUCore queue LUT, 512 x u8 indexed by (rss & 0x1FF) */
+ *   [384, 512) GetRSSCPUCore queue LUT, 512 x u8 indexed by (rss & 0x1FF)
+ *   (the first MOSRX_TAB_WORDS are staged in LDS by every header wave)
+ *   [512]      number of local addresses, [513, 529) the addresses (read with
+ *              scalar loads by waves that hold an ICMP frame) */
 #define MOSRX_TAB_RSS_WORDS   384
 #define MOSRX_TAB_QLUT_WORDS  128
 #define MOSRX_TAB_WORDS       512
+#define MOSRX_TAB_LOCAL       512
+#define MOSRX_TAB_ALLOC_WORDS (MOSRX_TAB_LOCAL + 1 + MOSRX_MAX_LOCAL)
 
 enum {
 	MOSRX_KF_VERIFY    = 1u << 0,  /* num_msp || num_esp: checksums verified (ip_in.c:67) */
@@ -36,32 +41,23 @@ typedef struct mosrx_kparams {
 	uint32_t       *counters;   /* MOSRX_R_COUNT u32, accumulated with atomics; may be NULL */
 	uint32_t       *fhash;      /* n flow hashes (HashFlow before the NUM_BINS mask); may be NULL */
 	uint32_t       *bmatch;     /* fused BPF match masks (hipRTC-built kernels only); else NULL */
+	mosrx_tcpinfo  *tinfo;      /* n pkt_info TCP field records; may be NULL */
 	uint32_t        frames_bytes;
 	uint32_t        n;
 	uint32_t        flags;      /* MOSRX_KF_* */
 } mosrx_kparams;
 
-/* Kernel shapes ("kinds"):
- *   SMALL  256 frames / 4 waves, every frame fits the header window (64 B configs)
- *   LARGE   64 frames / 1 header wave + 4 streamer waves that stream whole tails
- *   MID    256 frames / 4 header waves + 4 streamer waves
- *   L12     64 frames / 1 header wave + 2 streamers
- *   L24    128 frames / 2 header waves + 4 streamers
- *   L28    128 frames / 2 header waves + 8 streamers
- *   S1s     64 frames / 1 header wave + s streamer waves that read the tile's
+/* Kernel shapes ("kinds") the library builds:
+ *   SMALL  256 frames / 4 waves, lane per frame, every frame fits the header
+ *          window (the 64 B configs)
+ *   S13     64 frames / 1 header wave + 3 streamer waves that read the tile's
  *          tail span in buffer order with a prefix scan (frames sorted and
- *          disjoint, checked per tile; unsorted tiles stream whole tails like
- *          LARGE): S13 and S14 are the defaults (measured), S12 and S16 tune */
-enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_LARGE = 1, MOSRX_KIND_MID = 2, MOSRX_KIND_L12 = 3, MOSRX_KIND_L24 = 4,
-       MOSRX_KIND_L28 = 5, MOSRX_KIND_S14 = 6, MOSRX_KIND_S12 = 7, MOSRX_KIND_S13 = 8, MOSRX_KIND_S16 = 9,
-       MOSRX_KIND_COUNT = 10 };
-#define MOSRX_KIND_IS_STREAM(k) ((k) >= MOSRX_KIND_S14)
-/* header waves / streamer waves of a large-type or stream kind */
-#define MOSRX_KIND_H(k) ((k) == MOSRX_KIND_MID ? 4 : ((k) == MOSRX_KIND_L24 || (k) == MOSRX_KIND_L28) ? 2 : 1)
-#define MOSRX_KIND_S(k)                                                                                           \
-	(((k) == MOSRX_KIND_L12 || (k) == MOSRX_KIND_S12) ? 2 : (k) == MOSRX_KIND_S13 ? 3                            \
-	 : (k) == MOSRX_KIND_S16 ? 6 : (k) == MOSRX_KIND_L28 ? 8 : 4)
-#define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_SMALL ? 256u : 64u * (unsigned)MOSRX_KIND_H(k))
+ *          disjoint, checked per tile; unsorted tiles stream tail by tail)
+ * Tuning shapes (LARGE, MID, L12/L24/L28, S12/S14/S16) live in scripts/probe_*
+ * (DESIGN.md §4.3 has their measurements). */
+enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_S13 = 1, MOSRX_KIND_COUNT = 2 };
+#define MOSRX_STREAMERS 3
+#define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_SMALL ? 256u : 64u)
 /* Frames whose IP datagram ends at or before this frame byte are finished in
  * the per-lane header window; longer ones stream their tail cooperatively. */
 #define MOSRX_WINDOW_END 94

@@ -49,13 +49,11 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 #define WIN_RAW 24     // raw dwords per lane window (96 B)
 #define WIN_DW  23     // realigned dwords: frame bytes [2, 94)
-#define TAIL_G  4      // tails per group
-#define TAIL_U  2      // 1 KiB loads per tail issued up front (tails <= 2 KiB need no extra pass)
 
 static_assert(2 + 4 * WIN_DW == MOSRX_WINDOW_END, "window end");
 static_assert(sizeof(mosrx_result) == 16, "record size");
-// small: 4 waves, one frame per lane; large: 1 header + 4 streamer waves; mid: 4 + 4
-#define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? 256 : 64 * (MOSRX_KIND_H(kind) + MOSRX_KIND_S(kind)))
+// small: 4 waves, one frame per lane; stream: 1 header wave + MOSRX_STREAMERS streamer waves
+#define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? 256 : 64 * (1 + MOSRX_STREAMERS))
 
 
 // 16 bytes at byte offset c (OOB offsets read zero).  No data-dependent branch:
@@ -75,6 +73,9 @@ __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t c, ui
 #define IS_TX(v) (((v) & VAR_TX) != 0)
 // Variant bit 5: BPF program set fused into the header wave (hipRTC builds only, bpf_jit.c).
 #define VAR_BPF 32
+// Variant bit 6: also write pkt_info's TCP fields (mosrx_tcpinfo side array, kp.tinfo).
+#define VAR_TI 64
+#define IS_TI(v) (((v) & VAR_TI) != 0)
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 __device__ __forceinline__ uint32_t be16hi(uint32_t w) { return ((w >> 8) & 0xFF00u) | (w >> 24); } // bytes 2,3
@@ -126,19 +127,6 @@ __device__ __forceinline__ uint32_t chunk_sum(u32x4 v, uint32_t c, uint32_t hi, 
 	return add16x2(acc, v.w);
 }
 
-// Sum of a tail [lo, hi) (lo 16-aligned) beyond its first TAIL_U KiB.
-template <int AUX>
-__device__ __forceinline__ uint32_t tail_rest(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo,
-                                              uint32_t hi, uint32_t lane, uint32_t acc)
-{
-#pragma unroll 1
-	for (uint32_t base = lo + 1024u * TAIL_U; base < hi; base += 1024u) {
-		const uint32_t c = base + 16u * lane;
-		acc = chunk_sum(load16<AUX>(rs, c < hi ? c : nbytes, nbytes), c, hi, acc);
-	}
-	return acc;
-}
-
 // ---------------------------------------------------------------------------
 // Per-frame header state (lane per frame)
 // ---------------------------------------------------------------------------
@@ -146,6 +134,7 @@ struct hdr_t {
 	uint32_t o, fend, split_abs;
 	uint32_t wsum;                 // segment-grid sum of the segment bytes in the window (before the split)
 	uint32_t saddr, daddr, ip_len, ihl, doff, th0, th3;
+	uint32_t th1, th2;             // TI: TCP header dwords 1, 2 (seq, ack_seq; network order)
 	uint32_t rss, queue, ipc, reason;
 	uint32_t tcw, ipc_tx;          // TX: segment-grid TCP check word, IP checksum with check = 0
 	int verdict;
@@ -205,10 +194,10 @@ __device__ __forceinline__ uint32_t ip_chain(const uint32_t *w, uint32_t ihl, ui
 template <int VAR, bool F5>
 __device__ __forceinline__ void hdr_ihl(const uint32_t (&w)[WIN_DW], uint32_t ihl_l, int wend, uint32_t &th0,
                                         uint32_t &th3, uint32_t &tcw, uint32_t &ipc, uint32_t &ipc_tx,
-                                        uint32_t &wsum)
+                                        uint32_t &wsum, uint32_t &th1, uint32_t &th2)
 {
 	const uint32_t ihl = F5 ? 5u : ihl_l;
-	th0 = 0; th3 = 0; tcw = 0;
+	th0 = 0; th3 = 0; tcw = 0; th1 = 0; th2 = 0;
 #pragma unroll
 	for (int k = 0; k < 16; k++) {
 		if (ihl == (uint32_t)k) {
@@ -216,6 +205,10 @@ __device__ __forceinline__ void hdr_ihl(const uint32_t (&w)[WIN_DW], uint32_t ih
 			th3 = w[6 + k];
 			if (IS_TX(VAR))
 				tcw = w[7 + k] & 0xFFFFu;                  // tcph->check (frame bytes 30+4ihl, +1)
+			if (IS_TI(VAR)) {
+				th1 = w[4 + k];                             // tcph->seq
+				th2 = w[5 + k];                             // tcph->ack_seq
+			}
 		}
 	}
 	ipc = ip_chain(w, ihl, w[5]);
@@ -237,7 +230,8 @@ __device__ __forceinline__ void hdr_ihl(const uint32_t (&w)[WIN_DW], uint32_t ih
 #define VERDICT_TAB                                                                                                    \
 	(VT(MOSRX_R_TCP_OK, 1) | VT(MOSRX_R_ARP, 1) | VT(MOSRX_R_NON_IPV4, -1) | VT(MOSRX_R_IP_SHORT, -1) |                \
 	 VT(MOSRX_R_IP_BADVER, 0) | VT(MOSRX_R_NOVERIFY_PASS, 1) | VT(MOSRX_R_IP_BADCSUM, -1) | VT(MOSRX_R_NOT_TCP, 0) |   \
-	 VT(MOSRX_R_TCP_SHORT, -1) | VT(MOSRX_R_TCP_BADCSUM, -1) | VT(MOSRX_R_TRUNCATED, -1) | VT(MOSRX_R_TCP_LEN_OK, 1))
+	 VT(MOSRX_R_TCP_SHORT, -1) | VT(MOSRX_R_TCP_BADCSUM, -1) | VT(MOSRX_R_TRUNCATED, -1) | VT(MOSRX_R_TCP_LEN_OK, 1) | \
+	 VT(MOSRX_R_ICMP_LOCAL, 1))
 static_assert(MOSRX_R_COUNT <= 16, "verdict table holds 16 codes");
 
 // Parse + checks + IP checksum + RSS + in-window TCP sum.  Mirrors
@@ -245,7 +239,7 @@ static_assert(MOSRX_R_COUNT <= 16, "verdict table holds 16 codes");
 // ProcessInTCPPacket prefix (tcp.c:408-445); see oracle/mosrx_oracle.c.
 template <int VAR>
 __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uint32_t cap, bool active,
-                                           uint32_t kflags, const uint32_t *s_tab)
+                                           uint32_t kflags, const uint32_t *s_tab, const uint32_t *g_tab)
 {
 	hdr_t h;
 	uint32_t w[WIN_DW];
@@ -270,11 +264,11 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	// streamers take over there).
 	const bool in_win = fend <= (uint32_t)MOSRX_WINDOW_END;
 	const int wend = (int)(in_win ? fend : split);
-	uint32_t th0, th3, tcw, ipc, ipc_tx, wsum;
+	uint32_t th0, th3, tcw, ipc, ipc_tx, wsum, th1, th2;
 	if (__ballot(active && ihl != 5u) == 0)            // no IP options in the wave: constant positions
-		hdr_ihl<VAR, true>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum);
+		hdr_ihl<VAR, true>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum, th1, th2);
 	else
-		hdr_ihl<VAR, false>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum);
+		hdr_ihl<VAR, false>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum, th1, th2);
 	const uint32_t doff = is_tcp ? ((th3 >> 4) & 0xFu) : 0u;
 
 	// Toeplitz over saddr|daddr|sport|dport in wire order (util.c:61-99, host-order args)
@@ -297,6 +291,17 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	}
 	const uint32_t queue = (s_tab[MOSRX_TAB_RSS_WORDS + ((rss & 0x1FFu) >> 2)] >> (8 * (rss & 3u))) & 0xFFu;
 
+	// ICMP to one of the netdevs' addresses (ip_in.c:83-85, icmp.c:193-200):
+	// ProcessICMPPacket returns TRUE.  Rare, so the address list is read with
+	// scalar loads only by a wave that holds an ICMP frame.
+	bool icmp_local = false;
+	if (__ballot(active && proto == 1u)) {
+		const uint32_t nl = min(g_tab[MOSRX_TAB_LOCAL], (uint32_t)MOSRX_MAX_LOCAL);
+		for (uint32_t i = 0; i < nl; i++)
+			icmp_local |= daddr == g_tab[MOSRX_TAB_LOCAL + 1 + i];
+		icmp_local = icmp_local && proto == 1u;
+	}
+
 	// verdict chain (eth_in.c:27 -> ip_in.c:30 -> tcp.c:408), evaluated without
 	// branches: the reason is a select chain applied from the last check back to
 	// the first (so the first failing check wins, as in the reference's early
@@ -309,7 +314,7 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	const bool fields = cap >= 14u && !c_nonip && !c_trunc && ip_len >= 20u && ver == 4u;
 	uint32_t reason = (kflags & MOSRX_KF_SKIP_TCP) ? MOSRX_R_TCP_LEN_OK : MOSRX_R_TRUNCATED;   // TRUNCATED: pending TCP sum
 	reason = c_tshort ? MOSRX_R_TCP_SHORT : reason;                     // tcp.c:429-430
-	reason = !is_tcp ? MOSRX_R_NOT_TCP : reason;                        // ip_in.c:82-93
+	reason = !is_tcp ? (icmp_local ? MOSRX_R_ICMP_LOCAL : MOSRX_R_NOT_TCP) : reason;   // ip_in.c:79-93
 	reason = ipc != 0u ? MOSRX_R_IP_BADCSUM : reason;                   // ip_in.c:74-77
 	reason = !verify ? MOSRX_R_NOVERIFY_PASS : reason;                  // ip_in.c:67-72
 	reason = ver != 4u ? MOSRX_R_IP_BADVER : reason;                    // ip_in.c:47-51
@@ -337,6 +342,7 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 
 	h.o = o; h.fend = fend; h.split_abs = split_abs; h.wsum = wsum;
 	h.saddr = saddr; h.daddr = daddr; h.ip_len = ip_len; h.ihl = ihl; h.doff = doff; h.th0 = th0; h.th3 = th3;
+	h.th1 = th1; h.th2 = th2;
 	h.rss = rss; h.queue = queue; h.ipc = ipc; h.reason = reason; h.verdict = verdict;
 	h.tcw = tcw; h.ipc_tx = ipc_tx; h.tx_ip = tx_ip;
 	h.fields = fields; h.need_tcp = need_tcp; h.has_tail = need_tcp && !in_win; h.is_tcp = is_tcp;
@@ -404,6 +410,21 @@ __device__ __forceinline__ uint32_t flow_hash(const hdr_t &h)
 	hash ^= hash << 25;
 	hash += hash >> 6;
 	return (h.fields && h.is_tcp) ? hash : 0u;
+}
+
+// pkt_info's TCP fields (FillPacketContextTCPInfo, tcp.c:258-270): seq,
+// ack_seq, window in host order, plus ip_len (FillInPacketIPContext,
+// ip_in.c:21-27); zero where the record has no TCP header fields.  One
+// 12-byte store per lane.
+__device__ __forceinline__ void store_tcpinfo(mosrx_tcpinfo *ti, uint32_t p, const hdr_t &h)
+{
+	const bool def = h.fields && h.is_tcp;
+	typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+	u32x3 v;
+	v.x = def ? __builtin_bswap32(h.th1) : 0u;
+	v.y = def ? __builtin_bswap32(h.th2) : 0u;
+	v.z = def ? (((h.th3 >> 24) | ((h.th3 >> 8) & 0xFF00u)) | (h.ip_len << 16)) : 0u;   // window = tcph bytes 14,15
+	*reinterpret_cast<u32x3 *>(reinterpret_cast<uint32_t *>(ti) + 3u * p) = v;
 }
 
 // TX: write the fresh checksums into the frame (little-endian u16 stores, as
@@ -496,7 +517,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 			s_cnt[t] = 0;
 		__syncthreads();
 	}
-	const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab);
+	const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab, kp.tables);
 	uint32_t tail = 0;
 	for (uint64_t m = __ballot(h.has_tail); m; m &= m - 1) {
 		const uint32_t f = (uint32_t)__builtin_ctzll(m);
@@ -526,6 +547,10 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 			store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (active && kp.fhash)
 			kp.fhash[p] = flow_hash(h);
+		if constexpr (IS_TI(VAR)) {
+			if (active)
+				store_tcpinfo(kp.tinfo, p, h);
+		}
 	}
 #ifdef MOSRX_RTC_BPF
 	if constexpr ((VAR & VAR_BPF) != 0) {
@@ -536,120 +561,6 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	}
 #endif
 	flush_counters(kp, s_cnt, t);
-}
-
-// ---------------------------------------------------------------------------
-// large tile: 64 frames, headers by wave 0, speculative tail streaming by all waves
-// ---------------------------------------------------------------------------
-struct tail_grp_t {
-	u32x4 v[TAIL_G][TAIL_U];
-};
-
-// Frame of streamer q's j-th tail candidate within a 64-frame subtile served by
-// SP streamers.  Candidates (frames whose capture reaches past the split) are
-// ranked in frame order; group g takes candidates [SP*4g, SP*4(g+1)), four
-// consecutive ones per streamer, so each streamer reads ~6 KB of contiguous
-// frames per group.  Returns 64 when there is no such candidate.
-template <int SP>
-__device__ __forceinline__ uint32_t cand_frame(bool cand, uint32_t rank_l, uint32_t q, uint32_t j)
-{
-	const uint32_t r = SP * TAIL_G * (j / TAIL_G) + TAIL_G * q + (j % TAIL_G);
-	const uint64_t m = __ballot(cand && rank_l == r);
-	return m ? (uint32_t)__builtin_ctzll(m) : 64u;
-}
-
-// Issue the loads of group g of this streamer's tail candidates (speculative bounds).
-template <int AUX, int SP>
-__device__ __forceinline__ void tail_issue(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
-                                           uint32_t hi_l, bool cand, uint32_t rank_l, uint32_t q,
-                                           uint32_t lane, uint32_t g, tail_grp_t &b, uint32_t (&fr)[TAIL_G])
-{
-#pragma unroll
-	for (int u = 0; u < TAIL_G; u++) {
-		const uint32_t f = cand_frame<SP>(cand, rank_l, q, TAIL_G * g + u);
-		fr[u] = f;
-		const uint32_t lo = f < 64u ? __builtin_amdgcn_readlane(lo_l, f) : 0u;
-		const uint32_t hi = f < 64u ? __builtin_amdgcn_readlane(hi_l, f) : 0u;
-#pragma unroll
-		for (int q = 0; q < TAIL_U; q++) {
-			const uint32_t c = lo + 1024u * q + 16u * lane;
-			b.v[u][q] = load16<AUX>(rs, c < hi ? c : nbytes, nbytes);   // empty slots read out of range: no traffic
-		}
-	}
-}
-
-// Reduce a group over its speculative range [split, off + caplen) into s_spec.
-template <int AUX, int DBG = 0>
-__device__ __forceinline__ void tail_consume(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
-                                             uint32_t hi_l, uint32_t lane, const tail_grp_t &b,
-                                             const uint32_t (&fr)[TAIL_G], uint32_t *s_spec)
-{
-	if constexpr (DBG & 4) {
-		uint32_t x = 0;
-#pragma unroll
-		for (int u = 0; u < TAIL_G; u++)
-#pragma unroll
-			for (int q = 0; q < TAIL_U; q++)
-				x ^= b.v[u][q].x ^ b.v[u][q].y ^ b.v[u][q].z ^ b.v[u][q].w;
-		if (x == 0x9E3779B9u)
-			s_spec[lane] = x;
-		return;
-	}
-#pragma unroll
-	for (int u = 0; u < TAIL_G; u++) {
-		const uint32_t f = fr[u];
-		if (f < 64u) {
-			const uint32_t lo = __builtin_amdgcn_readlane(lo_l, f);
-			const uint32_t hi = __builtin_amdgcn_readlane(hi_l, f);
-			uint32_t acc = 0;
-#pragma unroll
-			for (int q = 0; q < TAIL_U; q++)
-				acc = chunk_sum(b.v[u][q], lo + 1024u * q + 16u * lane, hi, acc);
-			if (hi - lo > 1024u * TAIL_U)
-				acc = tail_rest<AUX>(rs, nbytes, lo, hi, lane, acc);
-			const uint32_t s = wave_sum(acc);
-			if (lane == 0)
-				s_spec[f] = s;
-		}
-	}
-}
-
-// Streamer q of SP sharing a 64-frame subtile: candidates [SP*4g + 4q, +4) of
-// group g, sums into spec[frame].  Groups come in pairs (double buffered);
-// slots past the count are issued anyway (out-of-range loads, no traffic) so
-// the load counts stay static and every wait is a counted vmcnt(N), never a
-// drain.
-template <int SP, int AUX, int DBG = 0>
-__device__ __forceinline__ void tail_streamers(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
-                                               uint32_t hi_l, bool cand, uint64_t cmask, uint32_t rank_l,
-                                               uint32_t q, uint32_t lane, uint32_t *spec)
-{
-	const uint32_t ngrp = (__builtin_popcountll(cmask) + SP * TAIL_G - 1u) / (SP * TAIL_G);
-	tail_grp_t b0, b1;
-	uint32_t f0[TAIL_G], f1[TAIL_G];
-	tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 0, b0, f0);
-	tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 1, b1, f1);
-	if constexpr (SP == 4) {
-		// at most 4 groups (64 candidates / 16 per group): straight-line code
-		tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
-		if (ngrp > 2) {
-			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 2, b0, f0);
-			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
-			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 3, b1, f1);
-			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
-			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
-		} else {
-			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
-		}
-	} else {
-#pragma unroll 1
-		for (uint32_t g = 0; g < ngrp; g += 2) {
-			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
-			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 2, b0, f0);
-			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
-			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 3, b1, f1);
-		}
-	}
 }
 
 // Absolute-grid word sum of the bytes [a, b) (any alignment), whole wave.
@@ -698,96 +609,9 @@ __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffe
 		store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (kp.fhash)
 			kp.fhash[p] = flow_hash(h);
+		if constexpr (IS_TI(VAR))
+			store_tcpinfo(kp.tinfo, p, h);
 	}
-}
-
-// One tile per workgroup of 5 waves: wave 0 parses the 64 headers while waves
-// 1..4 stream the tails over their SPECULATIVE ranges [split, off + caplen)
-// (known from the descriptors alone), so the header work is off the streaming
-// critical path and the workgroup has a single barrier between loads and
-// records.  (A persistent walk over tiles with the next tile's descriptors
-// prefetched measured slower at every grid cap: per-workgroup concurrency, not
-// launch startup, bounds this kernel; profiles/r01_tune_persistent.log.)
-//
-// H = header waves (64 frames each, TILE = 64 H); S streamer waves follow them,
-// SP = S / H per 64-frame subtile sharing its candidates.  LARGE is H=1, S=4.
-// DBG (diagnostic builds of scripts/probe_shape.hip only; the library uses 0)
-// removes work to time its share: 1 header parse/records, 2 header window
-// loads, 4 streamer sums (the loads stay live through an XOR).
-template <int H, int S, int VAR, int DBG = 0>
-__device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uint32_t tile)
-{
-	constexpr uint32_t TILE = 64u * H;
-	constexpr int SP = S / H;                 // streamers per 64-frame subtile
-	constexpr int AUX = TAIL_AUX(VAR);
-	static_assert(SP >= 1 && S % H == 0, "shape");
-	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
-	__shared__ uint32_t s_spec[TILE];
-	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
-
-	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
-	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
-	const uint32_t nbytes = kp.frames_bytes;
-	// subtile of this wave: header wave h -> h; streamer s -> s / SP
-	const uint32_t sub = wave < (uint32_t)H ? wave : (wave - H) / SP;
-
-	// every wave reads its subtile's descriptors (lane = frame)
-	const uint32_t p = tile * TILE + 64u * sub + lane;
-	const bool active = p < kp.n;
-	uint32_t o = 0, cap = 0;
-	if (active) {
-		o = kp.off[p];
-		cap = eff_caplen(o, kp.len[p], nbytes);
-	}
-	// speculative tail bounds from the capture length: [split, off + caplen)
-	const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
-	const uint32_t hi_l = active ? o + cap : 0u;
-	const bool cand = hi_l > lo_l;
-	const uint64_t cmask = __ballot(cand);
-	const uint32_t rank_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(cmask >> 32),
-	                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)cmask, 0u));
-
-	if (wave < (uint32_t)H) {
-		// ---- header wave: parse while the streamers pull the tails.  It fills the
-		// LDS tables itself (no barrier: a wave's LDS accesses are ordered; header
-		// waves write identical words) ----
-		hdr_win_t win;
-		if constexpr (DBG & 2) {
-#pragma unroll
-			for (int i = 0; i < WIN_RAW; i++)
-				win.raw[i] = o + i;
-		} else {
-			hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
-		}
-		{
-			const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
-			const u32x4 a = tg[lane], b = tg[lane + 64];
-			reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
-			reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
-			if (lane <= MOSRX_R_COUNT)
-				s_cnt[lane] = 0;
-		}
-		if constexpr (DBG & 1) {
-			uint32_t x = 0;
-#pragma unroll
-			for (int i = 0; i < WIN_RAW; i++)
-				x ^= win.raw[i];
-			__syncthreads();   // B
-			if (active && (x ^ s_spec[64u * sub + lane]) == 0x9E3779B9u)
-				kp.out[p].rss = x;
-		} else {
-			const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab);
-			__syncthreads();   // B: s_spec ready
-			hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, h.has_tail ? s_spec[64u * sub + lane] : 0u, p, active,
-			              lane, s_cnt);
-		}
-	} else {
-		// ---- streamer waves ----
-		tail_streamers<SP, AUX, DBG>(rs, nbytes, lo_l, hi_l, cand, cmask, rank_l, (wave - H) % SP, lane,
-		                             s_spec + 64u * sub);
-		__syncthreads();   // B
-	}
-	flush_counters(kp, s_cnt, t);
 }
 
 // ---------------------------------------------------------------------------
@@ -1001,7 +825,7 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 			if (active && (x ^ s_part[0][lane]) == 0x9E3779B9u)
 				kp.out[p].rss = x;
 		} else {
-			const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab);
+			const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab, kp.tables);
 			__syncthreads();   // B: s_part ready
 			uint32_t tail = 0;
 			if (h.has_tail) {
@@ -1049,15 +873,12 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 {
 	if constexpr (KIND == MOSRX_KIND_SMALL)
 		classify_tile_small<VAR>(kp, tile);
-	else if constexpr (MOSRX_KIND_IS_STREAM(KIND))
-		classify_tile_stream<MOSRX_KIND_S(KIND), VAR>(kp, tile);
 	else
-		classify_tile_large<MOSRX_KIND_H(KIND), MOSRX_KIND_S(KIND), VAR>(kp, tile);
+		classify_tile_stream<MOSRX_STREAMERS, VAR>(kp, tile);
 }
 
-// Stream shapes are held to 64 VGPRs: 8 waves per SIMD (7 for S16, whose
-// 7-wave workgroups fit 4 per CU).
-#define MIN_WAVES(kind) (!MOSRX_KIND_IS_STREAM(kind) ? 1 : (kind) == MOSRX_KIND_S16 ? 7 : 8)
+// The stream tile is held to 64 VGPRs: 8 waves per SIMD.
+#define MIN_WAVES(kind) ((kind) == MOSRX_KIND_S13 ? 8 : 1)
 
 template <int KIND, int VAR>
 __global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))
@@ -1095,6 +916,7 @@ void mosrx_classify_queue_kernel(mosrx_qparams qp)
 	kp.counters = qp.counters;
 	kp.fhash = nullptr;
 	kp.bmatch = nullptr;
+	kp.tinfo = nullptr;
 	kp.frames_bytes = d->frames_bytes;
 	kp.n = d->n;
 	kp.flags = qp.flags;
@@ -1161,9 +983,7 @@ extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles,
 	const hipStream_t s = (hipStream_t)stream;
 #define QROW(k) {launch_queue_v<k, 0>, launch_queue_v<k, 2>}
 	static void (*const tab[MOSRX_KIND_COUNT][2])(const mosrx_qparams *, uint32_t, hipStream_t) = {
-		QROW(MOSRX_KIND_SMALL), QROW(MOSRX_KIND_LARGE), QROW(MOSRX_KIND_MID),
-		QROW(MOSRX_KIND_L12), QROW(MOSRX_KIND_L24), QROW(MOSRX_KIND_L28),
-		QROW(MOSRX_KIND_S14), QROW(MOSRX_KIND_S12), QROW(MOSRX_KIND_S13), QROW(MOSRX_KIND_S16)};
+		QROW(MOSRX_KIND_SMALL), QROW(MOSRX_KIND_S13)};
 #undef QROW
 	tab[kind][(variant >> 1) & 1](qp, total_tiles, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
@@ -1176,13 +996,12 @@ extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int vari
 	if (kind < 0 || kind >= MOSRX_KIND_COUNT)
 		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-#define KROW(k) {launch_v<k, 0>, launch_v<k, 2>, launch_v<k, 2 | VAR_TX>}
-	static void (*const tab[MOSRX_KIND_COUNT][3])(const mosrx_kparams *, hipStream_t) = {
-		KROW(MOSRX_KIND_SMALL), KROW(MOSRX_KIND_LARGE), KROW(MOSRX_KIND_MID),
-		KROW(MOSRX_KIND_L12), KROW(MOSRX_KIND_L24), KROW(MOSRX_KIND_L28),
-		KROW(MOSRX_KIND_S14), KROW(MOSRX_KIND_S12), KROW(MOSRX_KIND_S13), KROW(MOSRX_KIND_S16)};
+#define KROW(k) {launch_v<k, 0>, launch_v<k, 2>, launch_v<k, 2 | VAR_TX>, launch_v<k, 2 | VAR_TI>}
+	static void (*const tab[MOSRX_KIND_COUNT][4])(const mosrx_kparams *, hipStream_t) = {
+		KROW(MOSRX_KIND_SMALL), KROW(MOSRX_KIND_S13)};
 #undef KROW
-	tab[kind][(kp->flags & (MOSRX_KF_TX_IP | MOSRX_KF_TX_TCP)) ? 2 : (variant >> 1) & 1](kp, s);
+	const int v = (kp->flags & (MOSRX_KF_TX_IP | MOSRX_KF_TX_TCP)) ? 2 : kp->tinfo ? 3 : (variant >> 1) & 1;
+	tab[kind][v](kp, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 #endif   // __HIPCC_RTC__

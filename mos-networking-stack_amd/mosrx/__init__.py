@@ -28,8 +28,20 @@ RESULT_DTYPE = np.dtype([
 assert RESULT_DTYPE.itemsize == 16
 
 REASONS = ["TCP_OK", "ARP", "NON_IPV4", "IP_SHORT", "IP_BADVER", "NOVERIFY_PASS", "IP_BADCSUM",
-           "NOT_TCP", "TCP_SHORT", "TCP_BADCSUM", "TRUNCATED", "TCP_LEN_OK"]
+           "NOT_TCP", "TCP_SHORT", "TCP_BADCSUM", "TRUNCATED", "TCP_LEN_OK", "ICMP_LOCAL"]
 R = {name: i for i, name in enumerate(REASONS)}
+NREASON = len(REASONS)
+MAX_LOCAL = 16
+
+# mosrx_tcpinfo: pkt_info's TCP fields (FillPacketContextTCPInfo, tcp.c:258-270), host order
+TCPINFO_DTYPE = np.dtype([("seq", "<u4"), ("ack_seq", "<u4"), ("window", "<u2"), ("ip_len", "<u2")])
+assert TCPINFO_DTYPE.itemsize == 12
+KIND_SMALL, KIND_S13 = 0, 1
+
+
+def shape_variant(kind: int, nt_tails: bool = True) -> int:
+    """mosrx_set_variant value forcing a kernel shape (bits 2-6 = kind + 1; bit 1 = nt tails)."""
+    return ((kind + 1) << 2) | (2 if nt_tails else 0)
 
 QMAP_I40E, QMAP_IXGBE = 1, 0
 TRACE_FW64, TRACE_S64, TRACE_M1500, TRACE_IMIX = 0, 1, 2, 3
@@ -44,7 +56,13 @@ class Params(C.Structure):
     """mosrx_params: the mOS stack state the verdict depends on."""
     _fields_ = [("num_msp", C.c_uint32), ("num_esp", C.c_uint32), ("forward", C.c_int32),
                 ("num_queues", C.c_int32), ("queue_mode", C.c_int32), ("skip_tcp_csum", C.c_int32),
-                ("rss_key_len", C.c_uint32), ("rss_key", C.c_uint8 * 52)]
+                ("rss_key_len", C.c_uint32), ("rss_key", C.c_uint8 * 52),
+                ("num_local", C.c_uint32), ("local_ip", C.c_uint32 * MAX_LOCAL)]
+
+
+def ip_raw(a: str) -> int:
+    """Dotted quad -> the raw u32 mOS keeps in netdev ip_addr (network order, loaded little-endian)."""
+    return int.from_bytes(bytes(int(x) for x in a.split(".")), "little")
 
 
 class Batch(C.Structure):
@@ -71,7 +89,7 @@ class TraceC(C.Structure):
 
 class RxStats(C.Structure):
     _fields_ = [("rx_packets", C.c_uint64), ("rx_bytes", C.c_uint64), ("rx_errors", C.c_uint64),
-                ("rounds", C.c_uint64), ("batches", C.c_uint64), ("by_reason", C.c_uint64 * 12)]
+                ("rounds", C.c_uint64), ("batches", C.c_uint64), ("by_reason", C.c_uint64 * NREASON)]
 
 
 class ModuleCfg(C.Structure):
@@ -113,6 +131,8 @@ def lib():
             "mosrx_classify_host": (I, [P, C.POINTER(Batch), P]),
             "mosrx_classify_dev_fh": (I, [P, C.POINTER(Batch), P, P, P]),
             "mosrx_classify_host_fh": (I, [P, C.POINTER(Batch), P, P]),
+            "mosrx_classify_dev_ex": (I, [P, C.POINTER(Batch), P, P, P, P]),
+            "mosrx_classify_host_ex": (I, [P, C.POINTER(Batch), P, P, P]),
             "mosrx_classify_host_submit": (I, [P, I, C.POINTER(Batch), P]),
             "mosrx_classify_host_wait": (I, [P, I]),
             "mosrx_last_counters": (I, [P, C.POINTER(U64)]),
@@ -181,9 +201,18 @@ def _chk(rc: int, what: str):
 
 
 def default_params(**kw) -> Params:
+    """simple_firewall's state (mosrx_params_default) with fields overridden; `key`
+    = RSS key bytes, `local` = the netdevs' IPv4 addresses (dotted quads)."""
     p = Params()
     lib().mosrx_params_default(C.byref(p))
     key = kw.pop("key", None)
+    local = kw.pop("local", None)
+    if local is not None:
+        if len(local) > MAX_LOCAL:
+            raise ValueError("at most 16 local addresses")
+        p.num_local = len(local)
+        for i, a in enumerate(local):
+            p.local_ip[i] = ip_raw(a) if isinstance(a, str) else int(a)
     for k, v in kw.items():
         setattr(p, k, v)
     if key is not None:
@@ -306,6 +335,7 @@ class DevBatch:
         self.d_len.upload(ln)
         self.d_out = DevBuffer(ctx, max(self.n * 16, 16))
         self.d_fhash = None   # allocated on the first classify_dev(..., flow_hash=True)
+        self.d_tinfo = None   # allocated on the first classify_dev(..., tcpinfo=True)
         self.d_match = None   # allocated on the first bpf_dev
         self.max_len = int(max_len if max_len is not None else (int(ln.max()) if self.n else 0))
         self.caplen_sum = int(ln.astype(np.uint64).sum())
@@ -337,8 +367,14 @@ class DevBatch:
             self.d_fhash.download(out)
         return out
 
+    def tcpinfo(self) -> np.ndarray:
+        out = np.zeros(self.n, TCPINFO_DTYPE)
+        if self.n:
+            self.d_tinfo.download(out)
+        return out
+
     def free(self):
-        for b in (self.d_frames, self.d_off, self.d_len, self.d_out, self.d_fhash, self.d_match):
+        for b in (self.d_frames, self.d_off, self.d_len, self.d_out, self.d_fhash, self.d_match, self.d_tinfo):
             if b is not None:
                 b.free()
 
@@ -381,6 +417,20 @@ class Context:
                   off.ctypes.data, ln.ctypes.data, len(off), max_len)
         _chk(lib().mosrx_classify_host(self.handle, C.byref(b), out.ctypes.data), "mosrx_classify_host")
         return out
+
+    def classify_host_ex(self, frames, off, ln, frames_bytes=None, max_len=0):
+        """(records, flow hashes, pkt_info TCP fields) of a host batch in one GPU pass."""
+        frames = np.ascontiguousarray(frames, np.uint8)
+        off = np.ascontiguousarray(off, np.uint32)
+        ln = np.ascontiguousarray(ln, np.uint16)
+        out = np.zeros(len(off), RESULT_DTYPE)
+        fh = np.zeros(len(off), np.uint32)
+        ti = np.zeros(len(off), TCPINFO_DTYPE)
+        b = Batch(frames.ctypes.data, int(frames_bytes if frames_bytes is not None else len(frames)),
+                  off.ctypes.data, ln.ctypes.data, len(off), max_len)
+        _chk(lib().mosrx_classify_host_ex(self.handle, C.byref(b), out.ctypes.data, fh.ctypes.data,
+                                          ti.ctypes.data), "mosrx_classify_host_ex")
+        return out, fh, ti
 
     def classify_host_fh(self, frames, off, ln, frames_bytes=None, max_len=0):
         """Records plus the per-frame flow hash (HashFlow before the NUM_BINS mask)."""
@@ -475,7 +525,7 @@ class Context:
             _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
 
     def last_counters(self) -> np.ndarray:
-        c = (C.c_uint64 * 12)()
+        c = (C.c_uint64 * NREASON)()
         _chk(lib().mosrx_last_counters(self.handle, c), "mosrx_last_counters")
         return np.array(c[:], np.uint64)
 
@@ -483,11 +533,17 @@ class Context:
     def upload(self, frames, off, ln, frames_bytes=None, max_len=None) -> DevBatch:
         return DevBatch(self, frames, off, ln, frames_bytes, max_len)
 
-    def classify_dev(self, db: DevBatch, sync: bool = True, flow_hash: bool = False) -> None:
+    def classify_dev(self, db: DevBatch, sync: bool = True, flow_hash: bool = False, tcpinfo: bool = False) -> None:
         b = db.batch()
-        if flow_hash:
-            if db.d_fhash is None:
-                db.d_fhash = DevBuffer(self, max(db.n * 4, 4))
+        if flow_hash and db.d_fhash is None:
+            db.d_fhash = DevBuffer(self, max(db.n * 4, 4))
+        if tcpinfo and db.d_tinfo is None:
+            db.d_tinfo = DevBuffer(self, max(db.n * 12, 12))
+        if tcpinfo:
+            _chk(lib().mosrx_classify_dev_ex(self.handle, C.byref(b), db.d_out.ptr,
+                                             db.d_fhash.ptr if flow_hash else None, db.d_tinfo.ptr, None),
+                 "mosrx_classify_dev_ex")
+        elif flow_hash:
             _chk(lib().mosrx_classify_dev_fh(self.handle, C.byref(b), db.d_out.ptr, db.d_fhash.ptr, None),
                  "mosrx_classify_dev_fh")
         else:

@@ -196,23 +196,36 @@ uint32_t mo_flow_hash(const uint8_t *iph, const uint8_t *tcph)
 	return mo_superfasthash(key, 12);
 }
 
-int mo_classify_fh(const mosrx_params *p, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
-                   const uint16_t *len, uint32_t n, mosrx_result *out, uint32_t *fhash)
+int mo_classify_ex(const mosrx_params *p, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
+                   const uint16_t *len, uint32_t n, mosrx_result *out, uint32_t *fhash, mosrx_tcpinfo *tinfo)
 {
 	uint32_t i;
 	int rc = mo_classify(p, frames, frames_bytes, off, len, n, out);
-	if (rc || !fhash)
+	if (rc || (!fhash && !tinfo))
 		return rc;
 	for (i = 0; i < n; i++) {
 		/* defined for every TCP frame whose header fields are (payload_off != 0) */
-		if (out[i].payload_off) {
-			const uint8_t *iph = frames + off[i] + 14;
-			fhash[i] = mo_flow_hash(iph, iph + (out[i].ihl_doff >> 4) * 4);
-		} else {
-			fhash[i] = 0;
+		const uint8_t *iph = frames + off[i] + 14;
+		const uint8_t *tcph = iph + (out[i].ihl_doff >> 4) * 4;
+		if (fhash)
+			fhash[i] = out[i].payload_off ? mo_flow_hash(iph, tcph) : 0;
+		if (tinfo) {
+			memset(&tinfo[i], 0, sizeof(tinfo[i]));
+			if (out[i].payload_off) {   /* FillPacketContextTCPInfo, tcp.c:263-265 */
+				tinfo[i].seq = be32(tcph + 4);
+				tinfo[i].ack_seq = be32(tcph + 8);
+				tinfo[i].window = be16(tcph + 14);
+				tinfo[i].ip_len = be16(iph + 2);   /* FillInPacketIPContext, ip_in.c:21-27 */
+			}
 		}
 	}
 	return 0;
+}
+
+int mo_classify_fh(const mosrx_params *p, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
+                   const uint16_t *len, uint32_t n, mosrx_result *out, uint32_t *fhash)
+{
+	return mo_classify_ex(p, frames, frames_bytes, off, len, n, out, fhash, NULL);
 }
 
 /* TX checksum rewrite, mtcp_setlastpkt's MOS_UPDATE_IP_CHKSUM /
@@ -348,8 +361,18 @@ void mo_classify_one(const mosrx_params *p, const uint32_t cache[96],
 		VERDICT(r, -1, MOSRX_R_IP_BADCSUM);
 		return;
 	}
-	if (proto != 6) {                        /* ip_in.c:82-93: ICMP with no local IP, others */
-		VERDICT(r, 0, MOSRX_R_NOT_TCP);
+	if (proto != 6) {
+		/* ip_in.c:82-85: ICMP to one of the netdevs' addresses is processed
+		 * (ProcessICMPPacket returns TRUE whatever the type, icmp.c:193-227) */
+		if (proto == 1) {
+			uint32_t k;
+			for (k = 0; k < p->num_local && k < MOSRX_MAX_LOCAL; k++)
+				if (daddr == p->local_ip[k]) {
+					VERDICT(r, 1, MOSRX_R_ICMP_LOCAL);
+					return;
+				}
+		}
+		VERDICT(r, 0, MOSRX_R_NOT_TCP);   /* ip_in.c:86-93: other protocols */
 		return;
 	}
 	if (ip_len < (ihl + doff) * 4) {          /* tcp.c:429-430 */

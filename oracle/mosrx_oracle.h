@@ -42,6 +42,12 @@ uint32_t mo_flow_hash(const uint8_t *iph, const uint8_t *tcph);
 int mo_classify_fh(const mosrx_params *p, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
                    const uint16_t *len, uint32_t n, mosrx_result *out, uint32_t *fhash);
 
+/* mo_classify + both optional side arrays of mosrx_classify_dev_ex (either may
+ * be NULL): the flow hash and pkt_info's TCP fields as FillPacketContextTCPInfo
+ * (tcp.c:258-270) sets them, zero where payload_off == 0. */
+int mo_classify_ex(const mosrx_params *p, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
+                   const uint16_t *len, uint32_t n, mosrx_result *out, uint32_t *fhash, mosrx_tcpinfo *tinfo);
+
 /* sfbpf_filter (bpf/sf_bpf_filter.c:214-536) and sfbpf_validate (:548-691). */
 uint32_t mo_bpf_filter(const mosrx_bpf_insn *pc, const uint8_t *p, uint32_t wirelen, uint32_t buflen);
 int      mo_bpf_validate(const mosrx_bpf_insn *f, int len);

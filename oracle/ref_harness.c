@@ -9,15 +9,28 @@
  * a zeroed io_module_func instead of a running stack.
  *
  * Usage: mosref <trace.in> <results.out>
- *   trace.in : "MRXT" | u32 ver=1 | u32 n | u64 frames_bytes |
+ *   trace.in : "MRXT" | u32 ver (1 or 2) | u32 n | u64 frames_bytes |
  *              u32 num_msp | u32 num_esp | i32 forward | i32 num_queues | i32 queue_mode |
+ *              [ver 2: u32 nlocal | u32 local_ip[16] (netdev ip_addr, network order)] |
  *              u32 off[n] | u16 len[n] | u8 frames[frames_bytes]
  *   results  : n x { i8 verdict, u8 have, u16 ip_csum, u16 tcp_csum, u16 pad, u32 rss, i32 queue,
- *                    u32 fbucket }
+ *                    u32 fbucket,
+ *                    u16 payloadlen, u16 payload_off, u32 seq, u32 ack_seq, u16 window,
+ *                    u8 tcp_flags, u8 ihl_doff, u16 ip_len, u16 pad }
  *              then u64 rx_packets, rx_bytes, rx_errors (NETSTAT, eth_in.c:42-45,80-84)
  *   have bit0: ip_csum computed, bit1: tcp_csum computed, bit2: rss computed,
  *        bit3: frame skipped (would make the reference read past caplen),
- *        bit4: fbucket computed (TCP frames).
+ *        bit4: fbucket computed (TCP frames),
+ *        bit5: pkt_info TCP fields computed (TCP frames): mOS's own
+ *              FillInPacketIPContext (ip_in.c:21-27) + FillPacketContextTCPInfo
+ *              (tcp.c:258-270) on a pkt_ctx, so payloadlen, payload - ethh, seq,
+ *              ack_seq and window are the values ProcessInTCPPacket hands on;
+ *              tcp_flags / ihl_doff are the tcphdr / iphdr bitfields it reads.
+ *
+ * The local addresses become netdev_table entries (config.h:54-74): ICMP frames
+ * to one of them take ProcessICMPPacket's "to me" branch (icmp.c:187-227).  The
+ * route table is empty, so an echo request's reply finds no output interface
+ * (ip_out.c:12-37) and nothing is sent.
  *
  * forward must be 0: ForwardIPPacket/ForwardEthernetFrame need route/ARP
  * tables and TX buffers.
@@ -46,10 +59,12 @@
 #include "fhash.h"
 #include "logger.h"
 #include "mtcp_util.h"
+#include "tcp.h"
 
 int ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index,
                   uint32_t cur_ts, unsigned char *pkt_data, int len);
 uint16_t TCPCalcChecksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t daddr);
+void FillInPacketIPContext(struct pkt_ctx *pctx, struct iphdr *iph, int ip_len);   /* ip_in.c:21, gnu89 inline */
 
 static int g_qmode = 1;
 int __wrap_FetchEndianType(void) { return g_qmode; }
@@ -61,7 +76,13 @@ struct rec {
 	uint32_t rss;
 	int32_t queue;
 	uint32_t fbucket;   /* HashFlow() of FindStream's reversed tuple (tcp.c:185-190, fhash.c:72-92) */
+	uint16_t payloadlen, payload_off;   /* pctx->p.payloadlen, pctx->p.payload - ethh */
+	uint32_t seq, ack_seq;              /* pctx->p.seq, pctx->p.ack_seq (host order) */
+	uint16_t window;                    /* pctx->p.window (host order) */
+	uint8_t tcp_flags, ihl_doff;        /* tcph byte 13; (iph->ihl << 4) | tcph->doff */
+	uint16_t ip_len, pad2;              /* pctx->p.ip_len */
 };
+_Static_assert(sizeof(struct rec) == 40, "record layout");
 
 unsigned int HashFlow(const tcp_stream *flow);
 
@@ -134,7 +155,7 @@ int main(int argc, char **argv)
 	char magic[4];
 	uint32_t ver, n, i;
 	uint64_t fb;
-	uint32_t num_msp, num_esp;
+	uint32_t num_msp, num_esp, nlocal = 0, local_ip[16];
 	int32_t forward, nq, qmode;
 	uint32_t *off;
 	uint16_t *len;
@@ -143,6 +164,8 @@ int main(int argc, char **argv)
 	static struct mtcp_thread_context tctx;
 	static struct mos_conf mc;
 	static struct netdev_conf nd;
+	static struct netdev_entry nde[16];
+	static struct route_conf rt;
 	static io_module_func null_iom;
 	static log_thread_context lg;
 
@@ -154,9 +177,10 @@ int main(int argc, char **argv)
 	if (timing)
 		argv++;
 	in = fopen(argv[1], "rb");
-	if (!in || rd(in, magic, 4) || memcmp(magic, "MRXT", 4) || rd(in, &ver, 4) || ver != 1 ||
+	if (!in || rd(in, magic, 4) || memcmp(magic, "MRXT", 4) || rd(in, &ver, 4) || (ver != 1 && ver != 2) ||
 	    rd(in, &n, 4) || rd(in, &fb, 8) || rd(in, &num_msp, 4) || rd(in, &num_esp, 4) ||
-	    rd(in, &forward, 4) || rd(in, &nq, 4) || rd(in, &qmode, 4)) {
+	    rd(in, &forward, 4) || rd(in, &nq, 4) || rd(in, &qmode, 4) ||
+	    (ver == 2 && (rd(in, &nlocal, 4) || nlocal > 16 || rd(in, local_ip, sizeof(local_ip))))) {
 		fprintf(stderr, "bad trace header\n");
 		return 1;
 	}
@@ -178,9 +202,15 @@ int main(int argc, char **argv)
 		return time_mode(n, off, len, frames, nq, atof(argv[2]));
 
 	/* stack state: core.c:1079-1110 InitializeMTCPManager, reduced */
-	nd.num = 0;
+	nd.num = (int)nlocal;
+	for (i = 0; i < nlocal; i++) {
+		nde[i].ip_addr = local_ip[i];
+		nd.ent[i] = &nde[i];
+	}
+	rt.num = 0;
 	mc.forward = forward;
 	mc.netdev_table = &nd;
+	mc.route_table = &rt;
 	g_config.mos = &mc;
 	tctx.cpu = 0;
 	TAILQ_INIT(&m.monitors);
@@ -228,12 +258,27 @@ int main(int argc, char **argv)
 					r.have |= 4;
 					if (proto == 6) {   /* FindStream's temp stream, tcp.c:185-190 */
 						static tcp_stream ts;
+						struct pkt_ctx pctx;
 						ts.saddr = iph->daddr;
 						ts.sport = th->dest;
 						ts.daddr = iph->saddr;
 						ts.dport = th->source;
 						r.fbucket = HashFlow(&ts);
 						r.have |= 16;
+						/* ProcessInIPv4Packet -> ProcessInTCPPacket's context fill */
+						memset(&pctx, 0, sizeof(pctx));
+						pctx.p.ethh = (struct ethhdr *)f;
+						FillInPacketIPContext(&pctx, iph, (int)ip_len);
+						FillPacketContextTCPInfo(&pctx, th);
+						r.payloadlen = pctx.p.payloadlen;
+						r.payload_off = (uint16_t)(pctx.p.payload - (uint8_t *)pctx.p.ethh);
+						r.seq = pctx.p.seq;
+						r.ack_seq = pctx.p.ack_seq;
+						r.window = pctx.p.window;
+						r.tcp_flags = ((uint8_t *)th)[13];
+						r.ihl_doff = (uint8_t)((iph->ihl << 4) | th->doff);
+						r.ip_len = pctx.p.ip_len;
+						r.have |= 32;
 					}
 				}
 			}

@@ -4,6 +4,7 @@
 // and times each build on the BASELINE config #3 trace, back-to-back and one
 // launch at a time.  Results are meaningless for DBG != 0; only time counts.
 #include "../mos-networking-stack_amd/csrc/mosrx_kernels.hip"
+#include "probe_large.h"
 #include "../include/mosrx_trace.h"
 #include <stdio.h>
 #include <stdlib.h>
@@ -46,7 +47,7 @@ static void launch_sdbg(const mosrx_kparams *kp, hipStream_t s)
 }
 static void launch_product(const mosrx_kparams *kp, hipStream_t s)
 {
-	mosrx_launch_classify(kp, MOSRX_KIND_LARGE, 2, s);
+	launch_dbg<0, 1>(kp, s);   // LARGE (no longer in the library)
 }
 static void launch_stream(const mosrx_kparams *kp, hipStream_t s)
 {
@@ -106,8 +107,8 @@ int main(int argc, char **argv)
 	const int nb = 6;
 	mosrx_kparams kps[nb];
 	uint32_t *tables;
-	CHK(hipMalloc((void **)&tables, MOSRX_TAB_WORDS * 4));
-	CHK(hipMemset(tables, 0, MOSRX_TAB_WORDS * 4));
+	CHK(hipMalloc((void **)&tables, MOSRX_TAB_ALLOC_WORDS * 4));
+	CHK(hipMemset(tables, 0, MOSRX_TAB_ALLOC_WORDS * 4));
 	for (int i = 0; i < nb; i++) {
 		uint8_t *f; uint32_t *o; uint16_t *l; mosrx_result *r;
 		CHK(hipMalloc((void **)&f, t.frames_bytes + 64));
@@ -117,7 +118,7 @@ int main(int argc, char **argv)
 		CHK(hipMalloc((void **)&l, n * 2));
 		CHK(hipMemcpy(l, t.len, n * 2, hipMemcpyHostToDevice));
 		CHK(hipMalloc((void **)&r, n * 16));
-		kps[i] = (mosrx_kparams){f, o, l, r, tables, NULL, NULL, NULL, (uint32_t)t.frames_bytes, n, MOSRX_KF_VERIFY, 0};
+		kps[i] = (mosrx_kparams){f, o, l, r, tables, NULL, NULL, NULL, NULL, (uint32_t)t.frames_bytes, n, MOSRX_KF_VERIFY};
 	}
 	const double bytes = (double)t.caplen_sum + 22.0 * n;
 	printf("trace kind %d n %u: %.2f MB algorithmic\n", kind, n, bytes / 1e6);
@@ -127,7 +128,7 @@ int main(int argc, char **argv)
 		run("SMALL 64", launch_small<64>, kps, nb, bytes);
 		return 0;
 	}
-	run("product LARGE", launch_product, kps, nb, bytes);
+	run("LARGE", launch_product, kps, nb, bytes);
 	run("product S13", launch_stream, kps, nb, bytes);
 	// S13 as the library builds it (8 waves/SIMD, 4 blocks in flight) with pieces removed
 	run("S13 full", launch_sdbg<3, 0, 8, 4>, kps, nb, bytes);

@@ -1,0 +1,228 @@
+// probe_large.h — the LARGE / MID / L12 / L24 / L28 tile family (diagnostic only).
+//
+// Tuning shapes kept out of the product library (libmosrx.so builds SMALL and the
+// S13 stream tile only): one header wave per 64-frame subtile plus streamer waves
+// that each own whole tails, loads issued speculatively from the capture length.
+// Included after mosrx_kernels.hip by scripts/probe_classify.hip; measured in
+// DESIGN.md §4.3 (LARGE 20.8 us on the 1500 B config, 41.7 us on IMIX).
+#pragma once
+#define TAIL_G  4      // tails per group
+#define TAIL_U  2      // 1 KiB loads per tail issued up front (tails <= 2 KiB need no extra pass)
+
+// Sum of a tail [lo, hi) (lo 16-aligned) beyond its first TAIL_U KiB.
+template <int AUX>
+__device__ __forceinline__ uint32_t tail_rest(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo,
+                                              uint32_t hi, uint32_t lane, uint32_t acc)
+{
+#pragma unroll 1
+	for (uint32_t base = lo + 1024u * TAIL_U; base < hi; base += 1024u) {
+		const uint32_t c = base + 16u * lane;
+		acc = chunk_sum(load16<AUX>(rs, c < hi ? c : nbytes, nbytes), c, hi, acc);
+	}
+	return acc;
+}
+
+
+// ---------------------------------------------------------------------------
+// large tile: 64 frames, headers by wave 0, speculative tail streaming by all waves
+// ---------------------------------------------------------------------------
+struct tail_grp_t {
+	u32x4 v[TAIL_G][TAIL_U];
+};
+
+// Frame of streamer q's j-th tail candidate within a 64-frame subtile served by
+// SP streamers.  Candidates (frames whose capture reaches past the split) are
+// ranked in frame order; group g takes candidates [SP*4g, SP*4(g+1)), four
+// consecutive ones per streamer, so each streamer reads ~6 KB of contiguous
+// frames per group.  Returns 64 when there is no such candidate.
+template <int SP>
+__device__ __forceinline__ uint32_t cand_frame(bool cand, uint32_t rank_l, uint32_t q, uint32_t j)
+{
+	const uint32_t r = SP * TAIL_G * (j / TAIL_G) + TAIL_G * q + (j % TAIL_G);
+	const uint64_t m = __ballot(cand && rank_l == r);
+	return m ? (uint32_t)__builtin_ctzll(m) : 64u;
+}
+
+// Issue the loads of group g of this streamer's tail candidates (speculative bounds).
+template <int AUX, int SP>
+__device__ __forceinline__ void tail_issue(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
+                                           uint32_t hi_l, bool cand, uint32_t rank_l, uint32_t q,
+                                           uint32_t lane, uint32_t g, tail_grp_t &b, uint32_t (&fr)[TAIL_G])
+{
+#pragma unroll
+	for (int u = 0; u < TAIL_G; u++) {
+		const uint32_t f = cand_frame<SP>(cand, rank_l, q, TAIL_G * g + u);
+		fr[u] = f;
+		const uint32_t lo = f < 64u ? __builtin_amdgcn_readlane(lo_l, f) : 0u;
+		const uint32_t hi = f < 64u ? __builtin_amdgcn_readlane(hi_l, f) : 0u;
+#pragma unroll
+		for (int q = 0; q < TAIL_U; q++) {
+			const uint32_t c = lo + 1024u * q + 16u * lane;
+			b.v[u][q] = load16<AUX>(rs, c < hi ? c : nbytes, nbytes);   // empty slots read out of range: no traffic
+		}
+	}
+}
+
+// Reduce a group over its speculative range [split, off + caplen) into s_spec.
+template <int AUX, int DBG = 0>
+__device__ __forceinline__ void tail_consume(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
+                                             uint32_t hi_l, uint32_t lane, const tail_grp_t &b,
+                                             const uint32_t (&fr)[TAIL_G], uint32_t *s_spec)
+{
+	if constexpr (DBG & 4) {
+		uint32_t x = 0;
+#pragma unroll
+		for (int u = 0; u < TAIL_G; u++)
+#pragma unroll
+			for (int q = 0; q < TAIL_U; q++)
+				x ^= b.v[u][q].x ^ b.v[u][q].y ^ b.v[u][q].z ^ b.v[u][q].w;
+		if (x == 0x9E3779B9u)
+			s_spec[lane] = x;
+		return;
+	}
+#pragma unroll
+	for (int u = 0; u < TAIL_G; u++) {
+		const uint32_t f = fr[u];
+		if (f < 64u) {
+			const uint32_t lo = __builtin_amdgcn_readlane(lo_l, f);
+			const uint32_t hi = __builtin_amdgcn_readlane(hi_l, f);
+			uint32_t acc = 0;
+#pragma unroll
+			for (int q = 0; q < TAIL_U; q++)
+				acc = chunk_sum(b.v[u][q], lo + 1024u * q + 16u * lane, hi, acc);
+			if (hi - lo > 1024u * TAIL_U)
+				acc = tail_rest<AUX>(rs, nbytes, lo, hi, lane, acc);
+			const uint32_t s = wave_sum(acc);
+			if (lane == 0)
+				s_spec[f] = s;
+		}
+	}
+}
+
+// Streamer q of SP sharing a 64-frame subtile: candidates [SP*4g + 4q, +4) of
+// group g, sums into spec[frame].  Groups come in pairs (double buffered);
+// slots past the count are issued anyway (out-of-range loads, no traffic) so
+// the load counts stay static and every wait is a counted vmcnt(N), never a
+// drain.
+template <int SP, int AUX, int DBG = 0>
+__device__ __forceinline__ void tail_streamers(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t lo_l,
+                                               uint32_t hi_l, bool cand, uint64_t cmask, uint32_t rank_l,
+                                               uint32_t q, uint32_t lane, uint32_t *spec)
+{
+	const uint32_t ngrp = (__builtin_popcountll(cmask) + SP * TAIL_G - 1u) / (SP * TAIL_G);
+	tail_grp_t b0, b1;
+	uint32_t f0[TAIL_G], f1[TAIL_G];
+	tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 0, b0, f0);
+	tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 1, b1, f1);
+	if constexpr (SP == 4) {
+		// at most 4 groups (64 candidates / 16 per group): straight-line code
+		tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
+		if (ngrp > 2) {
+			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 2, b0, f0);
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, 3, b1, f1);
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+		} else {
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+		}
+	} else {
+#pragma unroll 1
+		for (uint32_t g = 0; g < ngrp; g += 2) {
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b0, f0, spec);
+			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 2, b0, f0);
+			tail_consume<AUX, DBG>(rs, nbytes, lo_l, hi_l, lane, b1, f1, spec);
+			tail_issue<AUX, SP>(rs, nbytes, lo_l, hi_l, cand, rank_l, q, lane, g + 3, b1, f1);
+		}
+	}
+}
+
+// One tile per workgroup of 5 waves: wave 0 parses the 64 headers while waves
+// 1..4 stream the tails over their SPECULATIVE ranges [split, off + caplen)
+// (known from the descriptors alone), so the header work is off the streaming
+// critical path and the workgroup has a single barrier between loads and
+// records.  (A persistent walk over tiles with the next tile's descriptors
+// prefetched measured slower at every grid cap: per-workgroup concurrency, not
+// launch startup, bounds this kernel; profiles/r01_tune_persistent.log.)
+//
+// H = header waves (64 frames each, TILE = 64 H); S streamer waves follow them,
+// SP = S / H per 64-frame subtile sharing its candidates.  LARGE is H=1, S=4.
+// DBG (diagnostic builds of scripts/probe_shape.hip only; the library uses 0)
+// removes work to time its share: 1 header parse/records, 2 header window
+// loads, 4 streamer sums (the loads stay live through an XOR).
+template <int H, int S, int VAR, int DBG = 0>
+__device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uint32_t tile)
+{
+	constexpr uint32_t TILE = 64u * H;
+	constexpr int SP = S / H;                 // streamers per 64-frame subtile
+	constexpr int AUX = TAIL_AUX(VAR);
+	static_assert(SP >= 1 && S % H == 0, "shape");
+	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
+	__shared__ uint32_t s_spec[TILE];
+	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
+
+	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
+	const uint32_t nbytes = kp.frames_bytes;
+	// subtile of this wave: header wave h -> h; streamer s -> s / SP
+	const uint32_t sub = wave < (uint32_t)H ? wave : (wave - H) / SP;
+
+	// every wave reads its subtile's descriptors (lane = frame)
+	const uint32_t p = tile * TILE + 64u * sub + lane;
+	const bool active = p < kp.n;
+	uint32_t o = 0, cap = 0;
+	if (active) {
+		o = kp.off[p];
+		cap = eff_caplen(o, kp.len[p], nbytes);
+	}
+	// speculative tail bounds from the capture length: [split, off + caplen)
+	const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
+	const uint32_t hi_l = active ? o + cap : 0u;
+	const bool cand = hi_l > lo_l;
+	const uint64_t cmask = __ballot(cand);
+	const uint32_t rank_l = __builtin_amdgcn_mbcnt_hi((uint32_t)(cmask >> 32),
+	                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)cmask, 0u));
+
+	if (wave < (uint32_t)H) {
+		// ---- header wave: parse while the streamers pull the tails.  It fills the
+		// LDS tables itself (no barrier: a wave's LDS accesses are ordered; header
+		// waves write identical words) ----
+		hdr_win_t win;
+		if constexpr (DBG & 2) {
+#pragma unroll
+			for (int i = 0; i < WIN_RAW; i++)
+				win.raw[i] = o + i;
+		} else {
+			hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
+		}
+		{
+			const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
+			const u32x4 a = tg[lane], b = tg[lane + 64];
+			reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
+			reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
+			if (lane <= MOSRX_R_COUNT)
+				s_cnt[lane] = 0;
+		}
+		if constexpr (DBG & 1) {
+			uint32_t x = 0;
+#pragma unroll
+			for (int i = 0; i < WIN_RAW; i++)
+				x ^= win.raw[i];
+			__syncthreads();   // B
+			if (active && (x ^ s_spec[64u * sub + lane]) == 0x9E3779B9u)
+				kp.out[p].rss = x;
+		} else {
+			const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab, kp.tables);
+			__syncthreads();   // B: s_spec ready
+			hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, h.has_tail ? s_spec[64u * sub + lane] : 0u, p, active,
+			              lane, s_cnt);
+		}
+	} else {
+		// ---- streamer waves ----
+		tail_streamers<SP, AUX, DBG>(rs, nbytes, lo_l, hi_l, cand, cmask, rank_l, (wave - H) % SP, lane,
+		                             s_spec + 64u * sub);
+		__syncthreads();   // B
+	}
+	flush_counters(kp, s_cnt, t);
+}
+

@@ -28,18 +28,23 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-from pktlib import ETH_ARP, REF_FIELDS, pack_frames, tcp_frame  # noqa: E402
+from pktlib import ETH_ARP, REF_FIELDS, icmp_frame, pack_frames, tcp_frame  # noqa: E402
 import oracle_py as O  # noqa: E402
 
-STATES = [  # (name, num_msp, num_esp, num_queues, queue_mode)
-    ("msp1", 1, 0, 1, 1),
-    ("noverify", 0, 0, 1, 1),
-    ("esp1", 0, 1, 1, 1),
-    ("q2_i40e", 1, 0, 2, 1),
-    ("q4_i40e", 1, 0, 4, 1),
-    ("q8_i40e", 1, 0, 8, 1),
-    ("q3_ixgbe", 1, 0, 3, 0),
-    ("q8_ixgbe", 1, 0, 8, 0),
+# the netdevs' addresses of the "local" states (netdev_table entries: ICMP to them is "to me")
+LOCAL = ("10.0.0.2", "192.168.1.1", "172.16.9.77")
+STATES = [  # (name, num_msp, num_esp, num_queues, queue_mode, local addresses)
+    ("msp1", 1, 0, 1, 1, ()),
+    ("noverify", 0, 0, 1, 1, ()),
+    ("esp1", 0, 1, 1, 1, ()),
+    ("q2_i40e", 1, 0, 2, 1, ()),
+    ("q4_i40e", 1, 0, 4, 1, ()),
+    ("q8_i40e", 1, 0, 8, 1, ()),
+    ("q3_ixgbe", 1, 0, 3, 0, ()),
+    ("q8_ixgbe", 1, 0, 8, 0, ()),
+    ("msp1_local", 1, 0, 1, 1, LOCAL),
+    ("esp1_local", 0, 1, 4, 1, LOCAL),
+    ("noverify_local", 0, 0, 1, 1, LOCAL),
 ]
 
 
@@ -92,6 +97,20 @@ def edge_frames() -> list[bytes]:
     f.append(tcp_frame(src="0.0.0.0", dst="0.0.0.0", sport=0, dport=0))
     # ip_fast_csum carry-chain corner: header words summing to 0 / 0xFFFF classes
     f.append(tcp_frame(src="255.255.255.255", dst="255.255.255.255", tos=0xFF, ip_id=0xFFFF, ttl=255))
+    # ICMP (ip_in.c:83-85, icmp.c:187-227): to a local address in the *_local states, else not
+    f.append(icmp_frame(dst="10.0.0.2", icmp_type=8, payload=b"echo request"))      # echo request
+    f.append(icmp_frame(dst="192.168.1.1", icmp_type=0))                           # echo reply
+    f.append(icmp_frame(dst="172.16.9.77", icmp_type=3, code=1))                   # dest unreachable
+    f.append(icmp_frame(dst="172.16.9.77", icmp_type=11))                          # time exceeded
+    f.append(icmp_frame(dst="10.0.0.2", icmp_type=42))                             # unsupported type
+    f.append(icmp_frame(dst="10.0.0.2", icmp_type=8, icmp_csum=0xDEAD))            # echo, bad ICMP csum
+    f.append(icmp_frame(dst="10.0.0.2", icmp_type=8, ip_csum=0x1111))              # bad IP csum first
+    f.append(icmp_frame(dst="10.0.0.2", icmp_type=8, ihl=7, payload=b"opts"))      # IP options
+    f.append(icmp_frame(dst="10.0.0.3", icmp_type=8))                              # not local
+    f.append(icmp_frame(src="10.0.0.2", dst="10.9.9.9", icmp_type=8))              # local source only
+    f.append(icmp_frame(dst="192.168.1.1", icmp_type=8, payload=b"", pad_to=60))   # padded minimum
+    f.append(tcp_frame(proto=17, dst="10.0.0.2", payload=b"udp to me"))            # UDP to a local address
+    f.append(tcp_frame(dst="192.168.1.1", payload=b"tcp to me"))                   # TCP to a local address
     return f
 
 
@@ -152,8 +171,8 @@ def random_frames(rng: random.Random, n: int, size_class: int) -> list[bytes]:
 def run_states(frames: list[bytes], name: str, phase: int = 2):
     buf, off, ln = pack_frames(frames, phase=phase)
     res = {}
-    for st, msp, esp, nq, qm in STATES:
-        rec, stats = O.run_ref(buf, off, ln, num_msp=msp, num_esp=esp, num_queues=nq, queue_mode=qm)
+    for st, msp, esp, nq, qm, loc in STATES:
+        rec, stats = O.run_ref(buf, off, ln, num_msp=msp, num_esp=esp, num_queues=nq, queue_mode=qm, local=loc)
         res[st] = rec
         res[st + "_stats"] = np.array([stats["rx_packets"], stats["rx_bytes"], stats["rx_errors"]],
                                       np.uint64)

@@ -29,17 +29,29 @@ MS_KEY = bytes([0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25
 class Params(C.Structure):
     _fields_ = [("num_msp", C.c_uint32), ("num_esp", C.c_uint32), ("forward", C.c_int32),
                 ("num_queues", C.c_int32), ("queue_mode", C.c_int32), ("skip_tcp_csum", C.c_int32),
-                ("rss_key_len", C.c_uint32), ("rss_key", C.c_uint8 * 52)]
+                ("rss_key_len", C.c_uint32), ("rss_key", C.c_uint8 * 52),
+                ("num_local", C.c_uint32), ("local_ip", C.c_uint32 * 16)]
+
+
+TCPINFO_DTYPE = np.dtype([("seq", "<u4"), ("ack_seq", "<u4"), ("window", "<u2"), ("ip_len", "<u2")])
+
+
+def ip_raw(a: str) -> int:
+    """Dotted quad -> the raw u32 mOS stores (network order loaded little-endian)."""
+    return int.from_bytes(bytes(int(x) for x in a.split(".")), "little")
 
 
 def params(num_msp=1, num_esp=0, forward=1, num_queues=1, queue_mode=1, skip_tcp_csum=0,
-           key=b"\x05" * 40) -> Params:
+           key=b"\x05" * 40, local=()) -> Params:
     p = Params()
     p.num_msp, p.num_esp, p.forward = num_msp, num_esp, forward
     p.num_queues, p.queue_mode, p.skip_tcp_csum = num_queues, queue_mode, skip_tcp_csum
     p.rss_key_len = len(key)
     for i, b in enumerate(key):
         p.rss_key[i] = b
+    p.num_local = len(local)
+    for i, a in enumerate(local):
+        p.local_ip[i] = ip_raw(a) if isinstance(a, str) else a
     return p
 
 
@@ -68,6 +80,8 @@ def lib():
         L.mo_classify_mt.argtypes = L.mo_classify.argtypes + [C.c_int]
         L.mo_classify_fh.restype = C.c_int
         L.mo_classify_fh.argtypes = L.mo_classify.argtypes + [C.c_void_p]
+        L.mo_classify_ex.restype = C.c_int
+        L.mo_classify_ex.argtypes = L.mo_classify.argtypes + [C.c_void_p, C.c_void_p]
         L.mo_superfasthash.restype = C.c_uint32
         L.mo_superfasthash.argtypes = [C.c_char_p, C.c_int]
         L.mo_bpf_filter.restype = C.c_uint32
@@ -121,6 +135,22 @@ def classify_fh(buf, off, ln, p: Params | None = None):
     return out, fh
 
 
+def classify_ex(buf, off, ln, p: Params | None = None):
+    """Records + flow hash + pkt_info TCP fields (mosrx_tcpinfo) per frame."""
+    p = p or params()
+    buf = np.ascontiguousarray(buf, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    ln = np.ascontiguousarray(ln, np.uint16)
+    out = np.zeros(len(off), RESULT_DTYPE)
+    fh = np.zeros(len(off), np.uint32)
+    ti = np.zeros(len(off), TCPINFO_DTYPE)
+    rc = lib().mo_classify_ex(C.byref(p), buf.ctypes.data, len(buf), off.ctypes.data, ln.ctypes.data,
+                              len(off), out.ctypes.data, fh.ctypes.data, ti.ctypes.data)
+    if rc:
+        raise OSError(-rc, "mo_classify_ex failed")
+    return out, fh, ti
+
+
 def tx_csum(buf, off, ln, flags: int) -> np.ndarray:
     """A rewritten copy of `buf` (mo_tx_csum: the MOS_UPDATE_*_CHKSUM rewrite)."""
     out = np.array(buf, np.uint8, copy=True)
@@ -134,12 +164,14 @@ def have_ref() -> bool:
     return os.path.exists(REF_BIN)
 
 
-def run_ref(buf, off, ln, *, num_msp=1, num_esp=0, num_queues=1, queue_mode=1):
-    """Run mOS's own compiled rx path (forward=0) over the frames."""
+def run_ref(buf, off, ln, *, num_msp=1, num_esp=0, num_queues=1, queue_mode=1, local=()):
+    """Run mOS's own compiled rx path (forward=0) over the frames.  `local`: the
+    netdev addresses (dotted quads) ICMP frames count as "to me" for."""
     with tempfile.TemporaryDirectory() as d:
         tin, tout = os.path.join(d, "t.in"), os.path.join(d, "t.out")
         write_ref_trace(tin, buf, off, ln, num_msp=num_msp, num_esp=num_esp, forward=0,
-                        num_queues=num_queues, queue_mode=queue_mode)
+                        num_queues=num_queues, queue_mode=queue_mode,
+                        local=[ip_raw(a) if isinstance(a, str) else a for a in local])
         subprocess.run([REF_BIN, tin, tout], check=True, stdout=subprocess.DEVNULL)
         return read_ref_results(tout, len(off))
 

@@ -21,7 +21,8 @@ RESULT_DTYPE = np.dtype([
 assert RESULT_DTYPE.itemsize == 16
 
 R = dict(TCP_OK=0, ARP=1, NON_IPV4=2, IP_SHORT=3, IP_BADVER=4, NOVERIFY_PASS=5, IP_BADCSUM=6,
-         NOT_TCP=7, TCP_SHORT=8, TCP_BADCSUM=9, TRUNCATED=10, TCP_LEN_OK=11)
+         NOT_TCP=7, TCP_SHORT=8, TCP_BADCSUM=9, TRUNCATED=10, TCP_LEN_OK=11, ICMP_LOCAL=12)
+NREASON = len(R)
 
 
 def csum16(data: bytes) -> int:
@@ -68,6 +69,28 @@ def tcp_frame(src="10.0.0.1", dst="10.0.0.2", sport=1234, dport=80, payload=b"",
     return frame
 
 
+def icmp_frame(src="10.0.0.1", dst="10.0.0.2", icmp_type=8, code=0, payload=b"ping", *, ihl=5,
+               ip_csum=None, icmp_csum=None, tot_len=None, pad_to=0) -> bytes:
+    """Build an Ethernet/IPv4/ICMP frame (echo-style header: type, code, check, id, seq)."""
+    ip_opts = b"\x01" * (ihl * 4 - 20 if ihl > 5 else 0)
+    body = struct.pack("!BBHHH", icmp_type, code, 0, 0x1234, 7) + payload
+    if icmp_csum is None:
+        icmp_csum = csum16(body)
+    body = body[:2] + struct.pack("!H", icmp_csum) + body[4:]
+    if tot_len is None:
+        tot_len = 20 + len(ip_opts) + len(body)
+    iph = struct.pack("!BBHHHBBH4s4s", 0x40 | (ihl & 0xF), 0, tot_len & 0xFFFF, 0, 0x4000, 64, 1, 0,
+                      ip4(src), ip4(dst)) + ip_opts
+    if ip_csum is None:
+        ip_csum = csum16(iph)
+    iph = iph[:10] + struct.pack("!H", ip_csum) + iph[12:]
+    eth = b"\x02\x00\x00\x00\x00\x02" + b"\x02\x00\x00\x00\x00\x01" + struct.pack("!H", ETH_IP)
+    frame = eth + iph + body
+    if len(frame) < pad_to:
+        frame += b"\0" * (pad_to - len(frame))
+    return frame
+
+
 def pack_frames(frames: list[bytes], align: int = 16, phase: int = 2, gap: int = 0):
     """Pack frames into one buffer; frame i starts at a multiple of `align` plus `phase`.
 
@@ -88,20 +111,29 @@ def pack_frames(frames: list[bytes], align: int = 16, phase: int = 2, gap: int =
 
 
 def write_ref_trace(path, buf, off, ln, *, num_msp=1, num_esp=0, forward=0, num_queues=1,
-                    queue_mode=1):
-    """Trace file consumed by oracle/_ref/mosref (format in oracle/ref_harness.c)."""
+                    queue_mode=1, local=()):
+    """Trace file consumed by oracle/_ref/mosref (format in oracle/ref_harness.c, version 2:
+    `local` = raw u32 netdev addresses)."""
+    loc = list(local) + [0] * (16 - len(local))
     with open(path, "wb") as fh:
-        fh.write(b"MRXT" + struct.pack("<IIQIIiii", 1, len(off), len(buf), num_msp, num_esp,
+        fh.write(b"MRXT" + struct.pack("<IIQIIiii", 2, len(off), len(buf), num_msp, num_esp,
                                        forward, num_queues, queue_mode))
+        fh.write(struct.pack("<I16I", len(local), *loc))
         fh.write(np.asarray(off, "<u4").tobytes())
         fh.write(np.asarray(ln, "<u2").tobytes())
         fh.write(np.asarray(buf, np.uint8).tobytes())
 
 
 REF_DTYPE = np.dtype([("verdict", "i1"), ("have", "u1"), ("ip_csum", "<u2"), ("tcp_csum", "<u2"),
-                      ("pad", "<u2"), ("rss", "<u4"), ("queue", "<i4"), ("fbucket", "<u4")])
-# fields stored per stack state in the golden fixtures (fbucket = HashFlow bucket, have bit 4)
-REF_FIELDS = ("verdict", "have", "ip_csum", "tcp_csum", "rss", "queue", "fbucket")
+                      ("pad", "<u2"), ("rss", "<u4"), ("queue", "<i4"), ("fbucket", "<u4"),
+                      ("payloadlen", "<u2"), ("payload_off", "<u2"), ("seq", "<u4"), ("ack_seq", "<u4"),
+                      ("window", "<u2"), ("tcp_flags", "u1"), ("ihl_doff", "u1"), ("ip_len", "<u2"),
+                      ("pad2", "<u2")])
+assert REF_DTYPE.itemsize == 40
+# fields stored per stack state in the golden fixtures (fbucket = HashFlow bucket, have bit 4;
+# payloadlen .. ihl_doff = mOS's FillPacketContextTCPInfo output, have bit 5)
+REF_FIELDS = ("verdict", "have", "ip_csum", "tcp_csum", "rss", "queue", "fbucket",
+              "payloadlen", "payload_off", "seq", "ack_seq", "window", "tcp_flags", "ihl_doff", "ip_len")
 
 
 def read_ref_results(path, n):

@@ -34,7 +34,7 @@ def test_every_declared_symbol_is_exported():
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
     assert hasattr(lib, "gpu_module_func")
-    assert mosrx.lib().mosrx_abi_version() == 1
+    assert mosrx.lib().mosrx_abi_version() == 2
 
 
 def test_no_oracle_in_product_library():
@@ -46,9 +46,24 @@ def test_no_oracle_in_product_library():
 
 
 def test_struct_layouts():
-    assert C.sizeof(mosrx.Params) == 80
+    assert C.sizeof(mosrx.Params) == 148          # + num_local, local_ip[16] (ABI 2)
+    assert C.sizeof(mosrx.Params) == C.sizeof(O.Params)
     assert C.sizeof(mosrx.Batch) == 40
     assert mosrx.RESULT_DTYPE.itemsize == 16
+    assert mosrx.TCPINFO_DTYPE.itemsize == 12
+
+
+def test_batch_size_limit():
+    """frames_bytes past MOSRX_MAX_FRAMES_BYTES is refused (-E2BIG) before any device
+    work: the 16-byte-rounded buffer range must stay below the no-load offset."""
+    chk = mosrx.lib().mosrx__check_batch
+    chk.restype, chk.argtypes = C.c_int, [C.POINTER(mosrx.Batch), C.c_int]
+    buf = np.zeros(64, np.uint8)
+    off = np.zeros(1, np.uint32)
+    ln = np.full(1, 60, np.uint16)
+    for fb, rc in [(64, 0), (0xFFFFFFE0, 0), (0xFFFFFFE1, -7), (0xFFFFFFF0, -7), (1 << 32, -7)]:
+        b = mosrx.Batch(buf.ctypes.data, fb, off.ctypes.data, ln.ctypes.data, 1, 60)
+        assert chk(C.byref(b), 0) == rc, hex(fb)
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd") and os.access("/dev/kfd", os.R_OK),
@@ -61,7 +76,7 @@ def test_open_without_gpu_fails_loudly():
 
 def test_param_validation_before_device():
     h = C.c_void_p()
-    for kw in (dict(num_queues=0), dict(num_queues=257), dict(queue_mode=5)):
+    for kw in (dict(num_queues=0), dict(num_queues=257), dict(queue_mode=5), dict(num_local=17)):
         p = mosrx.default_params(**kw)
         assert mosrx.lib().mosrx_open(0, C.byref(p), C.byref(h)) == -22
     p = mosrx.default_params()

@@ -11,8 +11,8 @@ import pytest
 
 import mosrx
 import oracle_py as O
-from pktlib import R, REF_FIELDS, pack_frames, tcp_frame
-from test_oracle_golden import FIXTURES, GOLDEN, STATES, compare_with_ref
+from pktlib import NREASON, R, REF_FIELDS, icmp_frame, pack_frames, tcp_frame
+from test_oracle_golden import FIXTURES, GOLDEN, LOCAL, STATES, compare_with_ref
 
 pytestmark = pytest.mark.gpu
 
@@ -33,31 +33,67 @@ def assert_records_equal(gpu, ora, what=""):
         raise AssertionError(f"{what}: {len(bad)} records differ; first #{i}: gpu={gpu[i]} oracle={ora[i]}")
 
 
-def run_both(ctx, buf, off, ln, p, frames_bytes=None, dev=True, max_len=None):
+def run_both(ctx, buf, off, ln, p, frames_bytes=None, dev=True, max_len=None, side=False):
+    """Records through classify_host and classify_dev against the oracle; with
+    `side`, also the flow hashes and pkt_info TCP fields (classify_*_ex)."""
     ctx.set_params(p)
     fb = len(buf) if frames_bytes is None else frames_bytes
-    ora = O.classify(buf[:fb], off, ln, oparams(p))
+    ora, ofh, oti = O.classify_ex(buf[:fb], off, ln, oparams(p))
     host = ctx.classify_host(buf, off, ln, frames_bytes=fb, max_len=max_len or 0)
     assert_records_equal(host, ora, "classify_host")
+    if side:
+        host, fh, ti = ctx.classify_host_ex(buf, off, ln, frames_bytes=fb, max_len=max_len or 0)
+        assert_records_equal(host, ora, "classify_host_ex")
+        np.testing.assert_array_equal(fh, ofh)
+        np.testing.assert_array_equal(ti, oti)
     if dev:
         db = ctx.upload(buf, off, ln, frames_bytes=fb, max_len=max_len)
         ctx.classify_dev(db)
         assert_records_equal(db.results(), ora, "classify_dev")
+        if side:
+            ctx.classify_dev(db, flow_hash=True, tcpinfo=True)
+            assert_records_equal(db.results(), ora, "classify_dev_ex")
+            np.testing.assert_array_equal(db.flow_hashes(), ofh)
+            np.testing.assert_array_equal(db.tcpinfo(), oti)
         db.free()
     return ora
+
+
+def state_params(state, **kw):
+    msp, esp, nq, qm, loc = STATES[state]
+    return mosrx.default_params(num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm,
+                                local=loc, **kw)
 
 
 @pytest.mark.parametrize("fix", FIXTURES)
 @pytest.mark.parametrize("state", list(STATES))
 def test_golden_fixtures(gpu_ctx, fix, state):
+    """Every record field, the flow hash and pkt_info's TCP fields against mOS's
+    own outputs (ProcessPacket, ip_fast_csum, TCPCalcChecksum, GetRSSHash /
+    GetRSSCPUCore, HashFlow, FillPacketContextTCPInfo) under all 11 stack states."""
     z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
-    msp, esp, nq, qm = STATES[state]
-    p = mosrx.default_params(num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm)
+    p = state_params(state)
     gpu_ctx.set_params(p)
-    out = gpu_ctx.classify_host(z["frames"], z["off"], z["len"])
+    out, fh, ti = gpu_ctx.classify_host_ex(z["frames"], z["off"], z["len"])
     ref = {k: z[f"{state}__{k}"] for k in REF_FIELDS}
-    compare_with_ref(out, ref, p)                                  # against mOS itself
-    assert_records_equal(out, O.classify(z["frames"], z["off"], z["len"], oparams(p)), fix)
+    compare_with_ref(out, ref, p, fh, ti)                          # against mOS itself
+    ora, ofh, oti = O.classify_ex(z["frames"], z["off"], z["len"], oparams(p))
+    assert_records_equal(out, ora, fix)
+    np.testing.assert_array_equal(fh, ofh)
+    np.testing.assert_array_equal(ti, oti)
+    # the device-resident form on the same frames, every shape
+    for v in (mosrx.shape_variant(mosrx.KIND_SMALL), mosrx.shape_variant(mosrx.KIND_S13), 2):
+        gpu_ctx.set_variant(v)
+        try:
+            db = gpu_ctx.upload(z["frames"], z["off"], z["len"])
+            gpu_ctx.classify_dev(db, flow_hash=True, tcpinfo=True)
+            res, dfh, dti = db.results(), db.flow_hashes(), db.tcpinfo()
+            db.free()
+        finally:
+            gpu_ctx.set_variant(2)
+        assert_records_equal(res, ora, f"{fix} dev variant {v}")
+        np.testing.assert_array_equal(dfh, ofh)
+        np.testing.assert_array_equal(dti, oti)
 
 
 @pytest.mark.parametrize("kind,n", [(mosrx.TRACE_FW64, 10_000), (mosrx.TRACE_S64, 32_768),
@@ -167,7 +203,7 @@ def test_counters_match_records(gpu_ctx):
     gpu_ctx.set_params(mosrx.default_params())
     out = gpu_ctx.classify_host(t.frames, t.off, t.len, frames_bytes=t.frames_bytes)
     cnt = gpu_ctx.last_counters()
-    assert cnt.tolist() == np.bincount(out["reason"], minlength=12).tolist()
+    assert cnt.tolist() == np.bincount(out["reason"], minlength=NREASON).tolist()
 
 
 def test_repeatable(gpu_ctx):
@@ -195,7 +231,7 @@ def test_gpu_io_module_rx_loop(pipeline):
     assert st.rx_packets == t.n
     assert st.rx_bytes == int(t.len.astype(np.uint64).sum()) + 24 * t.n
     assert st.rx_errors == int((ora["verdict"] < 0).sum())
-    assert list(st.by_reason) == np.bincount(ora["reason"], minlength=12).tolist()
+    assert list(st.by_reason) == np.bincount(ora["reason"], minlength=NREASON).tolist()
     assert st.batches == (t.n + 4095) // 4096
 
 
@@ -288,12 +324,13 @@ def test_batch_queue_one_launch(gpu_ctx, kind, n, nb):
         d.free()
 
 
-# kernel shapes forced through variant bits 2-6 (value - 1: SMALL, LARGE, MID, L12, L24, L28, S14, S12,
-# S13, S16) with both tail-load cache policies; every shape must be exact on every frame mix
-STREAM_VARIANTS = [((k + 1) << 2) | 2 for k in range(6, 10)]
+# kernel shapes forced through variant bits 2-6 (value - 1: SMALL, S13) with both tail-load
+# cache policies; every shape must be exact on every frame mix
+STREAM_VARIANTS = [mosrx.shape_variant(mosrx.KIND_S13), mosrx.shape_variant(mosrx.KIND_S13, False)]
+ALL_VARIANTS = [2, 0, mosrx.shape_variant(mosrx.KIND_SMALL), mosrx.shape_variant(mosrx.KIND_SMALL, False)] + STREAM_VARIANTS
 
 
-@pytest.mark.parametrize("variant", [2, 6, 10, 14, 18, 22, 26, 0, 8, 12] + STREAM_VARIANTS + [28])
+@pytest.mark.parametrize("variant", ALL_VARIANTS)
 @pytest.mark.parametrize("kind,n", [(mosrx.TRACE_S64, 20_000), (mosrx.TRACE_M1500, 9_000),
                                     (mosrx.TRACE_IMIX, 30_000)])
 def test_forced_kernel_shapes(gpu_ctx, variant, kind, n):
@@ -322,7 +359,7 @@ def test_flow_hash_golden(gpu_ctx, fix):
     np.testing.assert_array_equal(fh, ofh)
 
 
-@pytest.mark.parametrize("variant", [2, 6, 10, 14, 30, 38])
+@pytest.mark.parametrize("variant", ALL_VARIANTS)
 @pytest.mark.parametrize("kind,n", [(mosrx.TRACE_S64, 32_768), (mosrx.TRACE_M1500, 16_384),
                                     (mosrx.TRACE_IMIX, 65_536)])
 def test_flow_hash_device(gpu_ctx, variant, kind, n):
@@ -334,12 +371,20 @@ def test_flow_hash_device(gpu_ctx, variant, kind, n):
         db = gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len)
         gpu_ctx.classify_dev(db, flow_hash=True)
         res, fh = db.results(), db.flow_hashes()
+        gpu_ctx.classify_dev(db, flow_hash=True, tcpinfo=True)
+        res2, fh2, ti = db.results(), db.flow_hashes(), db.tcpinfo()
         db.free()
     finally:
         gpu_ctx.set_variant(2)
-    ora, ofh = O.classify_fh(t.frames[:t.frames_bytes], t.off, t.len, oparams(p))
+    ora, ofh, oti = O.classify_ex(t.frames[:t.frames_bytes], t.off, t.len, oparams(p))
     assert_records_equal(res, ora, "classify_dev_fh")
     np.testing.assert_array_equal(fh, ofh)
+    assert_records_equal(res2, ora, "classify_dev_ex")
+    np.testing.assert_array_equal(fh2, ofh)
+    np.testing.assert_array_equal(ti, oti)
+    # size-independent property: the generator advances seq by the payload per flow and acks 1
+    tcp = ora["payload_off"] != 0
+    assert np.all(ti["ip_len"][tcp] == t.len[tcp] - 14)
     # size-independent property: frames of one flow share a bucket; 5000 flows -> <= 5000 buckets
     assert len(np.unique(fh[ora["payload_off"] != 0] & 0x1FFFF)) <= 5000
 

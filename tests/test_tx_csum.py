@@ -71,7 +71,7 @@ def test_tx_golden(gpu_ctx, fix, flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [6, 10, 14, 18, 22, 26, 30, 34, 38, 42])
+@pytest.mark.parametrize("variant", [mosrx.shape_variant(mosrx.KIND_SMALL), mosrx.shape_variant(mosrx.KIND_S13)])
 @pytest.mark.parametrize("fix", FIXTURES)
 def test_tx_forced_shapes(gpu_ctx, variant, fix):
     z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))

@@ -148,6 +148,8 @@ typedef struct mosrx_ctx mosrx_ctx;
 /* Open a context on HIP device `device`.  Fails with -ENODEV when no GPU or
  * the HIP kernels are unavailable: there is no CPU fallback. */
 int  mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out);
+/* Visible HIP devices (0 without a GPU or runtime). */
+int  mosrx_device_count(void);
 int  mosrx_set_params(mosrx_ctx *c, const mosrx_params *p);
 /* Tuning knob (0..127; results never depend on it): bit 1 = non-temporal tail
  * stream (bit 0, non-temporal header windows, measured slower and folded onto
@@ -213,6 +215,30 @@ int  mosrx_classify_host_ex(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_
 #define MOSRX_NSLOT 2
 int  mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out);
 int  mosrx_classify_host_wait(mosrx_ctx *c, int slot);
+
+/* The same with the pkt_info TCP fields into h_tcpinfo[n] (NULL: none). */
+int  mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out,
+                                   mosrx_tcpinfo *h_tcpinfo);
+
+/* A group of `nb` (1..MOSRX_MAX_GROUP) host batches through ONE kernel launch
+ * on a pipeline slot (the batch queue of mosrx_queue_*, for batches that start
+ * in host memory): the batches' frames and descriptors cross PCIe in as few
+ * copies as their layout allows (batches staged back to back in one pinned
+ * block, or runs lent one after another by a source, go in one), the kernel
+ * classifies all of them, records land in h_out[i] (and pkt_info fields in
+ * h_tcpinfo[i] when h_tcpinfo is not NULL).  Wait with
+ * mosrx_classify_host_wait; the counters are the group's sum.  Amortises the
+ * launch for small batches the way an rx ring of several batches would. */
+#define MOSRX_MAX_GROUP 64
+int  mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                      mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo);
+
+/* Kernel timing on the end-to-end path: with timing on, every submit records
+ * HIP events around its kernel on the slot's stream, and after the wait
+ * mosrx_last_kernel_ms gives that kernel's device time (-ENODATA if the last
+ * waited submit was not timed). */
+int  mosrx_set_timing(mosrx_ctx *c, int on);
+int  mosrx_last_kernel_ms(mosrx_ctx *c, float *ms);
 
 /* Per-reason counters of the last completed end-to-end batch (MOSRX_R_COUNT
  * entries), the NETSTAT rx view of eth_in.c:42-45,80-84. */

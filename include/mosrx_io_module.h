@@ -68,6 +68,10 @@ typedef struct {
 
 #define MOSRX_PKT_RX_RESULTS 0x10   /* argp: const mosrx_result ** (whole batch) */
 #define MOSRX_PKT_RX_MATCH   0x11   /* argp: const uint32_t ** (whole batch's BPF match masks, bit j = program j) */
+#define MOSRX_PKT_RX_TCPINFO 0x12   /* argp: const mosrx_tcpinfo ** (whole batch; cfg.tcpinfo set) */
+#define MOSRX_PKT_SET_PARAMS 0x13   /* argp: const mosrx_params * -- the stack state changed (a monitor
+                                     * socket was created: num_msp++, socket.c:77-78); applies from the
+                                     * next batch received on that netdev */
 #define MOSRX_MAX_DEVICES    16     /* MAX_DEVICES, io_module.h:87 */
 
 extern io_module_func gpu_module_func;
@@ -81,8 +85,25 @@ mosrx_source *mosrx_source_mem(const uint8_t *frames, const uint32_t *off, const
 /* Classic libpcap file (magic a1b2c3d4 / d4c3b2a1, usec or nsec), LINKTYPE_ETHERNET.
  * Native reader: libpcap is absent (pcap_module.c:13). */
 mosrx_source *mosrx_source_pcap(const char *path, uint32_t loops);
-/* AF_PACKET raw socket on an interface (e.g. "lo"); needs CAP_NET_RAW. */
+/* AF_PACKET raw socket on an interface (e.g. "lo") with a TPACKET_V3 PACKET_MMAP
+ * receive ring; needs CAP_NET_RAW.  Frames the host sends (PACKET_OUTGOING) are
+ * not received, as with libpcap's default direction.  When the ring can be
+ * registered with the HIP runtime, batches are lent zero-copy to the backend. */
 mosrx_source *mosrx_source_afpacket(const char *ifname);
+typedef struct mosrx_afpacket_opts {
+	uint32_t ring_blocks;    /* 4 MiB ring blocks (default 8, at most 64) */
+	uint32_t retire_ms;      /* a partly filled block is handed over after this long (default 1) */
+	uint32_t fanout_group;   /* != 0: join this PACKET_FANOUT_HASH group (one socket per mTCP
+	                          * thread; flows split by hash, as RSS splits them over NIC queues) */
+	int32_t  copy;           /* 1: never lend the ring (frames are copied into the stage) */
+} mosrx_afpacket_opts;
+mosrx_source *mosrx_source_afpacket_ex(const char *ifname, const mosrx_afpacket_opts *opts);
+typedef struct mosrx_afpacket_info {
+	int32_t  zero_copy;        /* the ring is registered: batches are lent, not copied */
+	uint64_t ring_bytes;
+	uint64_t dropped_outgoing; /* outgoing frames skipped (kernels without PACKET_IGNORE_OUTGOING) */
+} mosrx_afpacket_info;
+int           mosrx_source_afpacket_info(const mosrx_source *s, mosrx_afpacket_info *info);
 /* Pull the next frame into dst (at most cap bytes); returns its caplen, 0 when none. */
 int           mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap);
 /* How gpu_module_func takes batches from an in-memory source: 0 = best (the
@@ -91,6 +112,16 @@ int           mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap);
  * does).  Results never depend on it.  0 or -EINVAL (not a memory source). */
 int           mosrx_source_mem_set_mode(mosrx_source *s, int mode);
 void          mosrx_source_close(mosrx_source *s);
+
+/* Transmit one frame through the source (pcap_inject, pcap_module.c:67-79): the
+ * AF_PACKET socket; -EOPNOTSUPP for sources that cannot send (a trace file)
+ * unless a TX dump is set.  0 or -errno. */
+int           mosrx_source_send(mosrx_source *s, const uint8_t *frame, uint32_t len);
+/* Divert the source's transmit into a classic pcap file (path NULL: back to
+ * the native transmit).  Works for every source. */
+int           mosrx_source_tx_pcap(mosrx_source *s, const char *path);
+int           mosrx_source_tx_flush(mosrx_source *s);
+int           mosrx_source_tx_stats(const mosrx_source *s, uint64_t *packets, uint64_t *bytes, uint64_t *errors);
 
 /* ---- backend configuration (before load_module_upper_half) ---- */
 typedef struct mosrx_gpu_module_cfg {
@@ -105,13 +136,38 @@ typedef struct mosrx_gpu_module_cfg {
 	mosrx_params  params;                           /* stack state (num_msp, forward, key, ...) */
 	const mosrx_bpf_prog *bpf_progs;                /* monitor filters (SET_BPFFILTER output), evaluated in the */
 	uint32_t      bpf_nprog;                        /*   classify pass; kept by the caller until init_handle */
+	uint32_t      tx_batch;                         /* frames get_wptr buffers per netdev before send_pkts
+	                                                 * flushes them (default 64, MAX_PKT_BURST of dpdk_module.c:61) */
+	int32_t       tcpinfo;                          /* 1: also compute pkt_info's TCP fields per batch
+	                                                 * (dev_ioctl(MOSRX_PKT_RX_TCPINFO)) */
+	uint32_t      group;                            /* batches received per kernel launch (1..MOSRX_MAX_GROUP,
+	                                                 * default 1): a group is classified by one launch and
+	                                                 * handed out one batch per recv_pkts; needs bpf_nprog 0 */
 } mosrx_gpu_module_cfg;
 
 void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg);
 int  mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg);
+/* The configuration in effect (after load_module_upper_half took mOS's own
+ * state into it, when built inside mOS). */
+int  mosrx_gpu_module_get_cfg(mosrx_gpu_module_cfg *cfg);
 /* Bind a thread context pointer to a cpu index before init_handle (standalone use;
  * inside mOS the module reads nothing from ctx and uses the registration order). */
 int  mosrx_gpu_module_bind(struct mtcp_thread_context *ctx, int cpu);
+/* Give mTCP thread `cpu` its own source for netdev `ifidx` (e.g. one
+ * PACKET_FANOUT_HASH socket per thread), instead of cfg.src[ifidx]. */
+int  mosrx_gpu_module_bind_source(int cpu, int ifidx, mosrx_source *src);
+/* The GPU mTCP thread `cpu` runs on: gpu_base + cpu % ngpu (ngpu 0: all visible
+ * devices, `ndev`), the per-core sharding of SURVEY.md §8e.  -EINVAL if none. */
+int  mosrx_gpu_module_device_of(int cpu, int ndev);
+/* Frames a context sent, received and dropped on TX (per netdev summed). */
+typedef struct mosrx_gpu_module_stats {
+	uint64_t rx_batches, rx_frames, tx_packets, tx_bytes, tx_errors;
+	uint64_t kernel_launches;   /* timed launches (mosrx_set_timing on the thread's contexts) */
+	double   kernel_ms;         /* their summed device time (HIP events around each kernel) */
+} mosrx_gpu_module_stats;
+/* Time every kernel this thread's contexts launch (for the stats above). */
+int  mosrx_gpu_module_set_timing(struct mtcp_thread_context *ctx, int on);
+int  mosrx_gpu_module_stats_of(struct mtcp_thread_context *ctx, mosrx_gpu_module_stats *st);
 
 /* ---- RunMainLoop-shaped driver (core.c:897-909) ---- */
 typedef struct mosrx_rx_stats {
@@ -129,6 +185,33 @@ typedef void (*mosrx_pkt_fn)(void *arg, int ifidx, int index, const uint8_t *pkt
  * source is exhausted (recv_pkts == 0 on all netdevs for a whole round). */
 int mosrx_rx_loop(const io_module_func *iom, struct mtcp_thread_context *ctx, int nif,
                   uint64_t max_pkts, mosrx_pkt_fn fn, void *arg, mosrx_rx_stats *st);
+
+/* The same loop for live sources: a round that receives nothing sleeps
+ * `idle_us` and the loop ends after `idle_rounds` such rounds in a row (0:
+ * only at max_pkts / max_us), or after `max_us` microseconds (0: no limit).
+ * Every round ends with send_pkts on each netdev (core.c:999-1007), so frames
+ * a consumer wrote with get_wptr leave in the same round. */
+typedef struct mosrx_rx_loop_opts {
+	uint64_t max_pkts;
+	uint32_t idle_rounds;
+	uint32_t idle_us;
+	uint64_t max_us;
+} mosrx_rx_loop_opts;
+int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx, int nif,
+                     const mosrx_rx_loop_opts *opts, mosrx_pkt_fn fn, void *arg, mosrx_rx_stats *st);
+
+/* A consumer for mosrx_rx_loop*: ForwardEthernetFrame (eth_out.c:105-129) for
+ * every frame the checks accepted (verdict 1) -- out_if[in_ifidx] from the
+ * nic_forward_table, get_wptr, copy; -1 in out_if drops.  `arg` points at a
+ * mosrx_forwarder.  The round's send_pkts sends what it wrote. */
+typedef struct mosrx_forwarder {
+	const io_module_func *iom;
+	struct mtcp_thread_context *ctx;
+	int32_t out_if[MOSRX_MAX_DEVICES];
+	uint64_t forwarded, dropped;
+} mosrx_forwarder;
+void mosrx_forward_frame(void *arg, int ifidx, int index, const uint8_t *pkt, uint16_t len,
+                         const mosrx_result *res);
 
 #ifdef __cplusplus
 }

@@ -2,17 +2,29 @@
  * gpu_module.c — `gpu_module_func`, an io_module_func backend (io_module.h:63-78)
  * that receives frames from a raw-socket / loopback source into pinned
  * staging and classifies each batch on the GPU before the rx loop sees it.
+ * It is the peer of pcap_module_func (pcap_module.c:162-177): frames come in
+ * through recv_pkts / get_rptr and go out through get_wptr / send_pkts.
  *
- * recv_pkts (core.c:899) pulls up to `batch` frames into pinned memory, runs
- * H2D -> classify kernel -> D2H (mosrx_classify_host_*), and returns the
- * count; get_rptr (core.c:905) hands out the staged frames; the per-frame
- * verdicts are read through dev_ioctl(MOSRX_PKT_RX_RESULTS) or per packet
- * through dev_ioctl(PKT_RX_RSS) (dpdk_module.c:568-571).  With `pipeline` set,
- * batch k+1 is received and classified while the application consumes batch
- * k, keeping the reference's pointer lifetime (valid until the next recv_pkts).
- * A source that holds its frames in pinned memory lends a run of them as the
- * batch (mosrx_source.h `borrow`, no host copy); one that can copy a run at
- * once fills the stage in runs (`fill`); any other is read frame by frame.
+ * recv_pkts (core.c:899) hands out the next classified batch; get_rptr
+ * (core.c:905) the staged frames; the per-frame verdicts are read through
+ * dev_ioctl(MOSRX_PKT_RX_RESULTS) or per packet through dev_ioctl(PKT_RX_RSS)
+ * (dpdk_module.c:568-571).  Batches are received in groups of `group`
+ * (cfg.group, default 1): a group's batches are staged back to back in one
+ * pinned block and classified by ONE kernel launch (the batch queue), then
+ * handed out one per recv_pkts, so small batches do not pay a launch each.
+ * With `pipeline` set, the next group is received and classified while the
+ * application consumes the current one, keeping the reference's pointer
+ * lifetime (valid until the next recv_pkts).  A source that holds its frames
+ * in pinned memory lends a run of them as the batch (mosrx_source.h `borrow`,
+ * no host copy; the run goes back with `give_back` when its group is
+ * recycled); one that can copy a run at once fills the stage in runs (`fill`);
+ * any other is read frame by frame.
+ *
+ * TX: get_wptr (eth_out.c:80-84, :118-123) returns a slot of the netdev's TX
+ * buffer; send_pkts (core.c:1004-1006) hands every buffered frame to the
+ * netdev's source (AF_PACKET send = pcap_inject, or a pcap dump), as
+ * pcap_send_pkts does (pcap_module.c:67-79); a full buffer is flushed by the
+ * next get_wptr, like dpdk_get_wptr.
  *
  * Threading follows mOS: one context per mTCP thread, every call for a context
  * from that thread (core.c:1282-1349), so the module takes no locks on the fast
@@ -28,46 +40,63 @@
 
 #include "../../include/mosrx_io_module.h"
 #include "mosrx_source.h"
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+#include "config.h"    /* g_config, num_queues (config.h:160-170) */
+#endif
 
 #define MAX_THREADS 64
 #define TX_FRAME_LEN 2048    /* ETHERNET_FRAME_LEN (mtcp.h:64-68) */
 
-/* One pinned block per stage, descriptors first: off[batch] | len[batch] | frames.
- * A full batch is then one contiguous span and crosses PCIe in one copy
- * (mosrx_api.c batch_span). */
+/* One stage = one batch: off[batch] | len[batch] | frames, inside its group's
+ * pinned block.  A group's stages are packed back to back, so a whole group is
+ * (nearly) one contiguous span and crosses PCIe in one copy. */
 struct stage {
-	uint8_t *blk;             /* pinned block holding off, len and frames */
-	uint8_t *own;             /* the block's frame area */
-	uint8_t *frames;          /* this batch's frames: own, or a run borrowed from the source */
+	uint8_t *frames;          /* this batch's frames: in the group block, or a run borrowed from the source */
 	uint32_t *off;
 	uint16_t *len;
-	mosrx_result *res;        /* pinned */
+	mosrx_result *res;        /* pinned, in the group's record array */
+	mosrx_tcpinfo *ti;        /* pinned, pkt_info TCP fields (cfg.tcpinfo) */
 	uint32_t *match;          /* pinned, BPF match masks (monitor filters configured) */
-	uint64_t cap_bytes;
-	uint32_t n;
+	uint32_t n, max_len;
 	uint64_t bytes;
+	int borrowed;             /* frames lent by the source: give them back when the group is recycled */
+};
+
+struct group {
+	uint8_t *blk;             /* pinned block the group's stages are packed into */
+	uint64_t blk_bytes;
+	mosrx_result *res;        /* pinned, group * batch records */
+	mosrx_tcpinfo *ti;
+	uint32_t *match;
+	struct stage *st;         /* `group` stages */
+	uint32_t nst;             /* stages filled */
 };
 
 struct if_state {
 	mosrx_ctx *mc;
-	struct stage st[MOSRX_NSLOT];
-	int cur;                  /* stage exposed to the application, -1 none */
-	int inflight;             /* stage being classified, -1 none */
+	mosrx_source *src;
+	struct group g[MOSRX_NSLOT];
+	int cur;                  /* group exposed to the application, -1 none */
+	uint32_t cur_idx;         /* its batch exposed now */
+	int inflight;             /* group being classified, -1 none */
+	/* TX: frames written through get_wptr, sent by send_pkts */
+	uint8_t *tx_buf;          /* tx_cap x TX_FRAME_LEN */
+	uint16_t *tx_len;
+	uint32_t tx_n;
 };
 
 struct gpu_priv {
 	struct mtcp_thread_context *ctx;
 	int cpu;
 	struct if_state ifs[MOSRX_MAX_DEVICES];
-	uint8_t tx_buf[MOSRX_MAX_DEVICES][TX_FRAME_LEN];
-	uint32_t tx_pending[MOSRX_MAX_DEVICES];
-	uint64_t tx_packets, tx_bytes;
+	mosrx_gpu_module_stats stats;
 };
 
 static mosrx_gpu_module_cfg g_cfg;
 static int g_configured;
 static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
 static struct { struct mtcp_thread_context *ctx; int cpu; struct gpu_priv *priv; } g_tab[MAX_THREADS];
+static mosrx_source *g_src_cpu[MAX_THREADS][MOSRX_MAX_DEVICES];
 static int g_next_cpu;
 
 void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg)
@@ -78,17 +107,32 @@ void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg)
 	cfg->gpu_base = 0;
 	cfg->ngpu = 0;
 	cfg->pipeline = 1;
+	cfg->tx_batch = 64;
+	cfg->group = 1;
 	mosrx_params_default(&cfg->params);
 }
 
 int mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg)
 {
 	if (!cfg || cfg->num_ifs == 0 || cfg->num_ifs > MOSRX_MAX_DEVICES || cfg->batch == 0 ||
-	    cfg->max_frame < 64 || cfg->max_frame > 65535)
+	    cfg->max_frame < 64 || cfg->max_frame > 65535 || cfg->group < 1 || cfg->group > MOSRX_MAX_GROUP ||
+	    (cfg->bpf_nprog && cfg->group > 1) || cfg->params.num_local > MOSRX_MAX_LOCAL)
 		return -EINVAL;
 	pthread_mutex_lock(&g_lock);
 	g_cfg = *cfg;
+	if (!g_cfg.tx_batch)
+		g_cfg.tx_batch = 64;
 	g_configured = 1;
+	pthread_mutex_unlock(&g_lock);
+	return 0;
+}
+
+int mosrx_gpu_module_get_cfg(mosrx_gpu_module_cfg *cfg)
+{
+	if (!cfg || !g_configured)
+		return -EINVAL;
+	pthread_mutex_lock(&g_lock);
+	*cfg = g_cfg;
 	pthread_mutex_unlock(&g_lock);
 	return 0;
 }
@@ -108,6 +152,27 @@ int mosrx_gpu_module_bind(struct mtcp_thread_context *ctx, int cpu)
 	return rc;
 }
 
+int mosrx_gpu_module_bind_source(int cpu, int ifidx, mosrx_source *src)
+{
+	if (cpu < 0 || cpu >= MAX_THREADS || ifidx < 0 || ifidx >= MOSRX_MAX_DEVICES)
+		return -EINVAL;
+	pthread_mutex_lock(&g_lock);
+	g_src_cpu[cpu][ifidx] = src;
+	pthread_mutex_unlock(&g_lock);
+	return 0;
+}
+
+/* Per-core sharding: thread `cpu` drives GPU gpu_base + cpu % ngpu. */
+int mosrx_gpu_module_device_of(int cpu, int ndev)
+{
+	const int ngpu = g_cfg.ngpu > 0 ? g_cfg.ngpu : ndev - g_cfg.gpu_base;
+	int dev;
+	if (cpu < 0 || ngpu <= 0)
+		return -EINVAL;
+	dev = g_cfg.gpu_base + cpu % ngpu;
+	return dev < ndev ? dev : -EINVAL;
+}
+
 static struct gpu_priv *priv_of(struct mtcp_thread_context *ctx)
 {
 	int i;
@@ -117,20 +182,76 @@ static struct gpu_priv *priv_of(struct mtcp_thread_context *ctx)
 	return NULL;
 }
 
+int mosrx_gpu_module_set_timing(struct mtcp_thread_context *ctx, int on)
+{
+	struct gpu_priv *pv = priv_of(ctx);
+	uint32_t i;
+	if (!pv)
+		return -EINVAL;
+	for (i = 0; i < g_cfg.num_ifs; i++)
+		if (pv->ifs[i].mc)
+			mosrx_set_timing(pv->ifs[i].mc, on);
+	return 0;
+}
+
+int mosrx_gpu_module_stats_of(struct mtcp_thread_context *ctx, mosrx_gpu_module_stats *st)
+{
+	struct gpu_priv *pv = priv_of(ctx);
+	if (!pv || !st)
+		return -EINVAL;
+	*st = pv->stats;
+	return 0;
+}
+
 static void gpu_load_module_upper_half(void)
 {
 	if (!g_configured) {
 		fprintf(stderr, "[mosrx] gpu_module: mosrx_gpu_module_configure() not called\n");
 		exit(EXIT_FAILURE);   /* fatal init error, as pcap_module.c:141-155 */
 	}
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+	{
+		/* the stack state the verdicts depend on, from mOS's own configuration:
+		 * forward (eth_in.c:22) and the netdevs' addresses (icmp.c:193-200) */
+		int i;
+		g_cfg.params.forward = g_config.mos->forward;
+		if (!g_cfg.params.num_local)
+			for (i = 0; i < g_config.mos->netdev_table->num && i < MOSRX_MAX_LOCAL; i++)
+				g_cfg.params.local_ip[g_cfg.params.num_local++] = g_config.mos->netdev_table->ent[i]->ip_addr;
+	}
+	/* GetRSSCPUCore's queue count (util.c:114-131, api.c:1056): every backend
+	 * sets it (pcap_module.c:159, dpdk_module.c:704, :800) */
+	num_queues = g_cfg.params.num_queues;
+#endif
 }
 
-static void stage_free(mosrx_ctx *mc, struct stage *s)
+static void group_free(mosrx_ctx *mc, struct group *g)
 {
-	if (s->blk) mosrx_host_free(mc, s->blk);
-	if (s->res) mosrx_host_free(mc, s->res);
-	if (s->match) mosrx_host_free(mc, s->match);
-	memset(s, 0, sizeof(*s));
+	if (g->blk) mosrx_host_free(mc, g->blk);
+	if (g->res) mosrx_host_free(mc, g->res);
+	if (g->ti) mosrx_host_free(mc, g->ti);
+	if (g->match) mosrx_host_free(mc, g->match);
+	free(g->st);
+	memset(g, 0, sizeof(*g));
+}
+
+static uint64_t stage_bytes(void)
+{
+	const uint64_t dsc = ((uint64_t)g_cfg.batch * 6 + 15) & ~15ull;
+	return dsc + (uint64_t)g_cfg.batch * ((g_cfg.max_frame + 15u + 16u) & ~15u) + 512;
+}
+
+static int group_alloc(mosrx_ctx *mc, struct group *g)
+{
+	const size_t nrec = (size_t)g_cfg.batch * g_cfg.group;
+	g->blk_bytes = stage_bytes() * g_cfg.group;
+	g->st = calloc(g_cfg.group, sizeof(*g->st));
+	if (!g->st || mosrx_host_alloc(mc, g->blk_bytes, (void **)&g->blk) ||
+	    mosrx_host_alloc(mc, nrec * sizeof(mosrx_result), (void **)&g->res) ||
+	    (g_cfg.tcpinfo && mosrx_host_alloc(mc, nrec * sizeof(mosrx_tcpinfo), (void **)&g->ti)) ||
+	    (g_cfg.bpf_nprog && mosrx_host_alloc(mc, nrec * 4, (void **)&g->match)))
+		return -ENOMEM;
+	return 0;
 }
 
 static void gpu_destroy_handle(struct mtcp_thread_context *ctx);
@@ -138,7 +259,7 @@ static void gpu_destroy_handle(struct mtcp_thread_context *ctx);
 static void gpu_init_handle(struct mtcp_thread_context *ctx)
 {
 	struct gpu_priv *pv;
-	int i, k, cpu = -1, ngpu, slot = -1;
+	int i, k, cpu = -1, slot = -1, ndev = 0;
 
 	pthread_mutex_lock(&g_lock);
 	for (i = 0; i < MAX_THREADS; i++) {
@@ -156,131 +277,213 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 		exit(EXIT_FAILURE);
 	pv->ctx = ctx;
 	pv->cpu = cpu;
-	ngpu = g_cfg.ngpu;
+	ndev = mosrx_device_count();
 	for (i = 0; i < (int)g_cfg.num_ifs; i++) {
 		struct if_state *is = &pv->ifs[i];
-		int dev = g_cfg.gpu_base + (ngpu > 0 ? cpu % ngpu : cpu);
-		int rc = mosrx_open(dev, &g_cfg.params, &is->mc);
-		if (rc && ngpu <= 0)
-			rc = mosrx_open(g_cfg.gpu_base, &g_cfg.params, &is->mc);
+		int dev = mosrx_gpu_module_device_of(cpu, ndev);
+		int rc = dev < 0 ? -ENODEV : mosrx_open(dev, &g_cfg.params, &is->mc);
 		if (rc) {
 			fprintf(stderr, "[mosrx] gpu_module: mosrx_open(%d): %s\n", dev, mosrx_strerror(rc));
 			exit(EXIT_FAILURE);
 		}
+		is->src = (cpu < MAX_THREADS && g_src_cpu[cpu][i]) ? g_src_cpu[cpu][i] : g_cfg.src[i];
 		is->cur = is->inflight = -1;
 		if (g_cfg.bpf_nprog && (rc = mosrx_bpf_set(is->mc, g_cfg.bpf_progs, g_cfg.bpf_nprog))) {
 			fprintf(stderr, "[mosrx] gpu_module: mosrx_bpf_set: %s\n", mosrx_strerror(rc));
 			exit(EXIT_FAILURE);
 		}
-		for (k = 0; k < MOSRX_NSLOT; k++) {
-			struct stage *s = &is->st[k];
-			const uint64_t dsc = ((uint64_t)g_cfg.batch * 6 + 15) & ~15ull;
-			s->cap_bytes = (uint64_t)g_cfg.batch * ((g_cfg.max_frame + 15u + 16u) & ~15u) + 64;
-			if (mosrx_host_alloc(is->mc, dsc + s->cap_bytes, (void **)&s->blk) ||
-			    mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * sizeof(mosrx_result), (void **)&s->res) ||
-			    (g_cfg.bpf_nprog && mosrx_host_alloc(is->mc, (size_t)g_cfg.batch * 4, (void **)&s->match))) {
+		for (k = 0; k < MOSRX_NSLOT; k++)
+			if (group_alloc(is->mc, &is->g[k])) {
 				fprintf(stderr, "[mosrx] gpu_module: pinned staging allocation failed\n");
 				exit(EXIT_FAILURE);
 			}
-			s->off = (uint32_t *)s->blk;
-			s->len = (uint16_t *)(s->blk + (size_t)g_cfg.batch * 4);
-			s->own = s->frames = s->blk + dsc;
-		}
+		is->tx_buf = malloc((size_t)g_cfg.tx_batch * TX_FRAME_LEN);
+		is->tx_len = calloc(g_cfg.tx_batch, sizeof(uint16_t));
+		if (!is->tx_buf || !is->tx_len)
+			exit(EXIT_FAILURE);
 	}
+	pthread_mutex_lock(&g_lock);
 	g_tab[slot].priv = pv;
+	pthread_mutex_unlock(&g_lock);
 }
 
-/* Receive up to `batch` frames from the netdev's source into stage s. */
-static void stage_fill(struct stage *s, mosrx_source *src)
+/* Receive up to `batch` frames from the netdev's source into stage s, whose
+ * descriptors start at *pos in the group block (advanced past what it used). */
+static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint64_t *pos)
 {
-	uint64_t pos = 2;
-	uint32_t i = 0;
 	const uint32_t mf = g_cfg.max_frame;
-	s->frames = s->own;
-	if (src && src->borrow) {     /* zero-copy: the source's pinned run is the batch */
+	uint64_t at = (*pos + 255) & ~255ull, fpos = 2, cap;
+	uint32_t i = 0, m = 0;
+	s->off = (uint32_t *)(g->blk + at);
+	s->len = (uint16_t *)(g->blk + at + (size_t)g_cfg.batch * 4);
+	at += ((uint64_t)g_cfg.batch * 6 + 15) & ~15ull;
+	s->frames = g->blk + at;
+	cap = g->blk_bytes - at;
+	s->borrowed = 0;
+	s->n = 0;
+	if (src && src->borrow) {         /* zero-copy: the source's pinned run is the batch */
 		const uint8_t *f = NULL;
 		uint64_t fb = 0;
 		s->n = src->borrow(src, g_cfg.batch, mf, &f, &fb, s->off, s->len);
 		if (s->n) {
 			s->frames = (uint8_t *)f;
 			s->bytes = fb;
+			s->borrowed = 1;
 		} else {
 			s->bytes = 2;
 		}
-		return;
+		fpos = 0;
+	} else if (src && src->fill) {
+		s->n = src->fill(src, s->frames, cap, s->off, s->len, g_cfg.batch, mf, &s->bytes);
+		fpos = s->bytes;
+	} else {
+		while (i < g_cfg.batch && src && fpos + mf + 16 <= cap) {
+			int l = src->next(src, s->frames + fpos, mf);
+			if (l <= 0)
+				break;
+			s->off[i] = (uint32_t)fpos;
+			s->len[i] = (uint16_t)l;
+			i++;
+			fpos = ((fpos + (uint64_t)l - 2 + 15) & ~15ull) + 2;   /* next frame at 16 B + 2 */
+		}
+		s->n = i;
+		s->bytes = fpos;
 	}
-	if (src && src->fill) {
-		s->n = src->fill(src, s->frames, s->cap_bytes, s->off, s->len, g_cfg.batch, mf, &s->bytes);
-		return;
-	}
-	while (i < g_cfg.batch && src && pos + mf + 16 <= s->cap_bytes) {
-		int l = src->next(src, s->frames + pos, mf);
-		if (l <= 0)
-			break;
-		s->off[i] = (uint32_t)pos;
-		s->len[i] = (uint16_t)l;
-		i++;
-		pos = ((pos + (uint64_t)l - 2 + 15) & ~15ull) + 2;   /* next frame at 16 B + 2 */
-	}
-	s->n = i;
-	s->bytes = pos;
+	for (i = 0; i < s->n; i++)        /* the batch's real largest frame picks the kernel shape */
+		m = s->len[i] > m ? s->len[i] : m;
+	s->max_len = m;
+	*pos = at + fpos;
 }
 
-static int stage_submit(struct if_state *is, int k)
+/* Receive a group: up to `group` batches, stopping early when the source runs dry. */
+static void group_fill(struct group *g, mosrx_source *src)
 {
-	struct stage *s = &is->st[k];
-	mosrx_batch b;
-	b.frames = s->frames;
-	b.frames_bytes = s->bytes;
-	b.off = s->off;
-	b.len = s->len;
-	b.n = s->n;
-	b.max_len = g_cfg.max_frame;
+	uint64_t pos = 0;
+	uint32_t i;
+	g->nst = 0;
+	for (i = 0; i < g_cfg.group; i++) {
+		struct stage *s = &g->st[i];
+		if (pos + stage_bytes() > g->blk_bytes)
+			break;
+		stage_fill(g, s, src, &pos);
+		s->res = g->res + (size_t)i * g_cfg.batch;
+		s->ti = g->ti ? g->ti + (size_t)i * g_cfg.batch : NULL;
+		s->match = g->match ? g->match + (size_t)i * g_cfg.batch : NULL;
+		if (!s->n)
+			break;
+		g->nst++;
+		if (s->n < g_cfg.batch)
+			break;
+	}
+}
+
+/* Hand the group's borrowed runs back to the source (they are no longer exposed). */
+static void group_recycle(struct group *g, mosrx_source *src)
+{
+	uint32_t i;
+	for (i = 0; i < g->nst; i++)
+		if (g->st[i].borrowed && src && src->give_back)
+			src->give_back(src);
+	g->nst = 0;
+}
+
+static int group_submit(struct if_state *is, int k)
+{
+	struct group *g = &is->g[k];
+	mosrx_batch b[MOSRX_MAX_GROUP];
+	mosrx_result *out[MOSRX_MAX_GROUP];
+	mosrx_tcpinfo *ti[MOSRX_MAX_GROUP];
+	uint32_t i;
+	for (i = 0; i < g->nst; i++) {
+		const struct stage *s = &g->st[i];
+		b[i].frames = s->frames;
+		b[i].frames_bytes = s->bytes;
+		b[i].off = s->off;
+		b[i].len = s->len;
+		b[i].n = s->n;
+		b[i].max_len = s->max_len;
+		out[i] = s->res;
+		ti[i] = s->ti;
+	}
 	if (g_cfg.bpf_nprog)
-		return mosrx_classify_bpf_host_submit(is->mc, k, &b, s->res, s->match);
-	return mosrx_classify_host_submit(is->mc, k, &b, s->res);
+		return mosrx_classify_bpf_host_submit(is->mc, k, &b[0], g->st[0].res, g->st[0].match);
+	if (g_cfg.group == 1)
+		return mosrx_classify_host_submit_ex(is->mc, k, &b[0], g->st[0].res, g->st[0].ti);
+	return mosrx_classify_host_group_submit(is->mc, k, b, g->nst, out, g_cfg.tcpinfo ? ti : NULL);
+}
+
+static int group_wait(struct gpu_priv *pv, struct if_state *is, int k)
+{
+	float ms;
+	uint32_t i;
+	if (mosrx_classify_host_wait(is->mc, k))
+		return -1;
+	pv->stats.rx_batches += is->g[k].nst;
+	for (i = 0; i < is->g[k].nst; i++)
+		pv->stats.rx_frames += is->g[k].st[i].n;
+	if (mosrx_last_kernel_ms(is->mc, &ms) == 0) {
+		pv->stats.kernel_ms += ms;
+		pv->stats.kernel_launches++;
+	}
+	return 0;
 }
 
 static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 {
 	struct gpu_priv *pv = priv_of(ctx);
 	struct if_state *is;
-	mosrx_source *src;
 	int k;
 
 	if (!pv || ifidx < 0 || ifidx >= (int)g_cfg.num_ifs)
 		return -1;
 	is = &pv->ifs[ifidx];
-	src = g_cfg.src[ifidx];
+	/* the next batch of the group already classified */
+	if (is->cur >= 0 && is->cur_idx + 1 < is->g[is->cur].nst) {
+		is->cur_idx++;
+		return (int32_t)is->g[is->cur].st[is->cur_idx].n;
+	}
+	/* the exposed group is done with (get_rptr pointers expire here) */
+	if (is->cur >= 0)
+		group_recycle(&is->g[is->cur], is->src);
 	if (is->inflight < 0) {           /* nothing in flight: receive + classify now */
 		k = is->cur < 0 ? 0 : is->cur ^ 1;
-		stage_fill(&is->st[k], src);
-		if (stage_submit(is, k))
+		group_fill(&is->g[k], is->src);
+		if (!is->g[k].nst) {
+			is->cur = -1;
+			return 0;
+		}
+		if (group_submit(is, k))
 			return -1;
 		is->inflight = k;
 	}
 	k = is->inflight;
-	if (mosrx_classify_host_wait(is->mc, k))
+	if (group_wait(pv, is, k))
 		return -1;
 	is->cur = k;
+	is->cur_idx = 0;
 	is->inflight = -1;
-	if (g_cfg.pipeline && is->st[k].n) {   /* classify the next batch behind the app's work */
+	if (g_cfg.pipeline) {             /* classify the next group behind the app's work */
 		int nk = k ^ 1;
-		stage_fill(&is->st[nk], src);
-		if (is->st[nk].n && stage_submit(is, nk) == 0)
+		group_fill(&is->g[nk], is->src);
+		if (is->g[nk].nst && group_submit(is, nk) == 0)
 			is->inflight = nk;
 	}
-	return (int32_t)is->st[k].n;
+	return (int32_t)is->g[k].st[0].n;
+}
+
+static const struct stage *cur_stage(struct gpu_priv *pv, int ifidx)
+{
+	const struct if_state *is;
+	if (!pv || ifidx < 0 || ifidx >= (int)g_cfg.num_ifs || pv->ifs[ifidx].cur < 0)
+		return NULL;
+	is = &pv->ifs[ifidx];
+	return &is->g[is->cur].st[is->cur_idx];
 }
 
 static uint8_t *gpu_get_rptr(struct mtcp_thread_context *ctx, int ifidx, int index, uint16_t *len)
 {
-	struct gpu_priv *pv = priv_of(ctx);
-	struct stage *s;
-	if (!pv || ifidx < 0 || ifidx >= (int)g_cfg.num_ifs || pv->ifs[ifidx].cur < 0)
-		return NULL;
-	s = &pv->ifs[ifidx].st[pv->ifs[ifidx].cur];
-	if (index < 0 || (uint32_t)index >= s->n)
+	const struct stage *s = cur_stage(priv_of(ctx), ifidx);
+	if (!s || index < 0 || (uint32_t)index >= s->n)
 		return NULL;
 	*len = s->len[index];
 	return s->frames + s->off[index];
@@ -292,29 +495,48 @@ static void gpu_release_pkt(struct mtcp_thread_context *ctx, int ifidx, unsigned
 	(void)ctx; (void)ifidx; (void)pkt; (void)len;
 }
 
+/* Hand every buffered TX frame of netdev nif to its source. */
+static int32_t tx_flush(struct gpu_priv *pv, int nif)
+{
+	struct if_state *is = &pv->ifs[nif];
+	uint32_t i;
+	int32_t sent = 0;
+	for (i = 0; i < is->tx_n; i++) {
+		if (mosrx_source_send(is->src, is->tx_buf + (size_t)i * TX_FRAME_LEN, is->tx_len[i]) == 0) {
+			sent++;
+			pv->stats.tx_packets++;
+			pv->stats.tx_bytes += is->tx_len[i];
+		} else {
+			pv->stats.tx_errors++;
+		}
+	}
+	is->tx_n = 0;
+	if (sent && is->src)
+		mosrx_source_tx_flush(is->src);
+	return sent;
+}
+
 static uint8_t *gpu_get_wptr(struct mtcp_thread_context *ctx, int ifidx, uint16_t len)
 {
 	struct gpu_priv *pv = priv_of(ctx);
-	if (!pv || ifidx < 0 || ifidx >= MOSRX_MAX_DEVICES || len > TX_FRAME_LEN)
+	struct if_state *is;
+	if (!pv || ifidx < 0 || ifidx >= (int)g_cfg.num_ifs || len > TX_FRAME_LEN)
 		return NULL;
-	pv->tx_pending[ifidx] = len;
-	return pv->tx_buf[ifidx];
+	is = &pv->ifs[ifidx];
+	if (is->tx_n == g_cfg.tx_batch)   /* full: send what is buffered first (dpdk_get_wptr) */
+		tx_flush(pv, ifidx);
+	is->tx_len[is->tx_n] = len;
+	return is->tx_buf + (size_t)(is->tx_n++) * TX_FRAME_LEN;
 }
 
-/* TX is out of scope for the rx classifier: frames handed to send_pkts are
- * counted and dropped, like a pcap_inject to a closed interface. */
+/* Frames written since the last call leave through the netdev's source;
+ * returns how many were sent (pcap_send_pkts, pcap_module.c:67-79). */
 static int32_t gpu_send_pkts(struct mtcp_thread_context *ctx, int nif)
 {
 	struct gpu_priv *pv = priv_of(ctx);
-	if (!pv || nif < 0 || nif >= MOSRX_MAX_DEVICES)
+	if (!pv || nif < 0 || nif >= (int)g_cfg.num_ifs)
 		return 0;
-	if (pv->tx_pending[nif]) {
-		pv->tx_packets++;
-		pv->tx_bytes += pv->tx_pending[nif];
-		pv->tx_pending[nif] = 0;
-		return 1;
-	}
-	return 0;
+	return tx_flush(pv, nif);
 }
 
 static int gpu_get_nif(struct ifreq *ifr)
@@ -329,30 +551,35 @@ static int gpu_get_nif(struct ifreq *ifr)
 static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, void *argp)
 {
 	struct gpu_priv *pv = priv_of(ctx);
-	struct stage *s;
+	const struct stage *s;
 	if (!pv || !argp || nif < 0 || nif >= (int)g_cfg.num_ifs)
 		return -1;
+	s = cur_stage(pv, nif);
 	switch (cmd) {
 	case PKT_RX_RSS: {
 		RssInfo *ri = argp;
-		if (pv->ifs[nif].cur < 0)
-			return -1;
-		s = &pv->ifs[nif].st[pv->ifs[nif].cur];
-		if (ri->pktidx < 0 || (uint32_t)ri->pktidx >= s->n)
+		if (!s || ri->pktidx < 0 || (uint32_t)ri->pktidx >= s->n)
 			return -1;
 		ri->hash_value = s->res[ri->pktidx].rss;
 		return 0;
 	}
 	case MOSRX_PKT_RX_RESULTS:
-		if (pv->ifs[nif].cur < 0)
+		if (!s)
 			return -1;
-		*(const mosrx_result **)argp = pv->ifs[nif].st[pv->ifs[nif].cur].res;
+		*(const mosrx_result **)argp = s->res;
 		return 0;
 	case MOSRX_PKT_RX_MATCH:
-		if (pv->ifs[nif].cur < 0 || !g_cfg.bpf_nprog)
+		if (!s || !s->match)
 			return -1;
-		*(const uint32_t **)argp = pv->ifs[nif].st[pv->ifs[nif].cur].match;
+		*(const uint32_t **)argp = s->match;
 		return 0;
+	case MOSRX_PKT_RX_TCPINFO:
+		if (!s || !s->ti)
+			return -1;
+		*(const mosrx_tcpinfo **)argp = s->ti;
+		return 0;
+	case MOSRX_PKT_SET_PARAMS:   /* batches submitted from now on use the new stack state */
+		return mosrx_set_params(pv->ifs[nif].mc, (const mosrx_params *)argp) ? -1 : 0;
 	case DRV_NAME:
 		*(const char **)argp = "mosrx_gpu";
 		return 0;
@@ -374,8 +601,13 @@ static void gpu_destroy_handle(struct mtcp_thread_context *ctx)
 			continue;
 		if (is->inflight >= 0)
 			mosrx_classify_host_wait(is->mc, is->inflight);
-		for (k = 0; k < MOSRX_NSLOT; k++)
-			stage_free(is->mc, &is->st[k]);
+		tx_flush(pv, (int)i);
+		for (k = 0; k < MOSRX_NSLOT; k++) {
+			group_recycle(&is->g[k], is->src);
+			group_free(is->mc, &is->g[k]);
+		}
+		free(is->tx_buf);
+		free(is->tx_len);
 		mosrx_close(is->mc);
 	}
 	pthread_mutex_lock(&g_lock);

@@ -5,12 +5,16 @@
  *   mem       replays an in-memory trace (the loopback trace of BASELINE config #1)
  *   pcap      native reader for classic pcap files; the reference's pcap backend
  *             links libpcap (pcap_module.c:13, pcap_next :41), which the image lacks
- *   afpacket  raw AF_PACKET socket on an interface (pcap_create + pcap_activate,
- *             pcap_module.c:140-156, without libpcap)
+ *   afpacket  raw AF_PACKET socket on an interface with a TPACKET_V3 PACKET_MMAP
+ *             ring (pcap_create + pcap_activate, pcap_module.c:140-156, without
+ *             libpcap)
  *
  * Each source writes one frame straight into the caller's staging slot, so a
  * backend can receive directly into pinned memory; the memory source also
- * copies whole runs (fill) or lends its pinned replay buffer (borrow).
+ * copies whole runs (fill), and the memory and AF_PACKET sources lend their
+ * pinned memory as the batch itself (borrow).  Frames sent back out
+ * (send_pkts, pcap_module.c:67-89) leave through the source: the AF_PACKET
+ * socket, or a pcap dump file for any source.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -21,7 +25,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/socket.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "../../include/mosrx_io_module.h"
@@ -275,53 +281,331 @@ mosrx_source *mosrx_source_pcap(const char *path, uint32_t loops)
 	return &s->base;
 }
 
-/* ---------------- AF_PACKET raw socket ---------------- */
+/* ---------------- AF_PACKET raw socket: a TPACKET_V3 PACKET_MMAP ring ---------------- */
+/* The kernel writes received frames straight into a ring of blocks mapped into
+ * this process (what libpcap does for pcap_create + pcap_activate on Linux,
+ * pcap_module.c:140-156).  TPACKET_V3 places each frame's network header on a
+ * 16-byte boundary, so the Ethernet header sits at 16 B + 2: the staging layout
+ * the kernels read fastest.  When the ring can be registered with the HIP
+ * runtime (hipHostRegister) a run of frames is lent to the backend as the batch
+ * itself (borrow), and its blocks go back to the kernel when the backend
+ * releases the run (give_back); otherwise frames are copied out (fill / next)
+ * and each block is returned as soon as it is drained.  Frames the host sent
+ * itself (PACKET_OUTGOING) are never delivered: libpcap's default direction
+ * drops them too, so a frame sent on `lo` is received once. */
+#define AFP_BLOCK_SIZE (1u << 22)   /* 4 MiB blocks */
+#define AFP_MAX_BLOCKS 64
+#define AFP_MAX_RUNS   8            /* borrowed runs outstanding (the backend holds 2) */
+
 struct src_afp {
 	struct mosrx_source base;
 	int fd;
+	uint8_t *ring;
+	uint32_t nblocks;
+	int registered;                 /* ring registered with hipHostRegister: borrow is available */
+	/* cursor: block `blk`, `left` frames not yet taken, next frame at `fp` */
+	uint32_t blk, left;
+	uint8_t *fp;
+	/* blocks taken in full but not yet given back: [rel, blk) (mod nblocks), and
+	 * per outstanding run the block count it completes (FIFO) */
+	uint32_t rel;
+	uint32_t run_upto[AFP_MAX_RUNS];
+	uint32_t run_head, run_tail;
+	uint64_t dropped_outgoing;
 };
 
+static struct tpacket_block_desc *afp_block(struct src_afp *s, uint32_t b)
+{
+	return (struct tpacket_block_desc *)(s->ring + (size_t)(b % s->nblocks) * AFP_BLOCK_SIZE);
+}
+
+static void afp_release_upto(struct src_afp *s, uint32_t upto)
+{
+	while (s->rel != upto) {
+		struct tpacket_block_desc *bd = afp_block(s, s->rel);
+		__atomic_store_n(&bd->hdr.bh1.block_status, TP_STATUS_KERNEL, __ATOMIC_RELEASE);
+		s->rel++;
+	}
+}
+
+/* Make the cursor point at a frame; 0 when the kernel has retired no block. */
+static int afp_ready(struct src_afp *s)
+{
+	while (!s->left) {
+		struct tpacket_block_desc *bd;
+		if (s->fp) {                     /* the cursor's block is drained */
+			s->blk++;
+			s->fp = NULL;
+		}
+		if (s->blk - s->rel >= s->nblocks)
+			return 0;                    /* every block held by outstanding runs */
+		bd = afp_block(s, s->blk);
+		if (!(__atomic_load_n(&bd->hdr.bh1.block_status, __ATOMIC_ACQUIRE) & TP_STATUS_USER))
+			return 0;
+		s->left = bd->hdr.bh1.num_pkts;
+		s->fp = (uint8_t *)bd + bd->hdr.bh1.offset_to_first_pkt;
+		if (!s->left) {                  /* an empty retired block */
+			s->blk++;
+			s->fp = NULL;
+		}
+	}
+	return 1;
+}
+
+/* Blocks fully taken: those before the cursor's, and the cursor's own once drained. */
+static uint32_t afp_done(const struct src_afp *s)
+{
+	return (s->fp && !s->left) ? s->blk + 1 : s->blk;
+}
+
+/* Take the cursor's frame: its Ethernet header and capture length, or NULL for
+ * a frame to skip (outgoing). */
+static const uint8_t *afp_take(struct src_afp *s, uint32_t *caplen)
+{
+	const struct tpacket3_hdr *h = (const struct tpacket3_hdr *)s->fp;
+	const struct sockaddr_ll *sll = (const struct sockaddr_ll *)(s->fp + TPACKET_ALIGN(sizeof(*h)));
+	const uint8_t *mac = s->fp + h->tp_mac;
+	*caplen = h->tp_snaplen;
+	s->left--;
+	s->fp += h->tp_next_offset;
+	if (sll->sll_pkttype == PACKET_OUTGOING) {
+		s->dropped_outgoing++;
+		return NULL;
+	}
+	return mac;
+}
+
+/* Copying forms: blocks go back as soon as they are drained (no run is lent). */
 static int afp_next(struct mosrx_source *s_, uint8_t *dst, uint32_t cap)
 {
 	struct src_afp *s = (struct src_afp *)s_;
-	ssize_t r = recv(s->fd, dst, cap, MSG_DONTWAIT | MSG_TRUNC);
-	if (r <= 0)
+	for (;;) {
+		uint32_t l;
+		const uint8_t *mac;
+		if (!afp_ready(s)) {
+			if (s->run_head == s->run_tail)
+				afp_release_upto(s, afp_done(s));
+			return 0;
+		}
+		mac = afp_take(s, &l);
+		if (s->run_head == s->run_tail)
+			afp_release_upto(s, afp_done(s));
+		if (!mac)
+			continue;
+		l = l < cap ? l : cap;
+		memcpy(dst, mac, l);
+		return (int)l;
+	}
+}
+
+/* Zero-copy: frames of consecutive retired blocks, up to the ring's end (a run
+ * never wraps, so it is one contiguous span of the registered ring). */
+static uint32_t afp_borrow(struct mosrx_source *s_, uint32_t max_n, uint32_t max_frame, const uint8_t **frames,
+                           uint64_t *frames_bytes, uint32_t *off, uint16_t *len)
+{
+	struct src_afp *s = (struct src_afp *)s_;
+	const uint8_t *base = NULL;
+	uint32_t k = 0, first_blk;
+	uint64_t end = 0;
+	if ((s->run_tail - s->run_head) >= AFP_MAX_RUNS || !afp_ready(s))
 		return 0;
-	return (int)(r > (ssize_t)cap ? cap : (uint32_t)r);
+	first_blk = s->blk;
+	base = (const uint8_t *)afp_block(s, first_blk);
+	while (k < max_n) {
+		uint32_t l;
+		const uint8_t *mac;
+		if (!s->left) {
+			/* continue into the next block only if it is retired and contiguous */
+			if ((s->blk + 1) % s->nblocks == 0 || !afp_ready(s))
+				break;
+		}
+		mac = afp_take(s, &l);
+		if (!mac)
+			continue;
+		off[k] = (uint32_t)(mac - base);
+		len[k] = (uint16_t)(l < max_frame ? l : max_frame);
+		end = (uint64_t)off[k] + len[k];
+		k++;
+	}
+	/* the run completes every block before the cursor's (and the cursor's own when drained) */
+	s->run_upto[s->run_tail % AFP_MAX_RUNS] = afp_done(s);
+	s->run_tail++;
+	if (!k) {                        /* only outgoing frames: nothing to lend, release at once */
+		s_->give_back(s_);
+		return 0;
+	}
+	*frames = base;
+	*frames_bytes = end;
+	return k;
+}
+
+static void afp_give_back(struct mosrx_source *s_)
+{
+	struct src_afp *s = (struct src_afp *)s_;
+	if (s->run_head == s->run_tail)
+		return;
+	afp_release_upto(s, s->run_upto[s->run_head % AFP_MAX_RUNS]);
+	s->run_head++;
+}
+
+static int afp_send(struct mosrx_source *s_, const uint8_t *frame, uint32_t len)
+{
+	struct src_afp *s = (struct src_afp *)s_;
+	return send(s->fd, frame, len, 0) == (ssize_t)len ? 0 : -errno;   /* pcap_inject */
 }
 
 static void afp_close(struct mosrx_source *s_)
 {
 	struct src_afp *s = (struct src_afp *)s_;
+	if (s->registered)
+		hipHostUnregister(s->ring);
+	if (s->ring && s->ring != MAP_FAILED)
+		munmap(s->ring, (size_t)s->nblocks * AFP_BLOCK_SIZE);
 	if (s->fd >= 0)
 		close(s->fd);
 	free(s);
 }
 
-mosrx_source *mosrx_source_afpacket(const char *ifname)
+mosrx_source *mosrx_source_afpacket_ex(const char *ifname, const mosrx_afpacket_opts *o)
 {
 	struct src_afp *s = calloc(1, sizeof(*s));
 	struct sockaddr_ll sll;
-	int rcvbuf = 16 << 20;   /* PCAP_BUFFER_SIZE, pcap_module.c:26 */
-	if (!s)
+	struct tpacket_req3 req;
+	int v = TPACKET_V3, one = 1;
+	const uint32_t nb = o && o->ring_blocks ? o->ring_blocks : 8;
+	if (!s || !ifname || nb > AFP_MAX_BLOCKS) {
+		free(s);
 		return NULL;
+	}
+	s->base.close = afp_close;
 	s->fd = socket(AF_PACKET, SOCK_RAW, htons(ETH_P_ALL));
 	if (s->fd < 0) {
 		free(s);
 		return NULL;
 	}
+	memset(&req, 0, sizeof(req));
+	req.tp_block_size = AFP_BLOCK_SIZE;
+	req.tp_block_nr = nb;
+	req.tp_frame_size = 2048;
+	req.tp_frame_nr = (AFP_BLOCK_SIZE / 2048) * nb;
+	req.tp_retire_blk_tov = o && o->retire_ms ? o->retire_ms : 1;   /* hand partly filled blocks over after 1 ms */
 	memset(&sll, 0, sizeof(sll));
 	sll.sll_family = AF_PACKET;
 	sll.sll_protocol = htons(ETH_P_ALL);
 	sll.sll_ifindex = (int)if_nametoindex(ifname);
-	setsockopt(s->fd, SOL_SOCKET, SO_RCVBUF, &rcvbuf, sizeof(rcvbuf));
-	if (sll.sll_ifindex == 0 || bind(s->fd, (struct sockaddr *)&sll, sizeof(sll))) {
+	if (setsockopt(s->fd, SOL_PACKET, PACKET_VERSION, &v, sizeof(v)) ||
+	    setsockopt(s->fd, SOL_PACKET, PACKET_RX_RING, &req, sizeof(req))) {
 		afp_close(&s->base);
 		return NULL;
 	}
+	/* outgoing frames never reach the ring (kernels before 4.20 lack the option:
+	 * afp_take still drops them by sll_pkttype) */
+	setsockopt(s->fd, SOL_PACKET, PACKET_IGNORE_OUTGOING, &one, sizeof(one));
+	s->nblocks = nb;
+	s->ring = mmap(NULL, (size_t)nb * AFP_BLOCK_SIZE, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_LOCKED, s->fd, 0);
+	if (s->ring == MAP_FAILED)
+		s->ring = mmap(NULL, (size_t)nb * AFP_BLOCK_SIZE, PROT_READ | PROT_WRITE, MAP_SHARED, s->fd, 0);
+	if (s->ring == MAP_FAILED || sll.sll_ifindex == 0 || bind(s->fd, (struct sockaddr *)&sll, sizeof(sll))) {
+		afp_close(&s->base);
+		return NULL;
+	}
+	if (o && o->fanout_group) {      /* one socket per mTCP thread, flows split by hash (RSS-like) */
+		int fo = (int)((o->fanout_group & 0xFFFF) | (PACKET_FANOUT_HASH << 16));
+		if (setsockopt(s->fd, SOL_PACKET, PACKET_FANOUT, &fo, sizeof(fo))) {
+			afp_close(&s->base);
+			return NULL;
+		}
+	}
 	s->base.next = afp_next;
-	s->base.close = afp_close;
+	s->base.send = afp_send;
+	if (!(o && o->copy) &&
+	    hipHostRegister(s->ring, (size_t)nb * AFP_BLOCK_SIZE, hipHostRegisterDefault) == hipSuccess) {
+		s->registered = 1;
+		s->base.borrow = afp_borrow;
+		s->base.give_back = afp_give_back;
+	}
 	return &s->base;
+}
+
+mosrx_source *mosrx_source_afpacket(const char *ifname)
+{
+	return mosrx_source_afpacket_ex(ifname, NULL);
+}
+
+int mosrx_source_afpacket_info(const mosrx_source *s_, mosrx_afpacket_info *info)
+{
+	const struct src_afp *s = (const struct src_afp *)s_;
+	if (!s_ || !info || s_->close != afp_close)
+		return -EINVAL;
+	info->zero_copy = s->registered;
+	info->ring_bytes = (uint64_t)s->nblocks * AFP_BLOCK_SIZE;
+	info->dropped_outgoing = s->dropped_outgoing;
+	return 0;
+}
+
+/* ---------------- transmit ---------------- */
+/* A frame handed to send_pkts leaves through the source it belongs to: the
+ * AF_PACKET socket (pcap_inject, pcap_module.c:67-79) or, when a TX dump is
+ * set, a classic pcap file (any source; the only way out of a trace file). */
+int mosrx_source_send(mosrx_source *s, const uint8_t *frame, uint32_t len)
+{
+	int rc;
+	if (!s || !frame || len > 65535)
+		return -EINVAL;
+	if (s->tx_dump) {
+		struct timespec ts;
+		uint32_t rh[4];
+		clock_gettime(CLOCK_REALTIME, &ts);
+		rh[0] = (uint32_t)ts.tv_sec;
+		rh[1] = (uint32_t)(ts.tv_nsec / 1000);
+		rh[2] = rh[3] = len;
+		rc = (fwrite(rh, 4, 4, s->tx_dump) == 4 && fwrite(frame, 1, len, s->tx_dump) == len) ? 0 : -EIO;
+	} else {
+		rc = s->send ? s->send(s, frame, len) : -EOPNOTSUPP;
+	}
+	if (rc) {
+		s->tx_errors++;
+		return rc;
+	}
+	s->tx_packets++;
+	s->tx_bytes += len;
+	return 0;
+}
+
+int mosrx_source_tx_pcap(mosrx_source *s, const char *path)
+{
+	static const uint32_t gh[6] = {0xa1b2c3d4u, 2u | (4u << 16), 0, 0, 65535, 1};   /* LINKTYPE_ETHERNET */
+	if (!s)
+		return -EINVAL;
+	if (s->tx_dump) {
+		fclose(s->tx_dump);
+		s->tx_dump = NULL;
+	}
+	if (!path)
+		return 0;
+	s->tx_dump = fopen(path, "wb");
+	if (!s->tx_dump)
+		return -errno;
+	if (fwrite(gh, 4, 6, s->tx_dump) != 6)
+		return -EIO;
+	return 0;
+}
+
+int mosrx_source_tx_flush(mosrx_source *s)
+{
+	if (!s)
+		return -EINVAL;
+	return s->tx_dump && fflush(s->tx_dump) ? -EIO : 0;
+}
+
+int mosrx_source_tx_stats(const mosrx_source *s, uint64_t *packets, uint64_t *bytes, uint64_t *errors)
+{
+	if (!s)
+		return -EINVAL;
+	if (packets) *packets = s->tx_packets;
+	if (bytes) *bytes = s->tx_bytes;
+	if (errors) *errors = s->tx_errors;
+	return 0;
 }
 
 int mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap)
@@ -333,6 +617,10 @@ int mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap)
 
 void mosrx_source_close(mosrx_source *s)
 {
+	if (s && s->tx_dump) {
+		fclose(s->tx_dump);
+		s->tx_dump = NULL;
+	}
 	if (s && s->close)
 		s->close(s);
 }

@@ -147,6 +147,12 @@ int mosrx_set_params(mosrx_ctx *c, const mosrx_params *p)
 
 int mosrx__ensure_streams(mosrx_ctx *c, uint32_t n);
 
+int mosrx_device_count(void)
+{
+	int n = 0;
+	return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 {
 	mosrx_ctx *c;
@@ -167,6 +173,7 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 		return -ENOMEM;
 	c->device = device;
 	c->variant = MOSRX_DEFAULT_VARIANT;
+	c->last_kernel_ms = -1.0f;
 	if (getenv("MOSRX_KVARIANT"))
 		c->variant = atoi(getenv("MOSRX_KVARIANT")) & 127;
 	c->bpf_engine_req = MOSRX_BPF_ENGINE_JIT;
@@ -186,6 +193,10 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 	for (i = 0; i < NSLOT; i++) {
 		if (hipStreamCreateWithFlags(&c->slot[i].stream, hipStreamNonBlocking) != hipSuccess ||
 		    hipEventCreateWithFlags(&c->slot[i].done, hipEventDisableTiming) != hipSuccess ||
+		    hipEventCreate(&c->slot[i].kev0) != hipSuccess || hipEventCreate(&c->slot[i].kev1) != hipSuccess ||
+		    hipMalloc((void **)&c->slot[i].d_qdesc, MOSRX_MAX_GROUP * sizeof(mosrx_qdesc)) != hipSuccess ||
+		    hipHostMalloc((void **)&c->slot[i].h_qdesc, MOSRX_MAX_GROUP * sizeof(mosrx_qdesc),
+		                  hipHostMallocDefault) != hipSuccess ||
 		    hipMalloc((void **)&c->slot[i].d_cnt, MOSRX_R_COUNT * 4) != hipSuccess ||
 		    hipHostMalloc((void **)&c->slot[i].h_cnt, MOSRX_R_COUNT * 4, hipHostMallocDefault) != hipSuccess) {
 			mosrx_close(c);
@@ -226,6 +237,10 @@ void mosrx_close(mosrx_ctx *c)
 			hipStreamDestroy(c->slot[i].stream);
 		}
 		if (c->slot[i].done) hipEventDestroy(c->slot[i].done);
+		if (c->slot[i].kev0) hipEventDestroy(c->slot[i].kev0);
+		if (c->slot[i].kev1) hipEventDestroy(c->slot[i].kev1);
+		if (c->slot[i].d_qdesc) hipFree(c->slot[i].d_qdesc);
+		if (c->slot[i].h_qdesc) hipHostFree(c->slot[i].h_qdesc);
 		if (c->slot[i].d_cnt) hipFree(c->slot[i].d_cnt);
 		if (c->slot[i].h_cnt) hipHostFree(c->slot[i].h_cnt);
 		slot_free(&c->slot[i]);
@@ -523,6 +538,8 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 		HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
 	}
 	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_R_COUNT * 4, s->stream));
+	if (c->timing)
+		HIPCHK(hipEventRecord(s->kev0, s->stream));
 	if (h_match) {
 		mosrx_batch db = *b;
 		db.frames = dframes;
@@ -535,6 +552,9 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 	}
 	if (rc)
 		return rc;
+	if (c->timing)
+		HIPCHK(hipEventRecord(s->kev1, s->stream));
+	s->timed = c->timing;
 	HIPCHK(hipMemcpyAsync(h_out, s->d_res, (size_t)b->n * sizeof(mosrx_result), hipMemcpyDeviceToHost,
 	                      s->stream));
 	if (h_fhash || h_match)
@@ -644,8 +664,196 @@ int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
 	if (s->busy == 1)
 		HIPCHK(hipEventSynchronize(s->done));
 	memcpy(c->h_cnt, s->h_cnt, sizeof(c->h_cnt));
+	c->last_kernel_ms = -1.0f;
+	if (s->busy == 1 && s->timed && hipEventElapsedTime(&c->last_kernel_ms, s->kev0, s->kev1) != hipSuccess)
+		c->last_kernel_ms = -1.0f;
 	s->busy = 0;
 	return 0;
+}
+
+int mosrx_set_timing(mosrx_ctx *c, int on)
+{
+	if (!c)
+		return -EINVAL;
+	c->timing = on ? 1 : 0;
+	return 0;
+}
+
+int mosrx_last_kernel_ms(mosrx_ctx *c, float *ms)
+{
+	if (!c || !ms)
+		return -EINVAL;
+	if (c->last_kernel_ms < 0)
+		return -ENODATA;
+	*ms = c->last_kernel_ms;
+	return 0;
+}
+
+/* ---- a group of host batches in one launch (gpu_module_func's rx ring) ---- */
+struct region { const uint8_t *lo; uint64_t len; int own; uint8_t *dev; };
+
+/* Device copies of every region of the group: regions in address order are
+ * gathered into copy runs wherever the gap to the next one is under an eighth
+ * of the run + 4 KiB (packed stages, or consecutive runs lent by one source),
+ * and each run keeps its host address modulo 256 on the device, so a frame
+ * buffer stays 16-byte aligned.  A frame buffer that is not 16-byte aligned on
+ * the host is copied on its own to an aligned device address. */
+static int group_copy(struct slot *s, struct region *r, uint32_t nr, uint64_t *dev_bytes, int issue)
+{
+	uint32_t i, j;
+	uint64_t cur = 0;
+	struct region *ord[3 * MOSRX_MAX_GROUP];
+	for (i = 0; i < nr; i++) {        /* insertion sort by address (nr <= 192) */
+		for (j = i; j > 0 && ord[j - 1]->lo > r[i].lo; j--)
+			ord[j] = ord[j - 1];
+		ord[j] = &r[i];
+	}
+	for (i = 0; i < nr;) {
+		const uint8_t *lo = ord[i]->lo, *hi = lo + ord[i]->len;
+		uint64_t base;
+		j = i + 1;
+		if (!ord[i]->own)
+			while (j < nr && !ord[j]->own &&
+			       (uint64_t)(ord[j]->lo > hi ? ord[j]->lo - hi : 0) <= ((uint64_t)(hi - lo) >> 3) + 4096) {
+				if (ord[j]->lo + ord[j]->len > hi)
+					hi = ord[j]->lo + ord[j]->len;
+				j++;
+			}
+		base = ((cur + 255) & ~(uint64_t)255) + (ord[i]->own ? 0 : ((uintptr_t)lo & 255));
+		if (issue) {
+			uint32_t k;
+			for (k = i; k < j; k++)
+				ord[k]->dev = s->d_frames + base + (uint64_t)(ord[k]->lo - lo);
+			HIPCHK(hipMemcpyAsync(s->d_frames + base, lo, (size_t)(hi - lo), hipMemcpyHostToDevice, s->stream));
+		}
+		cur = base + (uint64_t)(hi - lo);
+		i = j;
+	}
+	*dev_bytes = cur;
+	return 0;
+}
+
+int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                     mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo)
+{
+	struct region r[3 * MOSRX_MAX_GROUP];
+	uint32_t i, nr = 0, tiles = 0, maxl = 0, ntot = 0, tile;
+	uint64_t dev_bytes = 0, pre = 0;
+	mosrx_qparams qp;
+	struct slot *s;
+	int rc, unknown = 0, kind, tpb_ok = 1;
+	if (!c || slot < 0 || slot >= NSLOT || !b || !h_out || nb == 0 || nb > MOSRX_MAX_GROUP)
+		return -EINVAL;
+	s = &c->slot[slot];
+	if (s->busy)
+		return -EBUSY;
+	for (i = 0; i < nb; i++) {
+		if ((rc = mosrx__check_batch(&b[i], 0)))
+			return rc;
+		if (b[i].n && (!h_out[i] || (h_tcpinfo && !h_tcpinfo[i])))
+			return -EINVAL;
+		if (!b[i].max_len)
+			unknown = 1;
+		maxl = b[i].max_len > maxl ? b[i].max_len : maxl;
+		ntot += b[i].n;
+		if (!b[i].n)
+			continue;
+		r[nr++] = (struct region){b[i].frames, b[i].frames_bytes, ((uintptr_t)b[i].frames & 15) != 0, NULL};
+		r[nr++] = (struct region){(const uint8_t *)b[i].off, (uint64_t)b[i].n * 4, 0, NULL};
+		r[nr++] = (struct region){(const uint8_t *)b[i].len, (uint64_t)b[i].n * 2, 0, NULL};
+	}
+	if (ntot == 0) {
+		memset(s->h_cnt, 0, MOSRX_R_COUNT * 4);
+		s->busy = 2;
+		return 0;
+	}
+	HIPCHK(hipSetDevice(c->device));
+	group_copy(s, r, nr, &dev_bytes, 0);
+	if ((rc = mosrx__slot_reserve(c, s, dev_bytes, ntot)))
+		return rc;
+	if ((rc = group_copy(s, r, nr, &dev_bytes, 1)))
+		return rc;
+	kind = kind_of(c, unknown ? 0 : maxl, dev_bytes, ntot);   /* one shape for the whole group */
+	tile = MOSRX_KIND_FRAMES(kind);
+	for (i = 0, nr = 0; i < nb; i++) {
+		mosrx_qdesc *d = &s->h_qdesc[i];
+		memset(d, 0, sizeof(*d));
+		d->tile_base = tiles;
+		d->out = s->d_res + pre;
+		d->tinfo = h_tcpinfo ? s->d_ti + pre : NULL;
+		if (b[i].n) {
+			d->frames = r[nr].dev;
+			d->off = (const uint32_t *)r[nr + 1].dev;
+			d->len = (const uint16_t *)r[nr + 2].dev;
+			d->frames_bytes = (uint32_t)b[i].frames_bytes;
+			d->n = b[i].n;
+			nr += 3;
+		}
+		tiles += (b[i].n + tile - 1) / tile;
+		if ((b[i].n + tile - 1) / tile != (b[0].n + tile - 1) / tile)
+			tpb_ok = 0;
+		pre += b[i].n;
+	}
+	HIPCHK(hipMemcpyAsync(s->d_qdesc, s->h_qdesc, nb * sizeof(mosrx_qdesc), hipMemcpyHostToDevice, s->stream));
+	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_R_COUNT * 4, s->stream));
+	qp.desc = s->d_qdesc;
+	qp.tables = c->d_tables;
+	qp.counters = s->d_cnt;
+	qp.nb = nb;
+	qp.flags = c->kflags;
+	qp.tpb = tpb_ok ? tiles / nb : 0;
+	qp.tinfo = h_tcpinfo ? 1u : 0u;
+	if (c->timing)
+		HIPCHK(hipEventRecord(s->kev0, s->stream));
+	if ((rc = mosrx_launch_queue(&qp, tiles, kind, c->variant, s->stream)))
+		return rc;
+	if (c->timing)
+		HIPCHK(hipEventRecord(s->kev1, s->stream));
+	s->timed = c->timing;
+	/* results: one copy when the host buffers follow each other, else per batch */
+	for (i = 0, pre = 0; i < nb;) {
+		uint32_t j = i + 1;
+		uint64_t n = b[i].n;
+		while (j < nb && h_out[j] == h_out[j - 1] + b[j - 1].n &&
+		       (!h_tcpinfo || h_tcpinfo[j] == h_tcpinfo[j - 1] + b[j - 1].n))
+			n += b[j++].n;
+		if (n) {
+			HIPCHK(hipMemcpyAsync(h_out[i], s->d_res + pre, (size_t)n * sizeof(mosrx_result),
+			                      hipMemcpyDeviceToHost, s->stream));
+			if (h_tcpinfo)
+				HIPCHK(hipMemcpyAsync(h_tcpinfo[i], s->d_ti + pre, (size_t)n * sizeof(mosrx_tcpinfo),
+				                      hipMemcpyDeviceToHost, s->stream));
+		}
+		pre += n;
+		i = j;
+	}
+	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_R_COUNT * 4, hipMemcpyDeviceToHost, s->stream));
+	HIPCHK(hipEventRecord(s->done, s->stream));
+	s->busy = 1;
+	return 0;
+}
+
+int mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out,
+                                  mosrx_tcpinfo *h_tcpinfo)
+{
+	int rc;
+	if (!h_tcpinfo)
+		return mosrx_classify_host_submit(c, slot, b, h_out);
+	if (!c || slot < 0 || slot >= NSLOT)
+		return -EINVAL;
+	if ((rc = mosrx__check_batch(b, 0)))
+		return rc;
+	if (c->slot[slot].busy)
+		return -EBUSY;
+	if (b->n == 0) {
+		memset(c->slot[slot].h_cnt, 0, MOSRX_R_COUNT * 4);
+		c->slot[slot].busy = 2;
+		return 0;
+	}
+	if (!h_out)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	return host_enqueue(c, &c->slot[slot], b, h_out, NULL, NULL, h_tcpinfo);
 }
 
 int mosrx_last_counters(mosrx_ctx *c, uint64_t counts[MOSRX_R_COUNT])
@@ -1029,6 +1237,7 @@ int mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream)
 	qp.nb = q->nb;
 	qp.flags = c->kflags;
 	qp.tpb = q->tpb;
+	qp.tinfo = 0;
 	return mosrx_launch_queue(&qp, q->total_tiles, q->tile, c->variant, stream ? stream : (void *)c->stream);
 }
 

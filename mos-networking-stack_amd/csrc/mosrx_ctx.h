@@ -30,6 +30,10 @@ struct slot {
 	hipStream_t stream;
 	hipEvent_t done;
 	uint32_t *h_cnt;   /* MOSRX_R_COUNT, pinned: a D2H copy into pageable memory blocks the host */
+	hipEvent_t kev0, kev1;     /* around the kernel of the last submit (when the context times) */
+	mosrx_qdesc *h_qdesc;      /* MOSRX_MAX_GROUP, pinned: a group's batch table */
+	mosrx_qdesc *d_qdesc;
+	int timed;
 	int busy;
 };
 
@@ -54,6 +58,8 @@ struct mosrx_ctx {
 	hipStream_t xs[MOSRX_MAX_STREAMS];   /* timing streams (mosrx_time_op), created on first use */
 	hipEvent_t xdone[MOSRX_MAX_STREAMS];
 	uint32_t nxs;
+	int timing;                      /* record kernel events on the end-to-end path (mosrx_set_timing) */
+	float last_kernel_ms;            /* kernel time of the last waited submit, -1 if not timed */
 };
 
 int mosrx__check_batch(const mosrx_batch *b, int dev);

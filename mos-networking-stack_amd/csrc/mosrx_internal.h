@@ -62,16 +62,17 @@ enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_S13 = 1, MOSRX_KIND_COUNT = 2 };
  * the per-lane header window; longer ones stream their tail cooperatively. */
 #define MOSRX_WINDOW_END 94
 
-/* Batch-queue descriptor (device resident), 48 bytes. */
+/* Batch-queue descriptor (device resident), 64 bytes. */
 typedef struct mosrx_qdesc {
 	const uint8_t  *frames;
 	const uint32_t *off;
 	const uint16_t *len;
 	mosrx_result   *out;
+	mosrx_tcpinfo  *tinfo;       /* NULL unless the queue was launched with pkt_info fields */
 	uint32_t        frames_bytes;
 	uint32_t        n;
 	uint32_t        tile_base;   /* first workgroup of this batch in the launch */
-	uint32_t        pad;
+	uint32_t        pad[3];
 } mosrx_qdesc;
 
 typedef struct mosrx_qparams {
@@ -81,6 +82,7 @@ typedef struct mosrx_qparams {
 	uint32_t           nb;
 	uint32_t           flags;
 	uint32_t           tpb;      /* tiles per batch when every batch has the same tile count, else 0 */
+	uint32_t           tinfo;    /* 1: the descriptors carry pkt_info TCP field buffers (VAR_TI) */
 } mosrx_qparams;
 
 /* Batched BPF launch: the program table rides in the kernel arguments, the

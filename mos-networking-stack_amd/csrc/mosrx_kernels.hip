@@ -916,7 +916,7 @@ void mosrx_classify_queue_kernel(mosrx_qparams qp)
 	kp.counters = qp.counters;
 	kp.fhash = nullptr;
 	kp.bmatch = nullptr;
-	kp.tinfo = nullptr;
+	kp.tinfo = d->tinfo;
 	kp.frames_bytes = d->frames_bytes;
 	kp.n = d->n;
 	kp.flags = qp.flags;
@@ -981,11 +981,11 @@ extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles,
 	if (kind < 0 || kind >= MOSRX_KIND_COUNT)
 		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-#define QROW(k) {launch_queue_v<k, 0>, launch_queue_v<k, 2>}
-	static void (*const tab[MOSRX_KIND_COUNT][2])(const mosrx_qparams *, uint32_t, hipStream_t) = {
+#define QROW(k) {launch_queue_v<k, 0>, launch_queue_v<k, 2>, launch_queue_v<k, 2 | VAR_TI>}
+	static void (*const tab[MOSRX_KIND_COUNT][3])(const mosrx_qparams *, uint32_t, hipStream_t) = {
 		QROW(MOSRX_KIND_SMALL), QROW(MOSRX_KIND_S13)};
 #undef QROW
-	tab[kind][(variant >> 1) & 1](qp, total_tiles, s);
+	tab[kind][qp->tinfo ? 2 : (variant >> 1) & 1](qp, total_tiles, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

@@ -3,6 +3,7 @@
 #define MOSRX_SOURCE_H
 
 #include <stdint.h>
+#include <stdio.h>
 
 struct mosrx_source {
 	/* write the next frame into dst (at most cap bytes); returns its caplen, 0 when none */
@@ -17,11 +18,23 @@ struct mosrx_source {
 	                 uint32_t max_n, uint32_t max_frame, uint64_t *end);
 	/* optional zero-copy form (NULL: none): hand out up to max_n frames that
 	 * already sit in pinned memory the source owns, as one run starting at
-	 * *frames (first frame at byte 2), writing off[]/len[] (len clamped to
-	 * max_frame) and the run's length in *frames_bytes; the bytes stay valid
-	 * and unmodified until the source is closed */
+	 * *frames, in buffer order, writing off[]/len[] (len clamped to max_frame)
+	 * and the run's length in *frames_bytes; the bytes stay valid and
+	 * unmodified until give_back releases the run (or, without give_back,
+	 * until the source is closed) */
 	uint32_t (*borrow)(struct mosrx_source *s, uint32_t max_n, uint32_t max_frame, const uint8_t **frames,
 	                   uint64_t *frames_bytes, uint32_t *off, uint16_t *len);
+	/* optional: release the OLDEST run borrow handed out that is not yet
+	 * released (runs come back in the order they were borrowed), e.g. return a
+	 * PACKET_MMAP ring's blocks to the kernel */
+	void (*give_back)(struct mosrx_source *s);
+	/* optional native transmit of one frame (pcap_inject, pcap_module.c:67-79):
+	 * 0 or -errno */
+	int  (*send)(struct mosrx_source *s, const uint8_t *frame, uint32_t len);
+	/* generic TX sink (mosrx_source_tx_pcap): when set, sent frames are
+	 * appended to this pcap file instead of the native transmit */
+	FILE    *tx_dump;
+	uint64_t tx_packets, tx_bytes, tx_errors;
 };
 
 #endif

@@ -1,30 +1,45 @@
 /*
  * rx_loop.c — the receive half of RunMainLoop (core.c:897-909) over any
- * io_module_func, consuming the GPU verdicts instead of re-running the checks.
+ * io_module_func, consuming the GPU verdicts instead of re-running the checks,
+ * and the per-round flush of frames written for transmission (core.c:999-1007).
  *
  *   for rx_inf in netdevs:                        core.c:897
  *     recv_cnt = iom->recv_pkts(ctx, rx_inf)      core.c:899
  *     for i < recv_cnt:                           core.c:902
  *       pkt = iom->get_rptr(ctx, rx_inf, i, &len) core.c:905
  *       ProcessPacket(...)                        core.c:906 -> here: NETSTAT + fn()
+ *   for tx_inf in netdevs:                        core.c:999-1007
+ *     iom->send_pkts(ctx, tx_inf)
  *
  * NETSTAT follows eth_in.c:42-45 and :80-84: rx_packets++, rx_bytes += len +
  * ETHER_OVR (24, mtcp.h:58), rx_errors++ when the verdict is negative.
  */
 #include <errno.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "../../include/mosrx_io_module.h"
 
 #define ETHER_OVR 24
 
-int mosrx_rx_loop(const io_module_func *iom, struct mtcp_thread_context *ctx, int nif,
-                  uint64_t max_pkts, mosrx_pkt_fn fn, void *arg, mosrx_rx_stats *st)
+static uint64_t now_us(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000u + (uint64_t)ts.tv_nsec / 1000u;
+}
+
+int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx, int nif,
+                     const mosrx_rx_loop_opts *o, mosrx_pkt_fn fn, void *arg, mosrx_rx_stats *st)
 {
 	int rx_inf;
-	if (!iom || !iom->recv_pkts || !iom->get_rptr || !st || nif <= 0)
+	uint32_t idle = 0;
+	uint64_t t0;
+	if (!iom || !iom->recv_pkts || !iom->get_rptr || !st || !o || nif <= 0)
 		return -EINVAL;
 	memset(st, 0, sizeof(*st));
+	t0 = o->max_us ? now_us() : 0;
 	for (;;) {
 		int any = 0;
 		st->rounds++;
@@ -55,10 +70,48 @@ int mosrx_rx_loop(const io_module_func *iom, struct mtcp_thread_context *ctx, in
 				if (fn)
 					fn(arg, rx_inf, i, pkt, len, r);
 			}
-			if (max_pkts && st->rx_packets >= max_pkts)
-				return 0;
 		}
-		if (!any)
+		if (iom->send_pkts)               /* core.c:999-1007: flush what the round wrote */
+			for (rx_inf = 0; rx_inf < nif; rx_inf++)
+				iom->send_pkts(ctx, rx_inf);
+		if (o->max_pkts && st->rx_packets >= o->max_pkts)
 			return 0;
+		if (o->max_us && now_us() - t0 >= o->max_us)
+			return 0;
+		if (any) {
+			idle = 0;
+			continue;
+		}
+		if (o->idle_rounds && ++idle >= o->idle_rounds)
+			return 0;
+		if (o->idle_us)
+			usleep(o->idle_us);
 	}
+}
+
+int mosrx_rx_loop(const io_module_func *iom, struct mtcp_thread_context *ctx, int nif,
+                  uint64_t max_pkts, mosrx_pkt_fn fn, void *arg, mosrx_rx_stats *st)
+{
+	const mosrx_rx_loop_opts o = {max_pkts, 1, 0, 0};   /* a finite source: stop at the first idle round */
+	return mosrx_rx_loop_ex(iom, ctx, nif, &o, fn, arg, st);
+}
+
+/* ForwardEthernetFrame (eth_out.c:105-129) for the frames the checks accepted
+ * (verdict 1): the output netdev from the NIC forwarding table, a TX buffer
+ * from get_wptr, a copy of the frame; the round's send_pkts sends it. */
+void mosrx_forward_frame(void *arg, int ifidx, int index, const uint8_t *pkt, uint16_t len,
+                         const mosrx_result *res)
+{
+	mosrx_forwarder *f = arg;
+	int out;
+	uint8_t *buf;
+	(void)index;
+	if (!f || res->verdict != 1 || ifidx < 0 || ifidx >= MOSRX_MAX_DEVICES || (out = f->out_if[ifidx]) < 0 ||
+	    !f->iom->get_wptr || !(buf = f->iom->get_wptr(f->ctx, out, len))) {
+		if (f)
+			f->dropped++;
+		return;
+	}
+	memcpy(buf, pkt, len);
+	f->forwarded++;
 }

@@ -96,7 +96,33 @@ class ModuleCfg(C.Structure):
     _fields_ = [("num_ifs", C.c_uint32), ("if_names", (C.c_char * 16) * 16),
                 ("src", C.c_void_p * 16), ("batch", C.c_uint32), ("max_frame", C.c_uint32),
                 ("gpu_base", C.c_int32), ("ngpu", C.c_int32), ("pipeline", C.c_int32),
-                ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32)]
+                ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32),
+                ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32)]
+
+
+class ModuleStats(C.Structure):
+    _fields_ = [("rx_batches", C.c_uint64), ("rx_frames", C.c_uint64), ("tx_packets", C.c_uint64),
+                ("tx_bytes", C.c_uint64), ("tx_errors", C.c_uint64), ("kernel_launches", C.c_uint64),
+                ("kernel_ms", C.c_double)]
+
+
+class RxLoopOpts(C.Structure):
+    _fields_ = [("max_pkts", C.c_uint64), ("idle_rounds", C.c_uint32), ("idle_us", C.c_uint32),
+                ("max_us", C.c_uint64)]
+
+
+class AfpOpts(C.Structure):
+    _fields_ = [("ring_blocks", C.c_uint32), ("retire_ms", C.c_uint32), ("fanout_group", C.c_uint32),
+                ("copy", C.c_int32)]
+
+
+class AfpInfo(C.Structure):
+    _fields_ = [("zero_copy", C.c_int32), ("ring_bytes", C.c_uint64), ("dropped_outgoing", C.c_uint64)]
+
+
+class Forwarder(C.Structure):
+    _fields_ = [("iom", C.c_void_p), ("ctx", C.c_void_p), ("out_if", C.c_int32 * 16),
+                ("forwarded", C.c_uint64), ("dropped", C.c_uint64)]
 
 
 class MosrxError(OSError):
@@ -186,6 +212,22 @@ def lib():
             "mosrx_gpu_module_configure": (I, [C.POINTER(ModuleCfg)]),
             "mosrx_gpu_module_bind": (I, [P, I]),
             "mosrx_rx_loop": (I, [P, P, I, U64, P, P, C.POINTER(RxStats)]),
+            "mosrx_rx_loop_ex": (I, [P, P, I, C.POINTER(RxLoopOpts), P, P, C.POINTER(RxStats)]),
+            "mosrx_device_count": (I, []),
+            "mosrx_classify_host_submit_ex": (I, [P, I, C.POINTER(Batch), P, P]),
+            "mosrx_classify_host_group_submit": (I, [P, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
+            "mosrx_set_timing": (I, [P, I]),
+            "mosrx_last_kernel_ms": (I, [P, C.POINTER(C.c_float)]),
+            "mosrx_source_afpacket_ex": (P, [C.c_char_p, C.POINTER(AfpOpts)]),
+            "mosrx_source_afpacket_info": (I, [P, C.POINTER(AfpInfo)]),
+            "mosrx_source_send": (I, [P, P, U32]),
+            "mosrx_source_tx_pcap": (I, [P, C.c_char_p]),
+            "mosrx_source_tx_flush": (I, [P]),
+            "mosrx_source_tx_stats": (I, [P, C.POINTER(U64), C.POINTER(U64), C.POINTER(U64)]),
+            "mosrx_gpu_module_bind_source": (I, [I, I, P]),
+            "mosrx_gpu_module_device_of": (I, [I, I]),
+            "mosrx_gpu_module_stats_of": (I, [P, C.POINTER(ModuleStats)]),
+            "mosrx_gpu_module_set_timing": (I, [P, I]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -671,7 +713,11 @@ _CTXFN = C.CFUNCTYPE(None, C.c_void_p)
 _IOCTLFN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int, C.c_int, C.c_void_p)
 _RECVFN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int)
 _RPTRFN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint16))
+_WPTRFN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_uint16)
+_SENDFN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int)
+PKT_TX_IP_CSUM, PKT_TX_TCP_CSUM = 0x01, 0x02
 PKT_RX_RSS, DRV_NAME, PKT_RX_RESULTS, PKT_RX_MATCH = 0x03, 0x08, 0x10, 0x11
+PKT_RX_TCPINFO, PKT_SET_PARAMS = 0x12, 0x13
 
 
 class IoModuleFunc(C.Structure):
@@ -695,7 +741,8 @@ class GpuBackend:
 
     def __init__(self, sources: list[int], params: Params | None = None, batch: int = 32768,
                  max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
-                 ngpu: int = 1, bpf=None):
+                 ngpu: int = 1, bpf=None, group: int = 1, tcpinfo: bool = False, tx_batch: int = 64,
+                 timing: bool = False):
         cfg = ModuleCfg()
         lib().mosrx_gpu_module_cfg_default(C.byref(cfg))
         cfg.num_ifs = len(sources)
@@ -704,6 +751,7 @@ class GpuBackend:
             cfg.if_names[i].value = f"gpu{i}".encode()
         cfg.batch, cfg.max_frame, cfg.pipeline = batch, max_frame, int(pipeline)
         cfg.gpu_base, cfg.ngpu = gpu_base, ngpu
+        cfg.group, cfg.tcpinfo, cfg.tx_batch = group, int(tcpinfo), tx_batch
         if params is not None:
             cfg.params = params
         self._bpf = None
@@ -723,6 +771,10 @@ class GpuBackend:
         self._recv = _RECVFN(self.m.recv_pkts)
         self._rptr = _RPTRFN(self.m.get_rptr)
         self._ioctl = _IOCTLFN(self.m.dev_ioctl)
+        self._wptr = _WPTRFN(self.m.get_wptr)
+        self._send = _SENDFN(self.m.send_pkts)
+        if timing:
+            _chk(lib().mosrx_gpu_module_set_timing(self.ctx, 1), "mosrx_gpu_module_set_timing")
 
     def recv_pkts(self, ifidx: int = 0) -> int:
         return self._recv(self.ctx, ifidx)
@@ -745,14 +797,57 @@ class GpuBackend:
             raise MosrxError(5, "dev_ioctl(MOSRX_PKT_RX_MATCH)")
         return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint32)), (n,)).copy()
 
+    def tcpinfo(self, ifidx: int, n: int) -> np.ndarray:
+        """dev_ioctl(MOSRX_PKT_RX_TCPINFO): the batch's pkt_info TCP fields."""
+        p = C.c_void_p()
+        if self._ioctl(self.ctx, ifidx, PKT_RX_TCPINFO, C.byref(p)):
+            raise MosrxError(5, "dev_ioctl(MOSRX_PKT_RX_TCPINFO)")
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), (n * 12,)).view(TCPINFO_DTYPE).copy()
+
+    def set_params(self, ifidx: int, params: Params) -> int:
+        """dev_ioctl(MOSRX_PKT_SET_PARAMS): the stack state changed (0 or -1)."""
+        return self._ioctl(self.ctx, ifidx, PKT_SET_PARAMS, C.byref(params))
+
+    def ioctl_raw(self, ifidx: int, cmd: int, argp) -> int:
+        return self._ioctl(self.ctx, ifidx, cmd, argp)
+
+    def send(self, ifidx: int, frame: bytes) -> None:
+        """get_wptr + copy (EthernetOutput, eth_out.c:80-84): the frame waits for send_pkts."""
+        p = self._wptr(self.ctx, ifidx, len(frame))
+        if not p:
+            raise MosrxError(5, "get_wptr")
+        C.memmove(p, frame, len(frame))
+
+    def send_pkts(self, ifidx: int) -> int:
+        return self._send(self.ctx, ifidx)
+
+    def stats(self) -> ModuleStats:
+        st = ModuleStats()
+        _chk(lib().mosrx_gpu_module_stats_of(self.ctx, C.byref(st)), "mosrx_gpu_module_stats_of")
+        return st
+
+    def forwarder(self, out_if: list[int]) -> Forwarder:
+        """A mosrx_forwarder for run_loop(forward=...): netdev i -> out_if[i]."""
+        f = Forwarder()
+        f.iom = C.addressof(self.m)
+        f.ctx = self.ctx
+        for i in range(16):
+            f.out_if[i] = out_if[i] if i < len(out_if) else -1
+        return f
+
     def rss_of(self, ifidx: int, pktidx: int) -> int | None:
         ri = RssInfo(pktidx, 0)
         return None if self._ioctl(self.ctx, ifidx, PKT_RX_RSS, C.byref(ri)) else ri.hash_value
 
-    def run_loop(self, max_pkts: int = 0) -> RxStats:
+    def run_loop(self, max_pkts: int = 0, idle_rounds: int = 1, idle_us: int = 0, max_us: int = 0,
+                 forward: Forwarder | None = None) -> RxStats:
+        """mosrx_rx_loop_ex over this backend; `forward`: the mosrx_forward_frame consumer."""
         st = RxStats()
-        _chk(lib().mosrx_rx_loop(C.addressof(self.m), self.ctx, self.nif, max_pkts, None, None,
-                                 C.byref(st)), "mosrx_rx_loop")
+        o = RxLoopOpts(max_pkts, idle_rounds, idle_us, max_us)
+        fn = C.cast(lib().mosrx_forward_frame, C.c_void_p) if forward is not None else None
+        _chk(lib().mosrx_rx_loop_ex(C.addressof(self.m), self.ctx, self.nif, C.byref(o), fn,
+                                    C.byref(forward) if forward is not None else None, C.byref(st)),
+             "mosrx_rx_loop_ex")
         return st
 
     def close(self):
@@ -777,6 +872,53 @@ def mem_source(frames: np.ndarray, off: np.ndarray, ln: np.ndarray, loops: int =
     if mode != SRC_BEST:
         _chk(lib().mosrx_source_mem_set_mode(s, mode), "mosrx_source_mem_set_mode")
     return s
+
+
+def afpacket_source(ifname: str, ring_blocks: int = 8, retire_ms: int = 1, fanout_group: int = 0,
+                    copy: bool = False) -> int:
+    """mosrx_source_afpacket_ex (TPACKET_V3 ring; needs CAP_NET_RAW)."""
+    o = AfpOpts(ring_blocks, retire_ms, fanout_group, int(copy))
+    s = lib().mosrx_source_afpacket_ex(ifname.encode(), C.byref(o))
+    if not s:
+        raise MosrxError(1, f"mosrx_source_afpacket_ex({ifname})")
+    return s
+
+
+def afpacket_info(src: int) -> AfpInfo:
+    i = AfpInfo()
+    _chk(lib().mosrx_source_afpacket_info(src, C.byref(i)), "mosrx_source_afpacket_info")
+    return i
+
+
+def source_tx_pcap(src: int, path: str | None) -> None:
+    _chk(lib().mosrx_source_tx_pcap(src, path.encode() if path else None), "mosrx_source_tx_pcap")
+
+
+def source_send(src: int, frame: bytes) -> int:
+    return lib().mosrx_source_send(src, frame, len(frame))
+
+
+def source_tx_stats(src: int) -> tuple[int, int, int]:
+    a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    _chk(lib().mosrx_source_tx_stats(src, C.byref(a), C.byref(b), C.byref(c)), "mosrx_source_tx_stats")
+    return a.value, b.value, c.value
+
+
+def read_pcap(path: str) -> list[bytes]:
+    """Frames of a classic pcap file through the library's own reader (mosrx_source_pcap)."""
+    s = lib().mosrx_source_pcap(path.encode(), 1)
+    if not s:
+        raise MosrxError(2, f"mosrx_source_pcap({path})")
+    buf = np.zeros(65536, np.uint8)
+    out = []
+    try:
+        while True:
+            n = lib().mosrx_source_next(s, buf.ctypes.data, len(buf))
+            if n <= 0:
+                return out
+            out.append(bytes(buf[:n]))
+    finally:
+        lib().mosrx_source_close(s)
 
 
 def shard_plan(nbatches: int, world: int, rank: int) -> list[int]:

@@ -1,0 +1,65 @@
+/*
+ * mos_boundary.c — TEST INFRASTRUCTURE ONLY (tests/test_boundary.py).
+ *
+ * Built twice by the test: once against mOS's own io_module.h / config.h
+ * (-DMOSRX_HAVE_MOS_IO_MODULE -I<reference>/core/src/include) and linked with
+ * csrc/gpu_module.c compiled the same way plus mOS's compiled core/src objects
+ * (oracle/_ref/obj), and once standalone against include/mosrx_io_module.h.
+ * Each build prints the layout of io_module_func and RssInfo; the mOS build
+ * also loads the backend's upper half as mtcp_init would (core.c:1735) and
+ * prints the globals it set.  The test compares the two layouts line by line.
+ */
+#include <stddef.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "mosrx_io_module.h"
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+#include "config.h"
+#endif
+
+#define OFF(m) printf("io_module_func.%s %zu\n", #m, offsetof(io_module_func, m))
+
+int main(void)
+{
+	OFF(load_module_upper_half); OFF(load_module_lower_half); OFF(init_handle); OFF(link_devices);
+	OFF(release_pkt); OFF(get_wptr); OFF(set_wptr); OFF(send_pkts); OFF(get_rptr); OFF(get_nif);
+	OFF(recv_pkts); OFF(select); OFF(destroy_handle); OFF(dev_ioctl);
+	printf("io_module_func.size %zu align %zu\n", sizeof(io_module_func), _Alignof(io_module_func));
+	printf("RssInfo.pktidx %zu RssInfo.hash_value %zu RssInfo.size %zu\n", offsetof(RssInfo, pktidx),
+	       offsetof(RssInfo, hash_value), sizeof(RssInfo));
+	printf("ioctl %d %d %d %d\n", PKT_TX_IP_CSUM, PKT_TX_TCP_CSUM, PKT_RX_RSS, DRV_NAME);
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+	{
+		int GetRSSCPUCore(uint32_t sip, uint32_t dip, uint16_t sp, uint16_t dp, int num_queues);
+		/* mOS's configuration as LoadConfigurationUpperHalf leaves it (config.c:1175) */
+		static struct mos_conf mc;
+		static struct netdev_conf nd;
+		static struct netdev_entry e[2];
+		mosrx_gpu_module_cfg cfg;
+		e[0].ip_addr = 0x0200000A;   /* 10.0.0.2 */
+		e[1].ip_addr = 0x0101A8C0;   /* 192.168.1.1 */
+		nd.num = 2;
+		nd.ent[0] = &e[0];
+		nd.ent[1] = &e[1];
+		mc.forward = 1;
+		mc.netdev_table = &nd;
+		g_config.mos = &mc;
+		num_queues = 0;
+		mosrx_gpu_module_cfg_default(&cfg);
+		cfg.num_ifs = 1;
+		cfg.params.num_queues = 3;
+		cfg.params.forward = 0;
+		if (mosrx_gpu_module_configure(&cfg))
+			return 1;
+		current_iomodule_func = &gpu_module_func;          /* core.c:1725-1733 */
+		current_iomodule_func->load_module_upper_half();   /* core.c:1735 */
+		mosrx_gpu_module_get_cfg(&cfg);
+		printf("num_queues %d\n", num_queues);
+		printf("forward %d num_local %u local %08x %08x\n", cfg.params.forward, cfg.params.num_local,
+		       cfg.params.local_ip[0], cfg.params.local_ip[1]);
+		printf("queue %d\n", GetRSSCPUCore(0x0A000001, 0x0A000002, 1234, 80, num_queues));   /* util.c:114 */
+	}
+#endif
+	return 0;
+}

@@ -1,0 +1,236 @@
+"""GPU tests of gpu_module_func as a faithful peer of pcap_module_func
+(pcap_module.c:34-89, :124-160), driven through the C ABI: records against the
+oracle for every way a batch reaches the GPU (per-frame, runs, zero-copy,
+groups of batches in one launch, a pcap file), pkt_info fields through
+dev_ioctl, stack-state updates, and TX (get_wptr / send_pkts) reaching the
+source."""
+import os
+import socket
+import struct
+
+import numpy as np
+import pytest
+
+import mosrx
+import oracle_py as O
+from pktlib import NREASON, icmp_frame, pack_frames, tcp_frame
+from test_parity_gpu import assert_records_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def write_pcap(path, frames, off, ln):
+    with open(path, "wb") as fh:
+        fh.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, 1))
+        for i, (o, n) in enumerate(zip(off.tolist(), ln.tolist())):
+            fh.write(struct.pack("<IIII", i, 0, n, n) + bytes(frames[o:o + n]))
+
+
+def drain(be, n_expect=None):
+    """recv_pkts until idle: (records, frames) in arrival order."""
+    recs, frames = [], []
+    while True:
+        n = be.recv_pkts(0)
+        assert n >= 0
+        if n == 0:
+            break
+        recs.append(be.results(0, n))
+        frames += [be.get_rptr(0, i) for i in range(n)]
+    return (np.concatenate(recs) if recs else np.zeros(0, mosrx.RESULT_DTYPE)), frames
+
+
+@pytest.mark.parametrize("group", [1, 3, 8])
+@pytest.mark.parametrize("mode", [mosrx.SRC_BEST, mosrx.SRC_FILL, mosrx.SRC_PER_FRAME])
+def test_groups_of_batches_one_launch(group, mode):
+    """cfg.group batches per kernel launch (the batch queue from host memory):
+    records equal the oracle over three replays of the trace, every batch a
+    separate recv_pkts, get_rptr frames intact, one timed launch per group."""
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 7000, nflows=300)
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=3, mode=mode)
+    be = mosrx.GpuBackend([src], batch=1024, pipeline=True, cpu=5, group=group, timing=True)
+    try:
+        seen, sizes = 0, []
+        ora = O.classify(t.frames, t.off, t.len, O.params())
+        while True:
+            n = be.recv_pkts(0)
+            assert n >= 0
+            if n == 0:
+                break
+            sizes.append(n)
+            idx = (seen + np.arange(n)) % t.n
+            assert_records_equal(be.results(0, n), ora[idx], f"group {group} batch@{seen}")
+            for i in (0, n - 1):
+                j = int(idx[i])
+                assert be.get_rptr(0, i) == bytes(t.frames[t.off[j]:t.off[j] + t.len[j]])
+            seen += n
+        assert seen == 3 * t.n
+        st = be.stats()
+        assert st.rx_frames == seen and st.rx_batches == len(sizes)
+        # a group ends early where the source runs dry (the replay's end), never later
+        assert -(-len(sizes) // group) <= st.kernel_launches <= len(sizes) and st.kernel_ms > 0
+        if group == 1:
+            assert st.kernel_launches == len(sizes)
+    finally:
+        be.close()
+
+
+@pytest.mark.parametrize("group", [1, 4])
+def test_tcpinfo_through_the_backend(group):
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 9000, nflows=700)
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=1)
+    be = mosrx.GpuBackend([src], batch=2048, cpu=6, group=group, tcpinfo=True)
+    try:
+        ora, _, oti = O.classify_ex(t.frames, t.off, t.len, O.params())
+        seen = 0
+        while (n := be.recv_pkts(0)) > 0:
+            assert_records_equal(be.results(0, n), ora[seen:seen + n], "records")
+            np.testing.assert_array_equal(be.tcpinfo(0, n), oti[seen:seen + n])
+            seen += n
+        assert seen == t.n
+    finally:
+        be.close()
+
+
+def test_backend_fed_from_a_pcap_file(tmp_path):
+    """mosrx_source_pcap (the libpcap-free pcap_next, pcap_module.c:41) behind the
+    backend: the trace written to a pcap file classifies exactly as the oracle
+    says, through the RunMainLoop-shaped loop and batch by batch."""
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 12000, nflows=900)
+    path = str(tmp_path / "trace.pcap")
+    write_pcap(path, t.frames, t.off, t.len)
+    ora = O.classify(t.frames, t.off, t.len, O.params())
+    src = mosrx.lib().mosrx_source_pcap(path.encode(), 1)
+    assert src
+    be = mosrx.GpuBackend([src], batch=4096, cpu=7)
+    try:
+        recs, frames = drain(be)
+        assert_records_equal(recs, ora, "pcap source")
+        assert frames[::997] == [bytes(t.frames[o:o + n]) for o, n in zip(t.off[::997], t.len[::997])]
+    finally:
+        be.close()
+    src = mosrx.lib().mosrx_source_pcap(path.encode(), 2)
+    be = mosrx.GpuBackend([src], batch=4096, cpu=8, group=2)
+    try:
+        st = be.run_loop()
+        assert st.rx_packets == 2 * t.n
+        assert list(st.by_reason) == (2 * np.bincount(ora["reason"], minlength=NREASON)).tolist()
+    finally:
+        be.close()
+
+
+def test_small_frames_through_the_backend():
+    """64 B frames (BASELINE config #2) through the backend: the batch's real max
+    caplen goes with it (not cfg.max_frame), so the SMALL tile classifies it;
+    records equal the oracle and every 32K batch is one timed launch."""
+    t = mosrx.Trace(mosrx.TRACE_S64, 32768 * 4)
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=4)
+    be = mosrx.GpuBackend([src], batch=32768, cpu=9, timing=True)
+    try:
+        recs, _ = drain(be)
+        st = be.stats()
+    finally:
+        be.close()
+    ora = O.classify(t.frames, t.off, t.len, O.params())
+    assert_records_equal(recs, np.concatenate([ora] * 4), "S64 via backend")
+    assert st.kernel_launches == 4 and st.kernel_ms > 0
+
+
+def test_set_params_ioctl_changes_the_stack_state():
+    """dev_ioctl(MOSRX_PKT_SET_PARAMS): a monitor socket appears (num_msp 0 -> 1,
+    socket.c:77-78), so checksums are verified from the next submitted batch."""
+    frames = [tcp_frame(ip_csum=0x1111), icmp_frame(dst="10.0.0.2")] * 600
+    buf, off, ln = pack_frames(frames)
+    src = mosrx.mem_source(buf, off, ln, loops=4)
+    p0 = mosrx.default_params(num_msp=0, num_esp=0)
+    be = mosrx.GpuBackend([src], batch=1200, cpu=10, params=p0, pipeline=False)
+    try:
+        n = be.recv_pkts(0)
+        r = be.results(0, n)
+        assert set(r["reason"].tolist()) == {mosrx.R["NOVERIFY_PASS"]}
+        p1 = mosrx.default_params(num_msp=1, local=["10.0.0.2"])
+        assert be.set_params(0, p1) == 0
+        n = be.recv_pkts(0)
+        r = be.results(0, n)
+        assert set(r["reason"][0::2].tolist()) == {mosrx.R["IP_BADCSUM"]}
+        assert set(r["reason"][1::2].tolist()) == {mosrx.R["ICMP_LOCAL"]}
+        assert set(r["verdict"][1::2].tolist()) == {1}
+    finally:
+        be.close()
+
+
+def test_tx_reaches_the_source(tmp_path):
+    """get_wptr + send_pkts (pcap_module.c:67-89): frames written by the
+    application leave through the source -- here its pcap dump -- in order; a
+    full TX buffer is flushed by get_wptr itself (dpdk_get_wptr).  Then the
+    RunMainLoop-shaped loop with the ForwardEthernetFrame consumer
+    (eth_out.c:105-129) sends back every frame the checks accepted."""
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 5000, nflows=300)
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=1)
+    path = str(tmp_path / "tx.pcap")
+    mosrx.source_tx_pcap(src, path)
+    be = mosrx.GpuBackend([src], batch=1024, cpu=11, tx_batch=16)
+    ora = O.classify(t.frames, t.off, t.len, O.params())
+    try:
+        mine = [tcp_frame(payload=bytes([i]) * (i * 11), seq=i) for i in range(40)]
+        for f in mine[:16]:
+            be.send(0, f)
+        assert be.send_pkts(0) == 16
+        for f in mine[16:]:               # 24 frames: the 17th get_wptr flushes the first 16
+            be.send(0, f)
+        assert be.stats().tx_packets == 32
+        assert be.send_pkts(0) == 8
+        fwd = be.forwarder([0])
+        st = be.run_loop(forward=fwd)
+        assert st.rx_packets == t.n
+        assert fwd.forwarded == int((ora["verdict"] == 1).sum()) and fwd.dropped == t.n - fwd.forwarded
+        assert be.stats().tx_packets == 40 + fwd.forwarded
+    finally:
+        be.close()
+    sent = mosrx.read_pcap(path)
+    keep = np.nonzero(ora["verdict"] == 1)[0]
+    assert sent[:40] == mine
+    assert sent[40:] == [bytes(t.frames[t.off[i]:t.off[i] + t.len[i]]) for i in keep]
+
+
+def _have_raw():
+    try:
+        socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(3)).close()
+        return True
+    except (PermissionError, OSError, AttributeError):
+        return False
+
+
+@pytest.mark.skipif(not _have_raw(), reason="needs CAP_NET_RAW for AF_PACKET")
+def test_afpacket_ring_lent_zero_copy_to_the_backend():
+    """The TPACKET_V3 ring registered with the HIP runtime: batches are runs of the
+    ring itself (no host copy), given back to the kernel when recycled."""
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 6000, nflows=100)
+    src = mosrx.afpacket_source("lo", ring_blocks=4)
+    info = mosrx.afpacket_info(src)
+    peer = socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(3))
+    peer.bind(("lo", 0))
+    be = mosrx.GpuBackend([src], batch=1024, cpu=12)
+    got = []
+    try:
+        import time
+        for k in range(0, t.n, 200):
+            for i in range(k, min(k + 200, t.n)):
+                peer.send(bytes(t.frames[t.off[i]:t.off[i] + t.len[i]]))
+            time.sleep(0.003)
+        t0 = time.time()
+        while len(got) < t.n and time.time() - t0 < 10:
+            n = be.recv_pkts(0)
+            if n <= 0:
+                time.sleep(0.002)
+                continue
+            r = be.results(0, n)
+            got += [(be.get_rptr(0, i), r[i]) for i in range(n)]
+    finally:
+        be.close()
+        peer.close()
+    mine = [(f, r) for f, r in got if f[0:6] == bytes(t.frames[t.off[0]:t.off[0] + 6])]
+    assert len(mine) == t.n
+    assert [f for f, _ in mine] == [bytes(t.frames[o:o + n]) for o, n in zip(t.off, t.len)]
+    ora = O.classify(t.frames, t.off, t.len, O.params())
+    assert_records_equal(np.array([r for _, r in mine], mosrx.RESULT_DTYPE), ora, "afpacket")
+    assert info.zero_copy == 1

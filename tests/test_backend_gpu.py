@@ -122,7 +122,7 @@ def test_small_frames_through_the_backend():
     """64 B frames (BASELINE config #2) through the backend: the batch's real max
     caplen goes with it (not cfg.max_frame), so the SMALL tile classifies it;
     records equal the oracle and every 32K batch is one timed launch."""
-    t = mosrx.Trace(mosrx.TRACE_S64, 32768 * 4)
+    t = mosrx.Trace(mosrx.TRACE_S64, 32768)
     src = mosrx.mem_source(t.frames, t.off, t.len, loops=4)
     be = mosrx.GpuBackend([src], batch=32768, cpu=9, timing=True)
     try:

@@ -1,19 +1,27 @@
 #!/usr/bin/env python3
 """bench.py — device-resident throughput of the MI355X rx classifier.
 
-One "step" = one pass of the hot path (mOS ProcessPacket checks + ip_fast_csum
-+ TCPCalcChecksum + Toeplitz RSS / queue map) over one batch per GPU, inputs
-already resident in HBM.  The headline workload is BASELINE config #3
-(1500 B MTU TCP segments, 1M flows, batch 64K) whose GB/s the north star
-prices against the HBM roofline; the same run also measures config #2
-(64 B, 1 flow, batch 32K; Mpkts/s) and config #4 (IMIX, batch 256K).
+The hot path: mOS's ProcessPacket checks + ip_fast_csum + TCPCalcChecksum +
+Toeplitz RSS / queue map, over batches of frames already resident in HBM.
 
-Multi-GPU (torchrun, one process per GPU): batches are split round-robin over
-the GPUs with no collective on the data path (`scaling: weak`); gloo carries
-only the barrier and the max-over-ranks of the timed region.
+One STEP = one rx round over the resident batches of one rx ring: R batches of
+the workload's batch size (each batch its own frames, descriptors and records),
+classified by ONE launch of the batch-queue kernel (mosrx_queue_run), which is
+how gpu_module_func services a group of received batches (cfg.group).  The
+headline workload is BASELINE config #3 (1500 B MTU TCP segments, 1M flows,
+batch 64K, R = 8); the same run measures config #2 (64 B, 1 flow, batch 32K,
+R = 256) and config #4 (IMIX, batch 256K, R = 8), the single-batch launches
+of each (`*_1`: one kernel per batch, 2 batches in flight), the §8f rows, the
+CPU baselines (the oracle and mOS's own compiled functions on this host's
+cores, config #1 included) and the end-to-end / backend rates.
 
-Each rank cycles over several copies of its batch at distinct HBM addresses so
-the working set exceeds the 256 MiB Infinity Cache: every timed pass reads HBM.
+Multi-GPU (torchrun, one process per GPU): the job is one sequence of batches
+split round-robin over the GPUs (mosrx.shard_plan), no
+collective on the data path (`scaling: weak`); gloo carries only the barrier
+and the max-over-ranks of the timed region.
+
+Each rank keeps >= 1.2 GB of distinct resident batches and cycles over them, so
+no timed pass is served from the 256 MiB Infinity Cache.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -36,31 +44,35 @@ import mosrx  # noqa: E402  (loads libmosrx.so before torch so one HIP runtime i
 METRIC = "Mpkts/s + GB/s device-resident checksum+RSS classify, 64B & 1500B batches"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 DESC_BYTES, RESULT_BYTES = 6, 16
-L3_BYTES = 256 << 20
+RESIDENT_BYTES = 1200 << 20    # working set per rank: well past the 256 MiB Infinity Cache
 
+# key: (trace kind, batch, batches per step (ring) or 0 (one launch per batch), label)
 WORKLOADS = {
-    # key: (trace kind, batch, label)
-    "M1500": (mosrx.TRACE_M1500, 65_536, "1xMI355X 1500B MTU TCP segments, 1M distinct 5-tuples, batch=64K (BASELINE config #3)"),
-    "S64": (mosrx.TRACE_S64, 32_768, "1xMI355X 64B TCP, 1 flow, batch=32K (BASELINE config #2), full verdict"),
-    "S64_hdr": (mosrx.TRACE_S64, 32_768, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum)"),
-    "IMIX": (mosrx.TRACE_IMIX, 262_144, "IMIX 60/590/1514 7:4:1, 1M flows, batch=256K (BASELINE config #4)"),
-    "S64_queue": (mosrx.TRACE_S64, 32_768, "config #2, 64 batches of 32K per launch (device batch queue)"),
-    "M1500_queue": (mosrx.TRACE_M1500, 65_536, "config #3, 4 batches of 64K per launch (device batch queue)"),
-    # SURVEY.md §8f rows measured on the same traces
-    "M1500_fh": (mosrx.TRACE_M1500, 65_536, "config #3 classify + flow-table hash (HashFlow of FindStream's tuple)"),
-    "M1500_tx": (mosrx.TRACE_M1500, 65_536, "config #3 TX checksum rewrite (MOS_UPDATE_IP|TCP_CHKSUM), in place"),
-    "IMIX_bpf": (mosrx.TRACE_IMIX, 262_144, "config #4 batched BPF, 8 mOS filter programs (sfbpf_compile output)"),
-    "IMIX_cls_bpf": (mosrx.TRACE_IMIX, 262_144, "config #4 classify + the 8 BPF programs fused in one pass"),
+    "M1500": (mosrx.TRACE_M1500, 65_536, 8, "1xMI355X 1500B MTU TCP segments, 1M distinct 5-tuples, batch=64K (BASELINE config #3)"),
+    "S64": (mosrx.TRACE_S64, 32_768, 256, "1xMI355X 64B TCP, 1 flow, batch=32K (BASELINE config #2), full verdict"),
+    "S64_hdr": (mosrx.TRACE_S64, 32_768, 256, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum)"),
+    "IMIX": (mosrx.TRACE_IMIX, 262_144, 8, "IMIX 60/590/1514 7:4:1, 1M flows, batch=256K (BASELINE config #4)"),
+    # one kernel launch per batch, two batches in flight (two rx queues)
+    "M1500_1": (mosrx.TRACE_M1500, 65_536, 0, "config #3, one launch per 64K batch"),
+    "S64_1": (mosrx.TRACE_S64, 32_768, 0, "config #2, one launch per 32K batch"),
+    "IMIX_1": (mosrx.TRACE_IMIX, 262_144, 0, "config #4, one launch per 256K batch"),
+    # SURVEY.md §8f rows measured on the same traces (one launch per batch)
+    "M1500_fh": (mosrx.TRACE_M1500, 65_536, 0, "config #3 classify + flow-table hash (HashFlow of FindStream's tuple)"),
+    "M1500_ti": (mosrx.TRACE_M1500, 65_536, 0, "config #3 classify + pkt_info TCP fields (FillPacketContextTCPInfo)"),
+    "M1500_tx": (mosrx.TRACE_M1500, 65_536, 0, "config #3 TX checksum rewrite (MOS_UPDATE_IP|TCP_CHKSUM), in place"),
+    "IMIX_bpf": (mosrx.TRACE_IMIX, 262_144, 0, "config #4 batched BPF, 8 mOS filter programs (sfbpf_compile output)"),
+    "IMIX_cls_bpf": (mosrx.TRACE_IMIX, 262_144, 0, "config #4 classify + the 8 BPF programs fused in one pass"),
 }
-OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_tx": mosrx.OP_TX_CSUM, "IMIX_bpf": mosrx.OP_BPF,
-       "IMIX_cls_bpf": mosrx.OP_CLASSIFY_BPF}
+DEFAULT_WORKLOADS = "M1500,S64,S64_hdr,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,M1500_tx,IMIX_bpf,IMIX_cls_bpf"
+OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_ti": mosrx.OP_CLASSIFY_TI, "M1500_tx": mosrx.OP_TX_CSUM,
+       "IMIX_bpf": mosrx.OP_BPF, "IMIX_cls_bpf": mosrx.OP_CLASSIFY_BPF}
 # filter expressions whose compiled programs (tests/golden/bpf.npz, mOS's own compiler) the BPF row runs
 BPF_BENCH = [("tcp", 0), ("tcp port 80", 0), ("tcp[tcpflags] & tcp-syn != 0", 1), ("net 192.168.0.0/16 and tcp", 1),
              ("host 10.0.0.1 and port 80", 0), ("ip[8] < 64", 1), ("tcp[((tcp[12:1] & 0xf0) >> 2):4] = 0x47455420", 1),
              ("portrange 1000-2000", 0)]
-QUEUE_DEPTH = {"S64_queue": 64, "M1500_queue": 4}   # resident batches per queue launch
 PREWARM_S = 0.3
-STREAMS = 2   # rx batches in flight per GPU (scripts/tune_streams.py: 2 beats 1 and 4)
+STREAMS = 2      # rx batches in flight per GPU for the one-launch-per-batch rows
+DISTINCT = 8     # distinct batch contents generated per rank (the rest are resident copies of them)
 
 
 def dist_env():
@@ -98,18 +110,29 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def job_seed(kind: int, b: int) -> int:
+    """Seed of the job's batch b: batch 0 is the default seeded trace of the config
+    (BASELINE.md §3), every later batch its own deterministic content."""
+    return 0 if b == 0 else ((mosrx.TRACE_SEED_BASE + kind) ^ (b * 0x9E3779B97F4A7C15)) & (2**64 - 1) or 1
+
+
+def job_batches(nbatches: int, world: int, rank: int) -> list[int]:
+    """The batches of the job this rank classifies: config #5's round-robin split."""
+    return mosrx.shard_plan(nbatches, world, rank)
+
+
 def algo_bytes(tr: mosrx.Trace, key: str = "") -> int:
     """B_i = caplen_i + 6 (offset+len descriptor) + 16 (result record).
-    Flow hash: + 4 B per frame.  TX rewrite: caplen + 6 read, 4 B written (no records).
-    BPF: the 6-byte descriptor + 4-byte mask + 64 header bytes per frame (the
-    line a filter reads; deeper loads are extra)."""
+    Flow hash: + 4 B per frame; pkt_info fields: + 12 B.  TX rewrite: caplen + 6 read,
+    4 B written (no records).  BPF: the 6-byte descriptor + 4-byte mask + 64 header
+    bytes per frame (the line a filter reads; deeper loads are extra)."""
     if key.endswith("_tx"):
         return tr.caplen_sum + tr.n * (DESC_BYTES + 4)
     if key.endswith("_cls_bpf"):   # the classify bytes + the 4-byte match mask
         return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES + 4)
     if key.endswith("_bpf"):
         return tr.n * (DESC_BYTES + 4) + int(np.minimum(tr.len, 64).astype(np.int64).sum())
-    extra = 4 if key.endswith("_fh") else 0
+    extra = 4 if key.endswith("_fh") else 12 if key.endswith("_ti") else 0
     return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES + extra)
 
 
@@ -147,45 +170,62 @@ def median_of(fn, reps: int = 5) -> float:
     return float(np.median([fn() for _ in range(reps)]))
 
 
+def resident_batches(ctx, key, world, rank, nres):
+    """`nres` resident batches of this rank's share of the job: the contents of its
+    first job batches (seeded per job batch; DISTINCT of them for a ring, 2 for the
+    one-launch rows), cycled over distinct HBM buffers.  Returns (device batches,
+    traces used, their job batch indices)."""
+    kind, batch, ring, _ = WORKLOADS[key]
+    nd = min(DISTINCT, ring) if ring else 2
+    mine = job_batches(world * nd, world, rank)[:nd]
+    trs = [mosrx.Trace(kind, batch, seed=job_seed(kind, b)) for b in mine]
+    dbs = [ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len)
+           for t in (trs[i % len(trs)] for i in range(nres))]
+    return dbs, trs, mine
+
+
 def measure(ctx, dist, key, steps, warmup, rank):
-    kind, batch, label = WORKLOADS[key]
+    kind, batch, ring, label = WORKLOADS[key]
     params = mosrx.default_params(skip_tcp_csum=1 if key == "S64_hdr" else 0)
     ctx.set_params(params)
-    # rank r owns the batches b = r, r+N, ... of the job's round-robin split; the
-    # synthetic content differs per rank (seed), the shape does not.
-    tr = mosrx.Trace(kind, batch, seed=0 if rank == 0 else 0x6D4F5321 + kind + 1000 * rank)
-    ncopy = max(2, -(-2 * L3_BYTES // max(tr.frames_bytes, 1)))
-    ncopy = min(max(ncopy, 2 * QUEUE_DEPTH.get(key, 1)), 256)
-    dbs = [ctx.upload(tr.frames, tr.off, tr.len, frames_bytes=tr.frames_bytes, max_len=tr.max_len)
-           for _ in range(ncopy)]
+    probe = mosrx.Trace(kind, batch)
+    per_batch = max(probe.frames_bytes, 1)
+    if ring:
+        nres = max(2 * ring, -(-RESIDENT_BYTES // per_batch))
+        nres = -(-nres // ring) * ring                     # whole rings
+    else:
+        nres = min(256, max(2, -(-RESIDENT_BYTES // per_batch)))
+    dbs, trs, mine = resident_batches(ctx, key, dist.ws, rank, nres)
+    tr = trs[0]
     ab = algo_bytes(tr, key)
     if key in OPS:
         op = OPS[key]
         arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op == mosrx.OP_TX_CSUM else 0
         if op in (mosrx.OP_BPF, mosrx.OP_CLASSIFY_BPF):
             ctx.bpf_set(bpf_bench_programs())
-        prewarm(lambda: ctx.time_op(op, dbs, 200, STREAMS, arg, kernels=False))
+        step_fn = lambda k, ns: ctx.time_op(op, dbs, k, ns, arg, kernels=False)[0]   # noqa: E731
+        prewarm(lambda: step_fn(200, STREAMS))
         if warmup:
-            ctx.time_op(op, dbs, warmup, STREAMS, arg, kernels=False)
+            step_fn(warmup, STREAMS)
         ctx.device_sync()
         dist.barrier()
         t0 = time.perf_counter()
-        dev_ms, _ = ctx.time_op(op, dbs, steps, STREAMS, arg, kernels=False)
+        dev_ms = step_fn(steps, STREAMS)
         ctx.device_sync()
         dist.barrier()
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         kk = 500
-        kern_ms = median_of(lambda: ctx.time_op(op, dbs, kk, 1, arg, kernels=False)[0] / kk)
-        _, kern_iso = ctx.time_op(op, dbs, kk, 1, arg, total=False)
-    elif key.endswith("_queue"):
-        # each step = one launch over `depth` distinct resident batches
-        depth = QUEUE_DEPTH[key]
-        # several queues over disjoint batch copies: the working set exceeds the L3
-        qs = [ctx.queue(dbs[i:i + depth]) for i in range(0, len(dbs) - depth + 1, depth)]
-        ab *= depth
-        batch *= depth
-        prewarm(lambda: qs[0].time(20, qs[1:], kernels=False))
+        kern_ms = median_of(lambda: step_fn(kk, 1) / kk)
+        kern_iso = None
+        frames_per_step, ab_step = batch, ab
+        method = f"one launch per batch, batch i on stream i % {STREAMS}"
+    elif ring:
+        # each step = ONE queue launch over `ring` distinct resident batches (an rx
+        # ring serviced at once, gpu_module_func cfg.group); several rings over
+        # disjoint resident copies cycle so the working set stays past the L3
+        qs = [ctx.queue(dbs[i:i + ring]) for i in range(0, len(dbs), ring)]
+        prewarm(lambda: qs[0].time(8, qs[1:], kernels=False))
         if warmup:
             qs[0].time(warmup, qs[1:], kernels=False)
         ctx.device_sync()
@@ -196,13 +236,14 @@ def measure(ctx, dist, key, steps, warmup, rank):
         dist.barrier()
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
-        kk = min(steps, 64)
+        kk = max(16, 4 * len(qs))
         kern_ms = median_of(lambda: qs[0].time(kk, qs[1:], kernels=False)[0] / kk)
-        _, kern_iso = qs[0].time(kk, qs[1:])
+        _, kern_iso = qs[0].time(min(kk, 32), qs[1:])
         for q in qs:
             q.destroy()
+        frames_per_step, ab_step = batch * ring, ab * ring
+        method = f"one batch-queue launch per step over {ring} resident batches"
     else:
-        # warmup (untimed)
         prewarm(lambda: ctx.time_dev_streams(dbs, 200, STREAMS))
         if warmup:
             ctx.time_dev_streams(dbs, warmup, STREAMS)
@@ -223,24 +264,30 @@ def measure(ctx, dist, key, steps, warmup, rank):
         kk = 500
         kern_ms = median_of(lambda: ctx.time_dev_streams(dbs, kk, 1) / kk)
         kern_iso = ctx.time_dev_kernels(dbs, kk)
+        frames_per_step, ab_step = batch, ab
+        method = f"one launch per batch, batch i on stream i % {STREAMS}"
     for d in dbs:
         d.free()
     n = dist.ws
     out = {
         "workload": label,
         "batch": batch,
+        "batches_per_step": ring or 1,
+        "method": method,
         "frames_bytes_per_batch": tr.frames_bytes,
         "algo_bytes_per_batch": ab,
-        "resident_copies": ncopy,
+        "resident_batches": len(dbs),
+        "resident_bytes": int(sum(t.frames_bytes for t in (trs[i % len(trs)] for i in range(len(dbs))))),
+        "job_batches": mine,
         "wall_s": wall_max,
         "ms_per_step": 1e3 * wall_max / steps,
-        "gbps": n * ab * steps / wall_max / 1e9,
-        "mpkts": n * batch * steps / wall_max / 1e6,
-        "device_ms_per_batch": dev_ms / steps,
+        "gbps": n * ab_step * steps / wall_max / 1e9,
+        "mpkts": n * frames_per_step * steps / wall_max / 1e6,
+        "device_ms_per_step": dev_ms / steps,
         "kernel_ms": kern_ms,
         "kernel_ms_isolated": kern_iso,
     }
-    achieved = ab / (kern_ms * 1e-3) / 1e9
+    achieved = ab_step / (kern_ms * 1e-3) / 1e9
     pmc = load_pmc(key)
     out["roofline"] = {
         "bound": "hbm",
@@ -255,7 +302,24 @@ def measure(ctx, dist, key, steps, warmup, rank):
     return out, tr
 
 
-def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0):
+def cpu_threads():
+    """Threads for the all-cores CPU leg: the process's CPU affinity, capped by the
+    box's CPU share when the environment states it (OMP_NUM_THREADS / MOSRX_CPU_THREADS:
+    16 per GPU on the pool's boxes, whose nproc shows the whole machine)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("MOSRX_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(cap))) if cap else aff, aff
+
+
+def host_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            return next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
+    except OSError:
+        return ""
+
+
+def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, all_cores: bool = True):
     """The oracle (bit-exact C restatement, oracle/mosrx_oracle.c) on this host's cores.
 
     Reported baseline only; never the measured product path."""
@@ -263,8 +327,6 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0):
     import oracle_py as O
     p = O.params(skip_tcp_csum=1 if key == "S64_hdr" else 0)
     ab = algo_bytes(tr, key)
-    cores_avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores_all = max(1, min(16, cores_avail))
 
     if key in OPS:
         return cpu_baseline_row(tr, key, min_s, O)
@@ -279,30 +341,31 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0):
                 return reps, el
 
     r1, e1 = run(1)
-    rn, en = run(cores_all)
-    model = ""
-    try:
-        with open("/proc/cpuinfo") as fh:
-            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), "")
-    except OSError:
-        pass
-    gb1, gbn = r1 * ab / e1 / 1e9, rn * ab / en / 1e9
-    return {
+    gb1 = r1 * ab / e1 / 1e9
+    out = {
         "value": round(gb1, 3), "unit": "GB/s", "cores": 1, "kind": "port",
         "mpkts": round(r1 * tr.n / e1 / 1e6, 3),
         "sample": f"{r1} passes over one {tr.n}-frame batch of this workload ({e1:.1f} s), "
-                  f"oracle/mosrx_oracle.c mo_classify, 1 thread; host '{model}', nproc {os.cpu_count()}",
-        "all_cores": {"value": round(gbn, 3), "unit": "GB/s", "cores": cores_all,
-                      "mpkts": round(rn * tr.n / en / 1e6, 3),
-                      "sample": f"{rn} passes, {cores_all} pthreads over disjoint slices ({en:.1f} s)"},
+                  f"oracle/mosrx_oracle.c mo_classify, 1 thread; host '{host_model()}', nproc {os.cpu_count()}",
     }
+    if all_cores:
+        nt, aff = cpu_threads()
+        rn, en = run(nt)
+        gbn = rn * ab / en / 1e9
+        out["all_cores"] = {"value": round(gbn, 3), "unit": "GB/s", "cores": nt, "affinity": aff,
+                            "mpkts": round(rn * tr.n / en / 1e6, 3),
+                            "sample": f"{rn} passes, {nt} pthreads over disjoint slices ({en:.1f} s); "
+                                      f"process affinity {aff} CPUs"}
+    return out
 
 
 def cpu_reference(tr: mosrx.Trace, key: str, seconds: float):
-    """mOS's own compiled functions (oracle/_ref/mosref --time: the header checks,
-    ip_fast_csum, TCPCalcChecksum, GetRSSHash, GetRSSCPUCore per frame) on one
-    host core, when the reference build travelled with the tree; else None.
-    A reported baseline beside the port, never the measured path."""
+    """mOS's own compiled functions (oracle/_ref/mosref --time: ref_frame, i.e. the
+    header checks of eth_in.c / ip_in.c / tcp.c, ip_fast_csum, TCPCalcChecksum,
+    GetRSSHash, GetRSSCPUCore per frame -- not ProcessPacket, whose stream
+    lookup is out of scope) on one host core, when the reference build
+    travelled with the tree; else None.  A reported baseline, never the
+    measured path."""
     exe = os.path.join(ROOT, "oracle", "_ref", "mosref")
     if not os.access(exe, os.X_OK):
         return None
@@ -323,17 +386,17 @@ def cpu_reference(tr: mosrx.Trace, key: str, seconds: float):
             "kind": "reference", "mpkts": round(r["mpkts"], 3),
             "sample": f"{r['passes']} passes over one {tr.n}-frame batch ({el:.1f} s), mOS core/src "
                       f"ip_fast_csum + TCPCalcChecksum + GetRSSHash + GetRSSCPUCore + header checks "
-                      f"(oracle/_ref/mosref --time), 1 thread"}
+                      f"(oracle/_ref/mosref --time: ref_frame, not ProcessPacket), 1 thread"}
 
 
 def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
-    """The oracle for a §8f row (flow hash / TX rewrite / BPF), one thread."""
+    """The oracle for a §8f row (flow hash / pkt_info / TX rewrite / BPF), one thread."""
     ab = algo_bytes(tr, key)
     progs = bpf_bench_programs() if key.endswith("_bpf") else None
     reps, t0 = 0, time.perf_counter()
     while True:
-        if key.endswith("_fh"):
-            O.classify_fh(tr.frames, tr.off, tr.len, O.params())
+        if key.endswith("_fh") or key.endswith("_ti"):
+            O.classify_ex(tr.frames, tr.off, tr.len, O.params())
         elif key.endswith("_tx"):
             O.tx_csum(tr.frames, tr.off, tr.len, mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM)
         elif key.endswith("_cls_bpf"):
@@ -346,10 +409,34 @@ def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
         if el >= min_s:
             break
     fn = ("mo_classify + mo_bpf_eval" if key.endswith("_cls_bpf") else
-          {"_fh": "mo_classify_fh", "_tx": "mo_tx_csum", "bpf": "mo_bpf_eval"}[key[-3:]])
+          {"_fh": "mo_classify_ex", "_ti": "mo_classify_ex", "_tx": "mo_tx_csum", "bpf": "mo_bpf_eval"}[key[-3:]])
     return {"value": round(reps * ab / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "mpkts": round(reps * tr.n / el / 1e6, 3),
             "sample": f"{reps} passes over one {tr.n}-frame batch ({el:.1f} s), oracle {fn}, 1 thread"}
+
+
+def measure_fw64(ctx, seconds: float):
+    """BASELINE config #1: simple_firewall's rx path on ONE core, 10 000 x 60 B
+    frames of one flow, the firewall's stack state (num_msp=1, forward=1,
+    num_queues=1, i40e map).  libpcap and the sample cannot be
+    built here, so the CPU-only run is timed as mOS's own
+    compiled per-frame functions (mosref --time) and as the oracle, both on one
+    core; the GPU classifying the same 10K batch is reported beside them."""
+    tr = mosrx.Trace(mosrx.TRACE_FW64, 10_000)
+    out = {"workload": "config #1: simple_firewall state, 1 core, 10k x 64B (60 B caplen), one flow",
+           "batch": tr.n, "algo_bytes_per_batch": algo_bytes(tr)}
+    ref = cpu_reference(tr, "FW64", seconds)
+    port = cpu_baseline(tr, "FW64", min_s=seconds, all_cores=False)
+    if ref:
+        port["reference"] = ref
+    out["cpu_baseline"] = port
+    ctx.set_params(mosrx.default_params())
+    db = ctx.upload(tr.frames, tr.off, tr.len, frames_bytes=tr.frames_bytes, max_len=tr.max_len)
+    k = ctx.time_dev_streams([db], 500, 1) / 500
+    db.free()
+    out["gpu_device_resident"] = {"kernel_ms": k, "mpkts": tr.n / (k * 1e-3) / 1e6,
+                                  "method": "500 back-to-back launches over the resident 10K batch"}
+    return out
 
 
 def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
@@ -379,42 +466,54 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
             "method": "pinned hipHostMalloc staging (one block: frames | off | len), one H2D copy, kernel, D2H records; 2 streams"}
 
 
-def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int):
+def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1):
     """The drop-in boundary's own rate: mosrx_rx_loop (RunMainLoop's rx section,
     core.c:897-909) over gpu_module_func (io_module.h:63-78) fed by an in-memory
-    source replaying the trace — per batch: source -> pinned staging, H2D,
-    classify, D2H records, then the per-frame get_rptr + NETSTAT walk on the
-    host, with batch k+1 in flight while k is consumed.  Recorded in DESIGN.md;
-    never the bench value."""
+    source replaying the trace — per group of batches: source -> pinned
+    staging, H2D, ONE classify launch, D2H records, then the per-frame get_rptr
+    + NETSTAT walk on the host, with the next group in flight while this one is
+    consumed.  The kernels are timed with HIP events (device time per batch);
+    the host loop's rate is reported beside it.  Never the bench value."""
     ctx_batch = {"S64": 32_768, "M1500": 65_536, "IMIX": 262_144}[key]
     loops = max(1, frames_target // tr.n)
     src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
-    be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu)
+    be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
+                          group=group, timing=True)
     try:
-        be.run_loop(max_pkts=2 * ctx_batch)            # warm-up: staging sized, module loaded
+        be.run_loop(max_pkts=2 * ctx_batch * group)    # warm-up: staging sized, module loaded
+        st0 = be.stats()
         t0 = time.perf_counter()
         st = be.run_loop()
         dt = time.perf_counter() - t0
+        st1 = be.stats()
     finally:
         be.close()
     n = int(st.rx_packets)
     nb = n / tr.n
+    launches = st1.kernel_launches - st0.kernel_launches
+    kms = st1.kernel_ms - st0.kernel_ms
+    batches = st1.rx_batches - st0.rx_batches
+    dev_us = 1e3 * kms / max(batches, 1)
+    ab = algo_bytes(tr) * (ctx_batch / tr.n)
     return {"mpkts": n / dt / 1e6, "gbps": nb * algo_bytes(tr) / dt / 1e9, "frames": n, "seconds": round(dt, 3),
-            "method": "mosrx_rx_loop over gpu_module_func (pipelined), in-memory source replaying the trace"}
+            "group": group, "kernel_launches": int(launches), "batches": int(batches),
+            "device_us_per_batch": round(dev_us, 3),
+            "device_roofline_frac": round(ab / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if dev_us > 0 else None,
+            "method": f"mosrx_rx_loop over gpu_module_func (pipelined, {group} batch(es) per launch), "
+                      f"in-memory source replaying the trace; device time = HIP events around each kernel"}
 
 
 def main():
     global STREAMS
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--workloads",
-                    default="M1500,S64,S64_hdr,S64_queue,M1500_queue,IMIX,M1500_fh,M1500_tx,IMIX_bpf,IMIX_cls_bpf")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workloads", default=DEFAULT_WORKLOADS)
     ap.add_argument("--streams", type=int, default=STREAMS,
-                    help="rx batches in flight (1 = strictly serial launches, as for rocprof summaries)")
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (PCIe) leg")
+                    help="batches in flight for the one-launch-per-batch rows (1 = strictly serial launches)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (PCIe) and backend legs")
     args = ap.parse_args()
     STREAMS = args.streams
 
@@ -423,7 +522,7 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {ws}", file=sys.stderr)
     dist = Dist(ws, rank)
     # MOSRX_BENCH_DEVICE pins every rank to one device: a rehearsal of the
-    # multi-rank path on a one-GPU box (scripts/gpu_r1_dist.sh), never a result
+    # multi-rank path on a one-GPU box, never a result
     device = int(os.environ.get("MOSRX_BENCH_DEVICE", local))
     ctx = mosrx.Context(device)
     keys = [k for k in args.workloads.split(",") if k]
@@ -439,8 +538,11 @@ def main():
     if not args.no_e2e and "M1500" in traces:
         e2e = {k: measure_e2e(ctx, traces[k], {"M1500": 60, "S64": 800}[k]) for k in ("M1500", "S64") if k in traces}
         # the gpu_module_func backend itself (host thread = this rank)
-        e2e["backend"] = {k: measure_backend(traces[k], k, {"S64": 16_000_000, "M1500": 2_000_000}.get(k, 4_000_000), device)
+        e2e["backend"] = {k: measure_backend(traces[k], k, {"S64": 16_000_000, "M1500": 2_000_000}.get(k, 4_000_000),
+                                             device)
                           for k in ("M1500", "S64", "IMIX") if k in traces}
+        if "S64" in traces:   # 64 batches of 32K per launch: the launch-amortised rx ring
+            e2e["backend"]["S64_group64"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=64)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
         head = "M1500" if "M1500" in traces else keys[0]
@@ -455,6 +557,11 @@ def main():
                     ref = cpu_reference(traces[k], k, 2.0)
                     if ref:
                         results[k]["cpu_baseline"]["reference"] = ref
+        results["FW64"] = measure_fw64(ctx, 2.0)
+    read_ceiling = None
+    if rank == 0:
+        # the box's streaming-read ceiling over a 1.5 GB working set (no Infinity-Cache hits)
+        read_ceiling = round(ctx.probe_read_bw(128 << 20, 12, 96), 1)
     ctx.close()
     dist.close()
     if rank != 0:
@@ -474,13 +581,16 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded splitmix64 traces, BASELINE.md §3)",
+        "data": "synthetic (seeded splitmix64 traces, BASELINE.md §3; one job trace split round-robin over ranks)",
         "config": {"workload": h["workload"], "batch": h["batch"],
+                   "batches_per_step": h["batches_per_step"],
+                   "step": h["method"],
                    "algo_bytes_per_batch": h["algo_bytes_per_batch"],
-                   "parallelism": f"replicas x{ws}: batches round-robin per GPU, no collectives",
-                   "streams_per_gpu": STREAMS,
-                   "resident_copies": h["resident_copies"]},
+                   "parallelism": f"replicas x{ws}: the job's batches round-robin per GPU (shard_plan), no collectives",
+                   "resident_batches": h["resident_batches"],
+                   "resident_bytes": h["resident_bytes"]},
         "roofline": h["roofline"],
+        "read_ceiling_gbps": read_ceiling,
         "cpu_baseline": cpu,
         "secondary": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in r.items()}
                       for k, r in results.items() if k != head},

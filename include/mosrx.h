@@ -280,7 +280,7 @@ int  mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
  * (TX_CSUM, `arg` = its flags); aux[i]: flow hashes (CLASSIFY_FH), match masks
  * (CLASSIFY_BPF). */
 enum { MOSRX_OP_CLASSIFY = 0, MOSRX_OP_CLASSIFY_FH = 1, MOSRX_OP_BPF = 2, MOSRX_OP_TX_CSUM = 3,
-       MOSRX_OP_CLASSIFY_BPF = 4 };
+       MOSRX_OP_CLASSIFY_BPF = 4, MOSRX_OP_CLASSIFY_TI = 5 /* aux[i]: mosrx_tcpinfo side arrays */ };
 int  mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
                    void *const *aux, uint32_t iters, uint32_t nstreams, float *total_ms, float *avg_kernel_ms);
 /* The device's streaming-read ceiling: `iters` coalesced 16-byte-load passes

@@ -991,6 +991,7 @@ static int run_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, void *out
 	case MOSRX_OP_BPF: return mosrx_bpf_dev(c, b, (uint32_t *)out, s);
 	case MOSRX_OP_TX_CSUM: return mosrx_tx_csum_dev(c, b, arg, s);
 	case MOSRX_OP_CLASSIFY_BPF: return mosrx_classify_bpf_dev(c, b, (mosrx_result *)out, (uint32_t *)aux, s);
+	case MOSRX_OP_CLASSIFY_TI: return mosrx_classify_dev_ex(c, b, (mosrx_result *)out, NULL, (mosrx_tcpinfo *)aux, s);
 	default: return -EINVAL;
 	}
 }
@@ -1077,8 +1078,8 @@ int mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t 
 {
 	int rc;
 	if (!c || !b || nb == 0 || iters == 0 || nstreams == 0 || nstreams > MOSRX_MAX_STREAMS ||
-	    op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_CLASSIFY_BPF || (op != MOSRX_OP_TX_CSUM && !out) ||
-	    ((op == MOSRX_OP_CLASSIFY_FH || op == MOSRX_OP_CLASSIFY_BPF) && !aux))
+	    op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_CLASSIFY_TI || (op != MOSRX_OP_TX_CSUM && !out) ||
+	    ((op == MOSRX_OP_CLASSIFY_FH || op == MOSRX_OP_CLASSIFY_BPF || op == MOSRX_OP_CLASSIFY_TI) && !aux))
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
 	if (total_ms && (rc = time_streams(c, op, arg, b, nb, out, aux, iters, nstreams, total_ms)))

@@ -45,6 +45,7 @@ def shape_variant(kind: int, nt_tails: bool = True) -> int:
 
 QMAP_I40E, QMAP_IXGBE = 1, 0
 TRACE_FW64, TRACE_S64, TRACE_M1500, TRACE_IMIX = 0, 1, 2, 3
+TRACE_SEED_BASE = 0x6D4F5321   # MOSRX_TRACE_SEED: seed 0 selects TRACE_SEED_BASE + kind
 WINDOW_END = 94
 
 MS_KEY = bytes([0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
@@ -73,7 +74,7 @@ class Batch(C.Structure):
 BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])   # mosrx_bpf_insn
 BPF_LEN_FRAME, BPF_LEN_IP = 0, 1
 TX_IP_CSUM, TX_TCP_CSUM = 1 << 4, 1 << 5   # MOS_UPDATE_IP_CHKSUM / MOS_UPDATE_TCP_CHKSUM
-OP_CLASSIFY, OP_CLASSIFY_FH, OP_BPF, OP_TX_CSUM, OP_CLASSIFY_BPF = 0, 1, 2, 3, 4
+OP_CLASSIFY, OP_CLASSIFY_FH, OP_BPF, OP_TX_CSUM, OP_CLASSIFY_BPF, OP_CLASSIFY_TI = 0, 1, 2, 3, 4, 5
 BPF_MAX_PROGS = 32
 
 
@@ -607,11 +608,14 @@ class Context:
         for d in dbs:
             if op == OP_CLASSIFY_FH and d.d_fhash is None:
                 d.d_fhash = DevBuffer(self, max(d.n * 4, 4))
+            if op == OP_CLASSIFY_TI and d.d_tinfo is None:
+                d.d_tinfo = DevBuffer(self, max(d.n * 12, 12))
             if op in (OP_BPF, OP_CLASSIFY_BPF) and d.d_match is None:
                 d.d_match = DevBuffer(self, max(d.n * 4, 4))
         bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
         outs = (C.c_void_p * len(dbs))(*[(d.d_match.ptr if op == OP_BPF else d.d_out.ptr) for d in dbs])
         aux = (C.c_void_p * len(dbs))(*[(d.d_match.ptr if op == OP_CLASSIFY_BPF else
+                                         d.d_tinfo.ptr if op == OP_CLASSIFY_TI else
                                          (d.d_fhash.ptr if d.d_fhash else None)) for d in dbs])
         tot, avg = C.c_float(), C.c_float()
         _chk(lib().mosrx_time_op(self.handle, op, arg, bs, len(dbs), outs, aux, iters, nstreams,

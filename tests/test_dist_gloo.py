@@ -30,7 +30,7 @@ def _worker(rank, world, port, out_dir):
     d = bench.Dist(world, rank)
     t = mosrx.Trace(mosrx.TRACE_IMIX, 12_000, nflows=3000)
     batches = mosrx.split_batches(t.frames, t.off, t.len, 1000)
-    mine = mosrx.shard_plan(len(batches), world, rank)
+    mine = bench.job_batches(len(batches), world, rank)     # the split bench.py runs
     d.barrier()
     res = {b: O.classify(batches[b][0], batches[b][1], batches[b][2]) for b in mine}
     d.barrier()
@@ -59,6 +59,24 @@ def test_round_robin_shards_cover_job(tmp_path, world):
     assert sorted(got) == list(range(12))        # complete
     joined = np.concatenate([got[b] for b in range(12)]).view(mosrx.RESULT_DTYPE)
     assert np.array_equal(joined.view(np.uint8), whole.view(np.uint8))
+
+
+def test_bench_job_split_is_round_robin():
+    """bench.py's own split of the job (config #5): rank r of W takes job batches
+    r, r + W, ...; the shards are disjoint, cover the job, and each rank's resident
+    contents are seeded by the job batch index (batch 0 = the default trace)."""
+    import bench
+    for world in (1, 2, 4, 8):
+        shards = [bench.job_batches(world * 8, world, r) for r in range(world)]
+        assert sorted(b for sh in shards for b in sh) == list(range(world * 8))
+        assert all(sh == list(range(r, world * 8, world)) for r, sh in enumerate(shards))
+    assert bench.job_seed(mosrx.TRACE_IMIX, 0) == 0
+    seeds = {bench.job_seed(mosrx.TRACE_IMIX, b) for b in range(64)}
+    assert len(seeds) == 64
+    a = mosrx.Trace(mosrx.TRACE_IMIX, 300, nflows=50, seed=bench.job_seed(mosrx.TRACE_IMIX, 3))
+    b = mosrx.Trace(mosrx.TRACE_IMIX, 300, nflows=50, seed=bench.job_seed(mosrx.TRACE_IMIX, 3))
+    c = mosrx.Trace(mosrx.TRACE_IMIX, 300, nflows=50, seed=bench.job_seed(mosrx.TRACE_IMIX, 4))
+    assert np.array_equal(a.frames, b.frames) and not np.array_equal(a.frames, c.frames)
 
 
 def test_shard_plan():

@@ -324,7 +324,13 @@ typedef struct mosrx_bpf_prog {
 } mosrx_bpf_prog;
 
 /* The admission check of mosrx_bpf_set for one program (no GPU needed):
- * 0 or -EINVAL. */
+ * 0 or -EINVAL.  Besides sfbpf_validate's rules it rejects the absolute word /
+ * halfword loads whose offset wraps sfbpf_filter's int bounds check (k of
+ * 0xFFFFFFFC.. for a word, 0xFFFFFFFE.. for a halfword: the reference reads
+ * before the frame).  The indexed loads cannot be checked at set time: where
+ * X + k wraps into those ranges the reference reads before the frame
+ * (undefined) and the GPU returns 0, as sfbpf_filter does for every other
+ * out-of-bounds offset. */
 int  mosrx_bpf_check(const mosrx_bpf_insn *insns, uint32_t len);
 /* Install a program set on the context (host arrays, copied).  Each program
  * must pass sfbpf_validate (sf_bpf_filter.c:548-691) and, beyond it, use only

@@ -35,8 +35,20 @@ int mosrx_bpf_check(const mosrx_bpf_insn *f, uint32_t len)
 		const uint32_t k = f[i].k;
 		const uint64_t from = (uint64_t)i + 1;
 		switch (f[i].code) {
+		case LD | W | ABS:
+			/* sfbpf_filter keeps k in an int: k + sizeof(int32) wraps in size_t for
+			 * k in [-4, -1] and the bounds check passes, reading before the frame
+			 * (undefined); every other k >= 2^31 fails the check and returns 0 there
+			 * as on the GPU (sf_bpf_filter.c:265-281) */
+			if (k >= 0xFFFFFFFCu)
+				return -EINVAL;
+			break;
+		case LD | H | ABS:   /* the same for k + sizeof(short), k in [-2, -1] (:283-299) */
+			if (k >= 0xFFFFFFFEu)
+				return -EINVAL;
+			break;
 		case RET | K: case RET | A:
-		case LD | W | ABS: case LD | H | ABS: case LD | B | ABS: case LD | W | LEN: case LDX | W | LEN:
+		case LD | B | ABS: case LD | W | LEN: case LDX | W | LEN:
 		case LD | W | IND: case LD | H | IND: case LD | B | IND: case LDX | MSH | B:
 		case LD | IMM: case LDX | IMM:
 		case ALU | ADD | X: case ALU | SUB | X: case ALU | MUL | X: case ALU | DIV | X: case ALU | AND | X:

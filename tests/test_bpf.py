@@ -129,6 +129,13 @@ def test_fixture_coverage():
     ("st_bits", prog(I_(0x22, 1), I_(0x16)), False),
     ("misc_other", prog(I_(0x27), I_(0x16)), False),
     ("alu_mod", prog(I_(0x94, 3), I_(0x16)), False),
+    # absolute loads whose k wraps sfbpf_filter's int bounds check (reads before the frame)
+    ("ld_w_abs_m1", prog(I_(0x20, 0xFFFFFFFF), I_(0x16)), False),
+    ("ld_w_abs_m4", prog(I_(0x20, 0xFFFFFFFC), I_(0x16)), False),
+    ("ld_w_abs_m5", prog(I_(0x20, 0xFFFFFFFB), I_(0x16)), True),     # fails the check: returns 0 there too
+    ("ld_h_abs_m2", prog(I_(0x28, 0xFFFFFFFE), I_(0x16)), False),
+    ("ld_h_abs_m3", prog(I_(0x28, 0xFFFFFFFD), I_(0x16)), True),
+    ("ld_b_abs_m1", prog(I_(0x30, 0xFFFFFFFF), I_(0x16)), True),     # k >= buflen as u_int: returns 0
 ])
 def test_bpf_check(name, p, ok):
     assert (mosrx.bpf_check(p) == 0) == ok, name

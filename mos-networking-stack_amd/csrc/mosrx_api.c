@@ -197,8 +197,8 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 		    hipMalloc((void **)&c->slot[i].d_qdesc, MOSRX_MAX_GROUP * sizeof(mosrx_qdesc)) != hipSuccess ||
 		    hipHostMalloc((void **)&c->slot[i].h_qdesc, MOSRX_MAX_GROUP * sizeof(mosrx_qdesc),
 		                  hipHostMallocDefault) != hipSuccess ||
-		    hipMalloc((void **)&c->slot[i].d_cnt, MOSRX_R_COUNT * 4) != hipSuccess ||
-		    hipHostMalloc((void **)&c->slot[i].h_cnt, MOSRX_R_COUNT * 4, hipHostMallocDefault) != hipSuccess) {
+		    hipMalloc((void **)&c->slot[i].d_cnt, MOSRX_CNT_WORDS * 4) != hipSuccess ||
+		    hipHostMalloc((void **)&c->slot[i].h_cnt, MOSRX_CNT_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
 			mosrx_close(c);
 			return -ENODEV;
 		}
@@ -537,7 +537,7 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 		HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
 		HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
 	}
-	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_R_COUNT * 4, s->stream));
+	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_CNT_WORDS * 4, s->stream));
 	if (c->timing)
 		HIPCHK(hipEventRecord(s->kev0, s->stream));
 	if (h_match) {
@@ -563,7 +563,7 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 	if (h_ti)
 		HIPCHK(hipMemcpyAsync(h_ti, s->d_ti, (size_t)b->n * sizeof(mosrx_tcpinfo), hipMemcpyDeviceToHost,
 		                      s->stream));
-	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_R_COUNT * 4, hipMemcpyDeviceToHost, s->stream));
+	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_CNT_WORDS * 4, hipMemcpyDeviceToHost, s->stream));
 	HIPCHK(hipEventRecord(s->done, s->stream));
 	s->busy = 1;
 	return 0;
@@ -614,7 +614,7 @@ int mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mos
 	if (c->slot[slot].busy)
 		return -EBUSY;
 	if (b->n == 0) {
-		memset(c->slot[slot].h_cnt, 0, MOSRX_R_COUNT * 4);
+		memset(c->slot[slot].h_cnt, 0, MOSRX_CNT_WORDS * 4);
 		c->slot[slot].busy = 2;   /* nothing enqueued */
 		return 0;
 	}
@@ -635,7 +635,7 @@ int mosrx_classify_bpf_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b,
 	if (c->slot[slot].busy)
 		return -EBUSY;
 	if (b->n == 0) {
-		memset(c->slot[slot].h_cnt, 0, MOSRX_R_COUNT * 4);
+		memset(c->slot[slot].h_cnt, 0, MOSRX_CNT_WORDS * 4);
 		c->slot[slot].busy = 2;   /* nothing enqueued */
 		return 0;
 	}
@@ -663,7 +663,15 @@ int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
 		return -EINVAL;
 	if (s->busy == 1)
 		HIPCHK(hipEventSynchronize(s->done));
-	memcpy(c->h_cnt, s->h_cnt, sizeof(c->h_cnt));
+	{
+		uint32_t r, k;
+		for (r = 0; r < MOSRX_R_COUNT; r++) {   /* the counter shards of the batch's workgroups */
+			uint32_t sum = 0;
+			for (k = 0; k < MOSRX_CNT_SHARDS; k++)
+				sum += s->h_cnt[k * MOSRX_CNT_STRIDE + r];
+			c->h_cnt[r] = sum;
+		}
+	}
 	c->last_kernel_ms = -1.0f;
 	if (s->busy == 1 && s->timed && hipEventElapsedTime(&c->last_kernel_ms, s->kev0, s->kev1) != hipSuccess)
 		c->last_kernel_ms = -1.0f;
@@ -763,7 +771,7 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 		r[nr++] = (struct region){(const uint8_t *)b[i].len, (uint64_t)b[i].n * 2, 0, NULL};
 	}
 	if (ntot == 0) {
-		memset(s->h_cnt, 0, MOSRX_R_COUNT * 4);
+		memset(s->h_cnt, 0, MOSRX_CNT_WORDS * 4);
 		s->busy = 2;
 		return 0;
 	}
@@ -795,7 +803,7 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 		pre += b[i].n;
 	}
 	HIPCHK(hipMemcpyAsync(s->d_qdesc, s->h_qdesc, nb * sizeof(mosrx_qdesc), hipMemcpyHostToDevice, s->stream));
-	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_R_COUNT * 4, s->stream));
+	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_CNT_WORDS * 4, s->stream));
 	qp.desc = s->d_qdesc;
 	qp.tables = c->d_tables;
 	qp.counters = s->d_cnt;
@@ -827,7 +835,7 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 		pre += n;
 		i = j;
 	}
-	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_R_COUNT * 4, hipMemcpyDeviceToHost, s->stream));
+	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_CNT_WORDS * 4, hipMemcpyDeviceToHost, s->stream));
 	HIPCHK(hipEventRecord(s->done, s->stream));
 	s->busy = 1;
 	return 0;
@@ -846,7 +854,7 @@ int mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, 
 	if (c->slot[slot].busy)
 		return -EBUSY;
 	if (b->n == 0) {
-		memset(c->slot[slot].h_cnt, 0, MOSRX_R_COUNT * 4);
+		memset(c->slot[slot].h_cnt, 0, MOSRX_CNT_WORDS * 4);
 		c->slot[slot].busy = 2;
 		return 0;
 	}

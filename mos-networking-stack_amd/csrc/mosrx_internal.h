@@ -38,7 +38,8 @@ typedef struct mosrx_kparams {
 	const uint16_t *len;
 	mosrx_result   *out;
 	const uint32_t *tables;     /* MOSRX_TAB_WORDS */
-	uint32_t       *counters;   /* MOSRX_R_COUNT u32, accumulated with atomics; may be NULL */
+	uint32_t       *counters;   /* MOSRX_CNT_SHARDS x MOSRX_CNT_STRIDE u32 (reason counts, summed over shards
+	                             * by the host), accumulated with atomics; may be NULL */
 	uint32_t       *fhash;      /* n flow hashes (HashFlow before the NUM_BINS mask); may be NULL */
 	uint32_t       *bmatch;     /* fused BPF match masks (hipRTC-built kernels only); else NULL */
 	mosrx_tcpinfo  *tinfo;      /* n pkt_info TCP field records; may be NULL */
@@ -46,6 +47,11 @@ typedef struct mosrx_kparams {
 	uint32_t        n;
 	uint32_t        flags;      /* MOSRX_KF_* */
 } mosrx_kparams;
+
+/* Reason counters: workgroup b adds to shard b % MOSRX_CNT_SHARDS, one 64-byte line each */
+#define MOSRX_CNT_SHARDS 256
+#define MOSRX_CNT_STRIDE 16
+#define MOSRX_CNT_WORDS  (MOSRX_CNT_SHARDS * MOSRX_CNT_STRIDE)
 
 /* Kernel shapes ("kinds") the library builds:
  *   SMALL  256 frames / 4 waves, lane per frame, every frame fits the header

@@ -463,11 +463,27 @@ __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffe
 // Wave-uniform value: readfirstlane tells the compiler it lives in an SGPR.
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// Per-reason counters (the NETSTAT view, eth_in.c:42-45, 80-84): the lanes of
+// a wave that store a record add one count per distinct reason to LDS (a ballot
+// per reason, usually one), and the workgroup adds its counts to its own shard
+// of the global counters (MOSRX_CNT_SHARDS lines of 16 words): adds from every
+// workgroup to ONE word serialise at the memory side (~0.01 us each, which cost
+// a 1024-workgroup launch ~11 us), spread over 256 lines they do not.
 __device__ __forceinline__ void store_record(const mosrx_kparams &kp, uint32_t p, u32x4 rec, uint32_t *s_cnt)
 {
 	*reinterpret_cast<u32x4 *>(kp.out + p) = rec;
-	if (kp.counters)
-		atomicAdd(&s_cnt[rec.w & 0xFFu], 1u);
+	if (kp.counters) {
+		const uint32_t reason = rec.w & 0xFFu;
+		uint64_t m = __ballot(1);
+		while (m) {
+			const uint32_t first = (uint32_t)__builtin_ctzll(m);
+			const uint32_t r = uni(__builtin_amdgcn_readlane(reason, first));
+			const uint64_t same = __ballot(reason == r);
+			if ((threadIdx.x & 63u) == first)
+				atomicAdd(&s_cnt[r], (uint32_t)__builtin_popcountll(same));
+			m &= ~same;
+		}
+	}
 }
 
 __device__ __forceinline__ void flush_counters(const mosrx_kparams &kp, const uint32_t *s_cnt, uint32_t t)
@@ -475,7 +491,7 @@ __device__ __forceinline__ void flush_counters(const mosrx_kparams &kp, const ui
 	if (kp.counters) {
 		__syncthreads();
 		if (t < MOSRX_R_COUNT && s_cnt[t])
-			atomicAdd(&kp.counters[t], s_cnt[t]);
+			atomicAdd(&kp.counters[(blockIdx.x % MOSRX_CNT_SHARDS) * MOSRX_CNT_STRIDE + t], s_cnt[t]);
 	}
 }
 

@@ -541,8 +541,10 @@ def main():
         e2e["backend"] = {k: measure_backend(traces[k], k, {"S64": 16_000_000, "M1500": 2_000_000}.get(k, 4_000_000),
                                              device)
                           for k in ("M1500", "S64", "IMIX") if k in traces}
-        if "S64" in traces:   # 64 batches of 32K per launch: the launch-amortised rx ring
+        # the launch-amortised rx ring: a group of batches per launch (cfg.group)
+        if "S64" in traces:
             e2e["backend"]["S64_group64"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=64)
+        e2e["backend"]["M1500_group8"] = measure_backend(traces["M1500"], "M1500", 4_000_000, device, group=8)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
         head = "M1500" if "M1500" in traces else keys[0]

@@ -102,8 +102,10 @@ typedef struct mosrx_afpacket_info {
 	int32_t  zero_copy;        /* the ring is registered: batches are lent, not copied */
 	uint64_t ring_bytes;
 	uint64_t dropped_outgoing; /* outgoing frames skipped (kernels without PACKET_IGNORE_OUTGOING) */
+	uint64_t ring_packets;     /* PACKET_STATISTICS since the socket opened (pcap_stats' ps_recv) */
+	uint64_t ring_drops;       /* frames the kernel dropped with every ring block owned by us (ps_drop) */
 } mosrx_afpacket_info;
-int           mosrx_source_afpacket_info(const mosrx_source *s, mosrx_afpacket_info *info);
+int           mosrx_source_afpacket_info(mosrx_source *s, mosrx_afpacket_info *info);
 /* Pull the next frame into dst (at most cap bytes); returns its caplen, 0 when none. */
 int           mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap);
 /* How gpu_module_func takes batches from an in-memory source: 0 = best (the

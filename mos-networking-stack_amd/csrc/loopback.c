@@ -312,6 +312,7 @@ struct src_afp {
 	uint32_t run_upto[AFP_MAX_RUNS];
 	uint32_t run_head, run_tail;
 	uint64_t dropped_outgoing;
+	uint64_t ring_packets, ring_drops;   /* PACKET_STATISTICS, accumulated (the kernel resets on read) */
 };
 
 static struct tpacket_block_desc *afp_block(struct src_afp *s, uint32_t b)
@@ -532,14 +533,23 @@ mosrx_source *mosrx_source_afpacket(const char *ifname)
 	return mosrx_source_afpacket_ex(ifname, NULL);
 }
 
-int mosrx_source_afpacket_info(const mosrx_source *s_, mosrx_afpacket_info *info)
+int mosrx_source_afpacket_info(mosrx_source *s_, mosrx_afpacket_info *info)
 {
-	const struct src_afp *s = (const struct src_afp *)s_;
+	struct src_afp *s = (struct src_afp *)s_;
 	if (!s_ || !info || s_->close != afp_close)
 		return -EINVAL;
+	struct tpacket_stats_v3 st;
+	socklen_t sl = sizeof(st);
+	memset(&st, 0, sizeof(st));
+	if (getsockopt(s->fd, SOL_PACKET, PACKET_STATISTICS, &st, &sl) == 0) {   /* pcap_stats' source */
+		s->ring_packets += st.tp_packets;
+		s->ring_drops += st.tp_drops;
+	}
 	info->zero_copy = s->registered;
 	info->ring_bytes = (uint64_t)s->nblocks * AFP_BLOCK_SIZE;
 	info->dropped_outgoing = s->dropped_outgoing;
+	info->ring_packets = s->ring_packets;
+	info->ring_drops = s->ring_drops;
 	return 0;
 }
 

@@ -59,7 +59,8 @@ typedef struct mosrx_kparams {
  *   S13     64 frames / 1 header wave + 3 streamer waves that read the tile's
  *          tail span in buffer order with a prefix scan (frames sorted and
  *          disjoint, checked per tile; unsorted tiles stream tail by tail)
- * Tuning shapes (LARGE, MID, L12/L24/L28, S12/S14/S16) live in scripts/probe_*
+ * Tuning shapes (LARGE, MID, L12/L24/L28, S12/S14/S16, the decoupled S13xN)
+ * live in scripts/probe_*
  * (DESIGN.md §4.3 has their measurements). */
 enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_S13 = 1, MOSRX_KIND_COUNT = 2 };
 #define MOSRX_STREAMERS 3

@@ -98,6 +98,11 @@ __device__ __forceinline__ uint32_t fold16(uint32_t s)
 	return (s & 0xFFFFu) + (s >> 16);
 }
 
+#define ZERO_OFF 0xFFFFFFF0u   // buffer offset past any batch (loads there are never consumed)
+
+// Wave-uniform value: readfirstlane tells the compiler it lives in an SGPR.
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
 // sum over the 64 lanes: 4 DPP row steps, then the four row sums via readlane
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
@@ -155,6 +160,49 @@ __device__ __forceinline__ void hdr_load(__amdgpu_buffer_rsrc_t rs, uint32_t nby
 		u32x4 v = load16<AUX>(rs, wbase + 16u * m, nbytes);
 		win.raw[4 * m + 0] = v.x; win.raw[4 * m + 1] = v.y; win.raw[4 * m + 2] = v.z; win.raw[4 * m + 3] = v.w;
 	}
+}
+
+// Staged header windows (SMALL tile): the 64 frames of a wave that sit in
+// buffer order within STAGE_BYTES are read with plain contiguous 1 KiB wave
+// loads into the wave's LDS stage, and every lane takes its 96-byte window from
+// there.  The gather form issues 6 loads of 64 distinct lines each per wave;
+// this one 4-5 loads of 16 lines, which is what a 64-byte-frame batch (the
+// windows of neighbouring frames overlap, the whole wave spans ~4 KiB) is
+// bound by.  Waves whose frames are not in order, or spread wider, gather.
+#define STAGE_BYTES 4224u      // 64 frames x 64 B + one window
+template <int AUX>
+__device__ __forceinline__ bool hdr_load_staged(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t o, bool active,
+                                                uint32_t lane, uint32_t *stage, hdr_win_t &win)
+{
+	const uint32_t wbase = (o + 2u) & ~3u;
+	const uint64_t act = __ballot(active);
+	if (!act)
+		return false;
+	const uint32_t first = (uint32_t)__builtin_ctzll(act), last = 63u - (uint32_t)__builtin_clzll(act);
+	const uint32_t onext = (uint32_t)__shfl_down((int)o, 1);
+	const bool in_order = __ballot(active && lane < last && onext < o) == 0;
+	const uint32_t A = uni(__builtin_amdgcn_readlane(wbase, first)) & ~15u;
+	const uint32_t Z = uni(__builtin_amdgcn_readlane(wbase, last)) + 96u;
+	if (!in_order || Z < A || Z - A > STAGE_BYTES || A >= nbytes)
+		return false;
+	u32x4 v[5];
+#pragma unroll
+	for (int i = 0; i < 5; i++) {
+		const uint32_t c = A + 1024u * i + 16u * lane;
+		v[i] = load16<AUX>(rs, c < Z ? c : ZERO_OFF, 0);
+	}
+#pragma unroll
+	for (int i = 0; i < 5; i++) {
+		const uint32_t r = 1024u * i + 16u * lane;
+		if (r < STAGE_BYTES)
+			*reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(stage) + r) = v[i];
+	}
+	// a wave's own LDS writes are ordered before its later reads (no barrier)
+	const uint32_t *wp = stage + (active ? (wbase - A) >> 2 : 0u);
+#pragma unroll
+	for (int j = 0; j < WIN_RAW; j++)
+		win.raw[j] = wp[j];
+	return true;
 }
 
 #ifdef MOSRX_RTC_BPF
@@ -458,10 +506,6 @@ __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffe
 	}
 }
 
-#define ZERO_OFF 0xFFFFFFF0u   // buffer offset past any batch (loads there are never consumed)
-
-// Wave-uniform value: readfirstlane tells the compiler it lives in an SGPR.
-__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 // Per-reason counters (the NETSTAT view, eth_in.c:42-45, 80-84): the lanes of
 // a wave that store a record add one count per distinct reason to LDS (a ballot
@@ -503,12 +547,17 @@ __device__ __forceinline__ void flush_counters(const mosrx_kparams &kp, const ui
 // barrier (each wave fills the LDS tables itself; a wave's LDS accesses are
 // ordered).  Longer frames (only when the shape is forced onto them) are
 // summed by their wave tail by tail, 4 KiB per pass.
-template <int VAR, uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL)>
+template <int VAR, uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL), int DBG = 0>
 __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uint32_t tile)
 {
 	constexpr int AUX = TAIL_AUX(VAR);
+	// windows gathered per lane (hdr_load); DBG 64 stages them through LDS instead
+	// (measured slower on S64: 192 vs 125 us per 8M frames), DBG 2 skips the
+	// window loads -- probe builds only
+	constexpr bool STAGED = (VAR & VAR_BPF) == 0 && (DBG & 64);
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
+	__shared__ __attribute__((aligned(16))) uint32_t s_stage[STAGED ? TILE / 64u : 1u][STAGED ? STAGE_BYTES / 4u : 1u];
 
 	const uint32_t t = threadIdx.x, lane = t & 63u;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
@@ -521,7 +570,16 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 		cap = eff_caplen(o, kp.len[p], nbytes);
 	}
 	hdr_win_t win;
-	hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
+	if constexpr (DBG & 2) {
+#pragma unroll
+		for (int i = 0; i < WIN_RAW; i++)
+			win.raw[i] = o + i;
+	} else if constexpr (STAGED) {
+		if (!hdr_load_staged<WIN_AUX(VAR)>(rs, nbytes, o, active, lane, s_stage[t >> 6], win))
+			hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
+	} else {
+		hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
+	}
 	{
 		const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
 		const u32x4 a = tg[lane], b = tg[lane + 64];
@@ -893,8 +951,8 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 		classify_tile_stream<MOSRX_STREAMERS, VAR>(kp, tile);
 }
 
-// The stream tile is held to 64 VGPRs: 8 waves per SIMD.
-#define MIN_WAVES(kind) ((kind) == MOSRX_KIND_S13 ? 8 : 1)
+// The stream tiles are held to 64 VGPRs: 8 waves per SIMD.
+#define MIN_WAVES(kind) ((kind) != MOSRX_KIND_SMALL ? 8 : 1)
 
 template <int KIND, int VAR>
 __global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))

@@ -118,7 +118,8 @@ class AfpOpts(C.Structure):
 
 
 class AfpInfo(C.Structure):
-    _fields_ = [("zero_copy", C.c_int32), ("ring_bytes", C.c_uint64), ("dropped_outgoing", C.c_uint64)]
+    _fields_ = [("zero_copy", C.c_int32), ("ring_bytes", C.c_uint64), ("dropped_outgoing", C.c_uint64),
+                ("ring_packets", C.c_uint64), ("ring_drops", C.c_uint64)]
 
 
 class Forwarder(C.Structure):

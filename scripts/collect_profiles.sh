@@ -5,7 +5,7 @@
 #   default bench          : profiles/r01_bench.log
 set -e
 cd "$(dirname "$0")/.."
-P=${1:-r01}
+P=${1:-r02}
 for d in gpurun_out/prof/kt_*/; do
   W=$(basename "$d"); W=${W#kt_}
   cp "$d/kt_kernel_stats.csv" "profiles/${P}_kt_${W}_kernel_stats.csv"
@@ -16,6 +16,6 @@ for d in gpurun_out/prof/pmcf_*/; do
   cp "$d/pmc_counter_collection.csv" "profiles/${P}_pmc_fetch_${W}.csv"
   cp "gpurun_out/prof/pmcw_${W}/pmc_counter_collection.csv" "profiles/${P}_pmc_write_${W}.csv"
 done
-cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json
+[ -f gpurun_out/pmc_traffic.json ] && cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json
 [ -f gpurun_out/bench_r.log ] && cp gpurun_out/bench_r.log "profiles/${P}_bench.log"
 ls -la profiles | head -60

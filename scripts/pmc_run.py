@@ -1,7 +1,9 @@
 """Isolated launches of one bench workload's kernel, for rocprofv3 --pmc passes.
 
-Same trace, resident copies (> 256 MiB Infinity Cache) and kernel as bench.py;
-N single launches on one stream.  Usage: python3 scripts/pmc_run.py M1500 [N]"""
+Same traces, resident batches (>= 1.2 GB, past the 256 MiB Infinity Cache) and
+kernel as bench.py: for a ring workload N queue launches (one per step), else
+N single classify launches, all on one stream.
+Usage: python3 scripts/pmc_run.py M1500 [N]"""
 import os
 import sys
 
@@ -13,19 +15,31 @@ import mosrx  # noqa: E402
 
 key = sys.argv[1] if len(sys.argv) > 1 else "M1500"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
-kind, batch, _ = bench.WORKLOADS[key]
+kind, batch, ring, _ = bench.WORKLOADS[key]
 ctx = mosrx.Context(0)
 ctx.set_params(mosrx.default_params(skip_tcp_csum=1 if key == "S64_hdr" else 0))
-tr = mosrx.Trace(kind, batch)
-ncopy = min(256, max(2, -(-2 * bench.L3_BYTES // tr.frames_bytes)))
-dbs = [ctx.upload(tr.frames, tr.off, tr.len, frames_bytes=tr.frames_bytes, max_len=tr.max_len) for _ in range(ncopy)]
-op = bench.OPS.get(key, mosrx.OP_CLASSIFY)
-if op == mosrx.OP_BPF:
-    ctx.bpf_set(bench.bpf_bench_programs())
-arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op == mosrx.OP_TX_CSUM else 0
-_, avg = ctx.time_op(op, dbs, iters, 1, arg, total=False)
+probe = mosrx.Trace(kind, batch)
+if ring:
+    nres = max(2 * ring, -(-bench.RESIDENT_BYTES // probe.frames_bytes))
+    nres = -(-nres // ring) * ring
+else:
+    nres = min(256, max(2, -(-bench.RESIDENT_BYTES // probe.frames_bytes)))
+dbs, trs, _ = bench.resident_batches(ctx, key, 1, 0, nres)
+tr = trs[0]
+ab = bench.algo_bytes(tr, key) * (ring or 1)
+if ring:
+    qs = [ctx.queue(dbs[i:i + ring]) for i in range(0, len(dbs), ring)]
+    _, avg = qs[0].time(iters, qs[1:])
+    for q in qs:
+        q.destroy()
+else:
+    op = bench.OPS.get(key, mosrx.OP_CLASSIFY)
+    if op in (mosrx.OP_BPF, mosrx.OP_CLASSIFY_BPF):
+        ctx.bpf_set(bench.bpf_bench_programs())
+    arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op == mosrx.OP_TX_CSUM else 0
+    _, avg = ctx.time_op(op, dbs, iters, 1, arg, total=False)
 print(f"{key}: {iters} isolated launches, avg {avg * 1e3:.2f} us (HIP events), "
-      f"algo bytes/launch {bench.algo_bytes(tr, key)}", flush=True)
+      f"algo bytes/launch {ab}", flush=True)
 for d in dbs:
     d.free()
 ctx.close()

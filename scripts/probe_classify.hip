@@ -5,6 +5,7 @@
 // launch at a time.  Results are meaningless for DBG != 0; only time counts.
 #include "../mos-networking-stack_amd/csrc/mosrx_kernels.hip"
 #include "probe_large.h"
+#include "probe_decoupled.h"
 #include "../include/mosrx_trace.h"
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,17 +24,17 @@ __global__ __launch_bounds__(64 * (1 + S)) __attribute__((amdgpu_waves_per_eu(W)
 	classify_tile_stream<S, 2, DBG, U, T>(kp, blockIdx.x);
 }
 
-template <uint32_t T>
-__global__ __launch_bounds__(T) void k_small(mosrx_kparams kp)
+template <uint32_t T, int DBG = 0>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8))) void k_small(mosrx_kparams kp)
 {
-	classify_tile_small<2, T>(kp, blockIdx.x);
+	classify_tile_small<2, T, DBG>(kp, blockIdx.x);
 }
 
 typedef void (*lfn)(const mosrx_kparams *, hipStream_t);
-template <uint32_t T>
+template <uint32_t T, int DBG = 0>
 static void launch_small(const mosrx_kparams *kp, hipStream_t s)
 {
-	hipLaunchKernelGGL((k_small<T>), dim3((kp->n + T - 1) / T), dim3(T), 0, s, *kp);
+	hipLaunchKernelGGL((k_small<T, DBG>), dim3((kp->n + T - 1) / T), dim3(T), 0, s, *kp);
 }
 template <int DBG, int MINB = 1>
 static void launch_dbg(const mosrx_kparams *kp, hipStream_t s)
@@ -52,6 +53,16 @@ static void launch_product(const mosrx_kparams *kp, hipStream_t s)
 static void launch_stream(const mosrx_kparams *kp, hipStream_t s)
 {
 	mosrx_launch_classify(kp, MOSRX_KIND_S13, 2, s);
+}
+template <int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_snt(mosrx_kparams kp)
+{
+	classify_tile_stream_nt<3, 2, NT>(kp, blockIdx.x);
+}
+template <int NT>
+static void launch_snt(const mosrx_kparams *kp, hipStream_t s)
+{
+	hipLaunchKernelGGL((k_snt<NT>), dim3((kp->n + 64 * NT - 1) / (64 * NT)), dim3(256), 0, s, *kp);
 }
 
 static int run(const char *name, lfn f, mosrx_kparams *kps, int nb, double bytes)
@@ -104,8 +115,8 @@ int main(int argc, char **argv)
 		}
 		printf("descriptors reversed\n");
 	}
-	const int nb = 6;
-	mosrx_kparams kps[nb];
+	const int nb = argc > 4 ? atoi(argv[4]) : 6;
+	mosrx_kparams kps[64];
 	uint32_t *tables;
 	CHK(hipMalloc((void **)&tables, MOSRX_TAB_ALLOC_WORDS * 4));
 	CHK(hipMemset(tables, 0, MOSRX_TAB_ALLOC_WORDS * 4));
@@ -123,13 +134,19 @@ int main(int argc, char **argv)
 	const double bytes = (double)t.caplen_sum + 22.0 * n;
 	printf("trace kind %d n %u: %.2f MB algorithmic\n", kind, n, bytes / 1e6);
 	if (kind == MOSRX_TRACE_S64 || kind == MOSRX_TRACE_FW64) {
-		run("SMALL 256", launch_small<256>, kps, nb, bytes);
+		run("product SMALL 256 (gathered windows)", launch_small<256>, kps, nb, bytes);
+		run("SMALL 256 LDS-staged windows", launch_small<256, 64>, kps, nb, bytes);
+		run("SMALL 256 no window loads", launch_small<256, 2>, kps, nb, bytes);
 		run("SMALL 128", launch_small<128>, kps, nb, bytes);
-		run("SMALL 64", launch_small<64>, kps, nb, bytes);
 		return 0;
 	}
-	run("LARGE", launch_product, kps, nb, bytes);
 	run("product S13", launch_stream, kps, nb, bytes);
+	run("S13 x2 decoupled", launch_snt<2>, kps, nb, bytes);
+	run("S13 x3 decoupled", launch_snt<3>, kps, nb, bytes);
+	run("S13 x4 decoupled", launch_snt<4>, kps, nb, bytes);
+	if (argc > 5)
+		return 0;
+	run("LARGE", launch_product, kps, nb, bytes);
 	// S13 as the library builds it (8 waves/SIMD, 4 blocks in flight) with pieces removed
 	run("S13 full", launch_sdbg<3, 0, 8, 4>, kps, nb, bytes);
 	run("S13 streamers: loads only", launch_sdbg<3, 4, 8, 4>, kps, nb, bytes);

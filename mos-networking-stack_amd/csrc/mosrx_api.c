@@ -287,7 +287,7 @@ static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_
 	const int force = (c->variant >> 2) & 31;
 	if (force && force <= MOSRX_KIND_COUNT)
 		return force - 1;
-	if (max_len && max_len <= MOSRX_WINDOW_END)
+	if (max_len && max_len <= MOSRX_WINDOW_END_SMALL)
 		return MOSRX_KIND_SMALL;
 	return MOSRX_KIND_S13;
 }

@@ -65,9 +65,16 @@ typedef struct mosrx_kparams {
 enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_S13 = 1, MOSRX_KIND_COUNT = 2 };
 #define MOSRX_STREAMERS 3
 #define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_SMALL ? 256u : 64u)
-/* Frames whose IP datagram ends at or before this frame byte are finished in
- * the per-lane header window; longer ones stream their tail cooperatively. */
-#define MOSRX_WINDOW_END 94
+/* Header windows.  Frames whose IP datagram ends at or before the window end
+ * are finished in the per-lane header window; longer ones stream their tail
+ * cooperatively from the first 16-byte boundary at or below it (the split).
+ * The SMALL tile reads 5 chunks (frame bytes [2, 78): every 64-byte frame
+ * ends inside), the stream tile 4 ([2, 62): the TCP header and the first
+ * payload bytes); a wave holding a frame with IP options reads the full 6
+ * ([2, 94)), whatever the tile. */
+#define MOSRX_WINDOW_END_SMALL  78
+#define MOSRX_WINDOW_END_STREAM 62
+#define MOSRX_WINDOW_END_FULL   94
 
 /* Batch-queue descriptor (device resident), 64 bytes. */
 typedef struct mosrx_qdesc {

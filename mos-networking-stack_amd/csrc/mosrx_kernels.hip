@@ -47,10 +47,14 @@
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-#define WIN_RAW 24     // raw dwords per lane window (96 B)
+#define WIN_RAW 24     // raw dwords a lane window holds at most (96 B)
 #define WIN_DW  23     // realigned dwords: frame bytes [2, 94)
+// realigned dwords and 16-byte loads of a window ending at frame byte `wend`
+#define WIN_NDW(wend)   (((wend) - 2) / 4)
+#define WIN_NLOAD(wend) ((WIN_NDW(wend) + 1 + 3) / 4)
 
-static_assert(2 + 4 * WIN_DW == MOSRX_WINDOW_END, "window end");
+static_assert(2 + 4 * WIN_DW == MOSRX_WINDOW_END_FULL, "window end");
+static_assert(WIN_NLOAD(MOSRX_WINDOW_END_SMALL) == 5 && WIN_NLOAD(MOSRX_WINDOW_END_STREAM) == 4, "window loads");
 static_assert(sizeof(mosrx_result) == 16, "record size");
 // small: 4 waves, one frame per lane; stream: 1 header wave + MOSRX_STREAMERS streamer waves
 #define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? 256 : 64 * (1 + MOSRX_STREAMERS))
@@ -150,13 +154,16 @@ struct hdr_win_t {
 	uint32_t raw[WIN_RAW];
 };
 
-template <int AUX>
+template <int AUX, int NLOAD = WIN_RAW / 4>
 __device__ __forceinline__ void hdr_load(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t o, bool active,
                                          hdr_win_t &win)
 {
 	const uint32_t wbase = active ? ((o + 2u) & ~3u) : nbytes;   // inactive lanes read out of range -> 0
 #pragma unroll
-	for (int m = 0; m < WIN_RAW / 4; m++) {
+	for (int m = NLOAD; m < WIN_RAW / 4; m++)
+		win.raw[4 * m + 0] = win.raw[4 * m + 1] = win.raw[4 * m + 2] = win.raw[4 * m + 3] = 0;
+#pragma unroll
+	for (int m = 0; m < NLOAD; m++) {
 		u32x4 v = load16<AUX>(rs, wbase + 16u * m, nbytes);
 		win.raw[4 * m + 0] = v.x; win.raw[4 * m + 1] = v.y; win.raw[4 * m + 2] = v.z; win.raw[4 * m + 3] = v.w;
 	}
@@ -205,6 +212,33 @@ __device__ __forceinline__ bool hdr_load_staged(__amdgpu_buffer_rsrc_t rs, uint3
 	return true;
 }
 
+// Cooperative header windows: the 64 windows of a wave are read as 384
+// 16-byte pieces, six consecutive lanes per window (so a wave instruction
+// touches ~21 cache lines instead of 64), passed through LDS (contiguous
+// writes) and read back lane-per-frame: the same 24 raw dwords hdr_load gives.
+template <int AUX>
+__device__ __forceinline__ void hdr_load_coop(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t o, bool active,
+                                              uint32_t lane, u32x4 *stage, hdr_win_t &win)
+{
+	const uint32_t wbase = active ? ((o + 2u) & ~3u) : nbytes;
+	u32x4 v[WIN_RAW / 4];
+#pragma unroll
+	for (int m = 0; m < WIN_RAW / 4; m++) {
+		const uint32_t q = 64u * m + lane, f = q / 6u, k = q - 6u * f;
+		const uint32_t wb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(f << 2), (int)wbase);
+		v[m] = load16<AUX>(rs, wb + 16u * k, nbytes);
+	}
+#pragma unroll
+	for (int m = 0; m < WIN_RAW / 4; m++)
+		stage[64 * m + lane] = v[m];
+	// a wave's own LDS writes are ordered before its later reads (no barrier)
+#pragma unroll
+	for (int k = 0; k < WIN_RAW / 4; k++) {
+		const u32x4 x = stage[(WIN_RAW / 4) * lane + k];
+		win.raw[4 * k + 0] = x.x; win.raw[4 * k + 1] = x.y; win.raw[4 * k + 2] = x.z; win.raw[4 * k + 3] = x.w;
+	}
+}
+
 #ifdef MOSRX_RTC_BPF
 #include "mosrx_bpf_hook.h"   // generated by bpf_jit.c: mosrx_bpf_hook(win, o, cap, live, rs, lds)
 #endif
@@ -238,8 +272,13 @@ __device__ __forceinline__ uint32_t ip_chain(const uint32_t *w, uint32_t ihl, ui
 // zeroed) and the segment sum over frame bytes [14+4*ihl, wend) on the
 // realigned grid (dword j = frame bytes [4j+2, 4j+6), the segment grid).  F5:
 // every active lane of the wave has ihl == 5 (no IP options, nearly all
-// traffic), so every position is a constant and the selects fold away.
-template <int VAR, bool F5>
+// traffic), so every position is a constant and the selects fold away; the
+// window holds NDW dwords.  Otherwise the full 23 are there, and a segment that
+// starts past wend (IP options beyond the split) has the bytes [wend, 14+4*ihl)
+// -- which the tail streamers sum -- taken out again: their one's-complement
+// negation 0xFFFF - fold(x) is added (the final fold only sees the sum mod
+// 0xFFFF, and the pseudo header keeps it positive).
+template <int VAR, bool F5, int NDW>
 __device__ __forceinline__ void hdr_ihl(const uint32_t (&w)[WIN_DW], uint32_t ihl_l, int wend, uint32_t &th0,
                                         uint32_t &th3, uint32_t &tcw, uint32_t &ipc, uint32_t &ipc_tx,
                                         uint32_t &wsum, uint32_t &th1, uint32_t &th2)
@@ -262,14 +301,22 @@ __device__ __forceinline__ void hdr_ihl(const uint32_t (&w)[WIN_DW], uint32_t ih
 	ipc = ip_chain(w, ihl, w[5]);
 	// TX: iph->check = 0 first (mos_api.c:1180-1181): the check is frame bytes 24,25 = w[5] bytes 2,3
 	ipc_tx = IS_TX(VAR) ? ip_chain(w, ihl, w[5] & 0xFFFFu) : 0u;
-	wsum = 0;
 	const int u = 8 * wend;
+	if constexpr (F5) {
+		wsum = 0;
 #pragma unroll
-	for (int j = 8; j < WIN_DW; j++) {
-		uint32_t m = keep_bits(32 * j + 48 - u);       // keep_lo(wend - (4j + 2))
-		if ((uint32_t)j < 3u + ihl)
-			m = 0;
-		wsum = add16x2(wsum, w[j] & m);
+		for (int j = 8; j < NDW; j++)
+			wsum = add16x2(wsum, w[j] & keep_bits(32 * j + 48 - u));   // keep_lo(wend - (4j + 2))
+	} else {
+		uint32_t pos = 0, neg = 0;
+#pragma unroll
+		for (int j = 8; j < WIN_DW; j++) {
+			const uint32_t keep = keep_bits(32 * j + 48 - u);
+			const bool inseg = (uint32_t)j >= 3u + ihl;
+			pos = add16x2(pos, w[j] & (inseg ? keep : 0u));
+			neg = add16x2(neg, w[j] & (inseg ? 0u : ~keep));
+		}
+		wsum = pos + (0xFFFFu - fold16(neg));
 	}
 }
 
@@ -285,15 +332,19 @@ static_assert(MOSRX_R_COUNT <= 16, "verdict table holds 16 codes");
 // Parse + checks + IP checksum + RSS + in-window TCP sum.  Mirrors
 // ProcessPacket (eth_in.c:27) -> ProcessInIPv4Packet (ip_in.c:30) ->
 // ProcessInTCPPacket prefix (tcp.c:408-445); see oracle/mosrx_oracle.c.
-template <int VAR>
-__device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uint32_t cap, bool active,
-                                           uint32_t kflags, const uint32_t *s_tab, const uint32_t *g_tab)
+// WEND: the window end of the tile (MOSRX_WINDOW_END_*); `win` holds
+// WIN_NLOAD(WEND) chunks, the rest are read here for a wave with IP options.
+template <int VAR, int WEND>
+__device__ __forceinline__ hdr_t hdr_parse(hdr_win_t win, uint32_t o, uint32_t cap, bool active, uint32_t kflags,
+                                           const uint32_t *s_tab, const uint32_t *g_tab, __amdgpu_buffer_rsrc_t rs,
+                                           uint32_t nbytes)
 {
+	constexpr int NDW = WIN_NDW(WEND), NLOAD = WIN_NLOAD(WEND);
 	hdr_t h;
 	uint32_t w[WIN_DW];
 	const uint32_t rsh = (o + 2u) & 3u;
 #pragma unroll
-	for (int j = 0; j < WIN_DW; j++)
+	for (int j = 0; j < NDW; j++)
 		w[j] = __builtin_amdgcn_alignbyte(win.raw[j + 1], win.raw[j], rsh);
 
 	// frame byte f sits in byte (f-2)&3 of w[(f-2)>>2]
@@ -305,18 +356,30 @@ __device__ __forceinline__ hdr_t hdr_parse(const hdr_win_t &win, uint32_t o, uin
 	const uint32_t saddr = w[6], daddr = w[7];        // raw network-order words
 	const bool is_tcp = (proto == 6u);
 	const uint32_t fend = 14u + ip_len;                // frame byte after the IP datagram
-	const uint32_t split_abs = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
-	const uint32_t split = split_abs - o;              // frame byte 79..94
+	const uint32_t split_abs = (o + (uint32_t)WEND) & ~15u;
+	const uint32_t split = split_abs - o;              // frame byte WEND-15 .. WEND
 	// TCP segment sum over frame bytes [14+4*ihl, wend): the whole segment when
 	// the datagram ends inside the window, else up to the split (the tail
 	// streamers take over there).
-	const bool in_win = fend <= (uint32_t)MOSRX_WINDOW_END;
+	const bool in_win = fend <= (uint32_t)WEND;
 	const int wend = (int)(in_win ? fend : split);
 	uint32_t th0, th3, tcw, ipc, ipc_tx, wsum, th1, th2;
-	if (__ballot(active && ihl != 5u) == 0)            // no IP options in the wave: constant positions
-		hdr_ihl<VAR, true>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum, th1, th2);
-	else
-		hdr_ihl<VAR, false>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum, th1, th2);
+	if (__ballot(active && ihl != 5u) == 0) {          // no IP options in the wave: constant positions
+		hdr_ihl<VAR, true, NDW>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum, th1, th2);
+	} else {
+		if constexpr (NLOAD < WIN_RAW / 4) {           // the rest of the full window (rare)
+			const uint32_t wbase = active ? ((o + 2u) & ~3u) : nbytes;
+#pragma unroll
+			for (int m = NLOAD; m < WIN_RAW / 4; m++) {
+				const u32x4 v = load16<0>(rs, wbase + 16u * m, nbytes);
+				win.raw[4 * m + 0] = v.x; win.raw[4 * m + 1] = v.y; win.raw[4 * m + 2] = v.z; win.raw[4 * m + 3] = v.w;
+			}
+		}
+#pragma unroll
+		for (int j = NDW; j < WIN_DW; j++)
+			w[j] = __builtin_amdgcn_alignbyte(win.raw[j + 1], win.raw[j], rsh);
+		hdr_ihl<VAR, false, WIN_DW>(w, ihl, wend, th0, th3, tcw, ipc, ipc_tx, wsum, th1, th2);
+	}
 	const uint32_t doff = is_tcp ? ((th3 >> 4) & 0xFu) : 0u;
 
 	// Toeplitz over saddr|daddr|sport|dport in wire order (util.c:61-99, host-order args)
@@ -551,6 +614,9 @@ template <int VAR, uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL), int DBG 
 __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uint32_t tile)
 {
 	constexpr int AUX = TAIL_AUX(VAR);
+	constexpr int WEND = MOSRX_WINDOW_END_SMALL;
+	// the fused BPF hook reads the whole 96-byte window
+	constexpr int NLOAD = (VAR & VAR_BPF) ? WIN_RAW / 4 : WIN_NLOAD(WEND);
 	// windows gathered per lane (hdr_load); DBG 64 stages them through LDS instead
 	// (measured slower on S64: 192 vs 125 us per 8M frames), DBG 2 skips the
 	// window loads -- probe builds only
@@ -576,9 +642,9 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 			win.raw[i] = o + i;
 	} else if constexpr (STAGED) {
 		if (!hdr_load_staged<WIN_AUX(VAR)>(rs, nbytes, o, active, lane, s_stage[t >> 6], win))
-			hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
+			hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, o, active, win);
 	} else {
-		hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
+		hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, o, active, win);
 	}
 	{
 		const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
@@ -591,7 +657,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 			s_cnt[t] = 0;
 		__syncthreads();
 	}
-	const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab, kp.tables);
+	const hdr_t h = hdr_parse<VAR, WEND>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
 	uint32_t tail = 0;
 	for (uint64_t m = __ballot(h.has_tail); m; m &= m - 1) {
 		const uint32_t f = (uint32_t)__builtin_ctzll(m);
@@ -838,11 +904,23 @@ __device__ __forceinline__ void stream_frames(__amdgpu_buffer_rsrc_t rs, uint32_
 
 // DBG (probe builds only, the library uses 0): 1 no parse/records, 2 no header
 // window loads, 4 streamer loads only, 16 no unsorted-tile path, 32 header wave
-// at raised issue priority.
+// at raised issue priority, 128 per-tile timeline stamps into kp.bmatch
+// (scripts/probe_timeline.hip: 16 words per tile, 100 MHz real-time clock).
+#define TILE_STAMP(i)                                                                             \
+	do {                                                                                          \
+		if constexpr ((DBG & 128) != 0) {                                                         \
+			__builtin_amdgcn_s_waitcnt(0);                                                        \
+			if (lane == 0)                                                                        \
+				kp.bmatch[tile * 16u + (i)] = (uint32_t)__builtin_amdgcn_s_memrealtime();         \
+		}                                                                                         \
+	} while (0)
 template <int S, int VAR, int DBG = 0, int U = STREAM_U, uint32_t T = 64>
 __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, uint32_t tile)
 {
 	constexpr int AUX = TAIL_AUX(VAR);
+	// DBG 2048: the full 96-byte window (the round-1 form, 4 % slower)
+	constexpr int WEND = (DBG & 2048) ? MOSRX_WINDOW_END_FULL : MOSRX_WINDOW_END_STREAM;
+	constexpr int NLOAD = (VAR & VAR_BPF) ? WIN_RAW / 4 : WIN_NLOAD(WEND);
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
 	__shared__ uint32_t s_part[S][64];   // streamer s's tail sums
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
@@ -852,6 +930,8 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 	const uint32_t nbytes = kp.frames_bytes;
 	const uint32_t nact = min(T, kp.n - tile * T);
 
+	if (wave == 0)
+		TILE_STAMP(0);
 	// every wave reads the tile's descriptors (lane = frame)
 	const uint32_t p = tile * T + lane;
 	const bool active = lane < nact;
@@ -861,7 +941,7 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		cap = eff_caplen(o, kp.len[p], nbytes);
 	}
 	// speculative tail bounds from the capture length: [split, off + caplen)
-	const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
+	const uint32_t lo_l = (o + (uint32_t)WEND) & ~15u;
 	const uint32_t hi_l = active ? o + cap : 0u;
 	// buffer order: the next frame starts at or after this capture's end
 	const uint32_t onext = (uint32_t)__shfl_down((int)o, 1);
@@ -871,13 +951,25 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		// ---- header wave (fills s_tab itself: a wave's LDS accesses are ordered) ----
 		if constexpr (DBG & 32)
 			__builtin_amdgcn_s_setprio(2);
+		TILE_STAMP(1);
+		if constexpr ((DBG & 128) != 0) {
+			if (lane == 0) {
+				kp.bmatch[tile * 16u + 10u] = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_ID
+				kp.bmatch[tile * 16u + 11u] = __builtin_amdgcn_s_getreg(20 | (31 << 11));   // XCC_ID
+			}
+		}
+		if constexpr ((DBG & 512) != 0)
+			__syncthreads();   // B first: windows read after the streamers passed them
 		hdr_win_t win;
 		if constexpr (DBG & 2) {
 #pragma unroll
 			for (int i = 0; i < WIN_RAW; i++)
 				win.raw[i] = o + i;
+		} else if constexpr ((DBG & 256) != 0) {
+			__shared__ u32x4 s_win[64 * (WIN_RAW / 4)];
+			hdr_load_coop<WIN_AUX(VAR)>(rs, nbytes, o, active, lane, s_win, win);
 		} else {
-			hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
+			hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, o, active, win);
 		}
 		// the chunk holding the capture's last byte (stream_scan sums it whole)
 		const bool cand = hi_l > lo_l;
@@ -899,8 +991,12 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 			if (active && (x ^ s_part[0][lane]) == 0x9E3779B9u)
 				kp.out[p].rss = x;
 		} else {
-			const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab, kp.tables);
-			__syncthreads();   // B: s_part ready
+			TILE_STAMP(2);
+			const hdr_t h = hdr_parse<VAR, WEND>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
+			TILE_STAMP(3);
+			if constexpr ((DBG & 512) == 0)
+				__syncthreads();   // B: s_part ready
+			TILE_STAMP(4);
 			uint32_t tail = 0;
 			if (h.has_tail) {
 #pragma unroll
@@ -910,6 +1006,12 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 					tail -= chunk_overshoot(ov, (hi_l - 1u) & ~15u, hi_l);
 			}
 			hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, tail, p, active, lane, s_cnt);
+			TILE_STAMP(5);
+			// only this wave counted (its LDS accesses are ordered): it adds the
+			// tile's counts to its shard without a second barrier, so the
+			// streamers retire at B and the next tile can start on their slots
+			if (kp.counters && lane < MOSRX_R_COUNT && s_cnt[lane])
+				atomicAdd(&kp.counters[(blockIdx.x % MOSRX_CNT_SHARDS) * MOSRX_CNT_STRIDE + lane], s_cnt[lane]);
 #ifdef MOSRX_RTC_BPF
 			if constexpr ((VAR & VAR_BPF) != 0) {
 				__shared__ uint32_t s_bw[25u * 64u];
@@ -923,6 +1025,8 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		// ---- streamer sidx ----
 		const uint32_t sidx = wave - 1u;
 		uint32_t *row = s_part[sidx];
+		if (sidx == 0)
+			TILE_STAMP(6);
 		row[lane] = 0;
 		const uint64_t cmask = __ballot(hi_l > lo_l);
 		if (sorted && cmask) {
@@ -930,16 +1034,291 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 			// candidate's capture end (in buffer order both are monotone, and a
 			// candidate's capture is clipped to the buffer, so a bogus offset on a
 			// frame without a tail can never stretch the span)
-			const uint32_t A = uni(__builtin_amdgcn_readlane(lo_l, (int)__builtin_ctzll(cmask)));
+			// (from the tile's first byte: the streamers pass over the header
+			// windows in buffer order too, measured 2 % faster than starting at
+			// the first split; DBG 1024 keeps the split start for comparison)
+			uint32_t A = uni(__builtin_amdgcn_readlane(lo_l, (int)__builtin_ctzll(cmask)));
 			const uint32_t Z = uni(__builtin_amdgcn_readlane(hi_l, 63 - (int)__builtin_clzll(cmask)));
+			if constexpr ((DBG & 1024) == 0)
+				A = min(A, uni(__builtin_amdgcn_readfirstlane(o)) & ~15u);
 			stream_scan<S, AUX, DBG, U>(rs, lo_l, hi_l, A, Z, sidx, lane, row);
 		} else if (!sorted) {
 			if constexpr (!(DBG & 16))
 				stream_frames<S, AUX>(rs, lo_l, hi_l, sidx, lane, row);
 		}
+		TILE_STAMP(7 + sidx);
 		__syncthreads();   // B
 	}
-	flush_counters(kp, s_cnt, t);
+}
+
+// ---------------------------------------------------------------------------
+// pipelined stream tiles (SP): NT consecutive 64-frame tiles per workgroup
+// ---------------------------------------------------------------------------
+// In the S13 tile every phase is paid once per tile and in series: descriptor
+// latency, then the header windows (one more HBM round trip) and the parse on
+// one side, the span stream on the other, one barrier, the records.  With two
+// or three rounds of tiles per launch those latencies are not hidden.  Here a
+// workgroup owns NT tiles and nothing waits on a workgroup barrier after the
+// start: the streamers stream the NT spans back to back (the loads of tile k+1
+// are in flight while tile k's last blocks are summed), publishing each tile's
+// rows with an LDS counter; the header wave prefetches tile k+1's windows into
+// LDS with buffer_load ... lds (no registers held) while it parses tile k,
+// waits on tile k's counter only to emit.
+#define SP_MAX_NT 2
+#define SP_CHUNKS 7            // the 6 window chunks + the chunk holding the capture's last byte
+typedef __attribute__((address_space(3))) void lds_void;
+
+struct sp_view {               // one tile's frames, lane = frame
+	uint32_t o, cap, lo_l, hi_l;
+	bool active, sorted;
+};
+
+__device__ __forceinline__ sp_view sp_tile_view(const uint32_t *s_o, const uint32_t *s_cap, uint32_t nact, uint32_t lane)
+{
+	sp_view v;
+	v.active = lane < nact;
+	v.o = s_o[lane];
+	v.cap = s_cap[lane];
+	v.lo_l = (v.o + (uint32_t)MOSRX_WINDOW_END_STREAM) & ~15u;
+	v.hi_l = v.active ? v.o + v.cap : 0u;
+	const uint32_t onext = s_o[min(lane + 1u, 63u)];
+	v.sorted = __ballot(lane + 1u < nact && onext < v.hi_l) == 0;
+	return v;
+}
+
+// Tile k's 64 header windows (6 chunks per lane) and the chunk holding each
+// capture's last byte, straight into LDS buffer `buf` (lane l's chunk m at
+// buf[m][l]): buffer_load ... lds, no registers held while they are in flight.
+template <int AUX>
+__device__ __forceinline__ void sp_issue_windows(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, const sp_view &v,
+                                                 u32x4 (*buf)[64])
+{
+	const uint32_t wbase = v.active ? ((v.o + 2u) & ~3u) : nbytes;   // out of range -> 0
+	const uint32_t ovoff = v.sorted && v.hi_l > v.lo_l ? (v.hi_l - 1u) & ~15u : ZERO_OFF;
+#pragma unroll
+	for (int m = 0; m < WIN_RAW / 4; m++)
+		__builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)&buf[m][0], 16, wbase + 16u * m, 0, 0, AUX);
+	__builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void *)&buf[WIN_RAW / 4][0], 16, ovoff, 0, 0, AUX);
+}
+
+// Streamer sidx's share of a tile's span: blocks [b0, b0 + nb) of 1 KiB from A
+// (nb = 0: nothing for this streamer, or the tile is not in buffer order).
+struct sp_share {
+	uint32_t A, b0, nb, R1;
+};
+template <int S>
+__device__ __forceinline__ sp_share sp_tile_share(const sp_view &v, uint32_t sidx)
+{
+	sp_share sh = {0u, 0u, 0u, 0u};
+	const uint64_t cmask = __ballot(v.hi_l > v.lo_l);
+	if (v.sorted && cmask) {
+		uint32_t A = uni(__builtin_amdgcn_readlane(v.lo_l, (int)__builtin_ctzll(cmask)));
+		const uint32_t Z = uni(__builtin_amdgcn_readlane(v.hi_l, 63 - (int)__builtin_clzll(cmask)));
+		A = min(A, uni(__builtin_amdgcn_readfirstlane(v.o)) & ~15u);   // from the tile's first byte
+		const uint32_t nblk = (Z - A + 1023u) >> 10;
+		const uint32_t b0 = uni((nblk * sidx) / S), b1 = uni((nblk * (sidx + 1u)) / S);
+		sh.A = A; sh.b0 = b0; sh.nb = b1 - b0; sh.R1 = A + (b1 << 10);
+	}
+	return sh;
+}
+
+template <int S, int VAR, int NT, int DBG = 0, int U = STREAM_U>
+__device__ __forceinline__ void classify_tile_sp(const mosrx_kparams &kp, uint32_t grp)
+{
+	constexpr int AUX = TAIL_AUX(VAR);
+	static_assert(NT >= 1 && NT <= SP_MAX_NT, "tiles per workgroup");
+	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
+	__shared__ __attribute__((aligned(16))) u32x4 s_win[2][SP_CHUNKS][64];
+	__shared__ uint32_t s_o[NT][64], s_cap[NT][64];
+	__shared__ uint32_t s_part[NT][S][64];
+	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
+	__shared__ uint32_t s_done[NT];
+
+	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
+	const uint32_t nbytes = kp.frames_bytes;
+	const uint32_t tile0 = grp * NT;
+	const uint32_t ntile = uni(min((uint32_t)NT, ((kp.n + 63u) >> 6) - tile0));
+
+	// every tile's descriptors into LDS (wave w loads tile w), rows zeroed, counters reset
+	if (wave < ntile) {
+		const uint32_t p = (tile0 + wave) * 64u + lane;
+		uint32_t o = 0, cap = 0;
+		if (p < kp.n) {
+			o = kp.off[p];
+			cap = eff_caplen(o, kp.len[p], nbytes);
+		}
+		s_o[wave][lane] = o;
+		s_cap[wave][lane] = cap;
+	}
+	if (wave >= 1) {
+#pragma unroll
+		for (int k = 0; k < NT; k++)
+			s_part[k][wave - 1][lane] = 0;
+	}
+	if (t < (uint32_t)NT)
+		s_done[t] = 0;
+	__syncthreads();   // the only workgroup barrier
+
+	if (wave == 0) {
+		// ---- header wave ----
+		{
+			const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
+			const u32x4 a = tg[lane], b = tg[lane + 64];
+			reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
+			reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
+			if (lane <= MOSRX_R_COUNT)
+				s_cnt[lane] = 0;
+		}
+		sp_issue_windows<WIN_AUX(VAR)>(rs, nbytes, sp_tile_view(s_o[0], s_cap[0], min(64u, kp.n - tile0 * 64u), lane),
+		                               s_win[0]);
+#pragma unroll
+		for (int k = 0; k < NT; k++) {
+			if ((uint32_t)k >= ntile)
+				break;
+			// tile k's windows: every vector memory op but the newest one (tile
+			// k-1's last record store) has completed
+			if (k == 0)
+				asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+			else
+				asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+			hdr_win_t win;
+#pragma unroll
+			for (int m = 0; m < WIN_RAW / 4; m++) {
+				const u32x4 x = s_win[k & 1][m][lane];
+				win.raw[4 * m + 0] = x.x; win.raw[4 * m + 1] = x.y; win.raw[4 * m + 2] = x.z; win.raw[4 * m + 3] = x.w;
+			}
+			const u32x4 ov = s_win[k & 1][WIN_RAW / 4][lane];
+			asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the buffer is refilled
+			if (k + 1 < NT && (uint32_t)k + 1u < ntile)
+				sp_issue_windows<WIN_AUX(VAR)>(
+					rs, nbytes, sp_tile_view(s_o[k + 1], s_cap[k + 1], min(64u, kp.n - (tile0 + k + 1) * 64u), lane),
+					s_win[(k + 1) & 1]);
+			const uint32_t nact = min(64u, kp.n - (tile0 + k) * 64u);
+			const sp_view v = sp_tile_view(s_o[k], s_cap[k], nact, lane);
+			const uint32_t p = (tile0 + k) * 64u + lane;
+			const hdr_t h = hdr_parse<VAR, MOSRX_WINDOW_END_STREAM>(win, v.o, v.cap, v.active, kp.flags, s_tab, kp.tables,
+			                                                       rs, nbytes);
+			while (__hip_atomic_load(&s_done[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)S)
+				__builtin_amdgcn_s_sleep(1);
+			uint32_t tail = 0;
+			if (h.has_tail) {
+#pragma unroll
+				for (int s2 = 0; s2 < S; s2++)
+					tail += s_part[k][s2][lane];
+				if (v.sorted)
+					tail -= chunk_overshoot(ov, (v.hi_l - 1u) & ~15u, v.hi_l);
+			}
+			hdr_emit<VAR>(kp, rs, nbytes, h, v.lo_l, v.hi_l, tail, p, v.active, lane, s_cnt);
+		}
+		if (kp.counters && lane < MOSRX_R_COUNT && s_cnt[lane])
+			atomicAdd(&kp.counters[(blockIdx.x % MOSRX_CNT_SHARDS) * MOSRX_CNT_STRIDE + lane], s_cnt[lane]);
+		return;
+	}
+
+	// ---- streamer sidx: its shares of the NT spans as one stream of blocks, U loads in flight ----
+	const uint32_t sidx = wave - 1u;
+	sp_share sh[NT];
+	uint32_t unsorted = 0, total = 0;
+#pragma unroll
+	for (int k = 0; k < NT; k++) {
+		sh[k] = (sp_share){0u, 0u, 0u, 0u};
+		if ((uint32_t)k < ntile) {
+			const sp_view v = sp_tile_view(s_o[k], s_cap[k], min(64u, kp.n - (tile0 + k) * 64u), lane);
+			if (!v.sorted)
+				unsorted |= 1u << k;
+			sh[k] = sp_tile_share<S>(v, sidx);
+		}
+		total += sh[k].nb;
+	}
+	// item j of the stream -> (tile, block address)
+	auto item_tile = [&](uint32_t j) -> uint32_t {
+		uint32_t k = 0, acc = sh[0].nb;
+#pragma unroll
+		for (int q = 1; q < NT; q++) {
+			k = j >= acc ? (uint32_t)q : k;
+			acc += sh[q].nb;
+		}
+		return k;
+	};
+	auto item_addr = [&](uint32_t j) -> uint32_t {
+		uint32_t a = sh[0].A + ((sh[0].b0 + j) << 10), acc = sh[0].nb;
+#pragma unroll
+		for (int q = 1; q < NT; q++) {
+			a = j >= acc ? sh[q].A + ((sh[q].b0 + j - acc) << 10) : a;
+			acc += sh[q].nb;
+		}
+		return a;
+	};
+	u32x4 v[U];
+#pragma unroll
+	for (int i = 0; i < U; i++)
+		v[i] = load16<AUX>(rs, (uint32_t)i < total ? item_addr(i) + 16u * lane : ZERO_OFF, 0);
+	uint32_t sk = 0xFFFFFFFFu, sR1 = 0, carry = 0, acc = 0, lo_l = 0, ec_l = 0, signalled = 0;
+	bool cand = false;
+#pragma unroll 1
+	for (uint32_t j0 = 0; j0 < total; j0 += U) {
+#pragma unroll
+		for (int i = 0; i < U; i++) {
+			const uint32_t j = j0 + (uint32_t)i;
+			if (j < total) {
+				const uint32_t k = uni(item_tile(j));
+				if (k != sk) {
+					// leave tile sk (its row, tails continuing past the run), signal every tile below k
+					if (sk != 0xFFFFFFFFu) {
+						if (cand && lo_l < sR1 && ec_l >= sR1)
+							acc += carry;
+						s_part[sk][sidx][lane] = acc;
+					}
+					for (; signalled < k; signalled++)
+						if (!((unsorted >> signalled) & 1u) && lane == 0)
+							__hip_atomic_fetch_add(&s_done[signalled], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+					const sp_view tv = sp_tile_view(s_o[k], s_cap[k], min(64u, kp.n - (tile0 + k) * 64u), lane);
+					sk = k;
+					sR1 = 0;
+#pragma unroll
+					for (int q = 0; q < NT; q++)
+						if ((uint32_t)q == k)
+							sR1 = sh[q].R1;
+					lo_l = tv.lo_l; ec_l = (tv.hi_l - 1u) & ~15u; cand = tv.hi_l > tv.lo_l;
+					carry = 0; acc = 0;
+				}
+				const uint32_t c0 = item_addr(j);
+				uint32_t s = add16x2(0u, v[i].x);
+				s = add16x2(s, v[i].y);
+				s = add16x2(s, v[i].z);
+				s = add16x2(s, v[i].w);
+				const uint32_t X = carry + wave_scan(s);
+				carry = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
+				const uint32_t rl = lo_l - c0, re = ec_l - c0;
+				const bool es = cand && rl < 1024u, ee = cand && re < 1024u;
+				if (__ballot(es || ee)) {
+					const uint32_t Es = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rl >> 2) & 0xFCu), (int)(X - s));
+					const uint32_t Xe = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((re >> 2) & 0xFCu), (int)X);
+					acc = es ? acc - Es : acc;
+					acc = ee ? acc + Xe : acc;
+				}
+			}
+			const uint32_t jn = j + U;
+			v[i] = load16<AUX>(rs, jn < total ? item_addr(jn) + 16u * lane : ZERO_OFF, 0);
+		}
+	}
+	if (sk != 0xFFFFFFFFu) {
+		if (cand && lo_l < sR1 && ec_l >= sR1)
+			acc += carry;
+		s_part[sk][sidx][lane] = acc;
+	}
+	for (; signalled < ntile; signalled++)
+		if (!((unsorted >> signalled) & 1u) && lane == 0)
+			__hip_atomic_fetch_add(&s_done[signalled], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+	// tiles whose frames are not in buffer order: tail by tail
+	for (uint32_t m = unsorted; m; m &= m - 1) {
+		const uint32_t k = (uint32_t)__builtin_ctz(m);
+		const sp_view tv = sp_tile_view(s_o[k], s_cap[k], min(64u, kp.n - (tile0 + k) * 64u), lane);
+		stream_frames<S, AUX>(rs, tv.lo_l, tv.hi_l, sidx, lane, s_part[k][sidx]);
+		if (lane == 0)
+			__hip_atomic_fetch_add(&s_done[k], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+	}
 }
 
 template <int KIND, int VAR>

@@ -46,7 +46,7 @@ def shape_variant(kind: int, nt_tails: bool = True) -> int:
 QMAP_I40E, QMAP_IXGBE = 1, 0
 TRACE_FW64, TRACE_S64, TRACE_M1500, TRACE_IMIX = 0, 1, 2, 3
 TRACE_SEED_BASE = 0x6D4F5321   # MOSRX_TRACE_SEED: seed 0 selects TRACE_SEED_BASE + kind
-WINDOW_END = 94
+WINDOW_END = 78       # MOSRX_WINDOW_END_SMALL: batches whose frames all fit take the SMALL tile
 
 MS_KEY = bytes([0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
                 0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,

@@ -51,7 +51,7 @@ __device__ __forceinline__ void classify_tile_stream_nt(const mosrx_kparams &kp,
 				o = kp.off[p];
 				cap = eff_caplen(o, kp.len[p], nbytes);
 			}
-			const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
+			const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END_FULL) & ~15u;
 			const uint32_t hi_l = active ? o + cap : 0u;
 			const uint32_t onext = (uint32_t)__shfl_down((int)o, 1);
 			const bool sorted = __ballot(lane + 1u < nact && onext < hi_l) == 0;
@@ -59,7 +59,7 @@ __device__ __forceinline__ void classify_tile_stream_nt(const mosrx_kparams &kp,
 			hdr_load<WIN_AUX(VAR)>(rs, nbytes, o, active, win);
 			const bool cand = hi_l > lo_l;
 			const u32x4 ov = load16<WIN_AUX(VAR)>(rs, sorted && cand ? (hi_l - 1u) & ~15u : ZERO_OFF, 0);
-			const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab, kp.tables);
+			const hdr_t h = hdr_parse<VAR, MOSRX_WINDOW_END_FULL>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
 			while (__hip_atomic_load(&s_done[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (uint32_t)S)
 				__builtin_amdgcn_s_sleep(1);
 			uint32_t tail = 0;
@@ -89,7 +89,7 @@ __device__ __forceinline__ void classify_tile_stream_nt(const mosrx_kparams &kp,
 				o = kp.off[base + lane];
 				cap = eff_caplen(o, kp.len[base + lane], nbytes);
 			}
-			const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
+			const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END_FULL) & ~15u;
 			const uint32_t hi_l = active ? o + cap : 0u;
 			const uint32_t onext = (uint32_t)__shfl_down((int)o, 1);
 			const bool sorted = __ballot(lane + 1u < nact && onext < hi_l) == 0;

@@ -176,7 +176,7 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 		cap = eff_caplen(o, kp.len[p], nbytes);
 	}
 	// speculative tail bounds from the capture length: [split, off + caplen)
-	const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END) & ~15u;
+	const uint32_t lo_l = (o + (uint32_t)MOSRX_WINDOW_END_FULL) & ~15u;
 	const uint32_t hi_l = active ? o + cap : 0u;
 	const bool cand = hi_l > lo_l;
 	const uint64_t cmask = __ballot(cand);
@@ -212,7 +212,7 @@ __device__ __forceinline__ void classify_tile_large(const mosrx_kparams &kp, uin
 			if (active && (x ^ s_spec[64u * sub + lane]) == 0x9E3779B9u)
 				kp.out[p].rss = x;
 		} else {
-			const hdr_t h = hdr_parse<VAR>(win, o, cap, active, kp.flags, s_tab, kp.tables);
+			const hdr_t h = hdr_parse<VAR, MOSRX_WINDOW_END_FULL>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
 			__syncthreads();   // B: s_spec ready
 			hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, h.has_tail ? s_spec[64u * sub + lane] : 0u, p, active,
 			              lane, s_cnt);

@@ -6,6 +6,7 @@
 // kernel would do anyway (s_waitcnt 0), so the phases are close to the library's.
 //   probe_timeline <trace kind> <frames> <resident batches>
 #include "../mos-networking-stack_amd/csrc/mosrx_kernels.hip"
+#include "probe_sp.h"
 #include "../include/mosrx_trace.h"
 #include <algorithm>
 #include <stdio.h>

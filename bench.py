@@ -562,8 +562,11 @@ def main():
         results["FW64"] = measure_fw64(ctx, 2.0)
     read_ceiling = None
     if rank == 0:
-        # the box's streaming-read ceiling over a 1.5 GB working set (no Infinity-Cache hits)
-        read_ceiling = round(ctx.probe_read_bw(128 << 20, 12, 96), 1)
+        # the box's streaming-read rate over a 1.5 GB working set (no Infinity-Cache
+        # hits), once with 128 MiB launches (the single-batch rows' size: their ramp
+        # and drain included) and once with 512 MiB launches (the ring rows' size)
+        read_ceiling = {"launch_128MiB": round(ctx.probe_read_bw(128 << 20, 12, 96), 1),
+                        "launch_512MiB": round(ctx.probe_read_bw(512 << 20, 3, 24), 1)}
     ctx.close()
     dist.close()
     if rank != 0:

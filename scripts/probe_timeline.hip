@@ -16,10 +16,10 @@
 
 #define CHK(x) do { if ((x) != hipSuccess) { printf("HIP error %s line %d\n", #x, __LINE__); return 1; } } while (0)
 
-template <int DBG, int S = 3, int U = 4, int W = 8, uint32_t T = 64>
+template <int DBG, int S = 3, int U = 4, int W = 8, uint32_t T = 64, int VAR = 2>
 __global__ __launch_bounds__(64 * (1 + S)) __attribute__((amdgpu_waves_per_eu(W))) void k_tl(mosrx_kparams kp)
 {
-	classify_tile_stream<S, 2, DBG, U, T>(kp, blockIdx.x);
+	classify_tile_stream<S, VAR, DBG, U, T>(kp, blockIdx.x);
 }
 
 template <int NT, int U = 4>
@@ -74,7 +74,7 @@ static int plain_sp(const char *name, std::vector<mosrx_kparams> &kps, uint32_t 
 	return 0;
 }
 
-template <int S, int U, int W, int DBG = 0, uint32_t T = 64>
+template <int S, int U, int W, int DBG = 0, uint32_t T = 64, int VAR = 2>
 static int plain(const char *name, std::vector<mosrx_kparams> &kps, uint32_t ntiles64, double bytes)
 {
 	const uint32_t ntiles = ntiles64 * (64 / T);
@@ -85,10 +85,10 @@ static int plain(const char *name, std::vector<mosrx_kparams> &kps, uint32_t nti
 	float best = 1e9;
 	for (int rep = 0; rep < 3; rep++) {
 		for (int i = 0; i < nb; i++)
-			hipLaunchKernelGGL((k_tl<DBG, S, U, W, T>), dim3(ntiles), dim3(64 * (1 + S)), 0, 0, kps[i]);
+			hipLaunchKernelGGL((k_tl<DBG, S, U, W, T, VAR>), dim3(ntiles), dim3(64 * (1 + S)), 0, 0, kps[i]);
 		CHK(hipEventRecord(a, 0));
 		for (int i = 0; i < 4 * nb; i++)
-			hipLaunchKernelGGL((k_tl<DBG, S, U, W, T>), dim3(ntiles), dim3(64 * (1 + S)), 0, 0, kps[i % nb]);
+			hipLaunchKernelGGL((k_tl<DBG, S, U, W, T, VAR>), dim3(ntiles), dim3(64 * (1 + S)), 0, 0, kps[i % nb]);
 		CHK(hipEventRecord(b, 0));
 		CHK(hipEventSynchronize(b));
 		float ms;
@@ -141,13 +141,17 @@ int main(int argc, char **argv)
 	// plain (DBG 0) back-to-back times over the resident batches, then stamped launches
 	printf("trace kind %d n %u tiles %u: %.2f MB\n", kind, n, ntiles, bytes / 1e6);
 	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);
-	plain_sp<1>("SP NT1", kps, ntiles, bytes);
-	plain_sp<2>("SP NT2", kps, ntiles, bytes);
-	plain_sp<2, 6>("SP NT2 U6", kps, ntiles, bytes);
+	plain<3, 4, 8, 0, 64, 3>("S13 windows nt, tails nt", kps, ntiles, bytes);
+	plain<3, 4, 8, 0, 64, 0>("S13 windows rt, tails rt", kps, ntiles, bytes);
+	plain<3, 4, 8, 0, 64, 1>("S13 windows nt, tails rt", kps, ntiles, bytes);
 	plain<3, 4, 8, 2>("S13 no window loads", kps, ntiles, bytes);
-	plain<3, 4, 8, 1024>("S13 split start (old)", kps, ntiles, bytes);
-	plain<3, 4, 8, 2048>("S13 4-load windows (from o0)", kps, ntiles, bytes);
 	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);
+	if (argc > 5) {
+		plain_sp<1>("SP NT1", kps, ntiles, bytes);
+		plain_sp<2>("SP NT2", kps, ntiles, bytes);
+		plain<3, 4, 8, 1024>("S13 split start (old)", kps, ntiles, bytes);
+		plain<3, 4, 8, 2048>("S13 full windows", kps, ntiles, bytes);
+	}
 	if (argc > 4) {
 		plain<4, 4, 8>("S14 U4", kps, ntiles, bytes);
 		plain<2, 4, 8, 0, 32>("S12 T32", kps, ntiles, bytes);

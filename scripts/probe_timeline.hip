@@ -99,6 +99,36 @@ static int plain(const char *name, std::vector<mosrx_kparams> &kps, uint32_t nti
 	return 0;
 }
 
+template <uint32_t T>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8))) void k_small(mosrx_kparams kp)
+{
+	classify_tile_small<2, T>(kp, blockIdx.x);
+}
+template <uint32_t T>
+static int plain_small(const char *name, std::vector<mosrx_kparams> &kps, double bytes)
+{
+	const int nb = (int)kps.size();
+	const uint32_t ng = (kps[0].n + T - 1) / T;
+	hipEvent_t a, b;
+	CHK(hipEventCreate(&a));
+	CHK(hipEventCreate(&b));
+	float best = 1e9;
+	for (int rep = 0; rep < 3; rep++) {
+		for (int i = 0; i < nb; i++)
+			hipLaunchKernelGGL((k_small<T>), dim3(ng), dim3(T), 0, 0, kps[i]);
+		CHK(hipEventRecord(a, 0));
+		for (int i = 0; i < 2 * nb; i++)
+			hipLaunchKernelGGL((k_small<T>), dim3(ng), dim3(T), 0, 0, kps[i % nb]);
+		CHK(hipEventRecord(b, 0));
+		CHK(hipEventSynchronize(b));
+		float ms;
+		CHK(hipEventElapsedTime(&ms, a, b));
+		best = std::min(best, ms / (2 * nb));
+	}
+	printf("%-24s back-to-back %6.2f us (%5.0f GB/s)\n", name, best * 1e3, bytes / (best * 1e-3) / 1e9);
+	return 0;
+}
+
 static double pct(std::vector<double> v, double q)
 {
 	if (v.empty()) return 0;
@@ -140,23 +170,23 @@ int main(int argc, char **argv)
 	CHK(hipEventCreate(&b));
 	// plain (DBG 0) back-to-back times over the resident batches, then stamped launches
 	printf("trace kind %d n %u tiles %u: %.2f MB\n", kind, n, ntiles, bytes / 1e6);
-	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);
-	plain<3, 4, 8, 0, 64, 3>("S13 windows nt, tails nt", kps, ntiles, bytes);
-	plain<3, 4, 8, 0, 64, 0>("S13 windows rt, tails rt", kps, ntiles, bytes);
-	plain<3, 4, 8, 0, 64, 1>("S13 windows nt, tails rt", kps, ntiles, bytes);
-	plain<3, 4, 8, 2>("S13 no window loads", kps, ntiles, bytes);
-	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);
-	if (argc > 5) {
-		plain_sp<1>("SP NT1", kps, ntiles, bytes);
-		plain_sp<2>("SP NT2", kps, ntiles, bytes);
-		plain<3, 4, 8, 1024>("S13 split start (old)", kps, ntiles, bytes);
-		plain<3, 4, 8, 2048>("S13 full windows", kps, ntiles, bytes);
+	if (kind == MOSRX_TRACE_S64 || kind == MOSRX_TRACE_FW64) {
+		plain_small<256>("SMALL 256 (library)", kps, bytes);
+		plain_small<128>("SMALL 128", kps, bytes);
+		plain_small<64>("SMALL 64", kps, bytes);
+		plain_small<256>("SMALL 256 (library)", kps, bytes);
+		return 0;
 	}
-	if (argc > 4) {
-		plain<4, 4, 8>("S14 U4", kps, ntiles, bytes);
-		plain<2, 4, 8, 0, 32>("S12 T32", kps, ntiles, bytes);
-		plain<2, 4, 8, 2048, 32>("S12 T32 4-load", kps, ntiles, bytes);
-	}
+	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);
+	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
+	plain<3, 6, 8, 0, 64, 0>("S13 U6 tails cached", kps, ntiles, bytes);
+	plain<3, 8, 8, 0, 64, 0>("S13 U8 tails cached", kps, ntiles, bytes);
+	plain<4, 4, 8, 0, 64, 0>("S14 U4 tails cached", kps, ntiles, bytes);
+	plain<4, 6, 8, 0, 64, 0>("S14 U6 tails cached", kps, ntiles, bytes);
+	plain<2, 8, 8, 0, 64, 0>("S12 U8 tails cached", kps, ntiles, bytes);
+	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
+	plain<3, 4, 8, 2, 64, 0>("S13 no window loads, cached", kps, ntiles, bytes);
+	plain<3, 4, 8>("S13 U4 W8 (nt tails)", kps, ntiles, bytes);
 	float ms;
 	const bool coop = argc > 5;
 	for (int i = 0; i < 2 * nb; i++) {

@@ -472,3 +472,54 @@ def test_host_one_block_layouts(gpu_ctx, layout):
     assert_records_equal(got, ora, layout)
     cnt = np.asarray(gpu_ctx.last_counters())
     assert cnt.sum() == n and np.array_equal(cnt, np.bincount(ora["reason"], minlength=len(cnt)))
+
+
+def _options_frames(seed):
+    """IP options of every length (ihl 5..15) and TCP options (doff 5..15) with
+    segments ending inside the header window, just past it and far past it: the
+    segment start 14+4*ihl then falls before, at and after the stream tile's
+    split (frame byte 47..62) and the SMALL tile's (63..78), so the option bytes
+    past the split are summed by the tail streamers and taken out again."""
+    rng = random.Random(seed)
+    frames = []
+    for ihl in range(5, 16):
+        for doff in (5, 8, 15):
+            for plen in (0, 1, 7, 16, 33, 64, 95, 300, 1400 - 4 * (ihl + doff)):
+                f = bytearray(tcp_frame(payload=bytes(rng.getrandbits(8) for _ in range(plen)), ihl=ihl, doff=doff,
+                                        seq=rng.getrandbits(32)))
+                if rng.random() < 0.3:                          # corrupt a byte of the segment or the options
+                    f[rng.randint(14 + 20, len(f) - 1)] ^= 1 << rng.randint(0, 7)
+                frames.append(bytes(f))
+    rng.shuffle(frames)
+    return frames
+
+
+@pytest.mark.parametrize("variant", ALL_VARIANTS)
+@pytest.mark.parametrize("phase", [0, 1, 2, 5, 9, 14])
+def test_ip_options_across_the_split(gpu_ctx, variant, phase):
+    frames = _options_frames(phase)
+    buf, off, ln = pack_frames(frames, phase=phase, align=16)
+    gpu_ctx.set_variant(variant)
+    try:
+        ora = run_both(gpu_ctx, buf, off, ln, mosrx.default_params(forward=0), side=True)
+    finally:
+        gpu_ctx.set_variant(2)
+    # the trace reaches both verdicts of the TCP checksum on option-bearing frames
+    ihl = (ora["ihl_doff"] >> 4)
+    assert ((ihl > 5) & (ora["reason"] == R["TCP_OK"])).sum() > 50
+    assert ((ihl > 5) & (ora["reason"] == R["TCP_BADCSUM"])).sum() > 5
+
+
+@pytest.mark.parametrize("variant", [mosrx.shape_variant(mosrx.KIND_SMALL), mosrx.shape_variant(mosrx.KIND_S13)])
+def test_ip_options_tx_rewrite(gpu_ctx, variant):
+    """The TX rewrite shares the in-window sum: checks of option-bearing frames
+    rewritten on the GPU equal the oracle's (mOS's arithmetic), both shapes."""
+    frames = _options_frames(99)
+    buf, off, ln = pack_frames(frames, phase=3)
+    flags = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM
+    exp = O.tx_csum(buf, off, ln, flags)
+    gpu_ctx.set_variant(variant)
+    try:
+        np.testing.assert_array_equal(gpu_ctx.tx_csum_host(buf, off, ln, flags), exp)
+    finally:
+        gpu_ctx.set_variant(2)

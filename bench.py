@@ -550,7 +550,7 @@ def main():
                           for k in ("M1500", "S64", "IMIX") if k in traces}
         # the launch-amortised rx ring: a group of batches per launch (cfg.group)
         if "S64" in traces:
-            e2e["backend"]["S64_group64"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=64)
+            e2e["backend"]["S64_group128"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=128)
         e2e["backend"]["M1500_group8"] = measure_backend(traces["M1500"], "M1500", 4_000_000, device, group=8)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:

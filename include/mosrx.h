@@ -229,7 +229,7 @@ int  mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b,
  * h_tcpinfo[i] when h_tcpinfo is not NULL).  Wait with
  * mosrx_classify_host_wait; the counters are the group's sum.  Amortises the
  * launch for small batches the way an rx ring of several batches would. */
-#define MOSRX_MAX_GROUP 64
+#define MOSRX_MAX_GROUP 256
 int  mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
                                       mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo);
 

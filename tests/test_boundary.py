@@ -102,7 +102,7 @@ def test_gpu_module_config_validation():
     L.mosrx_gpu_module_cfg_default(C.byref(cfg))
     assert (cfg.batch, cfg.tx_batch, cfg.group, cfg.pipeline) == (32768, 64, 1, 1)
     cfg.num_ifs = 1
-    for field, bad in [("group", 0), ("group", 65), ("max_frame", 63), ("num_ifs", 17)]:
+    for field, bad in [("group", 0), ("group", 257), ("max_frame", 63), ("num_ifs", 17)]:
         c2 = mosrx.ModuleCfg.from_buffer_copy(cfg)
         setattr(c2, field, bad)
         assert L.mosrx_gpu_module_configure(C.byref(c2)) == -22, field

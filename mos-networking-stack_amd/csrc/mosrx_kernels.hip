@@ -169,76 +169,6 @@ __device__ __forceinline__ void hdr_load(__amdgpu_buffer_rsrc_t rs, uint32_t nby
 	}
 }
 
-// Staged header windows (SMALL tile): the 64 frames of a wave that sit in
-// buffer order within STAGE_BYTES are read with plain contiguous 1 KiB wave
-// loads into the wave's LDS stage, and every lane takes its 96-byte window from
-// there.  The gather form issues 6 loads of 64 distinct lines each per wave;
-// this one 4-5 loads of 16 lines, which is what a 64-byte-frame batch (the
-// windows of neighbouring frames overlap, the whole wave spans ~4 KiB) is
-// bound by.  Waves whose frames are not in order, or spread wider, gather.
-#define STAGE_BYTES 4224u      // 64 frames x 64 B + one window
-template <int AUX>
-__device__ __forceinline__ bool hdr_load_staged(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t o, bool active,
-                                                uint32_t lane, uint32_t *stage, hdr_win_t &win)
-{
-	const uint32_t wbase = (o + 2u) & ~3u;
-	const uint64_t act = __ballot(active);
-	if (!act)
-		return false;
-	const uint32_t first = (uint32_t)__builtin_ctzll(act), last = 63u - (uint32_t)__builtin_clzll(act);
-	const uint32_t onext = (uint32_t)__shfl_down((int)o, 1);
-	const bool in_order = __ballot(active && lane < last && onext < o) == 0;
-	const uint32_t A = uni(__builtin_amdgcn_readlane(wbase, first)) & ~15u;
-	const uint32_t Z = uni(__builtin_amdgcn_readlane(wbase, last)) + 96u;
-	if (!in_order || Z < A || Z - A > STAGE_BYTES || A >= nbytes)
-		return false;
-	u32x4 v[5];
-#pragma unroll
-	for (int i = 0; i < 5; i++) {
-		const uint32_t c = A + 1024u * i + 16u * lane;
-		v[i] = load16<AUX>(rs, c < Z ? c : ZERO_OFF, 0);
-	}
-#pragma unroll
-	for (int i = 0; i < 5; i++) {
-		const uint32_t r = 1024u * i + 16u * lane;
-		if (r < STAGE_BYTES)
-			*reinterpret_cast<u32x4 *>(reinterpret_cast<char *>(stage) + r) = v[i];
-	}
-	// a wave's own LDS writes are ordered before its later reads (no barrier)
-	const uint32_t *wp = stage + (active ? (wbase - A) >> 2 : 0u);
-#pragma unroll
-	for (int j = 0; j < WIN_RAW; j++)
-		win.raw[j] = wp[j];
-	return true;
-}
-
-// Cooperative header windows: the 64 windows of a wave are read as 384
-// 16-byte pieces, six consecutive lanes per window (so a wave instruction
-// touches ~21 cache lines instead of 64), passed through LDS (contiguous
-// writes) and read back lane-per-frame: the same 24 raw dwords hdr_load gives.
-template <int AUX>
-__device__ __forceinline__ void hdr_load_coop(__amdgpu_buffer_rsrc_t rs, uint32_t nbytes, uint32_t o, bool active,
-                                              uint32_t lane, u32x4 *stage, hdr_win_t &win)
-{
-	const uint32_t wbase = active ? ((o + 2u) & ~3u) : nbytes;
-	u32x4 v[WIN_RAW / 4];
-#pragma unroll
-	for (int m = 0; m < WIN_RAW / 4; m++) {
-		const uint32_t q = 64u * m + lane, f = q / 6u, k = q - 6u * f;
-		const uint32_t wb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(f << 2), (int)wbase);
-		v[m] = load16<AUX>(rs, wb + 16u * k, nbytes);
-	}
-#pragma unroll
-	for (int m = 0; m < WIN_RAW / 4; m++)
-		stage[64 * m + lane] = v[m];
-	// a wave's own LDS writes are ordered before its later reads (no barrier)
-#pragma unroll
-	for (int k = 0; k < WIN_RAW / 4; k++) {
-		const u32x4 x = stage[(WIN_RAW / 4) * lane + k];
-		win.raw[4 * k + 0] = x.x; win.raw[4 * k + 1] = x.y; win.raw[4 * k + 2] = x.z; win.raw[4 * k + 3] = x.w;
-	}
-}
-
 #ifdef MOSRX_RTC_BPF
 #include "mosrx_bpf_hook.h"   // generated by bpf_jit.c: mosrx_bpf_hook(win, o, cap, live, rs, lds)
 #endif
@@ -617,13 +547,11 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	constexpr int WEND = MOSRX_WINDOW_END_SMALL;
 	// the fused BPF hook reads the whole 96-byte window
 	constexpr int NLOAD = (VAR & VAR_BPF) ? WIN_RAW / 4 : WIN_NLOAD(WEND);
-	// windows gathered per lane (hdr_load); DBG 64 stages them through LDS instead
-	// (measured slower on S64: 192 vs 125 us per 8M frames), DBG 2 skips the
-	// window loads -- probe builds only
-	constexpr bool STAGED = (VAR & VAR_BPF) == 0 && (DBG & 64);
+	// DBG 2 skips the window loads (probe builds only).  Tried and slower:
+	// windows staged through LDS from contiguous wave loads (64 B config 192 vs
+	// 125 us per 8M frames).
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
-	__shared__ __attribute__((aligned(16))) uint32_t s_stage[STAGED ? TILE / 64u : 1u][STAGED ? STAGE_BYTES / 4u : 1u];
 
 	const uint32_t t = threadIdx.x, lane = t & 63u;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
@@ -640,9 +568,6 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 #pragma unroll
 		for (int i = 0; i < WIN_RAW; i++)
 			win.raw[i] = o + i;
-	} else if constexpr (STAGED) {
-		if (!hdr_load_staged<WIN_AUX(VAR)>(rs, nbytes, o, active, lane, s_stage[t >> 6], win))
-			hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, o, active, win);
 	} else {
 		hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, o, active, win);
 	}
@@ -965,9 +890,6 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 #pragma unroll
 			for (int i = 0; i < WIN_RAW; i++)
 				win.raw[i] = o + i;
-		} else if constexpr ((DBG & 256) != 0) {
-			__shared__ u32x4 s_win[64 * (WIN_RAW / 4)];
-			hdr_load_coop<WIN_AUX(VAR)>(rs, nbytes, o, active, lane, s_win, win);
 		} else {
 			hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, o, active, win);
 		}

@@ -135,7 +135,6 @@ int main(int argc, char **argv)
 	printf("trace kind %d n %u: %.2f MB algorithmic\n", kind, n, bytes / 1e6);
 	if (kind == MOSRX_TRACE_S64 || kind == MOSRX_TRACE_FW64) {
 		run("product SMALL 256 (gathered windows)", launch_small<256>, kps, nb, bytes);
-		run("SMALL 256 LDS-staged windows", launch_small<256, 64>, kps, nb, bytes);
 		run("SMALL 256 no window loads", launch_small<256, 2>, kps, nb, bytes);
 		run("SMALL 128", launch_small<128>, kps, nb, bytes);
 		return 0;

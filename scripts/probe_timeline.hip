@@ -188,15 +188,15 @@ int main(int argc, char **argv)
 	plain<3, 4, 8, 2, 64, 0>("S13 no window loads, cached", kps, ntiles, bytes);
 	plain<3, 4, 8>("S13 U4 W8 (nt tails)", kps, ntiles, bytes);
 	float ms;
-	const bool coop = argc > 5;
+	const bool after_b = argc > 5;   // timeline of the windows-after-the-barrier variant (DBG 512)
 	for (int i = 0; i < 2 * nb; i++) {
-		if (coop)
+		if (after_b)
 			hipLaunchKernelGGL((k_tl<128 | 512>), dim3(ntiles), dim3(256), 0, 0, kps[i % nb]);
 		else
 			hipLaunchKernelGGL((k_tl<128>), dim3(ntiles), dim3(256), 0, 0, kps[i % nb]);
 	}
 	CHK(hipEventRecord(a, 0));
-	if (coop)
+	if (after_b)
 		hipLaunchKernelGGL((k_tl<128 | 512>), dim3(ntiles), dim3(256), 0, 0, kps[1 % nb]);
 	else
 		hipLaunchKernelGGL((k_tl<128>), dim3(ntiles), dim3(256), 0, 0, kps[1 % nb]);

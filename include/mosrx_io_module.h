@@ -108,6 +108,15 @@ typedef struct mosrx_afpacket_info {
 int           mosrx_source_afpacket_info(mosrx_source *s, mosrx_afpacket_info *info);
 /* Pull the next frame into dst (at most cap bytes); returns its caplen, 0 when none. */
 int           mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap);
+/* Zero-copy runs (what gpu_module_func lends to the GPU copy): up to max_n
+ * frames that sit in the source's own memory, as one run from *frames in
+ * buffer order -- off[]/len[] relative to it, len clamped to max_frame --
+ * valid until mosrx_source_give_back releases the run (oldest first; for the
+ * AF_PACKET ring that returns its blocks to the kernel).  Returns the count
+ * (0: nothing ready) or -EOPNOTSUPP for sources that cannot lend. */
+int           mosrx_source_borrow(mosrx_source *s, uint32_t max_n, uint32_t max_frame, const uint8_t **frames,
+                                  uint64_t *frames_bytes, uint32_t *off, uint16_t *len);
+int           mosrx_source_give_back(mosrx_source *s);
 /* How gpu_module_func takes batches from an in-memory source: 0 = best (the
  * replay buffer lent zero-copy when it is pinned, else copied in runs), 1 =
  * copied in runs, 2 = copied frame by frame (what a recvfrom-style source

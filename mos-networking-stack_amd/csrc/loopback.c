@@ -295,7 +295,7 @@ mosrx_source *mosrx_source_pcap(const char *path, uint32_t loops)
  * drops them too, so a frame sent on `lo` is received once. */
 #define AFP_BLOCK_SIZE (1u << 22)   /* 4 MiB blocks */
 #define AFP_MAX_BLOCKS 64
-#define AFP_MAX_RUNS   8            /* borrowed runs outstanding (the backend holds 2) */
+#define AFP_MAX_RUNS   (2 * MOSRX_MAX_GROUP + 2)   /* borrowed runs outstanding: two groups of batches */
 
 struct src_afp {
 	struct mosrx_source base;
@@ -399,6 +399,8 @@ static int afp_next(struct mosrx_source *s_, uint8_t *dst, uint32_t cap)
 	}
 }
 
+static void afp_give_back(struct mosrx_source *s_);
+
 /* Zero-copy: frames of consecutive retired blocks, up to the ring's end (a run
  * never wraps, so it is one contiguous span of the registered ring). */
 static uint32_t afp_borrow(struct mosrx_source *s_, uint32_t max_n, uint32_t max_frame, const uint8_t **frames,
@@ -432,7 +434,7 @@ static uint32_t afp_borrow(struct mosrx_source *s_, uint32_t max_n, uint32_t max
 	s->run_upto[s->run_tail % AFP_MAX_RUNS] = afp_done(s);
 	s->run_tail++;
 	if (!k) {                        /* only outgoing frames: nothing to lend, release at once */
-		s_->give_back(s_);
+		afp_give_back(s_);
 		return 0;
 	}
 	*frames = base;
@@ -615,6 +617,37 @@ int mosrx_source_tx_stats(const mosrx_source *s, uint64_t *packets, uint64_t *by
 	if (packets) *packets = s->tx_packets;
 	if (bytes) *bytes = s->tx_bytes;
 	if (errors) *errors = s->tx_errors;
+	return 0;
+}
+
+/* Zero-copy runs for any consumer: the backend's path (borrow/give_back) —
+ * for the AF_PACKET ring also when it is not registered with the HIP runtime
+ * (a host consumer needs no registration; the backend only lends registered
+ * rings to the GPU copy). */
+int mosrx_source_borrow(mosrx_source *s, uint32_t max_n, uint32_t max_frame, const uint8_t **frames,
+                        uint64_t *frames_bytes, uint32_t *off, uint16_t *len)
+{
+	if (!s || !frames || !frames_bytes || !off || !len || max_frame == 0)
+		return -EINVAL;
+	if (s->close == afp_close)
+		return (int)afp_borrow(s, max_n, max_frame, frames, frames_bytes, off, len);
+	if (!s->borrow)
+		return -EOPNOTSUPP;
+	return (int)s->borrow(s, max_n, max_frame, frames, frames_bytes, off, len);
+}
+
+int mosrx_source_give_back(mosrx_source *s)
+{
+	if (!s)
+		return -EINVAL;
+	if (s->close == afp_close) {
+		afp_give_back(s);
+		return 0;
+	}
+	if (!s->borrow)
+		return -EOPNOTSUPP;
+	if (s->give_back)
+		s->give_back(s);
 	return 0;
 }
 

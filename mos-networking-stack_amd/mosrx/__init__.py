@@ -209,6 +209,8 @@ def lib():
             "mosrx_source_afpacket": (P, [C.c_char_p]),
             "mosrx_source_close": (None, [P]),
             "mosrx_source_next": (I, [P, P, U32]),
+            "mosrx_source_borrow": (I, [P, U32, U32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), P, P]),
+            "mosrx_source_give_back": (I, [P]),
             "mosrx_source_mem_set_mode": (I, [P, I]),
             "mosrx_gpu_module_cfg_default": (None, [C.POINTER(ModuleCfg)]),
             "mosrx_gpu_module_configure": (I, [C.POINTER(ModuleCfg)]),
@@ -907,6 +909,26 @@ def source_tx_stats(src: int) -> tuple[int, int, int]:
     a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
     _chk(lib().mosrx_source_tx_stats(src, C.byref(a), C.byref(b), C.byref(c)), "mosrx_source_tx_stats")
     return a.value, b.value, c.value
+
+
+def source_borrow(src, max_n: int, max_frame: int = 65535):
+    """One zero-copy run of the source (mosrx_source_borrow): (frames as bytes
+    objects, the run's base address, off, len), or None when nothing is ready.
+    The run stays valid until source_give_back."""
+    off = np.zeros(max(1, max_n), np.uint32)
+    ln = np.zeros(max(1, max_n), np.uint16)
+    base, nbytes = C.c_void_p(), C.c_uint64()
+    n = lib().mosrx_source_borrow(src, max_n, max_frame, C.byref(base), C.byref(nbytes),
+                                  off.ctypes.data, ln.ctypes.data)
+    _chk(min(n, 0), "mosrx_source_borrow")
+    if n == 0:
+        return None
+    frames = [C.string_at(base.value + int(o), int(l)) for o, l in zip(off[:n], ln[:n])]
+    return frames, base.value, off[:n].copy(), ln[:n].copy()
+
+
+def source_give_back(src) -> None:
+    _chk(lib().mosrx_source_give_back(src), "mosrx_source_give_back")
 
 
 def read_pcap(path: str) -> list[bytes]:

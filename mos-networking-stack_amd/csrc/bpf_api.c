@@ -203,6 +203,7 @@ int mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
 	c->bpf_fn = NULL;   /* the compiled kernels of the previous set no longer apply */
 	c->bpf_fs = NULL;
 	c->bpf_fm = NULL;
+	c->bpf_fr = NULL;
 	if (c->bpf_engine_req == MOSRX_BPF_ENGINE_JIT && nprog)
 		mosrx__bpf_jit_build(c, staged);   /* on failure the interpreter runs the set */
 	return 0;

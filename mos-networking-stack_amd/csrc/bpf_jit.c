@@ -409,6 +409,8 @@ static const char k_fused_main[] =
 	"#include \"mosrx_kernels.hip\"\n"
 	"extern \"C\" __global__ __launch_bounds__(WG_THREADS(MOSRX_KIND_S13)) void mosrx_classify_bpf_stream(mosrx_kparams kp)\n"
 	"{ classify_tile<MOSRX_KIND_S13, 2 | VAR_BPF>(kp, blockIdx.x); }\n"
+	"extern \"C\" __global__ __launch_bounds__(WG_THREADS(MOSRX_KIND_S13)) void mosrx_classify_bpf_stream_rt(mosrx_kparams kp)\n"
+	"{ classify_tile<MOSRX_KIND_S13, VAR_BPF>(kp, blockIdx.x); }\n"
 	"extern \"C\" __global__ __launch_bounds__(WG_THREADS(MOSRX_KIND_SMALL)) void mosrx_classify_bpf_small(mosrx_kparams kp)\n"
 	"{ classify_tile<MOSRX_KIND_SMALL, 2 | VAR_BPF>(kp, blockIdx.x); }\n";
 
@@ -482,8 +484,8 @@ extern const char *const mosrx__src_names[];
 extern const char *const mosrx__src_texts[];
 
 /* The fused classify + BPF module: the embedded kernel sources + the hook. */
-static int compile_fused(const char *hook, hipModule_t *mod, hipFunction_t *fs, hipFunction_t *fm, char *log,
-                         size_t logsz, size_t *code_size)
+static int compile_fused(const char *hook, hipModule_t *mod, hipFunction_t *fs, hipFunction_t *fm,
+                         hipFunction_t *fr, char *log, size_t logsz, size_t *code_size)
 {
 	const char *names[8], *texts[8];
 	char *code;
@@ -504,6 +506,7 @@ static int compile_fused(const char *hook, hipModule_t *mod, hipFunction_t *fs, 
 	}
 	if (hipModuleLoadData(mod, code) != hipSuccess ||
 	    hipModuleGetFunction(fs, *mod, "mosrx_classify_bpf_stream") != hipSuccess ||
+	    hipModuleGetFunction(fr, *mod, "mosrx_classify_bpf_stream_rt") != hipSuccess ||
 	    hipModuleGetFunction(fm, *mod, "mosrx_classify_bpf_small") != hipSuccess)
 		rc = -EIO;
 	free(code);
@@ -529,7 +532,7 @@ int mosrx__bpf_jit_compile_fused(const mosrx_bpf_insn *insns, const mosrx_bparam
 	char *hook = NULL;
 	int rc = mosrx__bpf_jit_hook_source(insns, t, &hook);
 	if (!rc)
-		rc = compile_fused(hook, NULL, NULL, NULL, log, logsz, code_size);
+		rc = compile_fused(hook, NULL, NULL, NULL, NULL, log, logsz, code_size);
 	free(hook);
 	return rc;
 }
@@ -557,12 +560,14 @@ int mosrx__bpf_jit_build(mosrx_ctx *c, const mosrx_bpf_insn *insns)
 	c->bpf_fn = NULL;
 	c->bpf_fs = NULL;
 	c->bpf_fm = NULL;
+	c->bpf_fr = NULL;
 	c->bpf_jit_log[0] = 0;
 	for (i = 0; i < c->njit; i++)
 		if (c->jit[i].key == key) {
 			c->bpf_fn = c->jit[i].fn;
 			c->bpf_fs = c->jit[i].fs;
 			c->bpf_fm = c->jit[i].fm;
+			c->bpf_fr = c->jit[i].fr;
 			return 0;
 		}
 	if ((rc = mosrx__bpf_jit_source(insns, t, &src)))
@@ -575,12 +580,12 @@ int mosrx__bpf_jit_build(mosrx_ctx *c, const mosrx_bpf_insn *insns)
 		if (rc)
 			return rc;
 		hipModule_t fmod = NULL;
-		hipFunction_t fs = NULL, fm = NULL;
+		hipFunction_t fs = NULL, fm = NULL, fr = NULL;
 		char *hook = NULL;
 		if (mosrx__bpf_jit_hook_source(insns, t, &hook) ||
-		    compile_fused(hook, &fmod, &fs, &fm, c->bpf_jit_log, sizeof(c->bpf_jit_log), NULL)) {
+		    compile_fused(hook, &fmod, &fs, &fm, &fr, c->bpf_jit_log, sizeof(c->bpf_jit_log), NULL)) {
 			fmod = NULL;   /* no fused kernel: mosrx_classify_bpf_dev runs two launches */
-			fs = fm = NULL;
+			fs = fm = fr = NULL;
 		}
 		free(hook);
 		if (c->njit == MOSRX_BPF_JIT_CACHE) {   /* evict the oldest */
@@ -596,10 +601,12 @@ int mosrx__bpf_jit_build(mosrx_ctx *c, const mosrx_bpf_insn *insns)
 		c->jit[c->njit].fmod = fmod;
 		c->jit[c->njit].fs = fs;
 		c->jit[c->njit].fm = fm;
+		c->jit[c->njit].fr = fr;
 		c->njit++;
 		c->bpf_fn = fn;
 		c->bpf_fs = fs;
 		c->bpf_fm = fm;
+		c->bpf_fr = fr;
 	}
 	return 0;
 }
@@ -607,7 +614,9 @@ int mosrx__bpf_jit_build(mosrx_ctx *c, const mosrx_bpf_insn *insns)
 /* Fused classify + BPF launch (kp carries bmatch). */
 int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hipStream_t s)
 {
-	hipFunction_t f = small ? c->bpf_fm : c->bpf_fs;
+	/* the library's tail policy: cached tail loads for batches of small frames */
+	const int cached = !(mosrx__tail_variant(c, kp->frames_bytes, kp->n) & 2);
+	hipFunction_t f = small ? c->bpf_fm : cached && c->bpf_fr ? c->bpf_fr : c->bpf_fs;
 	const unsigned tile = small ? MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL) : MOSRX_KIND_FRAMES(MOSRX_KIND_S13);
 	const unsigned threads = small ? 256u : 64u * (1u + MOSRX_STREAMERS);
 	mosrx_kparams k = *kp;
@@ -647,4 +656,5 @@ void mosrx__bpf_jit_free(mosrx_ctx *c)
 	c->bpf_fn = NULL;
 	c->bpf_fs = NULL;
 	c->bpf_fm = NULL;
+	c->bpf_fr = NULL;
 }

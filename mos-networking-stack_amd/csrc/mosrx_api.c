@@ -299,7 +299,7 @@ static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_
  * non-temporal against 20.1 us cached; profiles/r02_probe/).  Only when the
  * context runs the library's default variant. */
 #define MOSRX_NT_TAIL_MIN_FRAME 768   /* mean bytes per frame */
-static int tail_variant(const mosrx_ctx *c, uint64_t bytes, uint64_t n)
+int mosrx__tail_variant(const mosrx_ctx *c, uint64_t bytes, uint64_t n)
 {
 	if (c->variant != MOSRX_DEFAULT_VARIANT || n == 0 || bytes / n >= MOSRX_NT_TAIL_MIN_FRAME)
 		return c->variant;
@@ -328,7 +328,7 @@ static int launch_flags(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frame
 	kp.frames_bytes = (uint32_t)b->frames_bytes;
 	kp.n = b->n;
 	kp.flags = kflags;
-	return mosrx_launch_classify(&kp, tile_for(c, b), tail_variant(c, b->frames_bytes, b->n), (void *)s);
+	return mosrx_launch_classify(&kp, tile_for(c, b), mosrx__tail_variant(c, b->frames_bytes, b->n), (void *)s);
 }
 
 static int launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
@@ -827,7 +827,7 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 	qp.tinfo = h_tcpinfo ? 1u : 0u;
 	if (c->timing)
 		HIPCHK(hipEventRecord(s->kev0, s->stream));
-	if ((rc = mosrx_launch_queue(&qp, tiles, kind, tail_variant(c, dev_bytes, ntot), s->stream)))
+	if ((rc = mosrx_launch_queue(&qp, tiles, kind, mosrx__tail_variant(c, dev_bytes, ntot), s->stream)))
 		return rc;
 	if (c->timing)
 		HIPCHK(hipEventRecord(s->kev1, s->stream));
@@ -1266,7 +1266,7 @@ int mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream)
 	qp.flags = c->kflags;
 	qp.tpb = q->tpb;
 	qp.tinfo = 0;
-	return mosrx_launch_queue(&qp, q->total_tiles, q->tile, tail_variant(c, q->bytes, q->n),
+	return mosrx_launch_queue(&qp, q->total_tiles, q->tile, mosrx__tail_variant(c, q->bytes, q->n),
 	                          stream ? stream : (void *)c->stream);
 }
 

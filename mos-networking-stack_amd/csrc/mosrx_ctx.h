@@ -53,7 +53,8 @@ struct mosrx_ctx {
 	int bpf_engine_req;              /* MOSRX_BPF_ENGINE_* for the next mosrx_bpf_set */
 	char bpf_jit_log[512];           /* hipRTC log of the last failed compile */
 	hipFunction_t bpf_fs, bpf_fm;    /* fused classify + BPF kernels (S13 / SMALL tiles), NULL: none */
-	struct { uint64_t key; hipModule_t mod, fmod; hipFunction_t fn, fs, fm; } jit[MOSRX_BPF_JIT_CACHE];
+	hipFunction_t bpf_fr;            /* the S13 one with cached tail loads (batches of small frames) */
+	struct { uint64_t key; hipModule_t mod, fmod; hipFunction_t fn, fs, fm, fr; } jit[MOSRX_BPF_JIT_CACHE];
 	uint32_t njit;
 	hipStream_t xs[MOSRX_MAX_STREAMS];   /* timing streams (mosrx_time_op), created on first use */
 	hipEvent_t xdone[MOSRX_MAX_STREAMS];
@@ -73,5 +74,10 @@ int mosrx__bpf_jit_compile_fused(const mosrx_bpf_insn *insns, const mosrx_bparam
 int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out);
 int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hipStream_t s);
 int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uint32_t n);
+
+/* The variant a launch of `n` frames in `bytes` runs: the context's, with the
+ * tail loads cached instead of non-temporal for batches of small frames when
+ * the context runs the library default (mosrx_api.c). */
+int mosrx__tail_variant(const mosrx_ctx *c, uint64_t bytes, uint64_t n);
 
 #endif

@@ -30,6 +30,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import struct
 import subprocess
 import sys
 import time
@@ -436,7 +437,39 @@ def measure_fw64(ctx, seconds: float):
     db.free()
     out["gpu_device_resident"] = {"kernel_ms": k, "mpkts": tr.n / (k * 1e-3) / 1e6,
                                   "method": "500 back-to-back launches over the resident 10K batch"}
+    out["e2e_boundary"] = measure_fw64_boundary(tr)
     return out
+
+
+def measure_fw64_boundary(tr: mosrx.Trace, loops: int = 50):
+    """Config #1 end to end through the drop-in boundary on one host thread: the
+    10K trace replayed from a pcap file by the libpcap-free pcap source,
+    gpu_module_func in simple_firewall's state, RunMainLoop's rx loop with the
+    ForwardEthernetFrame consumer sending every accepted frame out through the
+    source's TX (a pcap dump).  libpcap and raw sockets are not available to the
+    bench (no CAP_NET_RAW on the box), so the file stands in for the wire."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        path, out = os.path.join(d, "fw.pcap"), os.path.join(d, "tx.pcap")
+        with open(path, "wb") as fh:
+            fh.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, 1))
+            for i, (o, n) in enumerate(zip(tr.off.tolist(), tr.len.tolist())):
+                fh.write(struct.pack("<IIII", i, 0, n, n) + bytes(tr.frames[o:o + n]))
+        src = mosrx.lib().mosrx_source_pcap(path.encode(), loops)
+        mosrx.source_tx_pcap(src, out)
+        be = mosrx.GpuBackend([src], params=mosrx.default_params(), batch=tr.n, cpu=15, timing=True)
+        try:
+            fwd = be.forwarder([0])
+            t0 = time.perf_counter()
+            st = be.run_loop(forward=fwd)
+            dt = time.perf_counter() - t0
+            ms = be.stats()
+        finally:
+            be.close()
+    return {"mpkts": st.rx_packets / dt / 1e6, "frames": int(st.rx_packets), "forwarded": int(fwd.forwarded),
+            "seconds": round(dt, 3), "device_us_per_batch": round(1e3 * ms.kernel_ms / max(ms.kernel_launches, 1), 3),
+            "method": f"pcap file ({loops} replays of the 10K trace) -> gpu_module_func (simple_firewall state) -> "
+                      f"mosrx_rx_loop + mosrx_forward_frame -> source TX (pcap dump), one host thread"}
 
 
 def measure_e2e(ctx, tr: mosrx.Trace, iters: int):

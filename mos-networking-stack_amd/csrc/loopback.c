@@ -208,21 +208,23 @@ int mosrx_source_mem_set_mode(mosrx_source *s_, int mode)
 }
 
 /* ---------------- classic pcap file ---------------- */
+/* pcap_next (pcap_module.c:41) without libpcap.  The file is mapped and read
+ * in place: per frame (next) or a batch at a time straight into the backend's
+ * stage (fill: one memcpy per frame, no stdio); a file that cannot be mapped
+ * is read through stdio, per frame. */
 struct src_pcap {
 	struct mosrx_source base;
 	FILE *f;
-	char *path;
 	int swap;
 	uint32_t loops, done_loops;
+	const uint8_t *map;             /* the mapped file (NULL: stdio) */
+	size_t map_len, pos;            /* the next record header at map + pos */
 };
 
 static uint32_t sw32(uint32_t v, int swap) { return swap ? __builtin_bswap32(v) : v; }
 
-static int pcap_open_hdr(struct src_pcap *s)
+static int pcap_check_hdr(struct src_pcap *s, const uint32_t *gh)
 {
-	uint32_t gh[6];
-	if (fread(gh, 4, 6, s->f) != 6)
-		return -1;
 	if (gh[0] == 0xa1b2c3d4u || gh[0] == 0xa1b23c4du)
 		s->swap = 0;
 	else if (gh[0] == 0xd4c3b2a1u || gh[0] == 0x4d3cb2a1u)
@@ -234,10 +236,40 @@ static int pcap_open_hdr(struct src_pcap *s)
 	return 0;
 }
 
+/* The next record of the mapped file (wrapping for replays): its bytes and
+ * captured length, or NULL at the end of the last replay. */
+static const uint8_t *pcap_map_record(struct src_pcap *s, uint32_t *incl)
+{
+	for (;;) {
+		if (s->pos + 16 <= s->map_len) {
+			uint32_t rh[4];
+			memcpy(rh, s->map + s->pos, 16);
+			*incl = sw32(rh[2], s->swap);
+			if (s->pos + 16 + (size_t)*incl <= s->map_len)
+				return s->map + s->pos + 16;
+		}
+		s->done_loops++;             /* end of file (or a truncated last record) */
+		if (s->loops && s->done_loops >= s->loops)
+			return NULL;
+		if (s->map_len < 24 + 16 || s->pos == 24)
+			return NULL;             /* an empty file never yields a frame */
+		s->pos = 24;
+	}
+}
+
 static int pcap_next_frame(struct mosrx_source *s_, uint8_t *dst, uint32_t cap)
 {
 	struct src_pcap *s = (struct src_pcap *)s_;
 	uint32_t rh[4], incl, take;
+	if (s->map) {
+		const uint8_t *rec = pcap_map_record(s, &incl);
+		if (!rec)
+			return 0;
+		take = incl < cap ? incl : cap;
+		memcpy(dst, rec, take);
+		s->pos += 16 + (size_t)incl;
+		return (int)take;
+	}
 	for (;;) {
 		if (fread(rh, 4, 4, s->f) == 4)
 			break;
@@ -256,28 +288,68 @@ static int pcap_next_frame(struct mosrx_source *s_, uint8_t *dst, uint32_t cap)
 	return (int)take;
 }
 
+/* A batch into the stage, frames at 16-byte boundaries + 2 (the backend's layout). */
+static uint32_t pcap_fill(struct mosrx_source *s_, uint8_t *dst, uint64_t cap, uint32_t *off, uint16_t *len,
+                          uint32_t max_n, uint32_t max_frame, uint64_t *end)
+{
+	struct src_pcap *s = (struct src_pcap *)s_;
+	uint64_t pos = 2;
+	uint32_t k = 0, incl;
+	while (k < max_n && pos + max_frame + 16 <= cap) {
+		const uint8_t *rec = pcap_map_record(s, &incl);
+		uint32_t take;
+		if (!rec)
+			break;
+		take = incl < max_frame ? incl : max_frame;
+		memcpy(dst + pos, rec, take);
+		s->pos += 16 + (size_t)incl;
+		off[k] = (uint32_t)pos;
+		len[k] = (uint16_t)take;
+		k++;
+		pos = ((pos + (uint64_t)take - 2 + 15) & ~15ull) + 2;
+	}
+	*end = pos;
+	return k;
+}
+
 static void pcap_close_src(struct mosrx_source *s_)
 {
 	struct src_pcap *s = (struct src_pcap *)s_;
+	if (s->map)
+		munmap((void *)s->map, s->map_len);
 	if (s->f)
 		fclose(s->f);
-	free(s->path);
 	free(s);
 }
 
 mosrx_source *mosrx_source_pcap(const char *path, uint32_t loops)
 {
 	struct src_pcap *s = calloc(1, sizeof(*s));
+	uint32_t gh[6];
+	long sz;
 	if (!s)
 		return NULL;
 	s->f = fopen(path, "rb");
-	if (!s->f || pcap_open_hdr(s)) {
+	if (!s->f || fread(gh, 4, 6, s->f) != 6 || pcap_check_hdr(s, gh)) {
 		pcap_close_src(&s->base);
 		return NULL;
 	}
 	s->loops = loops ? loops : 1;
 	s->base.next = pcap_next_frame;
 	s->base.close = pcap_close_src;
+	if (fseek(s->f, 0, SEEK_END) == 0 && (sz = ftell(s->f)) >= 24) {
+		void *m = mmap(NULL, (size_t)sz, PROT_READ, MAP_PRIVATE, fileno(s->f), 0);
+		if (m != MAP_FAILED) {
+			s->map = m;
+			s->map_len = (size_t)sz;
+			s->pos = 24;
+			s->base.fill = pcap_fill;
+		}
+	}
+	if (!s->map && fseek(s->f, 24, SEEK_SET)) {
+		pcap_close_src(&s->base);
+		return NULL;
+	}
 	return &s->base;
 }
 

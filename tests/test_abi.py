@@ -168,3 +168,26 @@ def test_pcap_source_reads_classic_pcap(swap, nsec):
         mosrx.lib().mosrx_source_close(src)
     assert got == frames
     assert not mosrx.lib().mosrx_source_pcap(b"/nonexistent.pcap", 1)
+
+
+def test_pcap_source_replays_and_stops_at_a_truncated_record():
+    """Replays wrap to the first record; a last record cut short by the end of
+    the file ends each replay (as pcap_next does); an empty capture yields
+    nothing, however many replays are asked for."""
+    frames = [tcp_frame(payload=bytes([i]) * (i * 13)) for i in range(9)]
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "t.pcap")
+        with open(path, "wb") as fh:
+            fh.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, 1))
+            for i, f in enumerate(frames):
+                fh.write(struct.pack("<IIII", i, 0, len(f), len(f)) + f)
+            fh.write(struct.pack("<IIII", 99, 0, 500, 500) + b"cut")   # truncated record
+        src = mosrx.lib().mosrx_source_pcap(path.encode(), 3)
+        assert _drain(src) == frames * 3
+        mosrx.lib().mosrx_source_close(src)
+        empty = os.path.join(d, "e.pcap")
+        with open(empty, "wb") as fh:
+            fh.write(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, 1))
+        src = mosrx.lib().mosrx_source_pcap(empty.encode(), 5)
+        assert _drain(src) == []
+        mosrx.lib().mosrx_source_close(src)

@@ -234,3 +234,38 @@ def test_afpacket_ring_lent_zero_copy_to_the_backend():
     ora = O.classify(t.frames, t.off, t.len, O.params())
     assert_records_equal(np.array([r for _, r in mine], mosrx.RESULT_DTYPE), ora, "afpacket")
     assert info.zero_copy == 1
+
+
+def test_config1_simple_firewall_end_to_end(tmp_path):
+    """BASELINE config #1 through the drop-in boundary: 10 000 x 60 B frames of
+    one flow in a pcap file, read by the libpcap-free pcap source (pcap_next,
+    pcap_module.c:41), classified by gpu_module_func in simple_firewall's state
+    (num_msp 1, forward 1, num_queues 1, i40e map), consumed by RunMainLoop's rx
+    loop (core.c:897-909) with the ForwardEthernetFrame consumer (eth_out.c:105-129)
+    -- the firewall forwards what its checks accept -- whose frames leave
+    through the source's TX (pcap_inject's place, here a pcap dump).  NETSTAT,
+    the reason census and the forwarded frames equal what the oracle says mOS
+    does; nothing is dropped or reordered."""
+    t = mosrx.Trace(mosrx.TRACE_FW64, 10_000)
+    path, out = str(tmp_path / "fw.pcap"), str(tmp_path / "out.pcap")
+    write_pcap(path, t.frames, t.off, t.len)
+    src = mosrx.lib().mosrx_source_pcap(path.encode(), 1)
+    assert src
+    mosrx.source_tx_pcap(src, out)
+    be = mosrx.GpuBackend([src], params=mosrx.default_params(), batch=4096, cpu=13, timing=True)
+    try:
+        fwd = be.forwarder([0])
+        st = be.run_loop(forward=fwd)
+        ms = be.stats()
+    finally:
+        be.close()
+    ora = O.classify(t.frames, t.off, t.len, O.params())
+    assert st.rx_packets == t.n and st.batches == 3
+    assert st.rx_bytes == int(t.len.astype(np.int64).sum()) + 24 * t.n     # + ETHER_OVR per frame
+    assert st.rx_errors == int((ora["verdict"] < 0).sum())
+    assert list(st.by_reason) == np.bincount(ora["reason"], minlength=NREASON).tolist()
+    keep = np.nonzero(ora["verdict"] == 1)[0]
+    assert fwd.forwarded == len(keep) and fwd.dropped == t.n - len(keep)
+    assert ms.tx_packets == len(keep) and ms.kernel_launches == 3
+    sent = mosrx.read_pcap(out)
+    assert sent == [bytes(t.frames[t.off[i]:t.off[i] + t.len[i]]) for i in keep]

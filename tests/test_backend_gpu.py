@@ -321,3 +321,54 @@ def test_two_netdevs_forwarding_between_them(tmp_path):
     assert fwd.forwarded == len(ka) + len(kb)
     assert mosrx.read_pcap(outb) == [bytes(ta.frames[ta.off[i]:ta.off[i] + ta.len[i]]) for i in ka]
     assert mosrx.read_pcap(outa) == [bytes(tb.frames[tb.off[i]:tb.off[i] + tb.len[i]]) for i in kb]
+
+
+def test_two_mtcp_threads_run_concurrently():
+    """One context per mTCP thread (core.c:1282-1349), each thread with its own
+    source for the same netdev (mosrx_gpu_module_bind_source, as one
+    PACKET_FANOUT socket per thread would be) and its own GPU context, both
+    rx loops running at the same time on their own host threads: each thread's
+    census equals the oracle on its own frames."""
+    import ctypes as C
+    import threading
+    traces = [mosrx.Trace(mosrx.TRACE_IMIX, 20000, nflows=800, seed=31),
+              mosrx.Trace(mosrx.TRACE_M1500, 6000, nflows=800, seed=32)]
+    srcs = [mosrx.mem_source(t.frames, t.off, t.len, loops=3) for t in traces]
+    L = mosrx.lib()
+    cfg = mosrx.ModuleCfg()
+    L.mosrx_gpu_module_cfg_default(C.byref(cfg))
+    cfg.num_ifs, cfg.src[0], cfg.batch, cfg.ngpu, cfg.group = 1, srcs[0], 4096, 1, 2
+    assert L.mosrx_gpu_module_configure(C.byref(cfg)) == 0
+    m = mosrx.gpu_module()
+    mosrx._VOIDFN(m.load_module_upper_half)()
+    cpus = (40, 41)
+    ctx_objs = [C.c_uint64(0xBEEF0000 + c) for c in cpus]
+    ctxs = [C.addressof(o) for o in ctx_objs]
+    for c, x, s in zip(cpus, ctxs, srcs):
+        assert L.mosrx_gpu_module_bind(x, c) == 0
+        assert L.mosrx_gpu_module_bind_source(c, 0, s) == 0
+    for x in ctxs:
+        mosrx._CTXFN(m.init_handle)(x)
+    stats = [mosrx.RxStats(), mosrx.RxStats()]
+    rcs = [None, None]
+    opts = mosrx.RxLoopOpts(0, 1, 0, 0)
+
+    def run(i):
+        rcs[i] = L.mosrx_rx_loop_ex(C.addressof(m), ctxs[i], 1, C.byref(opts), None, None, C.byref(stats[i]))
+
+    th = [threading.Thread(target=run, args=(i,)) for i in (0, 1)]
+    try:
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+    finally:
+        for x in ctxs:
+            mosrx._CTXFN(m.destroy_handle)(x)
+        for s in srcs:
+            L.mosrx_source_close(s)
+    assert rcs == [0, 0]
+    for t, st in zip(traces, stats):
+        ora = O.classify(t.frames, t.off, t.len, O.params())
+        assert st.rx_packets == 3 * t.n
+        assert list(st.by_reason) == (3 * np.bincount(ora["reason"], minlength=NREASON)).tolist()

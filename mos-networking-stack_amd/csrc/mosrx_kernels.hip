@@ -732,6 +732,11 @@ __device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t 
 	const bool cand = hi_l > lo_l;
 	const uint32_t ec_l = (hi_l - 1u) & ~15u;
 	const uint32_t R1 = A + (b1 << 10);
+	// per frame lane, once per tile: the block and the lane (as a ds_bpermute
+	// byte address) of its tail's first and last chunk in the span (lo_l >= A
+	// for every candidate of a tile in buffer order)
+	const uint32_t blo = cand ? (lo_l - A) >> 10 : 0xFFFFFFFFu, bec = cand ? (ec_l - A) >> 10 : 0xFFFFFFFFu;
+	const int alo = (int)(((lo_l - A) >> 2) & 0xFCu), aec = (int)(((ec_l - A) >> 2) & 0xFCu);
 	uint32_t acc = 0, carry = 0;
 
 	u32x4 v[U];
@@ -748,19 +753,17 @@ __device__ __forceinline__ void stream_scan(__amdgpu_buffer_rsrc_t rs, uint32_t 
 			if constexpr (DBG & 4) {
 				acc ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
 			} else if (b < b1) {
-				const uint32_t c0 = A + (b << 10);
 				uint32_t s = add16x2(0u, v[i].x);
 				s = add16x2(s, v[i].y);
 				s = add16x2(s, v[i].z);
 				s = add16x2(s, v[i].w);
 				const uint32_t X = carry + wave_scan(s);   // inclusive prefix of the run
 				carry = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
-				const uint32_t rl = lo_l - c0, re = ec_l - c0;
-				const bool es = cand && rl < 1024u, ee = cand && re < 1024u;
+				const bool es = blo == b, ee = bec == b;
 				if (__ballot(es || ee)) {
 					// tail = X(end chunk) - E(start chunk), E = X - s the exclusive prefix
-					const uint32_t Es = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rl >> 2) & 0xFCu), (int)(X - s));
-					const uint32_t Xe = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((re >> 2) & 0xFCu), (int)X);
+					const uint32_t Es = (uint32_t)__builtin_amdgcn_ds_bpermute(alo, (int)(X - s));
+					const uint32_t Xe = (uint32_t)__builtin_amdgcn_ds_bpermute(aec, (int)X);
 					acc = es ? acc - Es : acc;
 					acc = ee ? acc + Xe : acc;
 				}
@@ -1058,6 +1061,40 @@ extern "C" int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sin
 {
 	hipLaunchKernelGGL(mosrx_read_bw_kernel, dim3(256 * 8), dim3(256), 0, (hipStream_t)stream,
 	                   (const u32x4 *)p, bytes / 16, sink);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+// The same slab walk plus writes: per 1024 chunks read a workgroup stores
+// 1024 / k chunks contiguously to `out` (16 B written per 16 k read: the
+// record-to-frame ratio of a row, k = 4 for 64 B frames, 32 for IMIX).  The
+// mixed read/write rate of the box for the roofline report.
+__global__ __launch_bounds__(256) void mosrx_rw_bw_kernel(const u32x4 *p, uint64_t n16, u32x4 *out, uint32_t k)
+{
+	uint32_t acc = 0;
+	const uint64_t per = ((n16 + gridDim.x - 1) / gridDim.x + 1023u) & ~(uint64_t)1023u;
+	const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n16, lo + per);
+	const uint32_t nw = 1024u / k;
+	for (uint64_t i = lo + threadIdx.x; i < hi; i += 1024u) {
+		u32x4 v[4];
+#pragma unroll
+		for (int u = 0; u < 4; u++) {
+			const uint64_t j = i + 256u * u;
+			v[u] = j < hi ? __builtin_nontemporal_load(p + j) : (u32x4){0, 0, 0, 0};
+		}
+#pragma unroll
+		for (int u = 0; u < 4; u++)
+			acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+		if (threadIdx.x < nw)
+			out[(i - threadIdx.x) / k + threadIdx.x] = (u32x4){acc, acc, acc, acc};
+	}
+}
+
+extern "C" int mosrx_launch_rw_bw(const void *p, uint64_t bytes, void *out, uint32_t k, void *stream)
+{
+	if (k < 4 || k > 1024 || (k & (k - 1)))
+		return -EINVAL;
+	hipLaunchKernelGGL(mosrx_rw_bw_kernel, dim3(256 * 8), dim3(256), 0, (hipStream_t)stream,
+	                   (const u32x4 *)p, bytes / 16, (u32x4 *)out, k);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

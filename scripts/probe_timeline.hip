@@ -7,6 +7,7 @@
 //   probe_timeline <trace kind> <frames> <resident batches>
 #include "../mos-networking-stack_amd/csrc/mosrx_kernels.hip"
 #include "probe_sp.h"
+#include "probe_h2.h"
 #include "../include/mosrx_trace.h"
 #include <algorithm>
 #include <stdio.h>
@@ -63,6 +64,57 @@ static int plain_sp(const char *name, std::vector<mosrx_kparams> &kps, uint32_t 
 		CHK(hipEventRecord(a, 0));
 		for (int i = 0; i < 4 * nb; i++)
 			hipLaunchKernelGGL((k_sp<NT, U>), dim3(ng), dim3(256), 0, 0, kps[i % nb]);
+		CHK(hipEventRecord(b, 0));
+		CHK(hipEventSynchronize(b));
+		float ms;
+		CHK(hipEventElapsedTime(&ms, a, b));
+		best = std::min(best, ms / (4 * nb));
+	}
+	printf("%-24s back-to-back %6.2f us (%5.0f GB/s)  records %s (%u differ, first %d)\n", name, best * 1e3,
+	       bytes / (best * 1e-3) / 1e9, bad ? "DIFFER" : "equal", bad, (int)first);
+	return 0;
+}
+
+template <int H, int S, int W, int VAR>
+__global__ __launch_bounds__(64 * (H + S)) __attribute__((amdgpu_waves_per_eu(W))) void k_h(mosrx_kparams kp)
+{
+	classify_tile_stream_h<H, S, VAR>(kp, blockIdx.x);
+}
+
+// H header waves per 64-frame tile: records against the library shape on batch 0, then timed
+template <int H, int S, int W, int VAR = 0>
+static int plain_h(const char *name, std::vector<mosrx_kparams> &kps, uint32_t ntiles, double bytes)
+{
+	const int nb = (int)kps.size();
+	hipEvent_t a, b;
+	CHK(hipEventCreate(&a));
+	CHK(hipEventCreate(&b));
+	const uint32_t n = kps[0].n;
+	mosrx_result *ref, *got;
+	CHK(hipMalloc((void **)&ref, n * 16));
+	CHK(hipMalloc((void **)&got, n * 16));
+	mosrx_kparams k0 = kps[0];
+	k0.out = ref;
+	hipLaunchKernelGGL((k_tl<0>), dim3(ntiles), dim3(256), 0, 0, k0);
+	k0.out = got;
+	CHK(hipMemset(got, 0xAB, n * 16));
+	hipLaunchKernelGGL((k_h<H, S, W, VAR>), dim3(ntiles), dim3(64 * (H + S)), 0, 0, k0);
+	CHK(hipDeviceSynchronize());
+	std::vector<uint8_t> hr(n * 16), hg(n * 16);
+	CHK(hipMemcpy(hr.data(), ref, n * 16, hipMemcpyDeviceToHost));
+	CHK(hipMemcpy(hg.data(), got, n * 16, hipMemcpyDeviceToHost));
+	uint32_t bad = 0, first = 0xFFFFFFFFu;
+	for (uint32_t i = 0; i < n; i++)
+		if (memcmp(&hr[16 * i], &hg[16 * i], 16)) { bad++; if (first == 0xFFFFFFFFu) first = i; }
+	CHK(hipFree(ref));
+	CHK(hipFree(got));
+	float best = 1e9;
+	for (int rep = 0; rep < 3; rep++) {
+		for (int i = 0; i < nb; i++)
+			hipLaunchKernelGGL((k_h<H, S, W, VAR>), dim3(ntiles), dim3(64 * (H + S)), 0, 0, kps[i]);
+		CHK(hipEventRecord(a, 0));
+		for (int i = 0; i < 4 * nb; i++)
+			hipLaunchKernelGGL((k_h<H, S, W, VAR>), dim3(ntiles), dim3(64 * (H + S)), 0, 0, kps[i % nb]);
 		CHK(hipEventRecord(b, 0));
 		CHK(hipEventSynchronize(b));
 		float ms;
@@ -179,13 +231,16 @@ int main(int argc, char **argv)
 	}
 	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);
 	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
-	plain<3, 6, 8, 0, 64, 0>("S13 U6 tails cached", kps, ntiles, bytes);
-	plain<3, 8, 8, 0, 64, 0>("S13 U8 tails cached", kps, ntiles, bytes);
-	plain<4, 4, 8, 0, 64, 0>("S14 U4 tails cached", kps, ntiles, bytes);
-	plain<4, 6, 8, 0, 64, 0>("S14 U6 tails cached", kps, ntiles, bytes);
-	plain<2, 8, 8, 0, 64, 0>("S12 U8 tails cached", kps, ntiles, bytes);
 	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
+	plain_h<1, 3, 8>("H1 S3 (probe copy)", kps, ntiles, bytes);
+	plain_h<2, 3, 8>("H2 S3 (32 frames/hdr)", kps, ntiles, bytes);
+	plain_h<2, 2, 8>("H2 S2 (32 frames/hdr)", kps, ntiles, bytes);
+	plain_h<2, 6, 8>("H2 S6 (32 frames/hdr)", kps, ntiles, bytes);
 	plain<3, 4, 8, 2, 64, 0>("S13 no window loads, cached", kps, ntiles, bytes);
+	plain<3, 4, 8, 1, 64, 0>("S13 no parse, cached", kps, ntiles, bytes);
+	plain<3, 4, 8, 4, 64, 0>("S13 streamer loads only, cached", kps, ntiles, bytes);
+	plain<3, 4, 8, 5, 64, 0>("S13 loads only (no parse, no sums)", kps, ntiles, bytes);
+	plain<3, 4, 8, 7, 64, 0>("S13 stream loads + descriptors only", kps, ntiles, bytes);
 	plain<3, 4, 8>("S13 U4 W8 (nt tails)", kps, ntiles, bytes);
 	float ms;
 	const bool after_b = argc > 5;   // timeline of the windows-after-the-barrier variant (DBG 512)

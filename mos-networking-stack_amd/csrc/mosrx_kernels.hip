@@ -679,6 +679,92 @@ __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffe
 	}
 }
 
+// The header wave's LDS state: the RSS nibble tables + queue map, and zeroed
+// reason counts (a wave's LDS accesses are ordered: no barrier needed for its
+// own use).
+__device__ __forceinline__ void tab_fill(const mosrx_kparams &kp, uint32_t *s_tab, uint32_t *s_cnt, uint32_t lane)
+{
+	const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
+	const u32x4 a = tg[lane], b = tg[lane + 64];
+	reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
+	reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
+	if (lane <= MOSRX_R_COUNT)
+		s_cnt[lane] = 0;
+}
+
+// What the stream tile's header wave keeps of a parsed frame across its
+// barrier: the record with everything but the TCP checksum verdict filled in,
+// the TCP sum before the tail, the overshoot of the capture's last chunk and
+// the datagram end (for the padding fix).  Everything that does not need the
+// tail sum is done before the barrier, where the header wave waits for the
+// streamers anyway: after it only the fold, the store and the counts remain,
+// and the workgroup's slots free sooner (0.3-0.7 % on every row, interleaved
+// medians of scripts/probe_timeline; DBG 8192 keeps the whole record after B).
+struct hdr_pend_t {
+	u32x4 rec;
+	uint32_t spre, ovs, true_hi, bits;   // bits: 1 need_tcp, 2 has_tail, 4 odd start
+};
+
+__device__ __forceinline__ hdr_pend_t hdr_pend(const hdr_t &h, uint32_t kflags, uint32_t ovs)
+{
+	hdr_pend_t q;
+	hdr_t hn = h;
+	hn.need_tcp = false;   // the TCP verdict bytes are filled in by pend_finish
+	q.rec = hdr_finish(hn, 0u, kflags);
+	q.spre = 0;
+	if (h.need_tcp) {
+		const uint32_t seglen = (h.ip_len - h.ihl * 4u) & 0xFFFFu;   // tcp_util.c:178-181, as hdr_finish
+		q.spre = h.wsum + (h.saddr & 0xFFFFu) + (h.saddr >> 16) + (h.daddr & 0xFFFFu) + (h.daddr >> 16) +
+		         bswap16(seglen) + 0x0600u;
+	}
+	q.ovs = ovs;
+	q.true_hi = h.o + h.fend;
+	q.bits = (h.need_tcp ? 1u : 0u) | (h.has_tail ? 2u : 0u) | ((h.o & 1u) ? 4u : 0u);
+	return q;
+}
+
+// hdr_finish's TCP part on a pending record
+__device__ __forceinline__ u32x4 pend_finish(const hdr_pend_t &q, uint32_t tail)
+{
+	u32x4 rec = q.rec;
+	if (q.bits & 1u) {
+		uint32_t s = q.spre;
+		if (q.bits & 2u) {
+			const uint32_t ts = fold16(tail);
+			s += (q.bits & 4u) ? bswap16(ts) : ts;
+		}
+		s = (s >> 16) + (s & 0xFFFFu);
+		s += s >> 16;
+		const uint32_t tcpc = (~s) & 0xFFFFu;
+		rec.y |= tcpc << 16;
+		rec.z = (rec.z & 0x00FFFFFFu) | (((uint32_t)(tcpc ? -1 : 1) & 0xFFu) << 24);
+		rec.w = (rec.w & ~0xFFu) | (tcpc ? MOSRX_R_TCP_BADCSUM : MOSRX_R_TCP_OK);
+	}
+	return rec;
+}
+
+// After the barrier: `tail` = the streamers' sum minus the overshoot.  Bytes
+// between the datagram end and the capture end (Ethernet padding of a long
+// capture) were summed too and come out here (rare: a wave-wide pass per such
+// frame), then the record.
+__device__ __forceinline__ void pend_emit(const mosrx_kparams &kp, __amdgpu_buffer_rsrc_t rs, uint32_t nbytes,
+                                          const hdr_pend_t &q, uint32_t lo_l, uint32_t hi_l, uint32_t tail,
+                                          uint32_t p, bool active, uint32_t lane, uint32_t *s_cnt)
+{
+	uint64_t fm = __ballot((q.bits & 2u) && q.true_hi < hi_l);
+#pragma unroll 1
+	while (fm) {
+		const uint32_t f = (uint32_t)__builtin_ctzll(fm);
+		fm &= fm - 1;
+		const uint32_t a = max(__builtin_amdgcn_readlane(lo_l, f), __builtin_amdgcn_readlane(q.true_hi, f));
+		const uint32_t sm = range_sum(rs, nbytes, a, __builtin_amdgcn_readlane(hi_l, f), lane);
+		if (lane == f)
+			tail -= sm;
+	}
+	if (active)
+		store_record(kp, p, pend_finish(q, tail), s_cnt);
+}
+
 // ---------------------------------------------------------------------------
 // stream tile: 64 frames, one header wave + S streamers over the tile's tail span
 // ---------------------------------------------------------------------------
@@ -888,6 +974,15 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		}
 		if constexpr ((DBG & 512) != 0)
 			__syncthreads();   // B first: windows read after the streamers passed them
+		// Small-frame mixes (cached tails) fill the LDS tables first: the window
+		// loads then leave a table round trip later, when the streamers (whose
+		// span starts at the tile's first byte) have the lines on the way (IMIX
+		// 256K 20.38 vs 20.66 us, 2M frames 140.4 vs 141.4, interleaved medians).
+		// Long frames (non-temporal tails) issue the windows first (1500 B 64K
+		// 17.68 vs 17.90 us).  DBG 4096 flips the order (probe builds).
+		constexpr bool TAB_FIRST = (TAIL_AUX(VAR) == 0) != ((DBG & 4096) != 0);
+		if constexpr (TAB_FIRST)
+			tab_fill(kp, s_tab, s_cnt, lane);
 		hdr_win_t win;
 		if constexpr (DBG & 2) {
 #pragma unroll
@@ -899,14 +994,8 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		// the chunk holding the capture's last byte (stream_scan sums it whole)
 		const bool cand = hi_l > lo_l;
 		const u32x4 ov = load16<WIN_AUX(VAR)>(rs, sorted && cand ? (hi_l - 1u) & ~15u : ZERO_OFF, 0);
-		{
-			const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
-			const u32x4 a = tg[lane], b = tg[lane + 64];
-			reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
-			reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
-			if (lane <= MOSRX_R_COUNT)
-				s_cnt[lane] = 0;
-		}
+		if constexpr (!TAB_FIRST)
+			tab_fill(kp, s_tab, s_cnt, lane);
 		if constexpr (DBG & 1) {
 			uint32_t x = 0;
 #pragma unroll
@@ -918,33 +1007,56 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		} else {
 			TILE_STAMP(2);
 			const hdr_t h = hdr_parse<VAR, WEND>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
-			TILE_STAMP(3);
-			if constexpr ((DBG & 512) == 0)
+			if constexpr (IS_TX(VAR) || (DBG & 8192) != 0) {   // DBG 8192: the whole record after the barrier
+				TILE_STAMP(3);
 				__syncthreads();   // B: s_part ready
-			TILE_STAMP(4);
-			uint32_t tail = 0;
-			if (h.has_tail) {
+				TILE_STAMP(4);
+				uint32_t tail = 0;
+				if (h.has_tail) {
 #pragma unroll
-				for (int s = 0; s < S; s++)
-					tail += s_part[s][lane];
-				if (sorted)
-					tail -= chunk_overshoot(ov, (hi_l - 1u) & ~15u, hi_l);
+					for (int s = 0; s < S; s++)
+						tail += s_part[s][lane];
+					if (sorted)
+						tail -= chunk_overshoot(ov, (hi_l - 1u) & ~15u, hi_l);
+				}
+				hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, tail, p, active, lane, s_cnt);
+			} else {
+				// the outputs that do not need the tail sum go out before the barrier
+				if (active && kp.fhash)
+					kp.fhash[p] = flow_hash(h);
+				if constexpr (IS_TI(VAR)) {
+					if (active)
+						store_tcpinfo(kp.tinfo, p, h);
+				}
+#ifdef MOSRX_RTC_BPF
+				if constexpr ((VAR & VAR_BPF) != 0) {
+					__shared__ uint32_t s_bw[25u * 64u];
+					const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * lane);
+					if (active)
+						kp.bmatch[p] = m;
+				}
+#endif
+				const hdr_pend_t q =
+				    hdr_pend(h, kp.flags, sorted && cand ? chunk_overshoot(ov, (hi_l - 1u) & ~15u, hi_l) : 0u);
+				TILE_STAMP(3);
+				if constexpr ((DBG & 512) == 0)
+					__syncthreads();   // B: s_part ready
+				TILE_STAMP(4);
+				uint32_t tail = 0;
+				if (q.bits & 2u) {
+#pragma unroll
+					for (int s = 0; s < S; s++)
+						tail += s_part[s][lane];
+					tail -= q.ovs;
+				}
+				pend_emit(kp, rs, nbytes, q, lo_l, hi_l, tail, p, active, lane, s_cnt);
 			}
-			hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, tail, p, active, lane, s_cnt);
 			TILE_STAMP(5);
 			// only this wave counted (its LDS accesses are ordered): it adds the
 			// tile's counts to its shard without a second barrier, so the
 			// streamers retire at B and the next tile can start on their slots
 			if (kp.counters && lane < MOSRX_R_COUNT && s_cnt[lane])
 				atomicAdd(&kp.counters[(blockIdx.x % MOSRX_CNT_SHARDS) * MOSRX_CNT_STRIDE + lane], s_cnt[lane]);
-#ifdef MOSRX_RTC_BPF
-			if constexpr ((VAR & VAR_BPF) != 0) {
-				__shared__ uint32_t s_bw[25u * 64u];
-				const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * lane);
-				if (active)
-					kp.bmatch[p] = m;
-			}
-#endif
 		}
 	} else {
 		// ---- streamer sidx ----

@@ -8,6 +8,7 @@
 #include "../mos-networking-stack_amd/csrc/mosrx_kernels.hip"
 #include "probe_sp.h"
 #include "probe_h2.h"
+#include "probe_t128.h"
 #include "../include/mosrx_trace.h"
 #include <algorithm>
 #include <stdio.h>
@@ -80,10 +81,17 @@ __global__ __launch_bounds__(64 * (H + S)) __attribute__((amdgpu_waves_per_eu(W)
 {
 	classify_tile_stream_h<H, S, VAR>(kp, blockIdx.x);
 }
+template <int F, int S, int U, int W, int VAR>
+__global__ __launch_bounds__(64 * (1 + S)) __attribute__((amdgpu_waves_per_eu(W))) void k_f(mosrx_kparams kp)
+{
+	classify_tile_stream_f<F, S, VAR, U>(kp, blockIdx.x);
+}
 
-// H header waves per 64-frame tile: records against the library shape on batch 0, then timed
-template <int H, int S, int W, int VAR = 0>
-static int plain_h(const char *name, std::vector<mosrx_kparams> &kps, uint32_t ntiles, double bytes)
+// a probe shape K (grid g, block w threads): records against the library shape
+// on batch 0, then timed back to back over the resident batches
+template <typename K>
+static int plain_k(const char *name, K kern, uint32_t g, uint32_t w, std::vector<mosrx_kparams> &kps,
+                   uint32_t ntiles, double bytes)
 {
 	const int nb = (int)kps.size();
 	hipEvent_t a, b;
@@ -98,7 +106,7 @@ static int plain_h(const char *name, std::vector<mosrx_kparams> &kps, uint32_t n
 	hipLaunchKernelGGL((k_tl<0>), dim3(ntiles), dim3(256), 0, 0, k0);
 	k0.out = got;
 	CHK(hipMemset(got, 0xAB, n * 16));
-	hipLaunchKernelGGL((k_h<H, S, W, VAR>), dim3(ntiles), dim3(64 * (H + S)), 0, 0, k0);
+	hipLaunchKernelGGL(kern, dim3(g), dim3(w), 0, 0, k0);
 	CHK(hipDeviceSynchronize());
 	std::vector<uint8_t> hr(n * 16), hg(n * 16);
 	CHK(hipMemcpy(hr.data(), ref, n * 16, hipMemcpyDeviceToHost));
@@ -111,10 +119,10 @@ static int plain_h(const char *name, std::vector<mosrx_kparams> &kps, uint32_t n
 	float best = 1e9;
 	for (int rep = 0; rep < 3; rep++) {
 		for (int i = 0; i < nb; i++)
-			hipLaunchKernelGGL((k_h<H, S, W, VAR>), dim3(ntiles), dim3(64 * (H + S)), 0, 0, kps[i]);
+			hipLaunchKernelGGL(kern, dim3(g), dim3(w), 0, 0, kps[i]);
 		CHK(hipEventRecord(a, 0));
 		for (int i = 0; i < 4 * nb; i++)
-			hipLaunchKernelGGL((k_h<H, S, W, VAR>), dim3(ntiles), dim3(64 * (H + S)), 0, 0, kps[i % nb]);
+			hipLaunchKernelGGL(kern, dim3(g), dim3(w), 0, 0, kps[i % nb]);
 		CHK(hipEventRecord(b, 0));
 		CHK(hipEventSynchronize(b));
 		float ms;
@@ -124,6 +132,40 @@ static int plain_h(const char *name, std::vector<mosrx_kparams> &kps, uint32_t n
 	printf("%-24s back-to-back %6.2f us (%5.0f GB/s)  records %s (%u differ, first %d)\n", name, best * 1e3,
 	       bytes / (best * 1e-3) / 1e9, bad ? "DIFFER" : "equal", bad, (int)first);
 	return 0;
+}
+template <int H, int S, int W, int VAR = 0>
+static int plain_h(const char *name, std::vector<mosrx_kparams> &kps, uint32_t ntiles, double bytes)
+{
+	return plain_k(name, k_h<H, S, W, VAR>, ntiles, 64 * (H + S), kps, ntiles, bytes);
+}
+template <int F, int S, int U, int W, int VAR = 0>
+static int plain_f(const char *name, std::vector<mosrx_kparams> &kps, uint32_t ntiles, double bytes)
+{
+	return plain_k(name, k_f<F, S, U, W, VAR>, (kps[0].n + 64 * F - 1) / (64 * F), 64 * (1 + S), kps, ntiles,
+	               bytes);
+}
+
+// one timing of a stream-tile variant: 4 passes over the resident batches, ms per launch
+template <int S, int U, int W, int DBG, uint32_t T, int VAR>
+static double time_tl(std::vector<mosrx_kparams> &kps, uint32_t ntiles64)
+{
+	const uint32_t ntiles = ntiles64 * (64 / T);
+	const int nb = (int)kps.size();
+	hipEvent_t a, b;
+	if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+		return -1;
+	for (int i = 0; i < nb; i++)
+		hipLaunchKernelGGL((k_tl<DBG, S, U, W, T, VAR>), dim3(ntiles), dim3(64 * (1 + S)), 0, 0, kps[i]);
+	hipEventRecord(a, 0);
+	for (int i = 0; i < 4 * nb; i++)
+		hipLaunchKernelGGL((k_tl<DBG, S, U, W, T, VAR>), dim3(ntiles), dim3(64 * (1 + S)), 0, 0, kps[i % nb]);
+	hipEventRecord(b, 0);
+	hipEventSynchronize(b);
+	float ms = 0;
+	hipEventElapsedTime(&ms, a, b);
+	hipEventDestroy(a);
+	hipEventDestroy(b);
+	return ms / (4 * nb);
 }
 
 template <int S, int U, int W, int DBG = 0, uint32_t T = 64, int VAR = 2>
@@ -232,10 +274,34 @@ int main(int argc, char **argv)
 	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);
 	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
 	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
-	plain_h<1, 3, 8>("H1 S3 (probe copy)", kps, ntiles, bytes);
-	plain_h<2, 3, 8>("H2 S3 (32 frames/hdr)", kps, ntiles, bytes);
-	plain_h<2, 2, 8>("H2 S2 (32 frames/hdr)", kps, ntiles, bytes);
-	plain_h<2, 6, 8>("H2 S6 (32 frames/hdr)", kps, ntiles, bytes);
+	if (argc > 4 && atoi(argv[4]) == 3) {
+		// interleaved rounds, median and min per variant (cross-variant drift cancels)
+		const char *names[] = {"cached: pend, tables first (lib)", "cached: pend, windows first",
+		                       "cached: record after B, tables first", "cached: record after B, windows first",
+		                       "nt: pend, tables first", "nt: pend, windows first (lib)", "nt: record after B, windows first (r2)"};
+		std::vector<double> ts[7];
+		for (int r = 0; r < 9; r++) {
+			ts[0].push_back(time_tl<3, 4, 8, 0, 64, 0>(kps, ntiles));
+			ts[1].push_back(time_tl<3, 4, 8, 4096, 64, 0>(kps, ntiles));
+			ts[2].push_back(time_tl<3, 4, 8, 8192, 64, 0>(kps, ntiles));
+			ts[3].push_back(time_tl<3, 4, 8, 8192 | 4096, 64, 0>(kps, ntiles));
+			ts[4].push_back(time_tl<3, 4, 8, 4096, 64, 2>(kps, ntiles));
+			ts[5].push_back(time_tl<3, 4, 8, 0, 64, 2>(kps, ntiles));
+			ts[6].push_back(time_tl<3, 4, 8, 8192, 64, 2>(kps, ntiles));
+		}
+		for (int v = 0; v < 7; v++)
+			printf("%-40s median %7.2f us  min %7.2f us  (%5.0f GB/s at the median)\n", names[v], pct(ts[v], 0.5) * 1e3,
+			       pct(ts[v], 0.0) * 1e3, bytes / (pct(ts[v], 0.5) * 1e-3) / 1e9);
+		return 0;
+	}
+	if (argc > 4 && atoi(argv[4]) == 2) {
+		plain_h<1, 3, 8>("H1 S3 (probe copy)", kps, ntiles, bytes);
+		plain_h<2, 3, 8>("H2 S3 (32 frames/hdr)", kps, ntiles, bytes);
+		plain_h<2, 2, 8>("H2 S2 (32 frames/hdr)", kps, ntiles, bytes);
+		plain_h<2, 6, 8>("H2 S6 (32 frames/hdr)", kps, ntiles, bytes);
+	}
+	plain_f<1, 3, 4, 8>("F1 S3 U4 (probe copy)", kps, ntiles, bytes);
+	plain_f<2, 3, 4, 8>("F2 S3 U4 (128 frames)", kps, ntiles, bytes);
 	plain<3, 4, 8, 2, 64, 0>("S13 no window loads, cached", kps, ntiles, bytes);
 	plain<3, 4, 8, 1, 64, 0>("S13 no parse, cached", kps, ntiles, bytes);
 	plain<3, 4, 8, 4, 64, 0>("S13 streamer loads only, cached", kps, ntiles, bytes);

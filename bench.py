@@ -602,15 +602,11 @@ def main():
         results["FW64"] = measure_fw64(ctx, 2.0)
     read_ceiling = None
     if rank == 0:
-        # the box's streaming-read rate over a 1.5 GB working set (no Infinity-Cache
-        # hits), once with 128 MiB launches (the single-batch rows' size: their ramp
-        # and drain included) and once with 512 MiB launches (the ring rows' size)
+        # the box's streaming-read rate over a >= 1.5 GB working set (no Infinity-
+        # Cache hits), with 128 MiB launches (the single-batch rows' size: their ramp
+        # and drain included) and 768 MiB launches (the ring rows' size, ~805 MB)
         read_ceiling = {"launch_128MiB": round(ctx.probe_read_bw(128 << 20, 12, 96), 1),
-                        "launch_512MiB": round(ctx.probe_read_bw(512 << 20, 3, 24), 1),
-                        # the same passes also writing 16 B per 64 B read (the 64 B rows'
-                        # record-to-frame ratio) and per 512 B read (IMIX's): GB/s moved
-                        "rw_1in4_512MiB": round(ctx.probe_rw_bw(4, 512 << 20, 3, 24), 1),
-                        "rw_1in32_512MiB": round(ctx.probe_rw_bw(32, 512 << 20, 3, 24), 1)}
+                        "launch_768MiB": round(ctx.probe_read_bw(768 << 20, 3, 48), 1)}
     ctx.close()
     dist.close()
     if rank != 0:

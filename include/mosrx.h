@@ -287,10 +287,6 @@ int  mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t
  * cycling over `nbuf` buffers of `bytes` each (sized past the 256 MiB Infinity
  * Cache), in GB/s.  The roofline figure next to the 8 TB/s spec peak. */
 int  mosrx_probe_read_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, float *gbps);
-/* The mixed rate: the same passes also writing 16 B per 16 k bytes read (k a
- * power of two in [4, 1024]; the record-to-frame ratio of a row: 4 for 64 B
- * frames, 32 for IMIX), in GB/s of bytes read + written. */
-int  mosrx_probe_rw_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, uint32_t k, float *gbps);
 /* hipDeviceSynchronize on the context's device. */
 int  mosrx_device_sync(mosrx_ctx *c);
 /* Same, end-to-end from host buffers through pinned staging, double-buffered. */

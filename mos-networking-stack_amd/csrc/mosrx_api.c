@@ -1127,22 +1127,16 @@ int mosrx_time_dev_streams(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosr
 	return mosrx_time_op(c, MOSRX_OP_CLASSIFY, 0, b, nb, (void *const *)d_out, NULL, iters, nstreams, ms, NULL);
 }
 
-/* k == 0: reads only (mosrx_probe_read_bw), else 16 B written per 16 k read */
-static int probe_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, uint32_t k, float *gbps)
+int mosrx_probe_read_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, float *gbps)
 {
 	void **bufs;
 	uint32_t *sink = NULL;
-	void *out = NULL;
 	uint32_t i;
 	float ms = 0;
 	int rc = 0;
 	if (!c || !gbps || nbuf == 0 || iters == 0 || bytes < 16)
 		return -EINVAL;
-	if (k && (k < 4 || k > 1024 || (k & (k - 1))))
-		return -EINVAL;
-	bytes &= ~(uint64_t)16383;
-	if (!bytes)
-		return -EINVAL;
+	bytes &= ~(uint64_t)15;
 	HIPCHK(hipSetDevice(c->device));
 	bufs = calloc(nbuf, sizeof(*bufs));
 	if (!bufs)
@@ -1153,45 +1147,25 @@ static int probe_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters,
 			rc = -ENOMEM;
 	if (!rc && hipMalloc((void **)&sink, 4) != hipSuccess)
 		rc = -ENOMEM;
-	/* the kernel's slabs are whole 1024-chunk steps: room for the last one */
-	if (!rc && k && hipMalloc(&out, bytes / k + 2048u * 1024u * 16u / k) != hipSuccess)
-		rc = -ENOMEM;
-#define PROBE_LAUNCH(buf) (k ? mosrx_launch_rw_bw((buf), bytes, out, k, c->stream) \
-                             : mosrx_launch_read_bw((buf), bytes, sink, c->stream))
 	for (i = 0; i < nbuf && !rc; i++)   /* warm-up pass */
-		rc = PROBE_LAUNCH(bufs[i]);
+		rc = mosrx_launch_read_bw(bufs[i], bytes, sink, c->stream);
 	if (!rc && hipEventRecord(c->ev0, c->stream) != hipSuccess)
 		rc = -EIO;
 	for (i = 0; i < iters && !rc; i++)
-		rc = PROBE_LAUNCH(bufs[i % nbuf]);
-#undef PROBE_LAUNCH
+		rc = mosrx_launch_read_bw(bufs[i % nbuf], bytes, sink, c->stream);
 	if (!rc && (hipEventRecord(c->ev1, c->stream) != hipSuccess || hipEventSynchronize(c->ev1) != hipSuccess ||
 	            hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess))
 		rc = -EIO;
 	if (!rc)
-		*gbps = (float)((double)(bytes + (k ? bytes / k : 0)) * iters / (ms * 1e-3) / 1e9);
+		*gbps = (float)((double)bytes * iters / (ms * 1e-3) / 1e9);
 	hipStreamSynchronize(c->stream);
 	for (i = 0; i < nbuf; i++)
 		if (bufs[i])
 			hipFree(bufs[i]);
 	if (sink)
 		hipFree(sink);
-	if (out)
-		hipFree(out);
 	free(bufs);
 	return rc;
-}
-
-int mosrx_probe_read_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, float *gbps)
-{
-	return probe_bw(c, bytes, nbuf, iters, 0, gbps);
-}
-
-int mosrx_probe_rw_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, uint32_t k, float *gbps)
-{
-	if (k == 0)
-		return -EINVAL;
-	return probe_bw(c, bytes, nbuf, iters, k, gbps);
 }
 
 int mosrx_device_sync(mosrx_ctx *c)

@@ -1144,69 +1144,43 @@ void mosrx_classify_queue_kernel(mosrx_qparams qp)
 }
 
 #ifndef __HIPCC_RTC__
-// Streaming-read ceiling of the box: each workgroup streams one contiguous slab
-// with coalesced non-temporal 16-byte loads, 4 in flight per lane; a
-// data-dependent sink keeps them live.  The fastest shape found by
-// scripts/probe_bw.hip (6.4 TB/s, vs 5.3 for a grid-stride default-policy
-// loop).  Diagnostic for the roofline report.
+// Streaming-read ceiling of the box: each workgroup reads one contiguous slab
+// with coalesced non-temporal 16-byte loads, 8 in flight per lane; a
+// data-dependent sink keeps them live.  32 KiB slabs (grid bytes / 32 KiB):
+// the fastest shape of scripts/probe_bw.hip (6.9-7.0 TB/s at 512-800 MiB per
+// launch vs 6.7-6.9 with 2048 slabs).  Diagnostic for the roofline report.
+#define BW_U 8
+#define BW_SLAB (32u << 10)
 __global__ __launch_bounds__(256) void mosrx_read_bw_kernel(const u32x4 *p, uint64_t n16, uint32_t *sink)
 {
 	uint32_t acc = 0;
 	const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
 	const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n16, lo + per);
-	for (uint64_t i = lo + threadIdx.x; i < hi; i += 1024u) {
-		u32x4 v[4];
+	for (uint64_t i = lo + threadIdx.x; i < hi; i += 256u * BW_U) {
+		u32x4 v[BW_U];
 #pragma unroll
-		for (int u = 0; u < 4; u++) {
+		for (int u = 0; u < BW_U; u++) {
 			const uint64_t j = i + 256u * u;
 			v[u] = j < hi ? __builtin_nontemporal_load(p + j) : (u32x4){0, 0, 0, 0};
 		}
 #pragma unroll
-		for (int u = 0; u < 4; u++)
+		for (int u = 0; u < BW_U; u++)
 			acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
 	}
 	if (acc == 0x9E3779B9u)
 		sink[0] = acc;
 }
 
+static uint32_t bw_grid(uint64_t bytes)
+{
+	const uint64_t g = bytes / BW_SLAB;
+	return (uint32_t)(g < 2048u ? 2048u : g > 65535u ? 65535u : g);
+}
+
 extern "C" int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sink, void *stream)
 {
-	hipLaunchKernelGGL(mosrx_read_bw_kernel, dim3(256 * 8), dim3(256), 0, (hipStream_t)stream,
+	hipLaunchKernelGGL(mosrx_read_bw_kernel, dim3(bw_grid(bytes)), dim3(256), 0, (hipStream_t)stream,
 	                   (const u32x4 *)p, bytes / 16, sink);
-	return hipGetLastError() == hipSuccess ? 0 : -EIO;
-}
-
-// The same slab walk plus writes: per 1024 chunks read a workgroup stores
-// 1024 / k chunks contiguously to `out` (16 B written per 16 k read: the
-// record-to-frame ratio of a row, k = 4 for 64 B frames, 32 for IMIX).  The
-// mixed read/write rate of the box for the roofline report.
-__global__ __launch_bounds__(256) void mosrx_rw_bw_kernel(const u32x4 *p, uint64_t n16, u32x4 *out, uint32_t k)
-{
-	uint32_t acc = 0;
-	const uint64_t per = ((n16 + gridDim.x - 1) / gridDim.x + 1023u) & ~(uint64_t)1023u;
-	const uint64_t lo = (uint64_t)blockIdx.x * per, hi = min(n16, lo + per);
-	const uint32_t nw = 1024u / k;
-	for (uint64_t i = lo + threadIdx.x; i < hi; i += 1024u) {
-		u32x4 v[4];
-#pragma unroll
-		for (int u = 0; u < 4; u++) {
-			const uint64_t j = i + 256u * u;
-			v[u] = j < hi ? __builtin_nontemporal_load(p + j) : (u32x4){0, 0, 0, 0};
-		}
-#pragma unroll
-		for (int u = 0; u < 4; u++)
-			acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-		if (threadIdx.x < nw)
-			out[(i - threadIdx.x) / k + threadIdx.x] = (u32x4){acc, acc, acc, acc};
-	}
-}
-
-extern "C" int mosrx_launch_rw_bw(const void *p, uint64_t bytes, void *out, uint32_t k, void *stream)
-{
-	if (k < 4 || k > 1024 || (k & (k - 1)))
-		return -EINVAL;
-	hipLaunchKernelGGL(mosrx_rw_bw_kernel, dim3(256 * 8), dim3(256), 0, (hipStream_t)stream,
-	                   (const u32x4 *)p, bytes / 16, (u32x4 *)out, k);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

@@ -179,7 +179,6 @@ def lib():
                                   C.POINTER(C.c_float), C.POINTER(C.c_float)]),
             "mosrx_time_dev_streams": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, U32, C.POINTER(C.c_float)]),
             "mosrx_probe_read_bw": (I, [P, U64, U32, U32, C.POINTER(C.c_float)]),
-            "mosrx_probe_rw_bw": (I, [P, U64, U32, U32, U32, C.POINTER(C.c_float)]),
             "mosrx_queue_create": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
             "mosrx_queue_run": (I, [P, P, P]),
             "mosrx_queue_destroy": (None, [P, P]),
@@ -652,12 +651,6 @@ class Context:
         """Measured streaming-read ceiling (GB/s) of this device."""
         g = C.c_float()
         _chk(lib().mosrx_probe_read_bw(self.handle, nbytes, nbuf, iters, C.byref(g)), "mosrx_probe_read_bw")
-        return float(g.value)
-
-    def probe_rw_bw(self, k: int, nbytes: int = 128 << 20, nbuf: int = 6, iters: int = 60) -> float:
-        """Measured mixed rate (GB/s read + written): 16 B written per 16*k read."""
-        g = C.c_float()
-        _chk(lib().mosrx_probe_rw_bw(self.handle, nbytes, nbuf, iters, k, C.byref(g)), "mosrx_probe_rw_bw")
         return float(g.value)
 
     def device_sync(self):

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -55,6 +56,32 @@ __global__ __launch_bounds__(256) void rd_slab(const u32x4 *p, uint64_t n16, uin
 		sink[0] = acc;
 }
 
+// C: each WAVE streams its own contiguous slab, 1 KiB per load, U in flight
+// (the classify streamers' access shape), buffer loads, AUX cache policy
+template <int U, int AUX>
+__global__ __launch_bounds__(256) void rd_wave(const u32x4 *p, uint64_t n16, uint32_t *sink)
+{
+	uint32_t acc = 0;
+	const uint32_t lane = threadIdx.x & 63u;
+	const uint64_t nw = (uint64_t)gridDim.x * 4u, w = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+	const uint64_t per = ((n16 + nw - 1) / nw + 63u) & ~(uint64_t)63u;
+	const uint64_t lo = w * per, hi = min(n16, lo + per);
+	const uint32_t nbytes = lo < hi ? (uint32_t)((hi - lo) * 16u) : 0u;
+	// records = the slab: offsets past it (the 0xFFFFFFF0 filler) read 0 without a memory access
+	const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(p + (lo < n16 ? lo : 0)), (short)0, (int)nbytes, 0x00020000);
+	for (uint32_t b = 0; b < nbytes; b += 1024u * U) {
+		u32x4 v[U];
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, b + 1024u * u + 16u * lane < nbytes ? b + 1024u * u + 16u * lane : 0xFFFFFFF0u, 0, AUX);
+#pragma unroll
+		for (int u = 0; u < U; u++)
+			acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+	}
+	if (acc == 0x9E3779B9u)
+		sink[0] = acc;
+}
+
 typedef void (*kfn)(const u32x4 *, uint64_t, uint32_t *);
 
 static int run(const char *name, kfn k, int grid, void **bufs, int nbuf, uint64_t bytes, uint32_t *sink)
@@ -77,27 +104,26 @@ static int run(const char *name, kfn k, int grid, void **bufs, int nbuf, uint64_
 	return 0;
 }
 
-int main()
+int main(int argc, char **argv)
 {
-	const uint64_t bytes = 96ull << 20;
-	const int nbuf = 8;
-	void *bufs[nbuf];
+	const uint64_t bytes = (argc > 1 ? (uint64_t)atoi(argv[1]) : 512ull) << 20;
+	const int nbuf = argc > 2 ? atoi(argv[2]) : 3;
+	void *bufs[16];
 	uint32_t *sink;
 	for (int i = 0; i < nbuf; i++) {
 		CHK(hipMalloc(&bufs[i], bytes));
 		CHK(hipMemset(bufs[i], i + 1, bytes));
 	}
 	CHK(hipMalloc(&sink, 4));
-	for (int g : {1024, 2048, 4096})
-		run("stride U=4", rd_stride<4>, g, bufs, nbuf, bytes, sink);
-	run("stride U=8", rd_stride<8>, 2048, bufs, nbuf, bytes, sink);
-	run("stride U=2", rd_stride<2>, 4096, bufs, nbuf, bytes, sink);
-	for (int g : {512, 1024, 2048, 4096})
-		run("slab U=4", rd_slab<4, false>, g, bufs, nbuf, bytes, sink);
-	run("slab U=8", rd_slab<8, false>, 1024, bufs, nbuf, bytes, sink);
-	run("slab U=8", rd_slab<8, false>, 2048, bufs, nbuf, bytes, sink);
-	run("slab U=4 nt", rd_slab<4, true>, 2048, bufs, nbuf, bytes, sink);
-	run("slab U=8 nt", rd_slab<8, true>, 1024, bufs, nbuf, bytes, sink);
-	run("slab U=16", rd_slab<16, false>, 1024, bufs, nbuf, bytes, sink);
+	for (int rep = 0; rep < 2; rep++) {
+		run("slab U=4 nt (library probe)", rd_slab<4, true>, 2048, bufs, nbuf, bytes, sink);
+		for (int g : {4096, 5461, 8192, 16384, 32768}) {
+			run("slab U=4 nt", rd_slab<4, true>, g, bufs, nbuf, bytes, sink);
+			run("slab U=8 nt", rd_slab<8, true>, g, bufs, nbuf, bytes, sink);
+		}
+		run("slab U=2 nt", rd_slab<2, true>, 8192, bufs, nbuf, bytes, sink);
+		run("wave U=4 nt", rd_wave<4, 2>, 8192, bufs, nbuf, bytes, sink);
+		run("wave U=4 nt", rd_wave<4, 2>, 16384, bufs, nbuf, bytes, sink);
+	}
 	return 0;
 }

@@ -540,11 +540,11 @@ __device__ __forceinline__ void flush_counters(const mosrx_kparams &kp, const ui
 // barrier (each wave fills the LDS tables itself; a wave's LDS accesses are
 // ordered).  Longer frames (only when the shape is forced onto them) are
 // summed by their wave tail by tail, 4 KiB per pass.
-template <int VAR, uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL), int DBG = 0>
+template <int VAR, uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL), int DBG = 0,
+          int WEND = MOSRX_WINDOW_END_SMALL>
 __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uint32_t tile)
 {
 	constexpr int AUX = TAIL_AUX(VAR);
-	constexpr int WEND = MOSRX_WINDOW_END_SMALL;
 	// the fused BPF hook reads the whole 96-byte window
 	constexpr int NLOAD = (VAR & VAR_BPF) ? WIN_RAW / 4 : WIN_NLOAD(WEND);
 	// DBG 2 skips the window loads (probe builds only).  Tried and slower:

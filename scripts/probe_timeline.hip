@@ -18,6 +18,13 @@
 
 #define CHK(x) do { if ((x) != hipSuccess) { printf("HIP error %s line %d\n", #x, __LINE__); return 1; } } while (0)
 
+static double pct(std::vector<double> v, double q)
+{
+	if (v.empty()) return 0;
+	std::sort(v.begin(), v.end());
+	return v[std::min(v.size() - 1, (size_t)(q * v.size()))];
+}
+
 template <int DBG, int S = 3, int U = 4, int W = 8, uint32_t T = 64, int VAR = 2>
 __global__ __launch_bounds__(64 * (1 + S)) __attribute__((amdgpu_waves_per_eu(W))) void k_tl(mosrx_kparams kp)
 {
@@ -193,10 +200,56 @@ static int plain(const char *name, std::vector<mosrx_kparams> &kps, uint32_t nti
 	return 0;
 }
 
-template <uint32_t T>
+template <uint32_t T, int WEND = MOSRX_WINDOW_END_SMALL>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8))) void k_small(mosrx_kparams kp)
 {
-	classify_tile_small<2, T>(kp, blockIdx.x);
+	classify_tile_small<2, T, 0, WEND>(kp, blockIdx.x);
+}
+template <uint32_t T, int WEND = MOSRX_WINDOW_END_SMALL>
+static double time_small(std::vector<mosrx_kparams> &kps)
+{
+	const int nb = (int)kps.size();
+	const uint32_t ng = (kps[0].n + T - 1) / T;
+	hipEvent_t a, b;
+	if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+		return -1;
+	for (int i = 0; i < nb; i++)
+		hipLaunchKernelGGL((k_small<T, WEND>), dim3(ng), dim3(T), 0, 0, kps[i]);
+	hipEventRecord(a, 0);
+	for (int i = 0; i < 2 * nb; i++)
+		hipLaunchKernelGGL((k_small<T, WEND>), dim3(ng), dim3(T), 0, 0, kps[i % nb]);
+	hipEventRecord(b, 0);
+	hipEventSynchronize(b);
+	float ms = 0;
+	hipEventElapsedTime(&ms, a, b);
+	hipEventDestroy(a);
+	hipEventDestroy(b);
+	return ms / (2 * nb);
+}
+// records of a SMALL variant against the library SMALL shape on batch 0
+template <uint32_t T, int WEND>
+static uint32_t small_diff(std::vector<mosrx_kparams> &kps)
+{
+	const uint32_t n = kps[0].n, ng = (n + T - 1) / T, ng0 = (n + 255) / 256;
+	mosrx_result *ref, *got;
+	if (hipMalloc((void **)&ref, n * 16) != hipSuccess || hipMalloc((void **)&got, n * 16) != hipSuccess)
+		return 0xFFFFFFFFu;
+	mosrx_kparams k0 = kps[0];
+	k0.out = ref;
+	hipLaunchKernelGGL((k_small<256>), dim3(ng0), dim3(256), 0, 0, k0);
+	k0.out = got;
+	hipMemset(got, 0xAB, n * 16);
+	hipLaunchKernelGGL((k_small<T, WEND>), dim3(ng), dim3(T), 0, 0, k0);
+	hipDeviceSynchronize();
+	std::vector<uint8_t> hr(n * 16), hg(n * 16);
+	hipMemcpy(hr.data(), ref, n * 16, hipMemcpyDeviceToHost);
+	hipMemcpy(hg.data(), got, n * 16, hipMemcpyDeviceToHost);
+	hipFree(ref);
+	hipFree(got);
+	uint32_t bad = 0;
+	for (uint32_t i = 0; i < n; i++)
+		bad += memcmp(&hr[16 * i], &hg[16 * i], 16) != 0;
+	return bad;
 }
 template <uint32_t T>
 static int plain_small(const char *name, std::vector<mosrx_kparams> &kps, double bytes)
@@ -223,12 +276,6 @@ static int plain_small(const char *name, std::vector<mosrx_kparams> &kps, double
 	return 0;
 }
 
-static double pct(std::vector<double> v, double q)
-{
-	if (v.empty()) return 0;
-	std::sort(v.begin(), v.end());
-	return v[std::min(v.size() - 1, (size_t)(q * v.size()))];
-}
 
 int main(int argc, char **argv)
 {
@@ -265,10 +312,16 @@ int main(int argc, char **argv)
 	// plain (DBG 0) back-to-back times over the resident batches, then stamped launches
 	printf("trace kind %d n %u tiles %u: %.2f MB\n", kind, n, ntiles, bytes / 1e6);
 	if (kind == MOSRX_TRACE_S64 || kind == MOSRX_TRACE_FW64) {
-		plain_small<256>("SMALL 256 (library)", kps, bytes);
-		plain_small<128>("SMALL 128", kps, bytes);
-		plain_small<64>("SMALL 64", kps, bytes);
-		plain_small<256>("SMALL 256 (library)", kps, bytes);
+		printf("SMALL 256 WEND 62: records %u differ\n", small_diff<256, MOSRX_WINDOW_END_STREAM>(kps));
+		std::vector<double> a, b;
+		for (int r = 0; r < 9; r++) {
+			a.push_back(time_small<256>(kps));
+			b.push_back(time_small<256, MOSRX_WINDOW_END_STREAM>(kps));
+		}
+		printf("SMALL 256 WEND 78 (library) median %7.2f us (%5.0f GB/s)\n", pct(a, 0.5) * 1e3,
+		       bytes / (pct(a, 0.5) * 1e-3) / 1e9);
+		printf("SMALL 256 WEND 62 (4 loads) median %7.2f us (%5.0f GB/s)\n", pct(b, 0.5) * 1e3,
+		       bytes / (pct(b, 0.5) * 1e-3) / 1e9);
 		return 0;
 	}
 	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);

@@ -543,6 +543,74 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
                       f"time = HIP events around each kernel (its frames were just copied in)"}
 
 
+def measure_backend_threads(key: str, nthreads: int, group: int, frames_per_thread: int, device: int):
+    """mOS's per-core layout at the boundary: `nthreads` mTCP threads, each with
+    its own context (core.c:1282-1349), its own source of distinct frames (as one
+    PACKET_FANOUT socket per thread would be, mosrx_gpu_module_bind_source) and
+    its own rx loop (mosrx_rx_loop_ex) on its own host thread, all on one GPU.
+    Aggregate = frames of all threads / wall time from the common start to the
+    last thread's end.  ctypes releases the GIL, so the loops run in parallel."""
+    import ctypes as C
+    import threading
+    batch = {"S64": 32_768, "M1500": 65_536, "IMIX": 262_144}[key]
+    kind = {"S64": mosrx.TRACE_S64, "M1500": mosrx.TRACE_M1500, "IMIX": mosrx.TRACE_IMIX}[key]
+    traces = [mosrx.Trace(kind, batch * group, seed=0x51 + i) for i in range(nthreads)]
+    L = mosrx.lib()
+    m = mosrx.gpu_module()
+    cfg = mosrx.ModuleCfg()
+    L.mosrx_gpu_module_cfg_default(C.byref(cfg))
+    srcs = [mosrx.mem_source(t.frames, t.off, t.len, loops=max(1, frames_per_thread // t.n)) for t in traces]
+    cfg.num_ifs, cfg.src[0], cfg.batch, cfg.max_frame = 1, srcs[0], batch, 2048
+    cfg.gpu_base, cfg.ngpu, cfg.pipeline, cfg.group = device, 1, 1, group
+    mosrx._chk(L.mosrx_gpu_module_configure(C.byref(cfg)), "mosrx_gpu_module_configure")
+    mosrx._VOIDFN(m.load_module_upper_half)()
+    cpus = list(range(32, 32 + nthreads))
+    objs = [C.c_uint64(0xFACE0000 + c) for c in cpus]
+    ctxs = [C.addressof(o) for o in objs]
+    stats = [mosrx.RxStats() for _ in cpus]
+    rcs, ends = [None] * nthreads, [0.0] * nthreads
+    try:
+        for c, x, s in zip(cpus, ctxs, srcs):
+            mosrx._chk(L.mosrx_gpu_module_bind(x, c), "mosrx_gpu_module_bind")
+            mosrx._chk(L.mosrx_gpu_module_bind_source(c, 0, s), "mosrx_gpu_module_bind_source")
+        for x in ctxs:
+            mosrx._CTXFN(m.init_handle)(x)
+        warm = mosrx.RxLoopOpts(2 * batch * group, 1, 0, 0)
+        for i in range(nthreads):                 # staging sized, kernels loaded
+            mosrx._chk(L.mosrx_rx_loop_ex(C.addressof(m), ctxs[i], 1, C.byref(warm), None, None,
+                                          C.byref(mosrx.RxStats())), "mosrx_rx_loop_ex")
+        opts = mosrx.RxLoopOpts(0, 1, 0, 0)
+        go = threading.Barrier(nthreads + 1)
+
+        def run(i):
+            go.wait()
+            rcs[i] = L.mosrx_rx_loop_ex(C.addressof(m), ctxs[i], 1, C.byref(opts), None, None, C.byref(stats[i]))
+            ends[i] = time.perf_counter()
+
+        th = [threading.Thread(target=run, args=(i,)) for i in range(nthreads)]
+        for t in th:
+            t.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for t in th:
+            t.join(300)
+        dt = max(ends) - t0
+    finally:
+        for x in ctxs:
+            mosrx._CTXFN(m.destroy_handle)(x)
+        for s in srcs:
+            L.mosrx_source_close(s)
+    if rcs != [0] * nthreads:
+        raise RuntimeError(f"rx loops returned {rcs}")
+    n = sum(int(s.rx_packets) for s in stats)
+    ab = sum(algo_bytes(t) * int(s.rx_packets) / t.n for t, s in zip(traces, stats))
+    return {"threads": nthreads, "group": group, "mpkts": round(n / dt / 1e6, 2), "gbps": round(ab / dt / 1e9, 2),
+            "frames": n, "seconds": round(dt, 3),
+            "per_thread_mpkts": [round(int(s.rx_packets) / (e - t0) / 1e6, 1) for s, e in zip(stats, ends)],
+            "method": f"{nthreads} mTCP threads x (own context, own in-memory source of distinct frames, own "
+                      f"mosrx_rx_loop_ex over gpu_module_func, {group} batch(es) per launch), one GPU"}
+
+
 def main():
     global STREAMS
     ap = argparse.ArgumentParser()
@@ -585,6 +653,12 @@ def main():
         if "S64" in traces:
             e2e["backend"]["S64_group128"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=128)
         e2e["backend"]["M1500_group8"] = measure_backend(traces["M1500"], "M1500", 4_000_000, device, group=8)
+        # one mTCP thread per core, each with its own context / source / rx loop
+        mt = {}
+        if "S64" in traces:
+            mt["S64"] = [measure_backend_threads("S64", t, 32, 32 * 2 ** 20, device) for t in (1, 2, 4, 8)]
+        mt["M1500"] = [measure_backend_threads("M1500", t, 1, 2_000_000, device) for t in (1, 2, 4)]
+        e2e["backend_threads"] = mt
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
         head = "M1500" if "M1500" in traces else keys[0]

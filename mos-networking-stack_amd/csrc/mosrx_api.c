@@ -272,8 +272,8 @@ int mosrx__check_batch(const mosrx_batch *b, int dev)
 	return 0;
 }
 
-/* Kernel shape: SMALL when every frame fits the header window (max_len known
- * and <= 94); otherwise S13 (one header wave + three span streamers, 50 VGPRs,
+/* Kernel shape: SMALL when every frame fits the SMALL header window (max_len
+ * known and <= MOSRX_WINDOW_END_SMALL, 78); otherwise S13 (one header wave + three span streamers, 50 VGPRs,
  * 8 waves per SIMD).  Measured on MI355X (profiles/r01_probe_w8.log,
  * back-to-back launches): 1500 B config S13 18.75 us, S14 18.73, S12 18.73,
  * LARGE 20.84; IMIX S13 20.5 us, S14 21.6, S12 21.7, LARGE 41.8; IMIX with

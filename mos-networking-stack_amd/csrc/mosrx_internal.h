@@ -64,7 +64,10 @@ typedef struct mosrx_kparams {
  * (DESIGN.md §4.3 has their measurements). */
 enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_S13 = 1, MOSRX_KIND_COUNT = 2 };
 #define MOSRX_STREAMERS 3
-#define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_SMALL ? 256u : 64u)
+#ifndef MOSRX_SMALL_FRAMES
+#define MOSRX_SMALL_FRAMES 256u   /* 256 x frames per lane */
+#endif
+#define MOSRX_KIND_FRAMES(k) ((k) == MOSRX_KIND_SMALL ? MOSRX_SMALL_FRAMES : 64u)
 /* Header windows.  Frames whose IP datagram ends at or before the window end
  * are finished in the per-lane header window; longer ones stream their tail
  * cooperatively from the first 16-byte boundary at or below it (the split).

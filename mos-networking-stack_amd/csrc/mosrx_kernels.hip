@@ -6,14 +6,15 @@
 // (tcp_util.c:157-190) and the Toeplitz RSS hash + queue map (util.c:27-131).
 // Integer byte work, HBM-bound: no MFMA.
 //
-// Header work is lane-per-frame ("hdr" below): each lane loads a 96-byte window
-// of its frame (6 x buffer_load_dwordx4 from frame byte 2, realigned with
-// v_alignbyte so the IP header sits dword-aligned in registers), parses every
-// field, runs the ip_fast_csum carry chain, the Toeplitz hash (24 nibble-table
-// lookups in LDS) and the TCP one's-complement sum of the segment bytes in the
-// window: all of them when the datagram ends by frame byte 94 (64-byte frames
-// finish there), else those before the frame's "split", the first
-// 16-byte-aligned buffer offset at or below frame byte 94.
+// Header work is lane-per-frame ("hdr" below): each lane loads a window of its
+// frame from byte 2 (5 x buffer_load_dwordx4 in the SMALL tile, 4 in the stream
+// tile, the full 6 = frame bytes [2, 94) for a wave holding IP options or a
+// fused BPF set), realigned with v_alignbyte so the IP header sits
+// dword-aligned in registers, then parses every field, runs the ip_fast_csum
+// carry chain, the Toeplitz hash (24 nibble-table lookups in LDS) and the TCP
+// one's-complement sum of the segment bytes in the window: all of them when the
+// datagram ends inside it (64-byte frames do), else those before the frame's
+// "split", the first 16-byte-aligned buffer offset at or below the window end.
 //
 // Bytes past the split (the "tail") are streamed by whole waves with
 // coalesced 16-byte-aligned loads, 1 KiB per wave instruction, summed as
@@ -22,19 +23,16 @@
 // absolute-grid sum, byte-swapped when the frame starts at an odd address
 // (256 * x == bswap16(x) mod 0xFFFF).
 //
-// Tile shapes ("kinds", mosrx_internal.h):
-//   small (TILE 256): every lane owns a frame and finishes it in registers when
-//     the datagram ends inside the window (the 64-byte configs); longer frames
-//     are summed by their wave.
-//   large (TILE 64): every wave loads the tile's 64 descriptors; wave 0 parses
-//     the headers while the streamer waves sum whole tails, loads issued
-//     SPECULATIVELY from the capture length (hi = off + caplen) right after
-//     the descriptor load; after one barrier the exact end (off + 14 + tot_len)
-//     corrects the sums.
-//   stream (TILE 64, the default for frames past the window): the streamers
-//     read the tile's tail span in buffer order as plain contiguous 1 KiB wave
-//     loads and attribute the bytes to tails with one prefix scan per block.
-//
+// Tile shapes ("kinds", mosrx_internal.h; the tuning shapes live in scripts/):
+//   small (MOSRX_SMALL_FRAMES per workgroup of 4 waves): every lane owns one or
+//     more frames and finishes them in registers (batches whose frames all end
+//     inside the window: the 64-byte configs); a longer frame, only when the
+//     shape is forced onto it, is summed by its wave.
+//   stream (TILE 64, any batch with longer frames): one header wave parses
+//     while three streamer waves read the tile's tail span in buffer order as
+//     plain contiguous 1 KiB wave loads and attribute the bytes to tails with
+//     one prefix scan per block.
+
 // All frame loads go through a buffer resource whose range is the batch
 // buffer: a bad offset can never fault, out-of-range dwords read as zero.
 
@@ -533,10 +531,10 @@ __device__ __forceinline__ void flush_counters(const mosrx_kparams &kp, const ui
 }
 
 // ---------------------------------------------------------------------------
-// small tile: 256 frames, lane per frame
+// small tile: MOSRX_SMALL_FRAMES frames, lane per frame (or per FPL frames)
 // ---------------------------------------------------------------------------
 // Every frame whose datagram ends inside the header window (all frames of a
-// batch with max_len <= 94) finishes in its lane: no cross-wave work, no
+// batch with max_len <= MOSRX_WINDOW_END_SMALL) finishes in its lane: no cross-wave work, no
 // barrier (each wave fills the LDS tables itself; a wave's LDS accesses are
 // ordered).  Longer frames (only when the shape is forced onto them) are
 // summed by their wave tail by tail, 4 KiB per pass.
@@ -553,23 +551,37 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
 
+	// FPL frames per lane: lane t owns frames tile*TILE + 256*i + t, and every
+	// one of its descriptor and window loads is issued before the first parse
+	// (FPL x the bytes in flight per wave).
+	constexpr uint32_t FPL = TILE / 256u;
+	static_assert(TILE % 256u == 0, "whole waves of frames");
 	const uint32_t t = threadIdx.x, lane = t & 63u;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
 	const uint32_t nbytes = kp.frames_bytes;
-	const uint32_t p = tile * TILE + t;
-	const bool active = p < kp.n;
-	uint32_t o = 0, cap = 0;
-	if (active) {
-		o = kp.off[p];
-		cap = eff_caplen(o, kp.len[p], nbytes);
-	}
-	hdr_win_t win;
-	if constexpr (DBG & 2) {
+	uint32_t pv[FPL], ov[FPL], capv[FPL];
+	bool actv[FPL];
 #pragma unroll
-		for (int i = 0; i < WIN_RAW; i++)
-			win.raw[i] = o + i;
-	} else {
-		hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, o, active, win);
+	for (uint32_t i = 0; i < FPL; i++) {
+		pv[i] = tile * TILE + 256u * i + t;
+		actv[i] = pv[i] < kp.n;
+		ov[i] = 0;
+		capv[i] = 0;
+		if (actv[i]) {
+			ov[i] = kp.off[pv[i]];
+			capv[i] = eff_caplen(ov[i], kp.len[pv[i]], nbytes);
+		}
+	}
+	hdr_win_t winv[FPL];
+#pragma unroll
+	for (uint32_t i = 0; i < FPL; i++) {
+		if constexpr (DBG & 2) {
+#pragma unroll
+			for (int j = 0; j < WIN_RAW; j++)
+				winv[i].raw[j] = ov[i] + j;
+		} else {
+			hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, ov[i], actv[i], winv[i]);
+		}
 	}
 	{
 		const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
@@ -582,6 +594,11 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 			s_cnt[t] = 0;
 		__syncthreads();
 	}
+#pragma unroll
+	for (uint32_t fi = 0; fi < FPL; fi++) {
+	const uint32_t p = pv[fi], o = ov[fi], cap = capv[fi];
+	const bool active = actv[fi];
+	const hdr_win_t &win = winv[fi];
 	const hdr_t h = hdr_parse<VAR, WEND>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
 	uint32_t tail = 0;
 	for (uint64_t m = __ballot(h.has_tail); m; m &= m - 1) {
@@ -619,12 +636,13 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	}
 #ifdef MOSRX_RTC_BPF
 	if constexpr ((VAR & VAR_BPF) != 0) {
-		__shared__ uint32_t s_bw[25u * TILE];
+		__shared__ uint32_t s_bw[25u * 256u];
 		const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * t);
 		if (active)
 			kp.bmatch[p] = m;
 	}
 #endif
+	}
 	flush_counters(kp, s_cnt, t);
 }
 

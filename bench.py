@@ -654,11 +654,13 @@ def main():
             e2e["backend"]["S64_group128"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=128)
         e2e["backend"]["M1500_group8"] = measure_backend(traces["M1500"], "M1500", 4_000_000, device, group=8)
         # one mTCP thread per core, each with its own context / source / rx loop
-        mt = {}
-        if "S64" in traces:
-            mt["S64"] = [measure_backend_threads("S64", t, 32, 32 * 2 ** 20, device) for t in (1, 2, 4, 8)]
-        mt["M1500"] = [measure_backend_threads("M1500", t, 1, 2_000_000, device) for t in (1, 2, 4)]
-        e2e["backend_threads"] = mt
+        # (one GPU's host side: single-rank runs only)
+        if ws == 1:
+            mt = {}
+            if "S64" in traces:
+                mt["S64"] = [measure_backend_threads("S64", t, 32, 32 * 2 ** 20, device) for t in (1, 2, 4, 8)]
+            mt["M1500"] = [measure_backend_threads("M1500", t, 1, 2_000_000, device) for t in (1, 2, 4)]
+            e2e["backend_threads"] = mt
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:
         head = "M1500" if "M1500" in traces else keys[0]

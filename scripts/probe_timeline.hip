@@ -200,12 +200,12 @@ static int plain(const char *name, std::vector<mosrx_kparams> &kps, uint32_t nti
 	return 0;
 }
 
-template <uint32_t T, int WEND = MOSRX_WINDOW_END_SMALL>
+template <uint32_t T, int WEND = MOSRX_WINDOW_END_SMALL, int DBG = 0>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(8))) void k_small(mosrx_kparams kp)
 {
-	classify_tile_small<2, T, 0, WEND>(kp, blockIdx.x);
+	classify_tile_small<0, T, DBG, WEND>(kp, blockIdx.x);
 }
-template <uint32_t T, int WEND = MOSRX_WINDOW_END_SMALL>
+template <uint32_t T, int WEND = MOSRX_WINDOW_END_SMALL, int DBG = 0>
 static double time_small(std::vector<mosrx_kparams> &kps)
 {
 	const int nb = (int)kps.size();
@@ -214,10 +214,10 @@ static double time_small(std::vector<mosrx_kparams> &kps)
 	if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
 		return -1;
 	for (int i = 0; i < nb; i++)
-		hipLaunchKernelGGL((k_small<T, WEND>), dim3(ng), dim3(T), 0, 0, kps[i]);
+		hipLaunchKernelGGL((k_small<T, WEND, DBG>), dim3(ng), dim3(T), 0, 0, kps[i]);
 	hipEventRecord(a, 0);
 	for (int i = 0; i < 2 * nb; i++)
-		hipLaunchKernelGGL((k_small<T, WEND>), dim3(ng), dim3(T), 0, 0, kps[i % nb]);
+		hipLaunchKernelGGL((k_small<T, WEND, DBG>), dim3(ng), dim3(T), 0, 0, kps[i % nb]);
 	hipEventRecord(b, 0);
 	hipEventSynchronize(b);
 	float ms = 0;
@@ -312,6 +312,21 @@ int main(int argc, char **argv)
 	// plain (DBG 0) back-to-back times over the resident batches, then stamped launches
 	printf("trace kind %d n %u tiles %u: %.2f MB\n", kind, n, ntiles, bytes / 1e6);
 	if (kind == MOSRX_TRACE_S64 || kind == MOSRX_TRACE_FW64) {
+		if (argc > 4 && atoi(argv[4]) == 4) {
+			// what bounds the SMALL tile: without the window loads / without the record stores
+			std::vector<double> a, b, c;
+			for (int r = 0; r < 9; r++) {
+				a.push_back(time_small<256>(kps));
+				b.push_back(time_small<256, MOSRX_WINDOW_END_SMALL, 2>(kps));
+				c.push_back(time_small<256, MOSRX_WINDOW_END_SMALL, 4>(kps));
+			}
+			const char *nm[3] = {"SMALL 256 (library)", "SMALL 256 no window loads", "SMALL 256 no record stores"};
+			std::vector<double> *v[3] = {&a, &b, &c};
+			for (int k = 0; k < 3; k++)
+				printf("%-28s median %8.2f us (%5.0f GB/s of algorithmic bytes)\n", nm[k], pct(*v[k], 0.5) * 1e3,
+				       bytes / (pct(*v[k], 0.5) * 1e-3) / 1e9);
+			return 0;
+		}
 		printf("SMALL 256 WEND 62: records %u differ\n", small_diff<256, MOSRX_WINDOW_END_STREAM>(kps));
 		std::vector<double> a, b;
 		for (int r = 0; r < 9; r++) {

@@ -298,7 +298,9 @@ static int kind_of(const mosrx_ctx *c, uint32_t max_len, uint64_t bytes, uint64_
  * in L2 behind the streamers (IMIX 256K: 22.1 -> 21.0 us; 1500 B: 17.7 us
  * non-temporal against 20.1 us cached; profiles/r02_probe/).  Only when the
  * context runs the library's default variant. */
+#ifndef MOSRX_NT_TAIL_MIN_FRAME
 #define MOSRX_NT_TAIL_MIN_FRAME 768   /* mean bytes per frame */
+#endif
 int mosrx__tail_variant(const mosrx_ctx *c, uint64_t bytes, uint64_t n)
 {
 	if (c->variant != MOSRX_DEFAULT_VARIANT || n == 0 || bytes / n >= MOSRX_NT_TAIL_MIN_FRAME)

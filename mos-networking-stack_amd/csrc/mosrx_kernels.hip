@@ -463,7 +463,7 @@ __device__ __forceinline__ void store_tcpinfo(mosrx_tcpinfo *ti, uint32_t p, con
 	v.x = def ? __builtin_bswap32(h.th1) : 0u;
 	v.y = def ? __builtin_bswap32(h.th2) : 0u;
 	v.z = def ? (((h.th3 >> 24) | ((h.th3 >> 8) & 0xFF00u)) | (h.ip_len << 16)) : 0u;   // window = tcph bytes 14,15
-	*reinterpret_cast<u32x3 *>(reinterpret_cast<uint32_t *>(ti) + 3u * p) = v;
+	__builtin_nontemporal_store(v, reinterpret_cast<u32x3 *>(reinterpret_cast<uint32_t *>(ti) + 3u * p));
 }
 
 // TX: write the fresh checksums into the frame (little-endian u16 stores, as
@@ -504,9 +504,13 @@ __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffe
 // of the global counters (MOSRX_CNT_SHARDS lines of 16 words): adds from every
 // workgroup to ONE word serialise at the memory side (~0.01 us each, which cost
 // a 1024-workgroup launch ~11 us), spread over 256 lines they do not.
+//
+// Records and side arrays are written once and read by the host after the
+// launch: non-temporal stores (rings 3-4 % faster than default-policy stores:
+// 1500 B 122 -> 119 us, IMIX 141 -> 135 us, 64 B 127 -> 123 us).
 __device__ __forceinline__ void store_record(const mosrx_kparams &kp, uint32_t p, u32x4 rec, uint32_t *s_cnt)
 {
-	*reinterpret_cast<u32x4 *>(kp.out + p) = rec;
+	__builtin_nontemporal_store(rec, reinterpret_cast<u32x4 *>(kp.out + p));
 	if (kp.counters) {
 		const uint32_t reason = rec.w & 0xFFu;
 		uint64_t m = __ballot(1);
@@ -632,7 +636,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 		if (active)
 			store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (active && kp.fhash)
-			kp.fhash[p] = flow_hash(h);
+			__builtin_nontemporal_store(flow_hash(h), kp.fhash + p);
 		if constexpr (IS_TI(VAR)) {
 			if (active)
 				store_tcpinfo(kp.tinfo, p, h);
@@ -643,7 +647,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 		__shared__ uint32_t s_bw[25u * 256u];
 		const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * t);
 		if (active)
-			kp.bmatch[p] = m;
+			__builtin_nontemporal_store(m, kp.bmatch + p);
 	}
 #endif
 	}
@@ -695,7 +699,7 @@ __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffe
 	} else if (active) {
 		store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (kp.fhash)
-			kp.fhash[p] = flow_hash(h);
+			__builtin_nontemporal_store(flow_hash(h), kp.fhash + p);
 		if constexpr (IS_TI(VAR))
 			store_tcpinfo(kp.tinfo, p, h);
 	}
@@ -1045,7 +1049,7 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 			} else {
 				// the outputs that do not need the tail sum go out before the barrier
 				if (active && kp.fhash)
-					kp.fhash[p] = flow_hash(h);
+					__builtin_nontemporal_store(flow_hash(h), kp.fhash + p);
 				if constexpr (IS_TI(VAR)) {
 					if (active)
 						store_tcpinfo(kp.tinfo, p, h);
@@ -1055,7 +1059,7 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 					__shared__ uint32_t s_bw[25u * 64u];
 					const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * lane);
 					if (active)
-						kp.bmatch[p] = m;
+						__builtin_nontemporal_store(m, kp.bmatch + p);
 				}
 #endif
 				const hdr_pend_t q =

@@ -175,6 +175,7 @@ typedef struct mosrx_gpu_module_stats {
 	uint64_t rx_batches, rx_frames, tx_packets, tx_bytes, tx_errors;
 	uint64_t kernel_launches;   /* timed launches (mosrx_set_timing on the thread's contexts) */
 	double   kernel_ms;         /* their summed device time (HIP events around each kernel) */
+	uint64_t rx_drops;          /* frames received but never handed out: their group's launch failed */
 } mosrx_gpu_module_stats;
 /* Time every kernel this thread's contexts launch (for the stats above). */
 int  mosrx_gpu_module_set_timing(struct mtcp_thread_context *ctx, int on);

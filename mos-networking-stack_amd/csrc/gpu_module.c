@@ -141,13 +141,21 @@ int mosrx_gpu_module_bind(struct mtcp_thread_context *ctx, int cpu)
 {
 	int i, rc = -ENOSPC;
 	pthread_mutex_lock(&g_lock);
-	for (i = 0; i < MAX_THREADS; i++)
-		if (g_tab[i].ctx == ctx || !g_tab[i].ctx) {
-			g_tab[i].ctx = ctx;
-			g_tab[i].cpu = cpu;
-			rc = 0;
+	if (!ctx || cpu < 0) {
+		pthread_mutex_unlock(&g_lock);
+		return -EINVAL;
+	}
+	for (i = 0; i < MAX_THREADS; i++)     /* this context's slot, else the first free one */
+		if (g_tab[i].ctx == ctx)
 			break;
-		}
+	if (i == MAX_THREADS)
+		for (i = 0; i < MAX_THREADS && g_tab[i].ctx; i++)
+			;
+	if (i < MAX_THREADS) {
+		g_tab[i].ctx = ctx;
+		g_tab[i].cpu = cpu;
+		rc = 0;
+	}
 	pthread_mutex_unlock(&g_lock);
 	return rc;
 }
@@ -173,10 +181,13 @@ int mosrx_gpu_module_device_of(int cpu, int ndev)
 	return dev < ndev ? dev : -EINVAL;
 }
 
+/* Slots are freed by destroy_handle, so the table can have holes: scan it all. */
 static struct gpu_priv *priv_of(struct mtcp_thread_context *ctx)
 {
 	int i;
-	for (i = 0; i < MAX_THREADS && g_tab[i].ctx; i++)
+	if (!ctx)
+		return NULL;
+	for (i = 0; i < MAX_THREADS; i++)
 		if (g_tab[i].ctx == ctx)
 			return g_tab[i].priv;
 	return NULL;
@@ -262,11 +273,11 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 	int i, k, cpu = -1, slot = -1, ndev = 0;
 
 	pthread_mutex_lock(&g_lock);
-	for (i = 0; i < MAX_THREADS; i++) {
+	for (i = 0; i < MAX_THREADS; i++)     /* bound by mosrx_gpu_module_bind */
 		if (g_tab[i].ctx == ctx) { slot = i; cpu = g_tab[i].cpu; break; }
-		if (!g_tab[i].ctx) { slot = i; g_tab[i].ctx = ctx; cpu = g_tab[i].cpu = g_next_cpu; break; }
-	}
-	g_next_cpu++;
+	if (slot < 0)                          /* else registration order, as mOS starts its threads */
+		for (i = 0; i < MAX_THREADS; i++)
+			if (!g_tab[i].ctx) { slot = i; g_tab[i].ctx = ctx; cpu = g_tab[i].cpu = g_next_cpu++; break; }
 	pthread_mutex_unlock(&g_lock);
 	if (slot < 0) {
 		fprintf(stderr, "[mosrx] gpu_module: too many threads\n");
@@ -387,6 +398,16 @@ static void group_recycle(struct group *g, mosrx_source *src)
 	g->nst = 0;
 }
 
+/* A received group that could not be classified: its frames are dropped and
+ * counted (rx_drops), borrowed runs go back to the source. */
+static void group_drop(struct gpu_priv *pv, struct if_state *is, int k)
+{
+	uint32_t i;
+	for (i = 0; i < is->g[k].nst; i++)
+		pv->stats.rx_drops += is->g[k].st[i].n;
+	group_recycle(&is->g[k], is->src);
+}
+
 static int group_submit(struct if_state *is, int k)
 {
 	struct group *g = &is->g[k];
@@ -452,8 +473,10 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 			is->cur = -1;
 			return 0;
 		}
-		if (group_submit(is, k))
+		if (group_submit(is, k)) {
+			group_drop(pv, is, k);
 			return -1;
+		}
 		is->inflight = k;
 	}
 	k = is->inflight;
@@ -465,8 +488,12 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 	if (g_cfg.pipeline) {             /* classify the next group behind the app's work */
 		int nk = k ^ 1;
 		group_fill(&is->g[nk], is->src);
-		if (is->g[nk].nst && group_submit(is, nk) == 0)
-			is->inflight = nk;
+		if (is->g[nk].nst) {
+			if (group_submit(is, nk) == 0)
+				is->inflight = nk;
+			else
+				group_drop(pv, is, nk);
+		}
 	}
 	return (int32_t)is->g[k].st[0].n;
 }
@@ -593,8 +620,14 @@ static void gpu_destroy_handle(struct mtcp_thread_context *ctx)
 	struct gpu_priv *pv = priv_of(ctx);
 	uint32_t i;
 	int k;
-	if (!pv)
+	if (!pv) {                         /* bound but never initialised: free the slot */
+		pthread_mutex_lock(&g_lock);
+		for (k = 0; ctx && k < MAX_THREADS; k++)
+			if (g_tab[k].ctx == ctx)
+				memset(&g_tab[k], 0, sizeof(g_tab[k]));
+		pthread_mutex_unlock(&g_lock);
 		return;
+	}
 	for (i = 0; i < g_cfg.num_ifs; i++) {
 		struct if_state *is = &pv->ifs[i];
 		if (!is->mc)
@@ -611,9 +644,9 @@ static void gpu_destroy_handle(struct mtcp_thread_context *ctx)
 		mosrx_close(is->mc);
 	}
 	pthread_mutex_lock(&g_lock);
-	for (k = 0; k < MAX_THREADS; k++)
+	for (k = 0; k < MAX_THREADS; k++)     /* the slot is free again */
 		if (g_tab[k].ctx == ctx)
-			g_tab[k].priv = NULL;
+			memset(&g_tab[k], 0, sizeof(g_tab[k]));
 	pthread_mutex_unlock(&g_lock);
 	free(pv);
 }

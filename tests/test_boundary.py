@@ -111,6 +111,41 @@ def test_gpu_module_config_validation():
     assert L.mosrx_gpu_module_configure(C.byref(c2)) == -22
 
 
+def test_gpu_module_thread_slots_are_reused():
+    """The module keeps one slot per mTCP thread context (64 of them); a
+    destroyed context frees its slot, so a long-lived process that starts and
+    stops threads never runs out, and a table with holes still finds every
+    bound context."""
+    L = mosrx.lib()
+    m = mosrx.gpu_module()
+    objs = [C.c_uint64(0xA110C000 + i) for i in range(70)]
+    ctxs = [C.addressof(o) for o in objs]
+    destroy = mosrx._CTXFN(m.destroy_handle)
+    bound = []
+    try:
+        for x in ctxs[:65]:                                       # fill the table (other tests may hold slots)
+            rc = L.mosrx_gpu_module_bind(x, 1)
+            if rc:
+                assert rc == -28                                  # -ENOSPC: every slot taken
+                break
+            bound.append(x)
+        assert 8 <= len(bound) <= 64
+        spare = ctxs[65:]
+        assert L.mosrx_gpu_module_bind(spare[0], 1) == -28
+        assert L.mosrx_gpu_module_bind(bound[0], 2) == 0          # rebinding a bound context is fine
+        destroy(bound[5])                                         # a hole in the middle of the table
+        assert L.mosrx_gpu_module_bind(spare[0], 3) == 0          # takes the freed slot
+        bound[5] = spare[0]
+        assert L.mosrx_gpu_module_bind(bound[-1], 4) == 0         # found past the hole, not duplicated
+        assert L.mosrx_gpu_module_bind(spare[1], 1) == -28
+        assert L.mosrx_gpu_module_bind(None, 1) == -22
+    finally:
+        for x in bound:
+            destroy(x)
+    assert L.mosrx_gpu_module_bind(spare[2], 1) == 0
+    destroy(spare[2])
+
+
 def test_source_tx_pcap_roundtrip(tmp_path):
     """send_pkts' way out of a trace file: frames appended to a pcap dump, read back
     bit-identical by the library's own pcap reader (pcap_inject's analogue)."""

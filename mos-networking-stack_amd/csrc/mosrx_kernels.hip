@@ -570,8 +570,9 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	// FPL frames per lane: lane t owns frames tile*TILE + 256*i + t, and every
 	// one of its descriptor and window loads is issued before the first parse
 	// (FPL x the bytes in flight per wave).
-	constexpr uint32_t FPL = TILE / 256u;
-	static_assert(TILE % 256u == 0, "whole waves of frames");
+	// (probe builds also launch tiles of 64 / 128 frames, one per lane)
+	constexpr uint32_t FPL = TILE > 256u ? TILE / 256u : 1u;
+	static_assert(TILE <= 256u || TILE % 256u == 0, "whole workgroups of frames");
 	const uint32_t t = threadIdx.x, lane = t & 63u;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
 	const uint32_t nbytes = kp.frames_bytes;

@@ -826,7 +826,9 @@ __device__ __forceinline__ void pend_emit(const mosrx_kparams &kp, __amdgpu_buff
 // run counts from 0, one leaving it ends at the run total.  No ownership
 // walk, no per-tail reduction; the header wave adds the S rows.  Tiles not in
 // buffer order stream tail by tail (stream_frames).
+#ifndef STREAM_U
 #define STREAM_U 4
+#endif
 
 // Inclusive prefix sum over the 64 lanes: row scans (4 DPP row shifts), then
 // row_bcast:15 and row_bcast:31 carry the row totals up.

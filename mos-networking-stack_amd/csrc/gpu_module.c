@@ -214,8 +214,41 @@ int mosrx_gpu_module_stats_of(struct mtcp_thread_context *ctx, mosrx_gpu_module_
 	return 0;
 }
 
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+/* Not configured by the application: do what pcap_load_module_upper_half does
+ * (pcap_module.c:124-160) -- one capture per netdev of mOS's configuration,
+ * here an AF_PACKET ring -- with the defaults (one batch per launch,
+ * num_queues 1 as pcap_module.c:159). */
+static void gpu_configure_from_mos(void)
+{
+	mosrx_gpu_module_cfg cfg;
+	const struct netdev_conf *nd = g_config.mos->netdev_table;
+	int i;
+	mosrx_gpu_module_cfg_default(&cfg);
+	if (nd->num <= 0 || nd->num > MOSRX_MAX_DEVICES) {
+		fprintf(stderr, "[mosrx] gpu_module: %d netdevs (1..%d supported)\n", nd->num, MOSRX_MAX_DEVICES);
+		exit(EXIT_FAILURE);
+	}
+	cfg.num_ifs = (uint32_t)nd->num;
+	for (i = 0; i < nd->num; i++) {
+		strncpy(cfg.if_names[i], nd->ent[i]->dev_name, sizeof(cfg.if_names[i]) - 1);
+		cfg.src[i] = mosrx_source_afpacket(cfg.if_names[i]);
+		if (!cfg.src[i]) {   /* as pcap_create failing (pcap_module.c:140-144) */
+			fprintf(stderr, "[mosrx] gpu_module: interface '%s' not found (or no CAP_NET_RAW)\n", cfg.if_names[i]);
+			exit(EXIT_FAILURE);
+		}
+	}
+	if (mosrx_gpu_module_configure(&cfg))
+		exit(EXIT_FAILURE);
+}
+#endif
+
 static void gpu_load_module_upper_half(void)
 {
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+	if (!g_configured)
+		gpu_configure_from_mos();
+#endif
 	if (!g_configured) {
 		fprintf(stderr, "[mosrx] gpu_module: mosrx_gpu_module_configure() not called\n");
 		exit(EXIT_FAILURE);   /* fatal init error, as pcap_module.c:141-155 */

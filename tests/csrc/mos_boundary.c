@@ -8,6 +8,8 @@
  * Each build prints the layout of io_module_func and RssInfo; the mOS build
  * also loads the backend's upper half as mtcp_init would (core.c:1735) and
  * prints the globals it set.  The test compares the two layouts line by line.
+ * With an interface name as argument the mOS build skips the configure call
+ * and lets load_module_upper_half open that netdev itself.
  */
 #include <stddef.h>
 #include <stdio.h>
@@ -20,7 +22,7 @@
 
 #define OFF(m) printf("io_module_func.%s %zu\n", #m, offsetof(io_module_func, m))
 
-int main(void)
+int main(int argc, char **argv)
 {
 	OFF(load_module_upper_half); OFF(load_module_lower_half); OFF(init_handle); OFF(link_devices);
 	OFF(release_pkt); OFF(get_wptr); OFF(set_wptr); OFF(send_pkts); OFF(get_rptr); OFF(get_nif);
@@ -46,6 +48,18 @@ int main(void)
 		mc.netdev_table = &nd;
 		g_config.mos = &mc;
 		num_queues = 0;
+		if (argc > 1) {
+			/* no mosrx_gpu_module_configure: the upper half opens the netdevs
+			 * itself, as pcap_load_module_upper_half does */
+			snprintf(e[0].dev_name, sizeof(e[0].dev_name), "%s", argv[1]);
+			nd.num = 1;
+			current_iomodule_func = &gpu_module_func;
+			current_iomodule_func->load_module_upper_half();
+			mosrx_gpu_module_get_cfg(&cfg);
+			printf("auto num_ifs %u if %s src %d num_queues %d forward %d\n", cfg.num_ifs, cfg.if_names[0],
+			       cfg.src[0] != NULL, num_queues, cfg.params.forward);
+			return 0;
+		}
 		mosrx_gpu_module_cfg_default(&cfg);
 		cfg.num_ifs = 1;
 		cfg.params.num_queues = 3;

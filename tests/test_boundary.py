@@ -69,6 +69,15 @@ def test_gpu_module_builds_inside_mos_and_sets_num_queues(tmp_path):
     # i40e map (util.c:120-126): 0x127 + {3,1,-1,-3}[0x127 & 3] = 0x124; 0x124 % 3 = 1 -- the
     # divisor is no longer 0
     assert kv["queue"] == ["1"]
+    # unconfigured: load_module_upper_half opens mOS's netdevs itself, as
+    # pcap_load_module_upper_half does (pcap_module.c:124-160); an unknown
+    # interface is a fatal init error like pcap_create's (pcap_module.c:140-144)
+    r = subprocess.run([str(exe), "nosuchif0"], capture_output=True, text=True)
+    assert r.returncode != 0 and "interface 'nosuchif0' not found" in r.stderr
+    if _have_raw():
+        out = _run([str(exe), "lo"])
+        assert out.splitlines()[-1].split() == ["auto", "num_ifs", "1", "if", "lo", "src", "1", "num_queues", "1",
+                                               "forward", "1"]
 
 
 def test_gpu_module_cpu_to_device_mapping():

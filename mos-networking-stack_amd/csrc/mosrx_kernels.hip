@@ -55,7 +55,8 @@ static_assert(2 + 4 * WIN_DW == MOSRX_WINDOW_END_FULL, "window end");
 static_assert(WIN_NLOAD(MOSRX_WINDOW_END_SMALL) == 5 && WIN_NLOAD(MOSRX_WINDOW_END_STREAM) == 4, "window loads");
 static_assert(sizeof(mosrx_result) == 16, "record size");
 // small: 4 waves, one frame per lane; stream: 1 header wave + MOSRX_STREAMERS streamer waves
-#define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? 256 : 64 * (1 + MOSRX_STREAMERS))
+#define SMALL_THREADS (MOSRX_SMALL_FRAMES < 256u ? MOSRX_SMALL_FRAMES : 256u)
+#define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? SMALL_THREADS : 64 * (1 + MOSRX_STREAMERS))
 
 
 // 16 bytes at byte offset c (OOB offsets read zero).  No data-dependent branch:

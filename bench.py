@@ -297,6 +297,11 @@ def measure(ctx, dist, key, steps, warmup, rank):
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+        # the launch duration behind `achieved` (HIP events around back-to-back
+        # launches on the launch stream, median of 5), and the timed region's own
+        # device time per step (HIP events around the K timed steps)
+        "launch_us": round(kern_ms * 1e3, 3),
+        "timed_region_device_us_per_step": round(1e3 * dev_ms / steps, 3),
     }
     if pmc:
         out["roofline"]["traffic_source"] = pmc.get("source")

@@ -342,6 +342,27 @@ int main(int argc, char **argv)
 	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);
 	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
 	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
+	if (argc > 4 && atoi(argv[4]) == 5) {
+		// streamer count x loads in flight: fewer streamers per tile = more tiles resident
+		// (S1: 2-wave tiles, 16 per CU), interleaved rounds, median per variant
+		const char *names[] = {"S3 U4 cached (library)", "S1 U8 cached", "S1 U6 cached", "S2 U6 cached",
+		                       "S2 U4 cached", "S3 U4 nt (library)", "S1 U8 nt", "S2 U6 nt"};
+		std::vector<double> ts[8];
+		for (int r = 0; r < 7; r++) {
+			ts[0].push_back(time_tl<3, 4, 8, 0, 64, 0>(kps, ntiles));
+			ts[1].push_back(time_tl<1, 8, 8, 0, 64, 0>(kps, ntiles));
+			ts[2].push_back(time_tl<1, 6, 8, 0, 64, 0>(kps, ntiles));
+			ts[3].push_back(time_tl<2, 6, 8, 0, 64, 0>(kps, ntiles));
+			ts[4].push_back(time_tl<2, 4, 8, 0, 64, 0>(kps, ntiles));
+			ts[5].push_back(time_tl<3, 4, 8, 0, 64, 2>(kps, ntiles));
+			ts[6].push_back(time_tl<1, 8, 8, 0, 64, 2>(kps, ntiles));
+			ts[7].push_back(time_tl<2, 6, 8, 0, 64, 2>(kps, ntiles));
+		}
+		for (int v = 0; v < 8; v++)
+			printf("%-28s median %7.2f us  min %7.2f us  (%5.0f GB/s at the median)\n", names[v], pct(ts[v], 0.5) * 1e3,
+			       pct(ts[v], 0.0) * 1e3, bytes / (pct(ts[v], 0.5) * 1e-3) / 1e9);
+		return 0;
+	}
 	if (argc > 4 && atoi(argv[4]) == 3) {
 		// interleaved rounds, median and min per variant (cross-variant drift cancels)
 		const char *names[] = {"cached: pend, tables first (lib)", "cached: pend, windows first",

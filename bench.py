@@ -717,6 +717,10 @@ def main():
                    "resident_bytes": h["resident_bytes"]},
         "roofline": h["roofline"],
         "read_ceiling_gbps": read_ceiling,
+        # the headline kernel's rate against the box's own streaming-read rate for
+        # launches of the ring's size (what the HBM delivers to a read-only kernel)
+        "frac_of_read_ceiling": (round(h["roofline"]["achieved"] / read_ceiling["launch_768MiB"], 4)
+                                 if read_ceiling and read_ceiling.get("launch_768MiB") else None),
         "cpu_baseline": cpu,
         "secondary": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in r.items()}
                       for k, r in results.items() if k != head},

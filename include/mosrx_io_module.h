@@ -186,6 +186,8 @@ typedef struct mosrx_rx_stats {
 	uint64_t rx_packets, rx_bytes, rx_errors;        /* NETSTAT, eth_in.c:42-45,80-84 (bytes + ETHER_OVR) */
 	uint64_t rounds, batches;
 	uint64_t by_reason[MOSRX_R_COUNT];
+	uint64_t recv_errors;                            /* recv_pkts calls that returned < 0: skipped, as core.c:899-902
+	                                                    (a round whose receives all failed counts as idle) */
 } mosrx_rx_stats;
 
 /* Per-frame consumer: the part of ProcessPacket after the checks (flow lookup,

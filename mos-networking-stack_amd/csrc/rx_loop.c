@@ -47,8 +47,10 @@ int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx,
 			const mosrx_result *res = NULL;
 			int32_t recv_cnt = iom->recv_pkts(ctx, rx_inf);
 			int32_t i;
-			if (recv_cnt < 0)
-				return -EIO;
+			if (recv_cnt < 0) {        /* RunMainLoop's for loop just skips it (core.c:899-902) */
+				st->recv_errors++;
+				continue;
+			}
 			if (recv_cnt == 0)
 				continue;
 			any = 1;

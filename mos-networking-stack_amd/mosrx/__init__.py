@@ -90,7 +90,8 @@ class TraceC(C.Structure):
 
 class RxStats(C.Structure):
     _fields_ = [("rx_packets", C.c_uint64), ("rx_bytes", C.c_uint64), ("rx_errors", C.c_uint64),
-                ("rounds", C.c_uint64), ("batches", C.c_uint64), ("by_reason", C.c_uint64 * NREASON)]
+                ("rounds", C.c_uint64), ("batches", C.c_uint64), ("by_reason", C.c_uint64 * NREASON),
+                ("recv_errors", C.c_uint64)]
 
 
 class ModuleCfg(C.Structure):
@@ -722,6 +723,17 @@ _RECVFN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int)
 _RPTRFN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint16))
 _WPTRFN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_int, C.c_uint16)
 _SENDFN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int)
+
+
+class ResultC(C.Structure):
+    """mosrx_result as a ctypes structure (RESULT_DTYPE's layout)."""
+    _fields_ = [("rss", C.c_uint32), ("ip_csum", C.c_uint16), ("tcp_csum", C.c_uint16),
+                ("payloadlen", C.c_uint16), ("payload_off", C.c_uint8), ("verdict", C.c_int8),
+                ("reason", C.c_uint8), ("queue", C.c_uint8), ("tcp_flags", C.c_uint8), ("ihl_doff", C.c_uint8)]
+
+
+# mosrx_pkt_fn: the rx loop's per-frame consumer (ProcessPacket's place)
+_PKTFN = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_uint16, C.POINTER(ResultC))
 PKT_TX_IP_CSUM, PKT_TX_TCP_CSUM = 0x01, 0x02
 PKT_RX_RSS, DRV_NAME, PKT_RX_RESULTS, PKT_RX_MATCH = 0x03, 0x08, 0x10, 0x11
 PKT_RX_TCPINFO, PKT_SET_PARAMS = 0x12, 0x13

@@ -63,6 +63,7 @@
 
 int ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index,
                   uint32_t cur_ts, unsigned char *pkt_data, int len);
+uint32_t GetRSSHash(in_addr_t sip, in_addr_t dip, in_port_t sp, in_port_t dp);   /* util.c:61-62, no header declares it */
 uint16_t TCPCalcChecksum(uint16_t *buf, uint16_t len, uint32_t saddr, uint32_t daddr);
 void FillInPacketIPContext(struct pkt_ctx *pctx, struct iphdr *iph, int ip_len);   /* ip_in.c:21, gnu89 inline */
 

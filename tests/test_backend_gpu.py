@@ -372,3 +372,53 @@ def test_two_mtcp_threads_run_concurrently():
         ora = O.classify(t.frames, t.off, t.len, O.params())
         assert st.rx_packets == 3 * t.n
         assert list(st.by_reason) == (3 * np.bincount(ora["reason"], minlength=NREASON)).tolist()
+
+
+# ---------------------------------------------------------------- inside mOS
+MOS_LOOP = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                        "mos_gpu_loop")
+
+
+def _raw_ip(s):
+    return struct.unpack("<I", socket.inet_aton(s))[0]
+
+
+@pytest.mark.skipif(not os.path.exists(MOS_LOOP),
+                    reason="needs oracle/_ref/mos_gpu_loop (make -C oracle ref, built where /root/reference is)")
+@pytest.mark.parametrize("fix,state,batch", [
+    ("edge", "msp1", 256), ("edge", "esp1_local", 100), ("edge", "noverify_local", 4096),
+    ("rand_small", "q3_ixgbe", 128), ("rand_mid", "msp1_local", 64), ("rand_large", "q8_i40e", 50),
+    ("imix_full", "msp1", 32768), ("m1500_full", "q4_i40e", 65536)])
+def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch):
+    """gpu_module_func compiled inside mOS's tree (its own io_module.h /
+    config.h) and registered as core.c:1725-1736 does, fed from a trace, with
+    mOS's own RunMainLoop rx section + ProcessPacket run on every frame get_rptr
+    hands out (oracle/mos_gpu_loop.c, linked from mOS's compiled objects): every
+    GPU verdict equals ProcessPacket's return value, every PKT_RX_RSS hash
+    (mOS's RssInfo) equals GetRSSHash, load_module_upper_half set mOS's
+    num_queues, and mOS's NETSTAT equals the GPU census."""
+    import json
+    import subprocess
+    from pktlib import write_ref_trace
+    from test_oracle_golden import GOLDEN, STATES
+    msp, esp, nq, qm, loc = STATES[state]
+    if fix == "imix_full":
+        t = mosrx.Trace(mosrx.TRACE_IMIX, 262_144)
+        frames, off, ln = t.frames, t.off, t.len
+    elif fix == "m1500_full":
+        t = mosrx.Trace(mosrx.TRACE_M1500, 65_536)
+        frames, off, ln = t.frames, t.off, t.len
+    else:
+        z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
+        frames, off, ln = z["frames"], z["off"], z["len"]
+    path = str(tmp_path / "trace.in")
+    write_ref_trace(path, frames, off, ln, num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm,
+                    local=[_raw_ip(a) for a in loc])
+    r = subprocess.run([MOS_LOOP, path, str(batch)], capture_output=True, text=True, timeout=120)
+    assert r.stdout.strip(), r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert r.returncode == 0, (d, r.stderr[-2000:])
+    assert d["frames"] == len(off) and d["verdict_diff"] == 0 and d["rss_diff"] == 0
+    assert d["num_queues"] == nq and d["nstat_ok"] == 1
+    assert d["compared"] + d["skipped"] == len(off) and d["compared"] > 0.5 * len(off)
+    assert d["batches"] == -(-len(off) // batch)

@@ -365,13 +365,15 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, all_cores: bool 
     return out
 
 
-def cpu_reference(tr: mosrx.Trace, key: str, seconds: float):
-    """mOS's own compiled functions (oracle/_ref/mosref --time: ref_frame, i.e. the
-    header checks of eth_in.c / ip_in.c / tcp.c, ip_fast_csum, TCPCalcChecksum,
-    GetRSSHash, GetRSSCPUCore per frame -- not ProcessPacket, whose stream
-    lookup is out of scope) on one host core, when the reference build
+def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: bool = False):
+    """mOS's own compiled functions on one host core, when the reference build
     travelled with the tree; else None.  A reported baseline, never the
-    measured path."""
+    measured path.  Default: `mosref --time` = ref_frame, i.e. the header
+    checks of eth_in.c / ip_in.c / tcp.c, ip_fast_csum, TCPCalcChecksum,
+    GetRSSHash, GetRSSCPUCore per frame (the GPU record's scope).
+    process_packet: `mosref --time-pp` = mOS's whole ProcessPacket per frame as
+    the rx loop calls it (checks + checksums + FindStream on an empty flow
+    table; no RSS, which the NIC computes in mOS)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "mosref")
     if not os.access(exe, os.X_OK):
         return None
@@ -382,17 +384,19 @@ def cpu_reference(tr: mosrx.Trace, key: str, seconds: float):
         path = os.path.join(td, "trace.mrxt")
         pktlib.write_ref_trace(path, tr.frames[:tr.frames_bytes], tr.off, tr.len)
         try:
-            out = subprocess.run([exe, "--time", path, str(seconds)], capture_output=True, text=True,
-                                 timeout=seconds + 60)
+            out = subprocess.run([exe, "--time-pp" if process_packet else "--time", path, str(seconds)],
+                                 capture_output=True, text=True, timeout=seconds + 60)
             r = json.loads(out.stdout.strip().splitlines()[-1])
         except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
             return None
     el = r["seconds"]
+    what = ("ProcessPacket per frame (oracle/_ref/mosref --time-pp; checks + checksums + FindStream, "
+            "no RSS)" if process_packet else
+            "ip_fast_csum + TCPCalcChecksum + GetRSSHash + GetRSSCPUCore + header checks "
+            "(oracle/_ref/mosref --time: ref_frame, not ProcessPacket)")
     return {"value": round(algo_bytes(tr, key) * r["passes"] / el / 1e9, 3), "unit": "GB/s", "cores": 1,
             "kind": "reference", "mpkts": round(r["mpkts"], 3),
-            "sample": f"{r['passes']} passes over one {tr.n}-frame batch ({el:.1f} s), mOS core/src "
-                      f"ip_fast_csum + TCPCalcChecksum + GetRSSHash + GetRSSCPUCore + header checks "
-                      f"(oracle/_ref/mosref --time: ref_frame, not ProcessPacket), 1 thread"}
+            "sample": f"{r['passes']} passes over one {tr.n}-frame batch ({el:.1f} s), mOS core/src {what}, 1 thread"}
 
 
 def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
@@ -435,6 +439,12 @@ def measure_fw64(ctx, seconds: float):
     port = cpu_baseline(tr, "FW64", min_s=seconds, all_cores=False)
     if ref:
         port["reference"] = ref
+    # mOS's ProcessPacket itself (the harness runs forward = 0: ForwardIPPacket
+    # needs route / ARP tables; for this trace of valid TCP frames of one flow
+    # only the non-IPv4 verdict depends on it)
+    ref = cpu_reference(tr, "FW64", seconds, process_packet=True)
+    if ref:
+        port["reference_processpacket"] = ref
     out["cpu_baseline"] = port
     ctx.set_params(mosrx.default_params())
     db = ctx.upload(tr.frames, tr.off, tr.len, frames_bytes=tr.frames_bytes, max_len=tr.max_len)
@@ -673,6 +683,9 @@ def main():
         ref = cpu_reference(traces[head], head, 10.0)
         if ref:
             cpu["reference"] = ref
+        ref = cpu_reference(traces[head], head, 5.0, process_packet=True)
+        if ref:
+            cpu["reference_processpacket"] = ref
         for k in keys:
             if k != head:
                 results[k]["cpu_baseline"] = cpu_baseline(traces[k], k, min_s=2.0)

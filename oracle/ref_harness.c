@@ -35,6 +35,13 @@
  * forward must be 0: ForwardIPPacket/ForwardEthernetFrame need route/ARP
  * tables and TX buffers.
  *
+ * Usage: mosref --time-pp <trace.in> <seconds>
+ *   mOS's whole ProcessPacket (eth_in.c:27-87) on every frame, under the trace
+ *   header's stack state (the flow table stays empty: no monitor socket is
+ *   listening, so FindStream creates nothing), passes repeated for at least
+ *   <seconds>; one JSON line.  The reference's per-frame rx cost as the rx loop
+ *   pays it, stream lookup included.
+ *
  * Usage: mosref --time <trace.in> <seconds>
  *   CPU baseline of the reference's own per-frame arithmetic on this host, one
  *   thread: the header checks of eth_in.c / ip_in.c / tcp.c, ip_fast_csum,
@@ -171,10 +178,13 @@ int main(int argc, char **argv)
 	static log_thread_context lg;
 
 	int timing = argc == 4 && !strcmp(argv[1], "--time");
-	if (argc != 3 && !timing) {
-		fprintf(stderr, "usage: %s trace.in results.out | %s --time trace.in seconds\n", argv[0], argv[0]);
+	const int timing_pp = argc == 4 && !strcmp(argv[1], "--time-pp");
+	if (argc != 3 && !timing && !timing_pp) {
+		fprintf(stderr, "usage: %s trace.in results.out | %s --time[-pp] trace.in seconds\n", argv[0], argv[0]);
 		return 2;
 	}
+	if (timing_pp)
+		argv++;
 	if (timing)
 		argv++;
 	in = fopen(argv[1], "rb");
@@ -224,6 +234,26 @@ int main(int argc, char **argv)
 	m.logger = &lg;
 	m.log_fp = fopen("/dev/null", "w");
 
+	if (timing_pp) {   /* every frame through ProcessPacket, as the rx loop calls it (core.c:906) */
+		uint64_t passes = 0, bytes = 0;
+		uint32_t sink = 0;
+		const double seconds = atof(argv[2]);
+		double t0, el;
+		for (i = 0; i < n; i++)
+			bytes += len[i];
+		t0 = now_s();
+		do {
+			for (i = 0; i < n; i++)
+				sink += (uint32_t)ProcessPacket(&m, 0, (int)i, 0, frames + off[i], (int)len[i]);
+			passes++;
+			el = now_s() - t0;
+		} while (el < seconds);
+		printf("{\"frames\": %u, \"passes\": %llu, \"seconds\": %.3f, \"mpkts\": %.4f, "
+		       "\"caplen_gbps\": %.4f, \"sink\": %u}\n",
+		       n, (unsigned long long)passes, el, (double)n * passes / el / 1e6, (double)bytes * passes / el / 1e9,
+		       sink);
+		return 0;
+	}
 	out = fopen(argv[2], "wb");
 	if (!out)
 		return 1;

@@ -176,6 +176,8 @@ typedef struct mosrx_gpu_module_stats {
 	uint64_t kernel_launches;   /* timed launches (mosrx_set_timing on the thread's contexts) */
 	double   kernel_ms;         /* their summed device time (HIP events around each kernel) */
 	uint64_t rx_drops;          /* frames received but never handed out: their group's launch failed */
+	uint64_t rx_reclassified;   /* batches classified again because mOS's stack state (num_msp /
+	                               num_esp) changed while they were in flight (mOS builds) */
 } mosrx_gpu_module_stats;
 /* Time every kernel this thread's contexts launch (for the stats above). */
 int  mosrx_gpu_module_set_timing(struct mtcp_thread_context *ctx, int on);

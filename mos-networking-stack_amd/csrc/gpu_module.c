@@ -42,6 +42,7 @@
 #include "mosrx_source.h"
 #ifdef MOSRX_HAVE_MOS_IO_MODULE
 #include "config.h"    /* g_config, num_queues (config.h:160-170) */
+#include "mtcp.h"      /* mtcp_thread_context.mtcp_manager -> num_msp / num_esp (mtcp.h:243-244, :304-312) */
 #endif
 
 #define MAX_THREADS 64
@@ -70,10 +71,12 @@ struct group {
 	uint32_t *match;
 	struct stage *st;         /* `group` stages */
 	uint32_t nst;             /* stages filled */
+	uint32_t msp, esp;        /* the stack state the group was classified under */
 };
 
 struct if_state {
 	mosrx_ctx *mc;
+	mosrx_params params;      /* the context's stack state (SET_PARAMS, or mOS's own counts) */
 	mosrx_source *src;
 	struct group g[MOSRX_NSLOT];
 	int cur;                  /* group exposed to the application, -1 none */
@@ -269,6 +272,38 @@ static void gpu_load_module_upper_half(void)
 #endif
 }
 
+/* The stack state ProcessPacket would see right now: inside an mOS build the
+ * thread's mtcp_manager counts its monitor and end-host sockets (num_msp /
+ * num_esp, incremented by socket creation, socket.c:77-78), and the backend
+ * follows them with no call from the core; standalone, 0 (the application
+ * passes changes with dev_ioctl(MOSRX_PKT_SET_PARAMS)). */
+static int mos_state(const struct gpu_priv *pv, uint32_t *msp, uint32_t *esp)
+{
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+	const struct mtcp_manager *m = pv->ctx ? pv->ctx->mtcp_manager : NULL;
+	if (m) {
+		*msp = m->num_msp;
+		*esp = m->num_esp;
+		return 1;
+	}
+#else
+	(void)pv; (void)msp; (void)esp;
+#endif
+	return 0;
+}
+
+/* Bring the context's stack state up to mOS's before a launch. */
+static int follow_mos_state(struct gpu_priv *pv, struct if_state *is)
+{
+	uint32_t msp, esp;
+	if (mos_state(pv, &msp, &esp) && (msp != is->params.num_msp || esp != is->params.num_esp)) {
+		is->params.num_msp = msp;
+		is->params.num_esp = esp;
+		return mosrx_set_params(is->mc, &is->params);
+	}
+	return 0;
+}
+
 static void group_free(mosrx_ctx *mc, struct group *g)
 {
 	if (g->blk) mosrx_host_free(mc, g->blk);
@@ -330,6 +365,7 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 			fprintf(stderr, "[mosrx] gpu_module: mosrx_open(%d): %s\n", dev, mosrx_strerror(rc));
 			exit(EXIT_FAILURE);
 		}
+		is->params = g_cfg.params;
 		is->src = (cpu < MAX_THREADS && g_src_cpu[cpu][i]) ? g_src_cpu[cpu][i] : g_cfg.src[i];
 		is->cur = is->inflight = -1;
 		if (g_cfg.bpf_nprog && (rc = mosrx_bpf_set(is->mc, g_cfg.bpf_progs, g_cfg.bpf_nprog))) {
@@ -441,13 +477,17 @@ static void group_drop(struct gpu_priv *pv, struct if_state *is, int k)
 	group_recycle(&is->g[k], is->src);
 }
 
-static int group_submit(struct if_state *is, int k)
+static int group_submit(struct gpu_priv *pv, struct if_state *is, int k)
 {
 	struct group *g = &is->g[k];
 	mosrx_batch b[MOSRX_MAX_GROUP];
 	mosrx_result *out[MOSRX_MAX_GROUP];
 	mosrx_tcpinfo *ti[MOSRX_MAX_GROUP];
 	uint32_t i;
+	if (follow_mos_state(pv, is))
+		return -1;
+	g->msp = is->params.num_msp;
+	g->esp = is->params.num_esp;
 	for (i = 0; i < g->nst; i++) {
 		const struct stage *s = &g->st[i];
 		b[i].frames = s->frames;
@@ -466,15 +506,17 @@ static int group_submit(struct if_state *is, int k)
 	return mosrx_classify_host_group_submit(is->mc, k, b, g->nst, out, g_cfg.tcpinfo ? ti : NULL);
 }
 
-static int group_wait(struct gpu_priv *pv, struct if_state *is, int k)
+static int group_wait(struct gpu_priv *pv, struct if_state *is, int k, int count)
 {
 	float ms;
 	uint32_t i;
 	if (mosrx_classify_host_wait(is->mc, k))
 		return -1;
-	pv->stats.rx_batches += is->g[k].nst;
-	for (i = 0; i < is->g[k].nst; i++)
-		pv->stats.rx_frames += is->g[k].st[i].n;
+	if (count) {
+		pv->stats.rx_batches += is->g[k].nst;
+		for (i = 0; i < is->g[k].nst; i++)
+			pv->stats.rx_frames += is->g[k].st[i].n;
+	}
 	if (mosrx_last_kernel_ms(is->mc, &ms) == 0) {
 		pv->stats.kernel_ms += ms;
 		pv->stats.kernel_launches++;
@@ -506,23 +548,38 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 			is->cur = -1;
 			return 0;
 		}
-		if (group_submit(is, k)) {
+		if (group_submit(pv, is, k)) {
 			group_drop(pv, is, k);
 			return -1;
 		}
 		is->inflight = k;
 	}
 	k = is->inflight;
-	if (group_wait(pv, is, k))
+	is->inflight = -1;
+	if (group_wait(pv, is, k, 1)) {
+		group_drop(pv, is, k);
 		return -1;
+	}
+	{
+		/* mOS's stack state changed while the group was in flight (a monitor or
+		 * end-host socket came or went): classify it again under the state the
+		 * rx loop runs with now, so every batch handed out matches ProcessPacket */
+		uint32_t msp, esp;
+		if (mos_state(pv, &msp, &esp) && (msp != is->g[k].msp || esp != is->g[k].esp)) {
+			pv->stats.rx_reclassified += is->g[k].nst;
+			if (group_submit(pv, is, k) || group_wait(pv, is, k, 0)) {
+				group_drop(pv, is, k);
+				return -1;
+			}
+		}
+	}
 	is->cur = k;
 	is->cur_idx = 0;
-	is->inflight = -1;
 	if (g_cfg.pipeline) {             /* classify the next group behind the app's work */
 		int nk = k ^ 1;
 		group_fill(&is->g[nk], is->src);
 		if (is->g[nk].nst) {
-			if (group_submit(is, nk) == 0)
+			if (group_submit(pv, is, nk) == 0)
 				is->inflight = nk;
 			else
 				group_drop(pv, is, nk);
@@ -639,7 +696,10 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
 		*(const mosrx_tcpinfo **)argp = s->ti;
 		return 0;
 	case MOSRX_PKT_SET_PARAMS:   /* batches submitted from now on use the new stack state */
-		return mosrx_set_params(pv->ifs[nif].mc, (const mosrx_params *)argp) ? -1 : 0;
+		if (mosrx_set_params(pv->ifs[nif].mc, (const mosrx_params *)argp))
+			return -1;
+		pv->ifs[nif].params = *(const mosrx_params *)argp;
+		return 0;
 	case DRV_NAME:
 		*(const char **)argp = "mosrx_gpu";
 		return 0;

@@ -20,8 +20,15 @@
  * ref_harness.c).  Frames whose headers claim bytes past the capture (the
  * reference reads past its buffer there) are passed over.
  *
- * Usage: mos_gpu_loop <trace.in> <batch>   -- prints one JSON line, exit 0 when
- * every compared value is equal.
+ * With a period P (third argument) the application changes the stack state
+ * every P batches -- mOS's num_msp toggles between the trace's value and 0, as
+ * a monitor socket being created and closed would (socket.c:77-78) -- and the
+ * backend must follow on its own: the thread context points at the
+ * mtcp_manager (mtcp.h:304-312), and a batch classified in flight under the old
+ * state is classified again before it is handed out.
+ *
+ * Usage: mos_gpu_loop <trace.in> <batch> [period]   -- prints one JSON line,
+ * exit 0 when every compared value is equal.
  */
 #include <arpa/inet.h>
 #include <execinfo.h>
@@ -94,14 +101,15 @@ int main(int argc, char **argv)
 	static io_module_func null_iom;
 	static log_thread_context lg;
 	mosrx_gpu_module_cfg cfg;
+	mosrx_gpu_module_stats st;
 	mosrx_source *src;
 	uint64_t frames_seen = 0, compared = 0, skipped = 0, verdict_diff = 0, rss_checked = 0, rss_diff = 0;
 	uint64_t batches = 0, census[MOSRX_R_COUNT], neg = 0, bytes = 0;
 	int64_t first_bad = -1;
 
 	signal(SIGSEGV, on_segv);
-	if (argc != 3) {
-		fprintf(stderr, "usage: %s trace.in batch\n", argv[0]);
+	if (argc != 3 && argc != 4) {
+		fprintf(stderr, "usage: %s trace.in batch [period]\n", argv[0]);
 		return 2;
 	}
 	in = fopen(argv[1], "rb");
@@ -139,6 +147,7 @@ int main(int argc, char **argv)
 	mc.route_table = &rt;
 	g_config.mos = &mc;
 	tctx.cpu = 0;
+	tctx.mtcp_manager = &m;     /* the backend reads num_msp / num_esp through it */
 	TAILQ_INIT(&m.monitors);
 	m.num_msp = num_msp;
 	m.num_esp = num_esp;
@@ -217,8 +226,11 @@ int main(int argc, char **argv)
 					first_bad = (int64_t)frames_seen;
 			}
 		}
+		if (argc == 4 && batches % (uint64_t)atoi(argv[3]) == 0)
+			m.num_msp = m.num_msp ? 0 : (num_msp ? num_msp : 1);   /* a monitor socket comes or goes */
 	}
 	g_stage = "destroy_handle";
+	mosrx_gpu_module_stats_of(&tctx, &st);
 	current_iomodule_func->destroy_handle(&tctx);
 	mosrx_source_close(src);
 	{
@@ -228,12 +240,13 @@ int main(int argc, char **argv)
 		                                 m.nstat.rx_bytes[0] == bytes);
 		printf("{\"frames\": %llu, \"batches\": %llu, \"compared\": %llu, \"skipped\": %llu, \"verdict_diff\": %llu, "
 		       "\"first_bad\": %lld, \"rss_checked\": %llu, \"rss_diff\": %llu, \"num_queues\": %d, "
-		       "\"nstat_rx_packets\": %llu, \"nstat_rx_errors\": %llu, \"nstat_ok\": %d, \"tcp_ok\": %llu}\n",
+		       "\"nstat_rx_packets\": %llu, \"nstat_rx_errors\": %llu, \"nstat_ok\": %d, \"tcp_ok\": %llu, "
+		       "\"reclassified\": %llu}\n",
 		       (unsigned long long)frames_seen, (unsigned long long)batches, (unsigned long long)compared,
 		       (unsigned long long)skipped, (unsigned long long)verdict_diff, (long long)first_bad,
 		       (unsigned long long)rss_checked, (unsigned long long)rss_diff, num_queues,
 		       (unsigned long long)m.nstat.rx_packets[0], (unsigned long long)m.nstat.rx_errors[0], nstat_ok,
-		       (unsigned long long)census[MOSRX_R_TCP_OK]);
+		       (unsigned long long)census[MOSRX_R_TCP_OK], (unsigned long long)st.rx_reclassified);
 		return (frames_seen == n && !verdict_diff && !rss_diff && nstat_ok) ? 0 : 1;
 	}
 }

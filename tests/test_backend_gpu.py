@@ -385,18 +385,23 @@ def _raw_ip(s):
 
 @pytest.mark.skipif(not os.path.exists(MOS_LOOP),
                     reason="needs oracle/_ref/mos_gpu_loop (make -C oracle ref, built where /root/reference is)")
-@pytest.mark.parametrize("fix,state,batch", [
-    ("edge", "msp1", 256), ("edge", "esp1_local", 100), ("edge", "noverify_local", 4096),
-    ("rand_small", "q3_ixgbe", 128), ("rand_mid", "msp1_local", 64), ("rand_large", "q8_i40e", 50),
-    ("imix_full", "msp1", 32768), ("m1500_full", "q4_i40e", 65536)])
-def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch):
+@pytest.mark.parametrize("fix,state,batch,period", [
+    ("edge", "msp1", 256, 0), ("edge", "esp1_local", 100, 0), ("edge", "noverify_local", 4096, 0),
+    ("rand_small", "q3_ixgbe", 128, 0), ("rand_mid", "msp1_local", 64, 0), ("rand_large", "q8_i40e", 50, 0),
+    ("imix_full", "msp1", 32768, 0), ("m1500_full", "q4_i40e", 65536, 0),
+    # the stack state changes under the backend: num_msp toggles every `period` batches
+    ("edge", "msp1_local", 64, 1), ("rand_mid", "msp1", 50, 2), ("imix_full", "msp1", 8192, 3)])
+def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch, period):
     """gpu_module_func compiled inside mOS's tree (its own io_module.h /
     config.h) and registered as core.c:1725-1736 does, fed from a trace, with
     mOS's own RunMainLoop rx section + ProcessPacket run on every frame get_rptr
     hands out (oracle/mos_gpu_loop.c, linked from mOS's compiled objects): every
     GPU verdict equals ProcessPacket's return value, every PKT_RX_RSS hash
     (mOS's RssInfo) equals GetRSSHash, load_module_upper_half set mOS's
-    num_queues, and mOS's NETSTAT equals the GPU census."""
+    num_queues, and mOS's NETSTAT equals the GPU census.  With a period, mOS's
+    num_msp changes every `period` batches (a monitor socket created / closed)
+    and the backend follows it through the thread context with no call from
+    the core, re-classifying the batch it had in flight."""
     import json
     import subprocess
     from pktlib import write_ref_trace
@@ -414,7 +419,8 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
     path = str(tmp_path / "trace.in")
     write_ref_trace(path, frames, off, ln, num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm,
                     local=[_raw_ip(a) for a in loc])
-    r = subprocess.run([MOS_LOOP, path, str(batch)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([MOS_LOOP, path, str(batch)] + ([str(period)] if period else []), capture_output=True,
+                       text=True, timeout=120)
     assert r.stdout.strip(), r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert r.returncode == 0, (d, r.stderr[-2000:])
@@ -422,3 +428,5 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
     assert d["num_queues"] == nq and d["nstat_ok"] == 1
     assert d["compared"] + d["skipped"] == len(off) and d["compared"] > 0.5 * len(off)
     assert d["batches"] == -(-len(off) // batch)
+    if period:                                    # every change caught a batch in flight
+        assert d["reclassified"] == (d["batches"] - 1) // period

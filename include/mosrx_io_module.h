@@ -216,16 +216,32 @@ typedef struct mosrx_rx_loop_opts {
 int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx, int nif,
                      const mosrx_rx_loop_opts *opts, mosrx_pkt_fn fn, void *arg, mosrx_rx_stats *st);
 
-/* A consumer for mosrx_rx_loop*: ForwardEthernetFrame (eth_out.c:105-129) for
- * every frame the checks accepted (verdict 1) -- out_if[in_ifidx] from the
- * nic_forward_table, get_wptr, copy; -1 in out_if drops.  `arg` points at a
- * mosrx_forwarder.  The round's send_pkts sends what it wrote. */
+/* A consumer for mosrx_rx_loop*: the frames mOS forwards with `forward` set,
+ * decided from the verdict reason and the stack state as ProcessPacket's paths
+ * do (mosrx_mos_forwards), each copied with ForwardEthernetFrame's steps
+ * (eth_out.c:105-129: out_if[in_ifidx] from the nic_forward_table, get_wptr,
+ * copy; -1 in out_if drops).  `arg` points at a mosrx_forwarder.  The round's
+ * send_pkts sends what it wrote. */
 typedef struct mosrx_forwarder {
 	const io_module_func *iom;
 	struct mtcp_thread_context *ctx;
 	int32_t out_if[MOSRX_MAX_DEVICES];
 	uint64_t forwarded, dropped;
+	int32_t forward;             /* mos.conf `forward` (pctx->forward) */
+	uint32_t num_msp, num_esp;   /* the stack state the records were made under */
 } mosrx_forwarder;
+/* 1 when mOS forwards a frame with this record, 0 when it consumes or drops it:
+ *   NON_IPV4, ARP            forward && num_msp: ForwardEthernetFrame, eth_in.c:60-77 (ARP
+ *                            is processed locally only when forwarding is off)
+ *   NOVERIFY_PASS            forward: ForwardIPPacket before the transport layer, ip_in.c:66-70
+ *   NOT_TCP (not to me)      forward && num_msp: ip_in.c:86-91
+ *   TCP_BADCSUM              forward && num_msp: tcp.c:438-442 (the verdict stays -1)
+ *   TCP_OK / TCP_LEN_OK      forward && num_msp && !num_esp: the stream engine of a
+ *                            monitor-only stack forwards every segment (HandleMonitorStream,
+ *                            tcp.c:386-390; the orphan path, :509-511); with end-host
+ *                            sockets the flow decides (out of scope), not forwarded here
+ *   ICMP_LOCAL               consumed locally; the rest are dropped. */
+int  mosrx_mos_forwards(const mosrx_result *res, int forward, uint32_t num_msp, uint32_t num_esp);
 void mosrx_forward_frame(void *arg, int ifidx, int index, const uint8_t *pkt, uint16_t len,
                          const mosrx_result *res);
 

@@ -98,9 +98,29 @@ int mosrx_rx_loop(const io_module_func *iom, struct mtcp_thread_context *ctx, in
 	return mosrx_rx_loop_ex(iom, ctx, nif, &o, fn, arg, st);
 }
 
-/* ForwardEthernetFrame (eth_out.c:105-129) for the frames the checks accepted
- * (verdict 1): the output netdev from the NIC forwarding table, a TX buffer
- * from get_wptr, a copy of the frame; the round's send_pkts sends it. */
+int mosrx_mos_forwards(const mosrx_result *res, int forward, uint32_t num_msp, uint32_t num_esp)
+{
+	if (!res || !forward)
+		return 0;
+	switch (res->reason) {
+	case MOSRX_R_NON_IPV4:
+	case MOSRX_R_ARP:             /* every non-IPv4 frame, ARP too, eth_in.c:60-77 */
+	case MOSRX_R_NOT_TCP:
+	case MOSRX_R_TCP_BADCSUM:
+		return num_msp != 0;
+	case MOSRX_R_NOVERIFY_PASS:
+		return 1;
+	case MOSRX_R_TCP_OK:
+	case MOSRX_R_TCP_LEN_OK:
+		return num_msp != 0 && num_esp == 0;
+	default:
+		return 0;
+	}
+}
+
+/* The frames mOS forwards (mosrx_mos_forwards), each as ForwardEthernetFrame
+ * does (eth_out.c:105-129): the output netdev from the NIC forwarding table, a
+ * TX buffer from get_wptr, a copy of the frame; the round's send_pkts sends it. */
 void mosrx_forward_frame(void *arg, int ifidx, int index, const uint8_t *pkt, uint16_t len,
                          const mosrx_result *res)
 {
@@ -108,7 +128,8 @@ void mosrx_forward_frame(void *arg, int ifidx, int index, const uint8_t *pkt, ui
 	int out;
 	uint8_t *buf;
 	(void)index;
-	if (!f || res->verdict != 1 || ifidx < 0 || ifidx >= MOSRX_MAX_DEVICES || (out = f->out_if[ifidx]) < 0 ||
+	if (!f || !mosrx_mos_forwards(res, f->forward, f->num_msp, f->num_esp) || ifidx < 0 ||
+	    ifidx >= MOSRX_MAX_DEVICES || (out = f->out_if[ifidx]) < 0 ||
 	    !f->iom->get_wptr || !(buf = f->iom->get_wptr(f->ctx, out, len))) {
 		if (f)
 			f->dropped++;

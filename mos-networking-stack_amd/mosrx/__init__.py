@@ -126,7 +126,8 @@ class AfpInfo(C.Structure):
 
 class Forwarder(C.Structure):
     _fields_ = [("iom", C.c_void_p), ("ctx", C.c_void_p), ("out_if", C.c_int32 * 16),
-                ("forwarded", C.c_uint64), ("dropped", C.c_uint64)]
+                ("forwarded", C.c_uint64), ("dropped", C.c_uint64),
+                ("forward", C.c_int32), ("num_msp", C.c_uint32), ("num_esp", C.c_uint32)]
 
 
 class MosrxError(OSError):
@@ -219,6 +220,7 @@ def lib():
             "mosrx_gpu_module_bind": (I, [P, I]),
             "mosrx_rx_loop": (I, [P, P, I, U64, P, P, C.POINTER(RxStats)]),
             "mosrx_rx_loop_ex": (I, [P, P, I, C.POINTER(RxLoopOpts), P, P, C.POINTER(RxStats)]),
+            "mosrx_mos_forwards": (I, [P, I, U32, U32]),
             "mosrx_device_count": (I, []),
             "mosrx_classify_host_submit_ex": (I, [P, I, C.POINTER(Batch), P, P]),
             "mosrx_classify_host_group_submit": (I, [P, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
@@ -774,6 +776,7 @@ class GpuBackend:
         cfg.group, cfg.tcpinfo, cfg.tx_batch = group, int(tcpinfo), tx_batch
         if params is not None:
             cfg.params = params
+        self.params = Params.from_buffer_copy(cfg.params)
         self._bpf = None
         if bpf:
             self._bpf = _bpf_progs(bpf)          # kept alive until init_handle has installed them
@@ -847,12 +850,14 @@ class GpuBackend:
         return st
 
     def forwarder(self, out_if: list[int]) -> Forwarder:
-        """A mosrx_forwarder for run_loop(forward=...): netdev i -> out_if[i]."""
+        """A mosrx_forwarder for run_loop(forward=...): netdev i -> out_if[i], the
+        frames mOS forwards under the backend's stack state (mosrx_mos_forwards)."""
         f = Forwarder()
         f.iom = C.addressof(self.m)
         f.ctx = self.ctx
         for i in range(16):
             f.out_if[i] = out_if[i] if i < len(out_if) else -1
+        f.forward, f.num_msp, f.num_esp = self.params.forward, self.params.num_msp, self.params.num_esp
         return f
 
     def rss_of(self, ifidx: int, pktidx: int) -> int | None:

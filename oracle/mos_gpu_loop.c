@@ -15,10 +15,14 @@
  *
  * The stack state comes from the trace header (oracle/ref_harness.c format):
  * num_msp / num_esp into the mtcp_manager, the netdevs' addresses into
- * g_config.mos->netdev_table (read back by load_module_upper_half), num_queues
- * and the queue map into the module's configuration.  forward must be 0 (see
- * ref_harness.c).  Frames whose headers claim bytes past the capture (the
- * reference reads past its buffer there) are passed over.
+ * g_config.mos->netdev_table and `forward` into g_config.mos (both read back
+ * by load_module_upper_half), num_queues and the queue map into the module's
+ * configuration.  With forward set, mOS's own ForwardIPPacket /
+ * ForwardEthernetFrame are wrapped (-Wl,--wrap: they would need route and ARP
+ * tables and TX buffers) to record which frames ProcessPacket forwards; that
+ * set must equal mosrx_mos_forwards() over the GPU records, the rule the rx
+ * loop's forwarding consumer applies.  Frames whose headers claim bytes past
+ * the capture (the reference reads past its buffer there) are passed over.
  *
  * With a period P (third argument) the application changes the stack state
  * every P batches -- mOS's num_msp toggles between the trace's value and 0, as
@@ -52,6 +56,11 @@ uint32_t GetRSSHash(in_addr_t sip, in_addr_t dip, in_port_t sp, in_port_t dp);  
 
 static int g_qmode = 1;
 int __wrap_FetchEndianType(void) { return g_qmode; }
+
+/* mOS's forwarding calls, recorded instead of transmitted */
+static int g_fwd;
+void __wrap_ForwardIPPacket(mtcp_manager_t mtcp, struct pkt_ctx *pctx) { (void)mtcp; (void)pctx; g_fwd++; }
+void __wrap_ForwardEthernetFrame(struct mtcp_manager *mtcp, struct pkt_ctx *pctx) { (void)mtcp; (void)pctx; g_fwd++; }
 
 static int rd(FILE *f, void *p, size_t n) { return fread(p, 1, n, f) == n ? 0 : -1; }
 
@@ -104,6 +113,7 @@ int main(int argc, char **argv)
 	mosrx_gpu_module_stats st;
 	mosrx_source *src;
 	uint64_t frames_seen = 0, compared = 0, skipped = 0, verdict_diff = 0, rss_checked = 0, rss_diff = 0;
+	uint64_t fwd_mos = 0, fwd_diff = 0;
 	uint64_t batches = 0, census[MOSRX_R_COUNT], neg = 0, bytes = 0;
 	int64_t first_bad = -1;
 
@@ -120,8 +130,8 @@ int main(int argc, char **argv)
 		fprintf(stderr, "bad trace header\n");
 		return 2;
 	}
-	if (forward != 0 || nq < 1) {
-		fprintf(stderr, "forward must be 0 and num_queues >= 1\n");
+	if ((forward != 0 && forward != 1) || nq < 1) {
+		fprintf(stderr, "forward must be 0 or 1 and num_queues >= 1\n");
 		return 2;
 	}
 	off = malloc((size_t)n * 4 + 4);
@@ -220,8 +230,15 @@ int main(int argc, char **argv)
 			}
 			compared++;
 			g_stage = "ProcessPacket";
+			g_fwd = 0;
 			if ((int)res[k].verdict != ProcessPacket(&m, 0, k, 0, pkt, (int)l)) {
 				verdict_diff++;
+				if (first_bad < 0)
+					first_bad = (int64_t)frames_seen;
+			}
+			fwd_mos += g_fwd > 0;
+			if ((g_fwd > 0) != (mosrx_mos_forwards(&res[k], forward, m.num_msp, m.num_esp) != 0)) {
+				fwd_diff++;
 				if (first_bad < 0)
 					first_bad = (int64_t)frames_seen;
 			}
@@ -241,12 +258,13 @@ int main(int argc, char **argv)
 		printf("{\"frames\": %llu, \"batches\": %llu, \"compared\": %llu, \"skipped\": %llu, \"verdict_diff\": %llu, "
 		       "\"first_bad\": %lld, \"rss_checked\": %llu, \"rss_diff\": %llu, \"num_queues\": %d, "
 		       "\"nstat_rx_packets\": %llu, \"nstat_rx_errors\": %llu, \"nstat_ok\": %d, \"tcp_ok\": %llu, "
-		       "\"reclassified\": %llu}\n",
+		       "\"reclassified\": %llu, \"forwarded_by_mos\": %llu, \"forward_diff\": %llu}\n",
 		       (unsigned long long)frames_seen, (unsigned long long)batches, (unsigned long long)compared,
 		       (unsigned long long)skipped, (unsigned long long)verdict_diff, (long long)first_bad,
 		       (unsigned long long)rss_checked, (unsigned long long)rss_diff, num_queues,
 		       (unsigned long long)m.nstat.rx_packets[0], (unsigned long long)m.nstat.rx_errors[0], nstat_ok,
-		       (unsigned long long)census[MOSRX_R_TCP_OK], (unsigned long long)st.rx_reclassified);
-		return (frames_seen == n && !verdict_diff && !rss_diff && nstat_ok) ? 0 : 1;
+		       (unsigned long long)census[MOSRX_R_TCP_OK], (unsigned long long)st.rx_reclassified,
+		       (unsigned long long)fwd_mos, (unsigned long long)fwd_diff);
+		return (frames_seen == n && !verdict_diff && !rss_diff && !fwd_diff && nstat_ok) ? 0 : 1;
 	}
 }

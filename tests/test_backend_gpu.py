@@ -26,6 +26,21 @@ def write_pcap(path, frames, off, ln):
             fh.write(struct.pack("<IIII", i, 0, n, n) + bytes(frames[o:o + n]))
 
 
+# the frames mOS forwards for a record under (forward, num_msp, num_esp): eth_in.c:60-77
+# (every non-IPv4 frame, ARP too), ip_in.c:66-70 (no monitor / stream socket),
+# ip_in.c:86-91 (other protocols), tcp.c:438-442 (bad TCP checksum), and the stream
+# engine of a monitor-only stack for accepted segments (tcp.c:386-390, :509-511);
+# pinned to mOS itself by test_backend_inside_mos_checked_by_processpacket
+def mos_forwarded(rec, forward=1, num_msp=1, num_esp=0):
+    r = rec["reason"]
+    R = mosrx.R
+    if not forward:
+        return np.zeros(len(rec), bool)
+    msp_only = (r == R["NON_IPV4"]) | (r == R["ARP"]) | (r == R["NOT_TCP"]) | (r == R["TCP_BADCSUM"])
+    ok = (r == R["TCP_OK"]) | (r == R["TCP_LEN_OK"])
+    return (msp_only & (num_msp != 0)) | (r == R["NOVERIFY_PASS"]) | (ok & (num_msp != 0) & (num_esp == 0))
+
+
 def drain(be, n_expect=None):
     """recv_pkts until idle: (records, frames) in arrival order."""
     recs, frames = [], []
@@ -182,12 +197,12 @@ def test_tx_reaches_the_source(tmp_path):
         fwd = be.forwarder([0])
         st = be.run_loop(forward=fwd)
         assert st.rx_packets == t.n
-        assert fwd.forwarded == int((ora["verdict"] == 1).sum()) and fwd.dropped == t.n - fwd.forwarded
+        assert fwd.forwarded == int(mos_forwarded(ora).sum()) and fwd.dropped == t.n - fwd.forwarded
         assert be.stats().tx_packets == 40 + fwd.forwarded
     finally:
         be.close()
     sent = mosrx.read_pcap(path)
-    keep = np.nonzero(ora["verdict"] == 1)[0]
+    keep = np.nonzero(mos_forwarded(ora))[0]
     assert sent[:40] == mine
     assert sent[40:] == [bytes(t.frames[t.off[i]:t.off[i] + t.len[i]]) for i in keep]
 
@@ -242,7 +257,7 @@ def test_config1_simple_firewall_end_to_end(tmp_path):
     pcap_module.c:41), classified by gpu_module_func in simple_firewall's state
     (num_msp 1, forward 1, num_queues 1, i40e map), consumed by RunMainLoop's rx
     loop (core.c:897-909) with the ForwardEthernetFrame consumer (eth_out.c:105-129)
-    -- the firewall forwards what its checks accept -- whose frames leave
+    -- the frames mOS forwards in that state (mosrx_mos_forwards) -- whose frames leave
     through the source's TX (pcap_inject's place, here a pcap dump).  NETSTAT,
     the reason census and the forwarded frames equal what the oracle says mOS
     does; nothing is dropped or reordered."""
@@ -264,7 +279,7 @@ def test_config1_simple_firewall_end_to_end(tmp_path):
     assert st.rx_bytes == int(t.len.astype(np.int64).sum()) + 24 * t.n     # + ETHER_OVR per frame
     assert st.rx_errors == int((ora["verdict"] < 0).sum())
     assert list(st.by_reason) == np.bincount(ora["reason"], minlength=NREASON).tolist()
-    keep = np.nonzero(ora["verdict"] == 1)[0]
+    keep = np.nonzero(mos_forwarded(ora))[0]
     assert fwd.forwarded == len(keep) and fwd.dropped == t.n - len(keep)
     assert ms.tx_packets == len(keep) and ms.kernel_launches == 3
     sent = mosrx.read_pcap(out)
@@ -317,7 +332,7 @@ def test_two_netdevs_forwarding_between_them(tmp_path):
     oa = O.classify(ta.frames, ta.off, ta.len, O.params())
     ob = O.classify(tb.frames, tb.off, tb.len, O.params())
     assert st.rx_packets == ta.n + tb.n
-    ka, kb = np.nonzero(oa["verdict"] == 1)[0], np.nonzero(ob["verdict"] == 1)[0]
+    ka, kb = np.nonzero(mos_forwarded(oa))[0], np.nonzero(mos_forwarded(ob))[0]
     assert fwd.forwarded == len(ka) + len(kb)
     assert mosrx.read_pcap(outb) == [bytes(ta.frames[ta.off[i]:ta.off[i] + ta.len[i]]) for i in ka]
     assert mosrx.read_pcap(outa) == [bytes(tb.frames[tb.off[i]:tb.off[i] + tb.len[i]]) for i in kb]
@@ -385,13 +400,16 @@ def _raw_ip(s):
 
 @pytest.mark.skipif(not os.path.exists(MOS_LOOP),
                     reason="needs oracle/_ref/mos_gpu_loop (make -C oracle ref, built where /root/reference is)")
-@pytest.mark.parametrize("fix,state,batch,period", [
-    ("edge", "msp1", 256, 0), ("edge", "esp1_local", 100, 0), ("edge", "noverify_local", 4096, 0),
-    ("rand_small", "q3_ixgbe", 128, 0), ("rand_mid", "msp1_local", 64, 0), ("rand_large", "q8_i40e", 50, 0),
-    ("imix_full", "msp1", 32768, 0), ("m1500_full", "q4_i40e", 65536, 0),
+@pytest.mark.parametrize("fix,state,batch,period,forward", [
+    ("edge", "msp1", 256, 0, 0), ("edge", "esp1_local", 100, 0, 0), ("edge", "noverify_local", 4096, 0, 0),
+    ("rand_small", "q3_ixgbe", 128, 0, 0), ("rand_mid", "msp1_local", 64, 0, 0), ("rand_large", "q8_i40e", 50, 0, 0),
+    ("imix_full", "msp1", 32768, 0, 0), ("m1500_full", "q4_i40e", 65536, 0, 0),
     # the stack state changes under the backend: num_msp toggles every `period` batches
-    ("edge", "msp1_local", 64, 1), ("rand_mid", "msp1", 50, 2), ("imix_full", "msp1", 8192, 3)])
-def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch, period):
+    ("edge", "msp1_local", 64, 1, 0), ("rand_mid", "msp1", 50, 2, 0), ("imix_full", "msp1", 8192, 3, 0),
+    # forward = 1 (simple_firewall): which frames mOS forwards, against mosrx_mos_forwards
+    ("edge", "msp1", 128, 0, 1), ("edge", "noverify_local", 128, 0, 1), ("rand_small", "msp1_local", 64, 0, 1),
+    ("rand_mid", "q4_i40e", 100, 2, 1), ("imix_full", "msp1", 32768, 0, 1)])
+def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch, period, forward):
     """gpu_module_func compiled inside mOS's tree (its own io_module.h /
     config.h) and registered as core.c:1725-1736 does, fed from a trace, with
     mOS's own RunMainLoop rx section + ProcessPacket run on every frame get_rptr
@@ -401,7 +419,12 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
     num_queues, and mOS's NETSTAT equals the GPU census.  With a period, mOS's
     num_msp changes every `period` batches (a monitor socket created / closed)
     and the backend follows it through the thread context with no call from
-    the core, re-classifying the batch it had in flight."""
+    the core, re-classifying the batch it had in flight.  With forward = 1
+    mOS's ForwardIPPacket / ForwardEthernetFrame are recorded instead of
+    transmitting, and the frames ProcessPacket forwards must be those
+    mosrx_mos_forwards() picks from the GPU records (the rx loop's forwarding
+    consumer); end-host states are left out there, since whether mOS forwards
+    a TCP segment then depends on its flow (listener, stream state)."""
     import json
     import subprocess
     from pktlib import write_ref_trace
@@ -417,7 +440,7 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
         z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
         frames, off, ln = z["frames"], z["off"], z["len"]
     path = str(tmp_path / "trace.in")
-    write_ref_trace(path, frames, off, ln, num_msp=msp, num_esp=esp, forward=0, num_queues=nq, queue_mode=qm,
+    write_ref_trace(path, frames, off, ln, num_msp=msp, num_esp=esp, forward=forward, num_queues=nq, queue_mode=qm,
                     local=[_raw_ip(a) for a in loc])
     r = subprocess.run([MOS_LOOP, path, str(batch)] + ([str(period)] if period else []), capture_output=True,
                        text=True, timeout=120)
@@ -430,3 +453,5 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
     assert d["batches"] == -(-len(off) // batch)
     if period:                                    # every change caught a batch in flight
         assert d["reclassified"] == (d["batches"] - 1) // period
+    assert d["forward_diff"] == 0
+    assert (d["forwarded_by_mos"] > 0) == bool(forward)

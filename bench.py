@@ -12,8 +12,10 @@ headline workload is BASELINE config #3 (1500 B MTU TCP segments, 1M flows,
 batch 64K, R = 8); the same run measures config #2 (64 B, 1 flow, batch 32K,
 R = 256) and config #4 (IMIX, batch 256K, R = 8), the single-batch launches
 of each (`*_1`: one kernel per batch, 2 batches in flight), the §8f rows, the
-CPU baselines (the oracle and mOS's own compiled functions on this host's
-cores, config #1 included) and the end-to-end / backend rates.
+CPU baselines (the oracle, mOS's own compiled per-frame functions and mOS's
+whole ProcessPacket on this host's cores, config #1 included), the box's
+streaming-read rate, and the end-to-end / backend rates (one rx loop per mTCP
+thread, 1-8 threads).
 
 Multi-GPU (torchrun, one process per GPU): the job is one sequence of batches
 split round-robin over the GPUs (mosrx.shard_plan), no

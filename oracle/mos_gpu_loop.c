@@ -31,8 +31,9 @@
  * mtcp_manager (mtcp.h:304-312), and a batch classified in flight under the old
  * state is classified again before it is handed out.
  *
- * Usage: mos_gpu_loop <trace.in> <batch> [period]   -- prints one JSON line,
- * exit 0 when every compared value is equal.
+ * Usage: mos_gpu_loop <trace.in> <batch> [period [group]]   -- prints one JSON
+ * line, exit 0 when every compared value is equal.  `group`: batches per launch
+ * (cfg.group, the rx ring serviced at once).
  */
 #include <arpa/inet.h>
 #include <execinfo.h>
@@ -118,8 +119,8 @@ int main(int argc, char **argv)
 	int64_t first_bad = -1;
 
 	signal(SIGSEGV, on_segv);
-	if (argc != 3 && argc != 4) {
-		fprintf(stderr, "usage: %s trace.in batch [period]\n", argv[0]);
+	if (argc < 3 || argc > 5) {
+		fprintf(stderr, "usage: %s trace.in batch [period [group]]\n", argv[0]);
 		return 2;
 	}
 	in = fopen(argv[1], "rb");
@@ -176,6 +177,8 @@ int main(int argc, char **argv)
 	cfg.num_ifs = 1;
 	cfg.src[0] = src;
 	cfg.batch = (uint32_t)atoi(argv[2]);
+	if (argc == 5)
+		cfg.group = (uint32_t)atoi(argv[4]);
 	cfg.params.num_msp = num_msp;
 	cfg.params.num_esp = num_esp;
 	cfg.params.num_queues = nq;
@@ -243,7 +246,7 @@ int main(int argc, char **argv)
 					first_bad = (int64_t)frames_seen;
 			}
 		}
-		if (argc == 4 && batches % (uint64_t)atoi(argv[3]) == 0)
+		if (argc >= 4 && atoi(argv[3]) > 0 && batches % (uint64_t)atoi(argv[3]) == 0)
 			m.num_msp = m.num_msp ? 0 : (num_msp ? num_msp : 1);   /* a monitor socket comes or goes */
 	}
 	g_stage = "destroy_handle";

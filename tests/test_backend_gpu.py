@@ -408,7 +408,9 @@ def _raw_ip(s):
     ("edge", "msp1_local", 64, 1, 0), ("rand_mid", "msp1", 50, 2, 0), ("imix_full", "msp1", 8192, 3, 0),
     # forward = 1 (simple_firewall): which frames mOS forwards, against mosrx_mos_forwards
     ("edge", "msp1", 128, 0, 1), ("edge", "noverify_local", 128, 0, 1), ("rand_small", "msp1_local", 64, 0, 1),
-    ("rand_mid", "q4_i40e", 100, 2, 1), ("imix_full", "msp1", 32768, 0, 1)])
+    ("rand_mid", "q4_i40e", 100, 2, 1), ("imix_full", "msp1", 32768, 0, 1),
+    # several batches per launch (cfg.group), the stack state changing between groups
+    ("rand_mid", "msp1", 32, (0, 8), 1), ("imix_full", "msp1_local", 4096, (16, 4), 0)])
 def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch, period, forward):
     """gpu_module_func compiled inside mOS's tree (its own io_module.h /
     config.h) and registered as core.c:1725-1736 does, fed from a trace, with
@@ -430,6 +432,7 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
     from pktlib import write_ref_trace
     from test_oracle_golden import GOLDEN, STATES
     msp, esp, nq, qm, loc = STATES[state]
+    period, group = period if isinstance(period, tuple) else (period, 1)
     if fix == "imix_full":
         t = mosrx.Trace(mosrx.TRACE_IMIX, 262_144)
         frames, off, ln = t.frames, t.off, t.len
@@ -442,7 +445,7 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
     path = str(tmp_path / "trace.in")
     write_ref_trace(path, frames, off, ln, num_msp=msp, num_esp=esp, forward=forward, num_queues=nq, queue_mode=qm,
                     local=[_raw_ip(a) for a in loc])
-    r = subprocess.run([MOS_LOOP, path, str(batch)] + ([str(period)] if period else []), capture_output=True,
+    r = subprocess.run([MOS_LOOP, path, str(batch), str(period), str(group)], capture_output=True,
                        text=True, timeout=120)
     assert r.stdout.strip(), r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
@@ -451,7 +454,8 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
     assert d["num_queues"] == nq and d["nstat_ok"] == 1
     assert d["compared"] + d["skipped"] == len(off) and d["compared"] > 0.5 * len(off)
     assert d["batches"] == -(-len(off) // batch)
-    if period:                                    # every change caught a batch in flight
-        assert d["reclassified"] == (d["batches"] - 1) // period
+    if period:                                    # every change caught a group in flight (changes fall on
+        assert period % group == 0                # group boundaries: a group is classified under one state)
+        assert d["reclassified"] == (d["batches"] - 1) // period * group
     assert d["forward_diff"] == 0
     assert (d["forwarded_by_mos"] > 0) == bool(forward)

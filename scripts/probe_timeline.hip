@@ -342,6 +342,22 @@ int main(int argc, char **argv)
 	plain<3, 4, 8>("S13 U4 W8 (library)", kps, ntiles, bytes);
 	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
 	plain<3, 4, 8, 0, 64, 0>("S13 tails cached (auto)", kps, ntiles, bytes);
+	if (argc > 4 && atoi(argv[4]) == 6) {
+		// header wave priority (DBG 32: s_setprio 2 on the header wave), interleaved medians
+		const char *names[] = {"S13 cached (library)", "S13 cached, header prio 2", "S13 nt (library)",
+		                       "S13 nt, header prio 2"};
+		std::vector<double> ts[4];
+		for (int r = 0; r < 9; r++) {
+			ts[0].push_back(time_tl<3, 4, 8, 0, 64, 0>(kps, ntiles));
+			ts[1].push_back(time_tl<3, 4, 8, 32, 64, 0>(kps, ntiles));
+			ts[2].push_back(time_tl<3, 4, 8, 0, 64, 2>(kps, ntiles));
+			ts[3].push_back(time_tl<3, 4, 8, 32, 64, 2>(kps, ntiles));
+		}
+		for (int v = 0; v < 4; v++)
+			printf("%-28s median %7.2f us  min %7.2f us  (%5.0f GB/s at the median)\n", names[v], pct(ts[v], 0.5) * 1e3,
+			       pct(ts[v], 0.0) * 1e3, bytes / (pct(ts[v], 0.5) * 1e-3) / 1e9);
+		return 0;
+	}
 	if (argc > 4 && atoi(argv[4]) == 5) {
 		// streamer count x loads in flight: fewer streamers per tile = more tiles resident
 		// (S1: 2-wave tiles, 16 per CU), interleaved rounds, median per variant

@@ -539,15 +539,14 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 		return (int32_t)is->g[is->cur].st[is->cur_idx].n;
 	}
 	/* the exposed group is done with (get_rptr pointers expire here) */
+	k = is->cur < 0 ? 0 : is->cur ^ 1;
 	if (is->cur >= 0)
 		group_recycle(&is->g[is->cur], is->src);
+	is->cur = -1;                     /* nothing exposed until a group is ready */
 	if (is->inflight < 0) {           /* nothing in flight: receive + classify now */
-		k = is->cur < 0 ? 0 : is->cur ^ 1;
 		group_fill(&is->g[k], is->src);
-		if (!is->g[k].nst) {
-			is->cur = -1;
+		if (!is->g[k].nst)
 			return 0;
-		}
 		if (group_submit(pv, is, k)) {
 			group_drop(pv, is, k);
 			return -1;

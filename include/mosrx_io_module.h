@@ -228,20 +228,26 @@ typedef struct mosrx_forwarder {
 	int32_t out_if[MOSRX_MAX_DEVICES];
 	uint64_t forwarded, dropped;
 	int32_t forward;             /* mos.conf `forward` (pctx->forward) */
-	uint32_t num_msp, num_esp;   /* the stack state the records were made under */
+	uint32_t num_msp;            /* monitor sockets of the stack the records were made under */
+	uint32_t listener;           /* 1 when an end-host socket listens (mtcp->listener, mtcp_listen) */
 } mosrx_forwarder;
-/* 1 when mOS forwards a frame with this record, 0 when it consumes or drops it:
+/* 1 when mOS forwards a frame with this record, 0 when it consumes or drops it,
+ * for a frame of a flow the stack holds no stream for (the standalone rx loop
+ * keeps no flow table; pinned to ProcessPacket with the forwarding calls
+ * recorded, tests/golden/forward.npz):
  *   NON_IPV4, ARP            forward && num_msp: ForwardEthernetFrame, eth_in.c:60-77 (ARP
  *                            is processed locally only when forwarding is off)
  *   NOVERIFY_PASS            forward: ForwardIPPacket before the transport layer, ip_in.c:66-70
  *   NOT_TCP (not to me)      forward && num_msp: ip_in.c:86-91
  *   TCP_BADCSUM              forward && num_msp: tcp.c:438-442 (the verdict stays -1)
- *   TCP_OK / TCP_LEN_OK      forward && num_msp && !num_esp: the stream engine of a
- *                            monitor-only stack forwards every segment (HandleMonitorStream,
- *                            tcp.c:386-390; the orphan path, :509-511); with end-host
- *                            sockets the flow decides (out of scope), not forwarded here
+ *   TCP_OK / TCP_LEN_OK      forward && num_msp && !listener: no stream is found, so
+ *                            CreateStream makes a monitor stream (SYN, HandleMonitorStream
+ *                            forwards, tcp.c:386-390) or none (the orphan path forwards,
+ *                            :507-510); with a listener the orphan gets a RST instead
+ *                            (:497-506); with no monitor socket the segment is consumed
+ *                            (:453-457).  Frames of end-host streams are the flow engine's.
  *   ICMP_LOCAL               consumed locally; the rest are dropped. */
-int  mosrx_mos_forwards(const mosrx_result *res, int forward, uint32_t num_msp, uint32_t num_esp);
+int  mosrx_mos_forwards(const mosrx_result *res, int forward, uint32_t num_msp, uint32_t listener);
 void mosrx_forward_frame(void *arg, int ifidx, int index, const uint8_t *pkt, uint16_t len,
                          const mosrx_result *res);
 

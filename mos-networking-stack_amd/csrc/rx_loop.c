@@ -98,7 +98,7 @@ int mosrx_rx_loop(const io_module_func *iom, struct mtcp_thread_context *ctx, in
 	return mosrx_rx_loop_ex(iom, ctx, nif, &o, fn, arg, st);
 }
 
-int mosrx_mos_forwards(const mosrx_result *res, int forward, uint32_t num_msp, uint32_t num_esp)
+int mosrx_mos_forwards(const mosrx_result *res, int forward, uint32_t num_msp, uint32_t listener)
 {
 	if (!res || !forward)
 		return 0;
@@ -112,7 +112,7 @@ int mosrx_mos_forwards(const mosrx_result *res, int forward, uint32_t num_msp, u
 		return 1;
 	case MOSRX_R_TCP_OK:
 	case MOSRX_R_TCP_LEN_OK:
-		return num_msp != 0 && num_esp == 0;
+		return num_msp != 0 && !listener;     /* tcp.c:453-510, no stream for the flow */
 	default:
 		return 0;
 	}
@@ -128,7 +128,7 @@ void mosrx_forward_frame(void *arg, int ifidx, int index, const uint8_t *pkt, ui
 	int out;
 	uint8_t *buf;
 	(void)index;
-	if (!f || !mosrx_mos_forwards(res, f->forward, f->num_msp, f->num_esp) || ifidx < 0 ||
+	if (!f || !mosrx_mos_forwards(res, f->forward, f->num_msp, f->listener) || ifidx < 0 ||
 	    ifidx >= MOSRX_MAX_DEVICES || (out = f->out_if[ifidx]) < 0 ||
 	    !f->iom->get_wptr || !(buf = f->iom->get_wptr(f->ctx, out, len))) {
 		if (f)

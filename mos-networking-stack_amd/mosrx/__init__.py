@@ -127,7 +127,7 @@ class AfpInfo(C.Structure):
 class Forwarder(C.Structure):
     _fields_ = [("iom", C.c_void_p), ("ctx", C.c_void_p), ("out_if", C.c_int32 * 16),
                 ("forwarded", C.c_uint64), ("dropped", C.c_uint64),
-                ("forward", C.c_int32), ("num_msp", C.c_uint32), ("num_esp", C.c_uint32)]
+                ("forward", C.c_int32), ("num_msp", C.c_uint32), ("listener", C.c_uint32)]
 
 
 class MosrxError(OSError):
@@ -849,15 +849,16 @@ class GpuBackend:
         _chk(lib().mosrx_gpu_module_stats_of(self.ctx, C.byref(st)), "mosrx_gpu_module_stats_of")
         return st
 
-    def forwarder(self, out_if: list[int]) -> Forwarder:
+    def forwarder(self, out_if: list[int], listener: bool = False) -> Forwarder:
         """A mosrx_forwarder for run_loop(forward=...): netdev i -> out_if[i], the
-        frames mOS forwards under the backend's stack state (mosrx_mos_forwards)."""
+        frames mOS forwards under the backend's stack state (mosrx_mos_forwards);
+        `listener`: an end-host socket listens (its orphans get a RST, not forwarded)."""
         f = Forwarder()
         f.iom = C.addressof(self.m)
         f.ctx = self.ctx
         for i in range(16):
             f.out_if[i] = out_if[i] if i < len(out_if) else -1
-        f.forward, f.num_msp, f.num_esp = self.params.forward, self.params.num_msp, self.params.num_esp
+        f.forward, f.num_msp, f.listener = self.params.forward, self.params.num_msp, int(listener)
         return f
 
     def rss_of(self, ifidx: int, pktidx: int) -> int | None:

@@ -240,7 +240,7 @@ int main(int argc, char **argv)
 					first_bad = (int64_t)frames_seen;
 			}
 			fwd_mos += g_fwd > 0;
-			if ((g_fwd > 0) != (mosrx_mos_forwards(&res[k], forward, m.num_msp, m.num_esp) != 0)) {
+			if ((g_fwd > 0) != (mosrx_mos_forwards(&res[k], forward, m.num_msp, m.listener != NULL) != 0)) {
 				fwd_diff++;
 				if (first_bad < 0)
 					first_bad = (int64_t)frames_seen;

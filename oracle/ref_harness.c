@@ -13,7 +13,7 @@
  *              u32 num_msp | u32 num_esp | i32 forward | i32 num_queues | i32 queue_mode |
  *              [ver 2: u32 nlocal | u32 local_ip[16] (netdev ip_addr, network order)] |
  *              u32 off[n] | u16 len[n] | u8 frames[frames_bytes]
- *   results  : n x { i8 verdict, u8 have, u16 ip_csum, u16 tcp_csum, u16 pad, u32 rss, i32 queue,
+ *   results  : n x { i8 verdict, u8 have, u16 ip_csum, u16 tcp_csum, u16 fwd, u32 rss, i32 queue,
  *                    u32 fbucket,
  *                    u16 payloadlen, u16 payload_off, u32 seq, u32 ack_seq, u16 window,
  *                    u8 tcp_flags, u8 ihl_doff, u16 ip_len, u16 pad }
@@ -32,8 +32,16 @@
  * route table is empty, so an echo request's reply finds no output interface
  * (ip_out.c:12-37) and nothing is sent.
  *
- * forward must be 0: ForwardIPPacket/ForwardEthernetFrame need route/ARP
- * tables and TX buffers.
+ * forward (mos.conf `forward`, 0 or 1): mOS's forwarding calls need route /
+ * ARP tables and TX buffers, so ForwardIPPacket and
+ * ForwardEthernetFrame are wrapped (-Wl,--wrap) to record the call instead:
+ * `fwd` is 1 when ProcessPacket forwarded the frame (eth_in.c:60-77,
+ * ip_in.c:66-70 / :86-91, tcp.c:438-442, the stream engine's forward of a
+ * monitor-only stack), which is what mosrx_mos_forwards must decide.
+ * MOSREF_LISTENER=<port> in the environment gives the manager an end-host
+ * listening socket on that port (INADDR_ANY, mtcp_listen's state that
+ * ProcessInTCPPacket reads: tcp.c:453, :497-506; DetectStreamType :54-75);
+ * with a port no frame targets, frames of unknown flows take the orphan path.
  *
  * Usage: mosref --time-pp <trace.in> <seconds>
  *   mOS's whole ProcessPacket (eth_in.c:27-87) on every frame, under the trace
@@ -67,6 +75,7 @@
 #include "logger.h"
 #include "mtcp_util.h"
 #include "tcp.h"
+#include "socket.h"
 
 int ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index,
                   uint32_t cur_ts, unsigned char *pkt_data, int len);
@@ -77,10 +86,14 @@ void FillInPacketIPContext(struct pkt_ctx *pctx, struct iphdr *iph, int ip_len);
 static int g_qmode = 1;
 int __wrap_FetchEndianType(void) { return g_qmode; }
 
+static int g_fwd;
+void __wrap_ForwardIPPacket(mtcp_manager_t mtcp, struct pkt_ctx *pctx) { (void)mtcp; (void)pctx; g_fwd++; }
+void __wrap_ForwardEthernetFrame(struct mtcp_manager *mtcp, struct pkt_ctx *pctx) { (void)mtcp; (void)pctx; g_fwd++; }
+
 struct rec {
 	int8_t verdict;
 	uint8_t have;
-	uint16_t ip_csum, tcp_csum, pad;
+	uint16_t ip_csum, tcp_csum, fwd;    /* fwd: ProcessPacket called a Forward* function */
 	uint32_t rss;
 	int32_t queue;
 	uint32_t fbucket;   /* HashFlow() of FindStream's reversed tuple (tcp.c:185-190, fhash.c:72-92) */
@@ -195,8 +208,8 @@ int main(int argc, char **argv)
 		fprintf(stderr, "bad trace header\n");
 		return 1;
 	}
-	if (forward != 0 || nq < 1) {
-		fprintf(stderr, "forward must be 0 and num_queues >= 1\n");
+	if ((forward != 0 && forward != 1) || nq < 1) {
+		fprintf(stderr, "forward must be 0 or 1 and num_queues >= 1\n");
 		return 1;
 	}
 	off = malloc((size_t)n * 4 + 1);
@@ -224,6 +237,7 @@ int main(int argc, char **argv)
 	mc.route_table = &rt;
 	g_config.mos = &mc;
 	tctx.cpu = 0;
+	tctx.mtcp_manager = &m;
 	TAILQ_INIT(&m.monitors);
 	m.num_msp = num_msp;
 	m.num_esp = num_esp;
@@ -233,6 +247,16 @@ int main(int argc, char **argv)
 	InitLogThreadContext(&lg, 0);
 	m.logger = &lg;
 	m.log_fp = fopen("/dev/null", "w");
+	if (getenv("MOSREF_LISTENER")) {
+		static struct tcp_listener lst;
+		static struct socket_map lsock;
+		lsock.socktype = MOS_SOCK_STREAM_LISTEN;
+		lsock.saddr.sin_family = AF_INET;
+		lsock.saddr.sin_addr.s_addr = INADDR_ANY;
+		lsock.saddr.sin_port = htons((uint16_t)atoi(getenv("MOSREF_LISTENER")));
+		lst.socket = &lsock;
+		m.listener = &lst;
+	}
 
 	if (timing_pp) {   /* every frame through ProcessPacket, as the rx loop calls it (core.c:906) */
 		uint64_t passes = 0, bytes = 0;
@@ -314,8 +338,11 @@ int main(int argc, char **argv)
 				}
 			}
 		}
-		if (!(r.have & 8))
+		if (!(r.have & 8)) {
+			g_fwd = 0;
 			r.verdict = (int8_t)ProcessPacket(&m, 0, (int)i, 0, f, (int)cap);
+			r.fwd = g_fwd > 0;
+		}
 		fwrite(&r, sizeof(r), 1, out);
 	}
 	fwrite(&m.nstat.rx_packets[0], 8, 1, out);

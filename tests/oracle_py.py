@@ -164,15 +164,23 @@ def have_ref() -> bool:
     return os.path.exists(REF_BIN)
 
 
-def run_ref(buf, off, ln, *, num_msp=1, num_esp=0, num_queues=1, queue_mode=1, local=()):
-    """Run mOS's own compiled rx path (forward=0) over the frames.  `local`: the
-    netdev addresses (dotted quads) ICMP frames count as "to me" for."""
+def run_ref(buf, off, ln, *, num_msp=1, num_esp=0, num_queues=1, queue_mode=1, local=(), forward=0,
+            listen_port=None):
+    """Run mOS's own compiled rx path over the frames.  `local`: the netdev
+    addresses (dotted quads) ICMP frames count as "to me" for; `forward`: mos.conf
+    `forward` (the record's `fwd` is 1 where ProcessPacket called ForwardIPPacket /
+    ForwardEthernetFrame, recorded by the harness instead of sent); `listen_port`:
+    an end-host socket listening on that port (INADDR_ANY)."""
+    env = dict(os.environ)
+    env.pop("MOSREF_LISTENER", None)
+    if listen_port is not None:
+        env["MOSREF_LISTENER"] = str(listen_port)
     with tempfile.TemporaryDirectory() as d:
         tin, tout = os.path.join(d, "t.in"), os.path.join(d, "t.out")
-        write_ref_trace(tin, buf, off, ln, num_msp=num_msp, num_esp=num_esp, forward=0,
+        write_ref_trace(tin, buf, off, ln, num_msp=num_msp, num_esp=num_esp, forward=forward,
                         num_queues=num_queues, queue_mode=queue_mode,
                         local=[ip_raw(a) if isinstance(a, str) else a for a in local])
-        subprocess.run([REF_BIN, tin, tout], check=True, stdout=subprocess.DEVNULL)
+        subprocess.run([REF_BIN, tin, tout], check=True, stdout=subprocess.DEVNULL, env=env)
         return read_ref_results(tout, len(off))
 
 

@@ -125,7 +125,7 @@ def write_ref_trace(path, buf, off, ln, *, num_msp=1, num_esp=0, forward=0, num_
 
 
 REF_DTYPE = np.dtype([("verdict", "i1"), ("have", "u1"), ("ip_csum", "<u2"), ("tcp_csum", "<u2"),
-                      ("pad", "<u2"), ("rss", "<u4"), ("queue", "<i4"), ("fbucket", "<u4"),
+                      ("fwd", "<u2"), ("rss", "<u4"), ("queue", "<i4"), ("fbucket", "<u4"),
                       ("payloadlen", "<u2"), ("payload_off", "<u2"), ("seq", "<u4"), ("ack_seq", "<u4"),
                       ("window", "<u2"), ("tcp_flags", "u1"), ("ihl_doff", "u1"), ("ip_len", "<u2"),
                       ("pad2", "<u2")])

@@ -26,19 +26,20 @@ def write_pcap(path, frames, off, ln):
             fh.write(struct.pack("<IIII", i, 0, n, n) + bytes(frames[o:o + n]))
 
 
-# the frames mOS forwards for a record under (forward, num_msp, num_esp): eth_in.c:60-77
+# the frames mOS forwards for a record under (forward, num_msp, listener): eth_in.c:60-77
 # (every non-IPv4 frame, ARP too), ip_in.c:66-70 (no monitor / stream socket),
-# ip_in.c:86-91 (other protocols), tcp.c:438-442 (bad TCP checksum), and the stream
-# engine of a monitor-only stack for accepted segments (tcp.c:386-390, :509-511);
-# pinned to mOS itself by test_backend_inside_mos_checked_by_processpacket
-def mos_forwarded(rec, forward=1, num_msp=1, num_esp=0):
+# ip_in.c:86-91 (other protocols), tcp.c:438-442 (bad TCP checksum), and, for accepted
+# segments of flows without a stream, the monitor stream / orphan path unless an
+# end-host socket listens (tcp.c:453-510); pinned to mOS itself by
+# test_backend_inside_mos_checked_by_processpacket and tests/golden/forward.npz
+def mos_forwarded(rec, forward=1, num_msp=1, listener=0):
     r = rec["reason"]
     R = mosrx.R
     if not forward:
         return np.zeros(len(rec), bool)
     msp_only = (r == R["NON_IPV4"]) | (r == R["ARP"]) | (r == R["NOT_TCP"]) | (r == R["TCP_BADCSUM"])
     ok = (r == R["TCP_OK"]) | (r == R["TCP_LEN_OK"])
-    return (msp_only & (num_msp != 0)) | (r == R["NOVERIFY_PASS"]) | (ok & (num_msp != 0) & (num_esp == 0))
+    return (msp_only & (num_msp != 0)) | (r == R["NOVERIFY_PASS"]) | (ok & (num_msp != 0) & (not listener))
 
 
 def drain(be, n_expect=None):

@@ -126,8 +126,8 @@ def test_ip_fast_csum_quirk():
 
 
 def test_forward_nonip_verdicts():
-    # eth_in.c:62-77: forward && num_msp makes every non-IPv4 frame 1 (read from the code:
-    # the reference harness cannot run ForwardEthernetFrame without TX tables).
+    # eth_in.c:62-77: forward && num_msp makes every non-IPv4 frame 1 (with mOS's own
+    # ProcessPacket on the fixtures under forward = 1: tests/test_forwarding.py)
     frames = [tcp_frame(ethertype=0x86DD, pad_to=60), tcp_frame(ethertype=0x0806, pad_to=60)]
     buf, off, ln = pack_frames(frames)
     a = O.classify(buf, off, ln, O.params(num_msp=1, forward=1))

@@ -96,6 +96,28 @@ def test_golden_fixtures(gpu_ctx, fix, state):
         np.testing.assert_array_equal(dti, oti)
 
 
+@pytest.mark.parametrize("fix", FIXTURES)
+@pytest.mark.parametrize("state", ["msp1", "noverify", "msp1_esp1_listen", "msp1_local"])
+def test_golden_forward_on(gpu_ctx, fix, state):
+    """mos.conf `forward = 1`: the GPU verdicts against mOS's own ProcessPacket
+    with forwarding on (tests/golden/forward.npz), and the frames the rx loop's
+    forwarding rule picks from the GPU records against the frames mOS forwarded."""
+    from test_forwarding import FSTATES, FWD, check
+    z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
+    msp, esp, loc, listen = FSTATES[state]
+    p = mosrx.default_params(num_msp=msp, num_esp=esp, forward=1, local=loc)
+    k = f"{fix}__{state}__"
+    for v in (mosrx.shape_variant(mosrx.KIND_SMALL), mosrx.shape_variant(mosrx.KIND_S13)):
+        gpu_ctx.set_variant(v)
+        try:
+            out = run_both(gpu_ctx, z["frames"], z["off"], z["len"], p)
+            gpu = gpu_ctx.classify_host(z["frames"], z["off"], z["len"])
+        finally:
+            gpu_ctx.set_variant(2)
+        assert_records_equal(gpu, out, f"{fix} variant {v}")
+        check(gpu, FWD[k + "verdict"], FWD[k + "fwd"], FWD[k + "have"], msp, listen)
+
+
 @pytest.mark.parametrize("kind,n", [(mosrx.TRACE_FW64, 10_000), (mosrx.TRACE_S64, 32_768),
                                     (mosrx.TRACE_M1500, 65_536), (mosrx.TRACE_IMIX, 262_144)])
 def test_baseline_configs_full_size(gpu_ctx, kind, n):

@@ -28,9 +28,10 @@
  *
  * Threading follows mOS: one context per mTCP thread, every call for a context
  * from that thread (core.c:1282-1349), so the module takes no locks on the fast
- * path.  Per-thread state is found by context pointer; the module never reads
- * `struct mtcp_thread_context` fields, so it builds against mOS's mtcp.h or
- * standalone.
+ * path.  Per-thread state is found by context pointer.  Inside an mOS build
+ * the module reads one field of `struct mtcp_thread_context`, `mtcp_manager`
+ * (the stack state it follows, mos_state); standalone it never dereferences the
+ * context, so it builds against mOS's mtcp.h or without it.
  */
 #include <errno.h>
 #include <pthread.h>

@@ -41,7 +41,8 @@ class FakeBackend:
         if n > 0:
             rng = np.random.default_rng(len(self.script) * 7 + ifidx)
             lens = rng.integers(60, 1515, n).astype(np.uint16)
-            bufs = [C.create_string_buffer(int(x)) for x in lens]
+            bufs = [C.create_string_buffer(rng.integers(0, 256, int(x), dtype=np.uint8).tobytes(), int(x))
+                    for x in lens]
             rec = np.zeros(n, mosrx.RESULT_DTYPE)
             rec["verdict"] = rng.choice([-1, 0, 1], n)
             rec["reason"] = rng.integers(0, mosrx.NREASON, n)
@@ -132,3 +133,63 @@ def test_backend_without_results_is_refused():
     fb._set("dev_ioctl", mosrx._IOCTLFN(lambda ctx, i, cmd, argp: -1))
     rc, _ = run(fb)
     assert rc == -95                              # -ENOTSUP: not a classifying backend
+
+
+def test_forwarder_consumer_sends_what_mos_forwards():
+    """mosrx_forward_frame as the rx loop's consumer (ForwardEthernetFrame,
+    eth_out.c:105-129): frames the rule picks (mosrx_mos_forwards) are copied into
+    get_wptr buffers of out_if[in_if] and leave with the round's send_pkts; netdev 1
+    maps to -1 (no output netdev): its forwardable frames count as dropped."""
+    fb = FakeBackend([6, 5, 9, 4, 0, 0], nif=2)
+    recs, tx, sent_rounds = [], [], []
+    orig = fb.recv
+
+    def recv(ctx, ifidx):
+        n = orig(ctx, ifidx)
+        if n > 0:
+            recs.append((ifidx, [bytes(C.string_at(C.addressof(b), len(b))) for b in fb.cur[ifidx][0]],
+                         fb.cur[ifidx][2].copy()))
+        return n
+
+    bufs = []
+
+    def wptr(ctx, ifidx, ln):
+        b = C.create_string_buffer(ln)
+        bufs.append(b)
+        tx.append((ifidx, b))
+        return C.addressof(b)
+
+    def send(ctx, ifidx):
+        sent_rounds.append((ifidx, len(tx)))
+        return 0
+
+    fb._set("recv_pkts", mosrx._RECVFN(recv))
+    fb._set("get_wptr", mosrx._WPTRFN(wptr))
+    fb._set("send_pkts", mosrx._SENDFN(send))
+    fw = mosrx.Forwarder()
+    fw.iom, fw.ctx = C.addressof(fb.m), None
+    for i in range(16):
+        fw.out_if[i] = -1
+    fw.out_if[0] = 1
+    fw.forward, fw.num_msp, fw.listener = 1, 1, 0
+    st = mosrx.RxStats()
+    o = mosrx.RxLoopOpts(0, 1, 0, 0)
+    rc = mosrx.lib().mosrx_rx_loop_ex(C.addressof(fb.m), None, 2, C.byref(o),
+                                      C.cast(mosrx.lib().mosrx_forward_frame, C.c_void_p), C.byref(fw), C.byref(st))
+    assert rc == 0
+    rule = mosrx.lib().mosrx_mos_forwards
+    exp, drop = [], 0
+    for ifidx, frames, rec in recs:
+        for i, f in enumerate(frames):
+            r = np.ascontiguousarray(rec[i:i + 1])
+            if rule(C.c_void_p(r.ctypes.data), 1, 1, 0):
+                if ifidx == 0:
+                    exp.append(f)
+                else:
+                    drop += 1
+            else:
+                drop += 1
+    assert fw.forwarded == len(exp) == len(tx) and fw.dropped == drop
+    assert all(ifx == 1 for ifx, _ in tx)                      # out_if[0] = 1
+    assert [b.raw for _, b in tx] == exp                       # copied byte for byte, in order
+    assert len(sent_rounds) == 2 * st.rounds                   # send_pkts per netdev per round

@@ -49,6 +49,7 @@
 #include "fhash.h"
 #include "logger.h"
 #include "mtcp_util.h"
+#include "socket.h"
 #include "mosrx_io_module.h"
 
 int ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index,
@@ -168,6 +169,16 @@ int main(int argc, char **argv)
 	InitLogThreadContext(&lg, 0);
 	m.logger = &lg;
 	m.log_fp = fopen("/dev/null", "w");
+	if (getenv("MOSREF_LISTENER")) {   /* an end-host socket listening on that port (as ref_harness.c) */
+		static struct tcp_listener lst;
+		static struct socket_map lsock;
+		lsock.socktype = MOS_SOCK_STREAM_LISTEN;
+		lsock.saddr.sin_family = AF_INET;
+		lsock.saddr.sin_addr.s_addr = INADDR_ANY;
+		lsock.saddr.sin_port = htons((uint16_t)atoi(getenv("MOSREF_LISTENER")));
+		lst.socket = &lsock;
+		m.listener = &lst;
+	}
 
 	/* the backend, registered and loaded as core.c:1725-1736 does */
 	src = mosrx_source_mem(frames, off, len, n, 1);

@@ -426,13 +426,43 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
     mOS's ForwardIPPacket / ForwardEthernetFrame are recorded instead of
     transmitting, and the frames ProcessPacket forwards must be those
     mosrx_mos_forwards() picks from the GPU records (the rx loop's forwarding
-    consumer); end-host states are left out there, since whether mOS forwards
-    a TCP segment then depends on its flow (listener, stream state)."""
+    consumer)."""
+    _inside_mos(tmp_path, fix, state, batch, period, forward)
+
+
+@pytest.mark.skipif(not os.path.exists(MOS_LOOP),
+                    reason="needs oracle/_ref/mos_gpu_loop (make -C oracle ref, built where /root/reference is)")
+@pytest.mark.parametrize("fix,msp,esp,listen", [
+    ("rand_mid", 1, 1, False), ("rand_mid", 1, 1, True), ("rand_small", 0, 1, True),
+    ("imix_full", 1, 2, False), ("imix_full", 1, 2, True)])
+def test_backend_inside_mos_forwarding_with_end_host_sockets(tmp_path, fix, msp, esp, listen):
+    """forward = 1 with end-host sockets: a client socket leaves the forwarding of
+    segments without a stream as it is (CreateStream's monitor stream / the orphan
+    path, tcp.c:453-510); an end-host socket listening (mtcp->listener, on a port
+    the trace does not use) turns the orphans into RSTs, not forwarded.  The GPU
+    records + mosrx_mos_forwards(listener) against mOS's own ProcessPacket."""
+    _inside_mos(tmp_path, fix, (msp, esp, 1, 1, ()), 256, 0, 1, listen=listen)
+
+
+def _unused_tcp_port(frames, off, ln):
+    """A port no TCP frame of the trace is sent to (the listener's SYNs would start end-host streams)."""
+    frames, off, ln = np.asarray(frames), np.asarray(off, np.int64), np.asarray(ln, np.int64)
+    ok = ln >= 38
+    o = off[ok]
+    tcp = (frames[o + 12] == 8) & (frames[o + 13] == 0) & (frames[o + 23] == 6)
+    o = o[tcp]
+    p = o + 14 + (frames[o + 14] & 0xF).astype(np.int64) * 4 + 2
+    p = p[p + 2 <= len(frames)]
+    used = set(((frames[p].astype(np.int64) << 8) | frames[p + 1]).tolist())
+    return next(x for x in range(1, 65536) if x not in used)
+
+
+def _inside_mos(tmp_path, fix, state, batch, period, forward, listen=False):
     import json
     import subprocess
     from pktlib import write_ref_trace
     from test_oracle_golden import GOLDEN, STATES
-    msp, esp, nq, qm, loc = STATES[state]
+    msp, esp, nq, qm, loc = STATES[state] if isinstance(state, str) else state
     period, group = period if isinstance(period, tuple) else (period, 1)
     if fix == "imix_full":
         t = mosrx.Trace(mosrx.TRACE_IMIX, 262_144)
@@ -446,8 +476,12 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
     path = str(tmp_path / "trace.in")
     write_ref_trace(path, frames, off, ln, num_msp=msp, num_esp=esp, forward=forward, num_queues=nq, queue_mode=qm,
                     local=[_raw_ip(a) for a in loc])
+    env = dict(os.environ)
+    env.pop("MOSREF_LISTENER", None)
+    if listen:
+        env["MOSREF_LISTENER"] = str(_unused_tcp_port(frames, off, ln))
     r = subprocess.run([MOS_LOOP, path, str(batch), str(period), str(group)], capture_output=True,
-                       text=True, timeout=120)
+                       text=True, timeout=120, env=env)
     assert r.stdout.strip(), r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert r.returncode == 0, (d, r.stderr[-2000:])
@@ -459,4 +493,5 @@ def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch
         assert period % group == 0                # group boundaries: a group is classified under one state)
         assert d["reclassified"] == (d["batches"] - 1) // period * group
     assert d["forward_diff"] == 0
-    assert (d["forwarded_by_mos"] > 0) == bool(forward)
+    # with forwarding on, mOS forwards something unless only end-host sockets exist (msp 0, esp > 0)
+    assert (d["forwarded_by_mos"] > 0) == bool(forward and (msp or not esp))

@@ -367,7 +367,7 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, all_cores: bool 
     return out
 
 
-def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: bool = False):
+def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: bool = False, forward: int = 0):
     """mOS's own compiled functions on one host core, when the reference build
     travelled with the tree; else None.  A reported baseline, never the
     measured path.  Default: `mosref --time` = ref_frame, i.e. the header
@@ -375,7 +375,9 @@ def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: boo
     GetRSSHash, GetRSSCPUCore per frame (the GPU record's scope).
     process_packet: `mosref --time-pp` = mOS's whole ProcessPacket per frame as
     the rx loop calls it (checks + checksums + FindStream on an empty flow
-    table; no RSS, which the NIC computes in mOS)."""
+    table; no RSS, which the NIC computes in mOS).  forward: mos.conf `forward`
+    under which ProcessPacket runs (1: its ForwardIPPacket / ForwardEthernetFrame
+    calls are recorded by the harness, not transmitted)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "mosref")
     if not os.access(exe, os.X_OK):
         return None
@@ -384,7 +386,7 @@ def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: boo
     import pktlib
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "trace.mrxt")
-        pktlib.write_ref_trace(path, tr.frames[:tr.frames_bytes], tr.off, tr.len)
+        pktlib.write_ref_trace(path, tr.frames[:tr.frames_bytes], tr.off, tr.len, forward=forward)
         try:
             out = subprocess.run([exe, "--time-pp" if process_packet else "--time", path, str(seconds)],
                                  capture_output=True, text=True, timeout=seconds + 60)
@@ -392,8 +394,9 @@ def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: boo
         except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
             return None
     el = r["seconds"]
-    what = ("ProcessPacket per frame (oracle/_ref/mosref --time-pp; checks + checksums + FindStream, "
-            "no RSS)" if process_packet else
+    what = (f"ProcessPacket per frame (oracle/_ref/mosref --time-pp; checks + checksums + FindStream, "
+            f"no RSS; forward={forward}" + (": the Forward* calls recorded, not transmitted)" if forward else ")")
+            if process_packet else
             "ip_fast_csum + TCPCalcChecksum + GetRSSHash + GetRSSCPUCore + header checks "
             "(oracle/_ref/mosref --time: ref_frame, not ProcessPacket)")
     return {"value": round(algo_bytes(tr, key) * r["passes"] / el / 1e9, 3), "unit": "GB/s", "cores": 1,
@@ -441,10 +444,10 @@ def measure_fw64(ctx, seconds: float):
     port = cpu_baseline(tr, "FW64", min_s=seconds, all_cores=False)
     if ref:
         port["reference"] = ref
-    # mOS's ProcessPacket itself (the harness runs forward = 0: ForwardIPPacket
-    # needs route / ARP tables; for this trace of valid TCP frames of one flow
-    # only the non-IPv4 verdict depends on it)
-    ref = cpu_reference(tr, "FW64", seconds, process_packet=True)
+    # mOS's ProcessPacket itself in the firewall's state, forward = 1: every
+    # segment of the flow takes the orphan path to ForwardIPPacket (tcp.c:507-510),
+    # which the harness records instead of transmitting (no route / ARP tables)
+    ref = cpu_reference(tr, "FW64", seconds, process_packet=True, forward=1)
     if ref:
         port["reference_processpacket"] = ref
     out["cpu_baseline"] = port

@@ -89,3 +89,5 @@ def test_forwarding_fuzz_vs_reference(seed):
                            listen_port=port if listen else None)
         ora = O.classify(buf, off, ln, O.params(num_msp=msp, num_esp=esp, forward=1))
         check(ora, rec["verdict"], rec["fwd"].astype(np.uint8), rec["have"], msp, listen)
+    rec, _ = O.run_ref(buf, off, ln, num_msp=1, forward=0)      # forwarding off: mOS forwards nothing
+    assert not rec["fwd"].any()

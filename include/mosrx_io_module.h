@@ -226,7 +226,9 @@ typedef struct mosrx_forwarder {
 	const io_module_func *iom;
 	struct mtcp_thread_context *ctx;
 	int32_t out_if[MOSRX_MAX_DEVICES];
-	uint64_t forwarded, dropped;
+	uint64_t forwarded;          /* frames copied into a TX buffer of the output netdev */
+	uint64_t dropped;            /* every other frame: not forwarded by the rule, or no output
+	                                netdev (out_if -1) / no TX buffer (get_wptr NULL) */
 	int32_t forward;             /* mos.conf `forward` (pctx->forward) */
 	uint32_t num_msp;            /* monitor sockets of the stack the records were made under */
 	uint32_t listener;           /* 1 when an end-host socket listens (mtcp->listener, mtcp_listen) */

@@ -6,8 +6,9 @@
  * (core/src/include/io_module.h:63-78); inside an mOS tree the maintainer
  * includes io_module.h instead (define MOSRX_HAVE_MOS_IO_MODULE) and registers
  * `gpu_module_func` exactly like pcap/dpdk/netmap (io_module.h:100-111,
- * core.c:1725-1733).  The backend never dereferences `struct
- * mtcp_thread_context`, so it compiles against either definition.
+ * core.c:1725-1733).  Standalone the backend never dereferences `struct
+ * mtcp_thread_context`, so it compiles against either definition; built
+ * inside mOS it reads the context's `cpu` and `mtcp_manager` (mtcp.h:304-312).
  *
  * Semantics kept from the reference:
  *   - recv_pkts returns the batch size (0 when idle, -1 on a bad ifidx,
@@ -161,8 +162,10 @@ int  mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg);
 /* The configuration in effect (after load_module_upper_half took mOS's own
  * state into it, when built inside mOS). */
 int  mosrx_gpu_module_get_cfg(mosrx_gpu_module_cfg *cfg);
-/* Bind a thread context pointer to a cpu index before init_handle (standalone use;
- * inside mOS the module reads nothing from ctx and uses the registration order). */
+/* Bind a thread context pointer to a cpu index before init_handle.  Unbound
+ * contexts get their cpu from ctx->cpu inside an mOS build (the mTCP core,
+ * mtcp.h:306, set by MTCPRunThread before init_handle, core.c:1302-1313) and
+ * from registration order standalone. */
 int  mosrx_gpu_module_bind(struct mtcp_thread_context *ctx, int cpu);
 /* Give mTCP thread `cpu` its own source for netdev `ifidx` (e.g. one
  * PACKET_FANOUT_HASH socket per thread), instead of cfg.src[ifidx]. */
@@ -177,7 +180,9 @@ typedef struct mosrx_gpu_module_stats {
 	double   kernel_ms;         /* their summed device time (HIP events around each kernel) */
 	uint64_t rx_drops;          /* frames received but never handed out: their group's launch failed */
 	uint64_t rx_reclassified;   /* batches classified again because mOS's stack state (num_msp /
-	                               num_esp) changed while they were in flight (mOS builds) */
+	                               num_esp) changed after they were classified (mOS builds) */
+	int32_t  cpu;               /* the mTCP core the context runs as (bind, or ctx->cpu in mOS builds) */
+	int32_t  device;            /* the GPU it drives: gpu_base + cpu % ngpu */
 } mosrx_gpu_module_stats;
 /* Time every kernel this thread's contexts launch (for the stats above). */
 int  mosrx_gpu_module_set_timing(struct mtcp_thread_context *ctx, int on);

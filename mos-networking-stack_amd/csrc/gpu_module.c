@@ -29,9 +29,11 @@
  * Threading follows mOS: one context per mTCP thread, every call for a context
  * from that thread (core.c:1282-1349), so the module takes no locks on the fast
  * path.  Per-thread state is found by context pointer.  Inside an mOS build
- * the module reads one field of `struct mtcp_thread_context`, `mtcp_manager`
- * (the stack state it follows, mos_state); standalone it never dereferences the
- * context, so it builds against mOS's mtcp.h or without it.
+ * the module reads two fields of `struct mtcp_thread_context`: `cpu` (the
+ * mTCP core, which picks the thread's GPU and per-thread source when the
+ * application did not bind the context) and `mtcp_manager` (the stack state it
+ * follows, mos_state); standalone it never dereferences the context, so it
+ * builds against mOS's mtcp.h or without it.
  */
 #include <errno.h>
 #include <pthread.h>
@@ -344,10 +346,23 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 	pthread_mutex_lock(&g_lock);
 	for (i = 0; i < MAX_THREADS; i++)     /* bound by mosrx_gpu_module_bind */
 		if (g_tab[i].ctx == ctx) { slot = i; cpu = g_tab[i].cpu; break; }
-	if (slot < 0)                          /* else registration order, as mOS starts its threads */
+	if (slot < 0) {
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+		/* the mTCP core the thread was created for: MTCPRunThread sets ctx->cpu
+		 * (core.c:1302) before it calls init_handle (core.c:1313), and the
+		 * threads call it concurrently, so registration order is not stable */
+		cpu = ctx ? ctx->cpu : -1;
+#else
+		cpu = g_next_cpu;                  /* standalone: registration order */
+#endif
 		for (i = 0; i < MAX_THREADS; i++)
-			if (!g_tab[i].ctx) { slot = i; g_tab[i].ctx = ctx; cpu = g_tab[i].cpu = g_next_cpu++; break; }
+			if (!g_tab[i].ctx) { slot = i; g_tab[i].ctx = ctx; g_tab[i].cpu = cpu; g_next_cpu++; break; }
+	}
 	pthread_mutex_unlock(&g_lock);
+	if (cpu < 0) {
+		fprintf(stderr, "[mosrx] gpu_module: context without a cpu\n");
+		exit(EXIT_FAILURE);
+	}
 	if (slot < 0) {
 		fprintf(stderr, "[mosrx] gpu_module: too many threads\n");
 		exit(EXIT_FAILURE);
@@ -358,6 +373,8 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 	pv->ctx = ctx;
 	pv->cpu = cpu;
 	ndev = mosrx_device_count();
+	pv->stats.cpu = cpu;
+	pv->stats.device = mosrx_gpu_module_device_of(cpu, ndev);
 	for (i = 0; i < (int)g_cfg.num_ifs; i++) {
 		struct if_state *is = &pv->ifs[i];
 		int dev = mosrx_gpu_module_device_of(cpu, ndev);

@@ -106,7 +106,7 @@ class ModuleStats(C.Structure):
     _fields_ = [("rx_batches", C.c_uint64), ("rx_frames", C.c_uint64), ("tx_packets", C.c_uint64),
                 ("tx_bytes", C.c_uint64), ("tx_errors", C.c_uint64), ("kernel_launches", C.c_uint64),
                 ("kernel_ms", C.c_double), ("rx_drops", C.c_uint64),
-                ("rx_reclassified", C.c_uint64)]
+                ("rx_reclassified", C.c_uint64), ("cpu", C.c_int32), ("device", C.c_int32)]
 
 
 class RxLoopOpts(C.Structure):

@@ -17,13 +17,80 @@
 
 #include "mosrx_io_module.h"
 #ifdef MOSRX_HAVE_MOS_IO_MODULE
+#include <pthread.h>
+#include <stdlib.h>
 #include "config.h"
+#include "mtcp.h"
+
+/* --map mode: the module's calls into libmosrx are wrapped (-Wl,--wrap) so
+ * init_handle runs without a GPU on a pretended device count; only the
+ * device choice is observed. */
+static int g_fake_ndev = 1;
+int __wrap_mosrx_device_count(void) { return g_fake_ndev; }
+int __wrap_mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
+{
+	(void)p;
+	if (device < 0 || device >= g_fake_ndev)
+		return -19;
+	*out = (mosrx_ctx *)calloc(1, 64);
+	return *out ? 0 : -12;
+}
+void __wrap_mosrx_close(mosrx_ctx *c) { free(c); }
+int __wrap_mosrx_host_alloc(mosrx_ctx *c, size_t bytes, void **p) { (void)c; *p = calloc(1, bytes); return *p ? 0 : -12; }
+int __wrap_mosrx_host_free(mosrx_ctx *c, void *p) { (void)c; free(p); return 0; }
+
+static void *init_thread(void *arg)
+{
+	current_iomodule_func->init_handle((struct mtcp_thread_context *)arg);   /* core.c:1313 */
+	return NULL;
+}
+
+/* mTCP threads created for cores in a scrambled order, each calling
+ * init_handle concurrently (as MTCPRunThread does): print cpu -> device. */
+static int map_mode(int ndev, int base, int ngpu)
+{
+	enum { NT = 12 };
+	static const int cores[NT] = {5, 2, 11, 0, 7, 3, 9, 1, 10, 4, 8, 6};
+	static struct mtcp_thread_context tc[NT];
+	pthread_t th[NT];
+	mosrx_gpu_module_cfg cfg;
+	int i;
+	g_fake_ndev = ndev;
+	mosrx_gpu_module_cfg_default(&cfg);
+	cfg.num_ifs = 1;
+	cfg.batch = 64;
+	cfg.gpu_base = base;
+	cfg.ngpu = ngpu;
+	if (mosrx_gpu_module_configure(&cfg))
+		return 1;
+	current_iomodule_func = &gpu_module_func;
+	for (i = 0; i < NT; i++) {
+		tc[i].cpu = cores[i];
+		if (pthread_create(&th[i], NULL, init_thread, &tc[i]))
+			return 1;
+	}
+	for (i = 0; i < NT; i++)
+		pthread_join(th[i], NULL);
+	for (i = 0; i < NT; i++) {
+		mosrx_gpu_module_stats st;
+		if (mosrx_gpu_module_stats_of(&tc[i], &st))
+			return 1;
+		printf("map %d %d %d\n", tc[i].cpu, st.cpu, st.device);
+	}
+	for (i = 0; i < NT; i++)
+		current_iomodule_func->destroy_handle(&tc[i]);
+	return 0;
+}
 #endif
 
 #define OFF(m) printf("io_module_func.%s %zu\n", #m, offsetof(io_module_func, m))
 
 int main(int argc, char **argv)
 {
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+	if (argc == 5 && !strcmp(argv[1], "--map"))
+		return map_mode(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]));
+#endif
 	OFF(load_module_upper_half); OFF(load_module_lower_half); OFF(init_handle); OFF(link_devices);
 	OFF(release_pkt); OFF(get_wptr); OFF(set_wptr); OFF(send_pkts); OFF(get_rptr); OFF(get_nif);
 	OFF(recv_pkts); OFF(select); OFF(destroy_handle); OFF(dev_ioctl);

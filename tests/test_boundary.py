@@ -80,6 +80,35 @@ def test_gpu_module_builds_inside_mos_and_sets_num_queues(tmp_path):
                                                "forward", "1"]
 
 
+@pytest.mark.skipif(not (os.path.isdir(REF_INC) and glob.glob(os.path.join(REF_OBJ, "*.o"))),
+                    reason="needs /root/reference and oracle/_ref (make -C oracle ref)")
+def test_gpu_module_inside_mos_maps_gpus_by_mtcp_core(tmp_path):
+    """Inside mOS no bind call is made: each mTCP thread's init_handle (called
+    concurrently, core.c:1313) takes its cpu from ctx->cpu (mtcp.h:306, set at
+    core.c:1302), so core c drives GPU gpu_base + c % ngpu whatever order the
+    threads register in.  The module's libmosrx calls are wrapped (no GPU
+    here): device counts 1/2/4/8 are pretended."""
+    inc = ["-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc")]
+    gm = tmp_path / "gpu_module_mos.o"
+    _run(["gcc", *MOS_CFLAGS, *inc, "-I/opt/rocm/include", "-Wall", "-Werror", "-Wno-unused-function", "-c",
+          os.path.join(PKG, "csrc", "gpu_module.c"), "-o", str(gm)])
+    hm = tmp_path / "harness_mos.o"
+    _run(["gcc", *MOS_CFLAGS, *inc, "-c", HARNESS, "-o", str(hm)])
+    exe = tmp_path / "mos_boundary_map"
+    objs = sorted(glob.glob(os.path.join(REF_OBJ, "*.o")))
+    wraps = [f"-Wl,--wrap={s}" for s in ("mosrx_device_count", "mosrx_open", "mosrx_close", "mosrx_host_alloc",
+                                         "mosrx_host_free")]
+    _run(["gcc", "-o", str(exe), str(hm), str(gm), *objs, *wraps, "-L" + PKG, "-lmosrx", "-Wl,-rpath," + PKG,
+          "-lpthread", "-lrt"])
+    for ndev, base, ngpu in [(1, 0, 0), (2, 0, 0), (4, 0, 0), (8, 0, 0), (8, 4, 0), (8, 2, 3)]:
+        out = _run([str(exe), "--map", str(ndev), str(base), str(ngpu)])
+        rows = [tuple(map(int, ln.split()[1:])) for ln in out.splitlines() if ln.startswith("map ")]
+        assert len(rows) == 12
+        n = ngpu or ndev - base
+        for core, cpu, dev in rows:
+            assert cpu == core and dev == base + core % n, (ndev, base, ngpu, core, cpu, dev)
+
+
 def test_gpu_module_cpu_to_device_mapping():
     """Thread `cpu` drives GPU gpu_base + cpu % ngpu; ngpu 0 = every visible device."""
     L = mosrx.lib()

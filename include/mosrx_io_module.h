@@ -71,8 +71,24 @@ typedef struct {
 #define MOSRX_PKT_RX_MATCH   0x11   /* argp: const uint32_t ** (whole batch's BPF match masks, bit j = program j) */
 #define MOSRX_PKT_RX_TCPINFO 0x12   /* argp: const mosrx_tcpinfo ** (whole batch; cfg.tcpinfo set) */
 #define MOSRX_PKT_SET_PARAMS 0x13   /* argp: const mosrx_params * -- the stack state changed (a monitor
-                                     * socket was created: num_msp++, socket.c:77-78); applies from the
-                                     * next batch received on that netdev */
+                                     * socket was created: num_msp++, socket.c:77-78); batches not yet
+                                     * handed out on that netdev are classified again under it */
+#define MOSRX_PKT_RX_STATE   0x14   /* argp: mosrx_rx_state * -- what the exposed batch was classified under */
+#define MOSRX_PKT_RX_RECLASSIFY 0x15 /* argp: unused (non-NULL) -- classify the exposed batch again now,
+                                     * under mOS's current state and BPF set (blocking) */
+#define MOSRX_PKT_SET_BPF    0x16   /* argp: const mosrx_bpf_set_arg * -- the monitor filters to evaluate in
+                                     * the classify pass from now on (nprog 0: none); batches not yet
+                                     * handed out are classified again with them */
+typedef struct mosrx_rx_state {
+	uint32_t num_msp, num_esp;   /* the stack state of the batch's verdicts */
+	uint32_t gen;                /* the netdev's parameter / filter generation they were made with */
+	uint32_t bpf_nprog;          /* programs in its match masks (0: no masks) */
+	uint32_t n;                  /* frames in the batch */
+} mosrx_rx_state;
+typedef struct mosrx_bpf_set_arg {
+	const mosrx_bpf_prog *progs;
+	uint32_t nprog;
+} mosrx_bpf_set_arg;
 #define MOSRX_MAX_DEVICES    16     /* MAX_DEVICES, io_module.h:87 */
 
 extern io_module_func gpu_module_func;
@@ -152,10 +168,17 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * flushes them (default 64, MAX_PKT_BURST of dpdk_module.c:61) */
 	int32_t       tcpinfo;                          /* 1: also compute pkt_info's TCP fields per batch
 	                                                 * (dev_ioctl(MOSRX_PKT_RX_TCPINFO)) */
-	uint32_t      group;                            /* batches received per kernel launch (1..MOSRX_MAX_GROUP,
-	                                                 * default 1): a group is classified by one launch and
-	                                                 * handed out one batch per recv_pkts; needs bpf_nprog 0 */
+	uint32_t      group;                            /* batches received per kernel launch: 1..MOSRX_MAX_GROUP,
+	                                                 * or MOSRX_GROUP_AUTO (0, the default): as many batches
+	                                                 * as the source has ready, up to `group_bytes` of frames.
+	                                                 * A group is classified by one launch and handed out one
+	                                                 * batch per recv_pkts.  With BPF filters installed a
+	                                                 * launch classifies one batch. */
+	uint64_t      group_bytes;                      /* MOSRX_GROUP_AUTO: frame bytes per launch aimed at
+	                                                 * (0 = MOSRX_GROUP_AUTO_BYTES) */
 } mosrx_gpu_module_cfg;
+#define MOSRX_GROUP_AUTO        0
+#define MOSRX_GROUP_AUTO_BYTES  (128ull << 20)   /* 64 B frames: ~55 batches of 32K per launch */
 
 void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg);
 int  mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg);

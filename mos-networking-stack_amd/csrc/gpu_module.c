@@ -60,21 +60,25 @@ struct stage {
 	uint16_t *len;
 	mosrx_result *res;        /* pinned, in the group's record array */
 	mosrx_tcpinfo *ti;        /* pinned, pkt_info TCP fields (cfg.tcpinfo) */
-	uint32_t *match;          /* pinned, BPF match masks (monitor filters configured) */
+	uint32_t *match;          /* pinned, BPF match masks (a filter set installed) */
 	uint32_t n, max_len;
 	uint64_t bytes;
 	int borrowed;             /* frames lent by the source: give them back when the group is recycled */
+	/* what its records were made under: mOS's socket counts, the netdev's
+	 * parameter / filter generation, the programs behind its masks */
+	uint32_t msp, esp, gen, nprog;
 };
 
 struct group {
 	uint8_t *blk;             /* pinned block the group's stages are packed into */
 	uint64_t blk_bytes;
-	mosrx_result *res;        /* pinned, group * batch records */
+	mosrx_result *res;        /* pinned, rec_cap records */
 	mosrx_tcpinfo *ti;
 	uint32_t *match;
-	struct stage *st;         /* `group` stages */
+	uint64_t rec_cap;         /* frames the record arrays hold */
+	struct stage *st;         /* cap_st stages */
+	uint32_t cap_st;
 	uint32_t nst;             /* stages filled */
-	uint32_t msp, esp;        /* the stack state the group was classified under */
 };
 
 struct if_state {
@@ -85,6 +89,8 @@ struct if_state {
 	int cur;                  /* group exposed to the application, -1 none */
 	uint32_t cur_idx;         /* its batch exposed now */
 	int inflight;             /* group being classified, -1 none */
+	uint32_t gen;             /* bumped by SET_PARAMS / SET_BPF: older records are classified again */
+	uint32_t nprog;           /* programs of the installed BPF set (0: none) */
 	/* TX: frames written through get_wptr, sent by send_pkts */
 	uint8_t *tx_buf;          /* tx_cap x TX_FRAME_LEN */
 	uint16_t *tx_len;
@@ -114,15 +120,16 @@ void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg)
 	cfg->ngpu = 0;
 	cfg->pipeline = 1;
 	cfg->tx_batch = 64;
-	cfg->group = 1;
+	cfg->group = MOSRX_GROUP_AUTO;
+	cfg->group_bytes = 0;
 	mosrx_params_default(&cfg->params);
 }
 
 int mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg)
 {
 	if (!cfg || cfg->num_ifs == 0 || cfg->num_ifs > MOSRX_MAX_DEVICES || cfg->batch == 0 ||
-	    cfg->max_frame < 64 || cfg->max_frame > 65535 || cfg->group < 1 || cfg->group > MOSRX_MAX_GROUP ||
-	    (cfg->bpf_nprog && cfg->group > 1) || cfg->params.num_local > MOSRX_MAX_LOCAL)
+	    cfg->max_frame < 64 || cfg->max_frame > 65535 || cfg->group > MOSRX_MAX_GROUP ||
+	    cfg->bpf_nprog > MOSRX_BPF_MAX_PROGS || cfg->params.num_local > MOSRX_MAX_LOCAL)
 		return -EINVAL;
 	pthread_mutex_lock(&g_lock);
 	g_cfg = *cfg;
@@ -223,8 +230,8 @@ int mosrx_gpu_module_stats_of(struct mtcp_thread_context *ctx, mosrx_gpu_module_
 #ifdef MOSRX_HAVE_MOS_IO_MODULE
 /* Not configured by the application: do what pcap_load_module_upper_half does
  * (pcap_module.c:124-160) -- one capture per netdev of mOS's configuration,
- * here an AF_PACKET ring -- with the defaults (one batch per launch,
- * num_queues 1 as pcap_module.c:159). */
+ * here an AF_PACKET ring -- with the defaults (groups sized to what the ring
+ * has ready, num_queues 1 as pcap_module.c:159). */
 static void gpu_configure_from_mos(void)
 {
 	mosrx_gpu_module_cfg cfg;
@@ -317,21 +324,40 @@ static void group_free(mosrx_ctx *mc, struct group *g)
 	memset(g, 0, sizeof(*g));
 }
 
+/* Room one stage may take in the block: descriptors + the largest frames. */
 static uint64_t stage_bytes(void)
 {
 	const uint64_t dsc = ((uint64_t)g_cfg.batch * 6 + 15) & ~15ull;
 	return dsc + (uint64_t)g_cfg.batch * ((g_cfg.max_frame + 15u + 16u) & ~15u) + 512;
 }
 
+static uint64_t auto_bytes(void)
+{
+	return g_cfg.group_bytes ? g_cfg.group_bytes : MOSRX_GROUP_AUTO_BYTES;
+}
+
+/* Explicit groups reserve `group` worst-case stages.  Auto groups hold up to
+ * MOSRX_MAX_GROUP stages in a block of auto_bytes() + one worst-case stage
+ * (a stage is started only while the frames so far are under auto_bytes()),
+ * with records for the frames that can fit (>= 48 bytes of block per frame). */
 static int group_alloc(mosrx_ctx *mc, struct group *g)
 {
-	const size_t nrec = (size_t)g_cfg.batch * g_cfg.group;
-	g->blk_bytes = stage_bytes() * g_cfg.group;
-	g->st = calloc(g_cfg.group, sizeof(*g->st));
+	if (g_cfg.group == MOSRX_GROUP_AUTO) {
+		g->cap_st = MOSRX_MAX_GROUP;
+		g->blk_bytes = auto_bytes() + stage_bytes();
+		g->rec_cap = auto_bytes() / 48 + g_cfg.batch;
+		if (g->rec_cap > (uint64_t)g_cfg.batch * MOSRX_MAX_GROUP)
+			g->rec_cap = (uint64_t)g_cfg.batch * MOSRX_MAX_GROUP;
+	} else {
+		g->cap_st = g_cfg.group;
+		g->blk_bytes = stage_bytes() * g_cfg.group;
+		g->rec_cap = (uint64_t)g_cfg.batch * g_cfg.group;
+	}
+	g->st = calloc(g->cap_st, sizeof(*g->st));
 	if (!g->st || mosrx_host_alloc(mc, g->blk_bytes, (void **)&g->blk) ||
-	    mosrx_host_alloc(mc, nrec * sizeof(mosrx_result), (void **)&g->res) ||
-	    (g_cfg.tcpinfo && mosrx_host_alloc(mc, nrec * sizeof(mosrx_tcpinfo), (void **)&g->ti)) ||
-	    (g_cfg.bpf_nprog && mosrx_host_alloc(mc, nrec * 4, (void **)&g->match)))
+	    mosrx_host_alloc(mc, g->rec_cap * sizeof(mosrx_result), (void **)&g->res) ||
+	    (g_cfg.tcpinfo && mosrx_host_alloc(mc, g->rec_cap * sizeof(mosrx_tcpinfo), (void **)&g->ti)) ||
+	    (g_cfg.bpf_nprog && mosrx_host_alloc(mc, g->rec_cap * 4, (void **)&g->match)))
 		return -ENOMEM;
 	return 0;
 }
@@ -390,6 +416,7 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 			fprintf(stderr, "[mosrx] gpu_module: mosrx_bpf_set: %s\n", mosrx_strerror(rc));
 			exit(EXIT_FAILURE);
 		}
+		is->nprog = g_cfg.bpf_nprog;
 		for (k = 0; k < MOSRX_NSLOT; k++)
 			if (group_alloc(is->mc, &is->g[k])) {
 				fprintf(stderr, "[mosrx] gpu_module: pinned staging allocation failed\n");
@@ -453,24 +480,32 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
 	*pos = at + fpos;
 }
 
-/* Receive a group: up to `group` batches, stopping early when the source runs dry. */
-static void group_fill(struct group *g, mosrx_source *src)
+/* Receive a group: up to cap_st batches (auto: until auto_bytes() of frames),
+ * stopping early when the source runs dry -- a batch that comes back short
+ * ends the group, so nothing waits for frames that are not there yet.  With a
+ * BPF set installed a group is one batch (the filters run in a per-batch pass). */
+static void group_fill(struct if_state *is, struct group *g)
 {
-	uint64_t pos = 0;
+	const uint32_t cap = is->nprog ? 1 : g->cap_st;
+	uint64_t pos = 0, recs = 0, fbytes = 0;
 	uint32_t i;
 	g->nst = 0;
-	for (i = 0; i < g_cfg.group; i++) {
+	for (i = 0; i < cap; i++) {
 		struct stage *s = &g->st[i];
-		if (pos + stage_bytes() > g->blk_bytes)
+		if (pos + stage_bytes() > g->blk_bytes || recs + g_cfg.batch > g->rec_cap)
 			break;
-		stage_fill(g, s, src, &pos);
-		s->res = g->res + (size_t)i * g_cfg.batch;
-		s->ti = g->ti ? g->ti + (size_t)i * g_cfg.batch : NULL;
-		s->match = g->match ? g->match + (size_t)i * g_cfg.batch : NULL;
+		stage_fill(g, s, is->src, &pos);
+		s->res = g->res + recs;
+		s->ti = g->ti ? g->ti + recs : NULL;
+		s->match = g->match ? g->match + recs : NULL;
 		if (!s->n)
 			break;
 		g->nst++;
+		recs += s->n;
+		fbytes += s->bytes;
 		if (s->n < g_cfg.batch)
+			break;
+		if (g_cfg.group == MOSRX_GROUP_AUTO && fbytes >= auto_bytes())
 			break;
 	}
 }
@@ -495,33 +530,51 @@ static void group_drop(struct gpu_priv *pv, struct if_state *is, int k)
 	group_recycle(&is->g[k], is->src);
 }
 
-static int group_submit(struct gpu_priv *pv, struct if_state *is, int k)
+static void stage_batch(const struct stage *s, mosrx_batch *b)
+{
+	b->frames = s->frames;
+	b->frames_bytes = s->bytes;
+	b->off = s->off;
+	b->len = s->len;
+	b->n = s->n;
+	b->max_len = s->max_len;
+}
+
+/* Classify stages [first, nst) of group k on pipeline slot k, under mOS's
+ * current stack state and the installed filter set: one launch for all of
+ * them (the batch queue); with filters, one classify + BPF pass per batch,
+ * all but the last waited here. */
+static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_t first)
 {
 	struct group *g = &is->g[k];
 	mosrx_batch b[MOSRX_MAX_GROUP];
 	mosrx_result *out[MOSRX_MAX_GROUP];
 	mosrx_tcpinfo *ti[MOSRX_MAX_GROUP];
-	uint32_t i;
+	uint32_t i, nb = g->nst - first;
 	if (follow_mos_state(pv, is))
 		return -1;
-	g->msp = is->params.num_msp;
-	g->esp = is->params.num_esp;
-	for (i = 0; i < g->nst; i++) {
-		const struct stage *s = &g->st[i];
-		b[i].frames = s->frames;
-		b[i].frames_bytes = s->bytes;
-		b[i].off = s->off;
-		b[i].len = s->len;
-		b[i].n = s->n;
-		b[i].max_len = s->max_len;
-		out[i] = s->res;
-		ti[i] = s->ti;
+	for (i = first; i < g->nst; i++) {
+		struct stage *s = &g->st[i];
+		stage_batch(s, &b[i - first]);
+		out[i - first] = s->res;
+		ti[i - first] = s->ti;
+		s->msp = is->params.num_msp;
+		s->esp = is->params.num_esp;
+		s->gen = is->gen;
+		s->nprog = is->nprog;
 	}
-	if (g_cfg.bpf_nprog)
-		return mosrx_classify_bpf_host_submit(is->mc, k, &b[0], g->st[0].res, g->st[0].match);
-	if (g_cfg.group == 1)
-		return mosrx_classify_host_submit_ex(is->mc, k, &b[0], g->st[0].res, g->st[0].ti);
-	return mosrx_classify_host_group_submit(is->mc, k, b, g->nst, out, g_cfg.tcpinfo ? ti : NULL);
+	if (is->nprog) {
+		for (i = first; i < g->nst; i++) {
+			if (mosrx_classify_bpf_host_submit(is->mc, k, &b[i - first], g->st[i].res, g->st[i].match))
+				return -1;
+			if (i + 1 < g->nst && mosrx_classify_host_wait(is->mc, k))
+				return -1;
+		}
+		return 0;
+	}
+	if (nb == 1)
+		return mosrx_classify_host_submit_ex(is->mc, k, &b[0], out[0], ti[0]);
+	return mosrx_classify_host_group_submit(is->mc, k, b, nb, out, g_cfg.tcpinfo ? ti : NULL);
 }
 
 static int group_wait(struct gpu_priv *pv, struct if_state *is, int k, int count)
@@ -542,6 +595,27 @@ static int group_wait(struct gpu_priv *pv, struct if_state *is, int k, int count
 	return 0;
 }
 
+/* Were the stage's records made under something other than what ProcessPacket
+ * would see now?  mOS's socket counts (a monitor or end-host socket came or
+ * went, socket.c:77-78), or the application's parameters / filter set. */
+static int stage_stale(const struct gpu_priv *pv, const struct if_state *is, const struct stage *s)
+{
+	uint32_t msp, esp;
+	if (s->gen != is->gen)
+		return 1;
+	return mos_state(pv, &msp, &esp) && (msp != s->msp || esp != s->esp);
+}
+
+/* Classify stages [first, nst) of the exposed / just-waited group k again,
+ * blocking (slot k is idle: its group was waited). */
+static int group_reclassify(struct gpu_priv *pv, struct if_state *is, int k, uint32_t first)
+{
+	pv->stats.rx_reclassified += is->g[k].nst - first;
+	if (group_submit(pv, is, k, first) || group_wait(pv, is, k, 0))
+		return -1;
+	return 0;
+}
+
 static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 {
 	struct gpu_priv *pv = priv_of(ctx);
@@ -551,10 +625,21 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 	if (!pv || ifidx < 0 || ifidx >= (int)g_cfg.num_ifs)
 		return -1;
 	is = &pv->ifs[ifidx];
-	/* the next batch of the group already classified */
+	/* the next batch of the group already classified -- again first if the
+	 * stack state or the filters changed since (ProcessPacket reads the
+	 * socket counts live, per frame) */
 	if (is->cur >= 0 && is->cur_idx + 1 < is->g[is->cur].nst) {
+		struct group *g = &is->g[is->cur];
 		is->cur_idx++;
-		return (int32_t)is->g[is->cur].st[is->cur_idx].n;
+		if (stage_stale(pv, is, &g->st[is->cur_idx]) && group_reclassify(pv, is, is->cur, is->cur_idx)) {
+			/* the rest of the group is lost; the next call moves on */
+			uint32_t i;
+			for (i = is->cur_idx; i < g->nst; i++)
+				pv->stats.rx_drops += g->st[i].n;
+			is->cur_idx = g->nst - 1;
+			return -1;
+		}
+		return (int32_t)g->st[is->cur_idx].n;
 	}
 	/* the exposed group is done with (get_rptr pointers expire here) */
 	k = is->cur < 0 ? 0 : is->cur ^ 1;
@@ -562,10 +647,10 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 		group_recycle(&is->g[is->cur], is->src);
 	is->cur = -1;                     /* nothing exposed until a group is ready */
 	if (is->inflight < 0) {           /* nothing in flight: receive + classify now */
-		group_fill(&is->g[k], is->src);
+		group_fill(is, &is->g[k]);
 		if (!is->g[k].nst)
 			return 0;
-		if (group_submit(pv, is, k)) {
+		if (group_submit(pv, is, k, 0)) {
 			group_drop(pv, is, k);
 			return -1;
 		}
@@ -577,26 +662,19 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 		group_drop(pv, is, k);
 		return -1;
 	}
-	{
-		/* mOS's stack state changed while the group was in flight (a monitor or
-		 * end-host socket came or went): classify it again under the state the
-		 * rx loop runs with now, so every batch handed out matches ProcessPacket */
-		uint32_t msp, esp;
-		if (mos_state(pv, &msp, &esp) && (msp != is->g[k].msp || esp != is->g[k].esp)) {
-			pv->stats.rx_reclassified += is->g[k].nst;
-			if (group_submit(pv, is, k) || group_wait(pv, is, k, 0)) {
-				group_drop(pv, is, k);
-				return -1;
-			}
-		}
+	/* classified in flight under a state that has changed since: again, under
+	 * the state the rx loop runs with now */
+	if (stage_stale(pv, is, &is->g[k].st[0]) && group_reclassify(pv, is, k, 0)) {
+		group_drop(pv, is, k);
+		return -1;
 	}
 	is->cur = k;
 	is->cur_idx = 0;
 	if (g_cfg.pipeline) {             /* classify the next group behind the app's work */
 		int nk = k ^ 1;
-		group_fill(&is->g[nk], is->src);
+		group_fill(is, &is->g[nk]);
 		if (is->g[nk].nst) {
-			if (group_submit(pv, is, nk) == 0)
+			if (group_submit(pv, is, nk, 0) == 0)
 				is->inflight = nk;
 			else
 				group_drop(pv, is, nk);
@@ -682,6 +760,29 @@ static int gpu_get_nif(struct ifreq *ifr)
 	return -1;
 }
 
+/* Install a BPF program set on netdev is (the monitors' filters, bit j =
+ * program j): the match arrays are allocated the first time, the stages of
+ * both groups pointed at them, and the generation bumped so every batch not
+ * yet handed out is classified again with the set. */
+static int32_t set_bpf(struct gpu_priv *pv, struct if_state *is, const mosrx_bpf_set_arg *a)
+{
+	int k;
+	uint32_t i;
+	(void)pv;
+	if (!a || a->nprog > MOSRX_BPF_MAX_PROGS || mosrx_bpf_set(is->mc, a->progs, a->nprog))
+		return -1;
+	for (k = 0; k < MOSRX_NSLOT && a->nprog; k++) {
+		struct group *g = &is->g[k];
+		if (!g->match && mosrx_host_alloc(is->mc, g->rec_cap * 4, (void **)&g->match))
+			return -1;
+		for (i = 0; i < g->nst; i++)
+			g->st[i].match = g->match + (g->st[i].res - g->res);
+	}
+	is->nprog = a->nprog;
+	is->gen++;
+	return 0;
+}
+
 static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, void *argp)
 {
 	struct gpu_priv *pv = priv_of(ctx);
@@ -703,7 +804,7 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
 		*(const mosrx_result **)argp = s->res;
 		return 0;
 	case MOSRX_PKT_RX_MATCH:
-		if (!s || !s->match)
+		if (!s || !s->match || !s->nprog)
 			return -1;
 		*(const uint32_t **)argp = s->match;
 		return 0;
@@ -712,11 +813,35 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
 			return -1;
 		*(const mosrx_tcpinfo **)argp = s->ti;
 		return 0;
-	case MOSRX_PKT_SET_PARAMS:   /* batches submitted from now on use the new stack state */
+	case MOSRX_PKT_SET_PARAMS:
+		/* batches submitted from now on use the new stack state; a group in
+		 * flight may have read the tables half rewritten, and every batch not
+		 * yet handed out was made under the old state: the generation makes
+		 * recv_pkts classify them again before they are exposed */
 		if (mosrx_set_params(pv->ifs[nif].mc, (const mosrx_params *)argp))
 			return -1;
 		pv->ifs[nif].params = *(const mosrx_params *)argp;
+		pv->ifs[nif].gen++;
 		return 0;
+	case MOSRX_PKT_SET_BPF:
+		return set_bpf(pv, &pv->ifs[nif], (const mosrx_bpf_set_arg *)argp);
+	case MOSRX_PKT_RX_STATE: {
+		mosrx_rx_state *st = argp;
+		if (!s)
+			return -1;
+		st->num_msp = s->msp;
+		st->num_esp = s->esp;
+		st->gen = s->gen;
+		st->bpf_nprog = s->nprog;
+		st->n = s->n;
+		return 0;
+	}
+	case MOSRX_PKT_RX_RECLASSIFY: {
+		struct if_state *is = &pv->ifs[nif];
+		if (!s)
+			return -1;
+		return group_reclassify(pv, is, is->cur, is->cur_idx) ? -1 : 0;
+	}
 	case DRV_NAME:
 		*(const char **)argp = "mosrx_gpu";
 		return 0;

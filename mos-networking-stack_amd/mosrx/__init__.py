@@ -99,7 +99,8 @@ class ModuleCfg(C.Structure):
                 ("src", C.c_void_p * 16), ("batch", C.c_uint32), ("max_frame", C.c_uint32),
                 ("gpu_base", C.c_int32), ("ngpu", C.c_int32), ("pipeline", C.c_int32),
                 ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32),
-                ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32)]
+                ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32),
+                ("group_bytes", C.c_uint64)]
 
 
 class ModuleStats(C.Structure):

@@ -1,0 +1,132 @@
+/*
+ * gpu_emul.c — TEST INFRASTRUCTURE ONLY (tests/test_mos_consumer.py, CPU leg).
+ *
+ * Stands in for the GPU under gpu_module_func in a container with no GPU:
+ * linked into oracle/_ref/mos_app_emul with -Wl,--wrap for each libmosrx call
+ * the module makes, it produces the records (and BPF match masks) with the
+ * oracle's C restatement (mosrx_oracle.c, bpf_oracle.c) at submit time.  It
+ * lets the CPU suite check the host logic above the kernels -- the backend's
+ * grouping / reclassification and the mOS-side consumer (csrc/mos_rx.c)
+ * against mOS's own ProcessPacket -- while the -m gpu test runs the same
+ * program with the real kernels.  Never part of a product build.
+ */
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mosrx_oracle.h"
+
+struct emul_ctx {
+	mosrx_params p;
+	mosrx_bpf_prog progs[MOSRX_BPF_MAX_PROGS];
+	mosrx_bpf_insn *insns[MOSRX_BPF_MAX_PROGS];
+	uint32_t nprog;
+};
+
+static int emul_gpus(void)
+{
+	const char *e = getenv("MOSRX_EMUL_NDEV");
+	return e ? atoi(e) : 1;
+}
+
+int __wrap_mosrx_device_count(void) { return emul_gpus(); }
+
+int __wrap_mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
+{
+	struct emul_ctx *c;
+	if (device < 0 || device >= emul_gpus() || !p)
+		return -ENODEV;
+	c = calloc(1, sizeof(*c));
+	if (!c)
+		return -ENOMEM;
+	c->p = *p;
+	*out = (mosrx_ctx *)c;
+	return 0;
+}
+
+static void drop_progs(struct emul_ctx *c)
+{
+	uint32_t i;
+	for (i = 0; i < c->nprog; i++)
+		free(c->insns[i]);
+	c->nprog = 0;
+}
+
+void __wrap_mosrx_close(mosrx_ctx *mc)
+{
+	struct emul_ctx *c = (struct emul_ctx *)mc;
+	if (c)
+		drop_progs(c);
+	free(c);
+}
+
+int __wrap_mosrx_set_params(mosrx_ctx *mc, const mosrx_params *p)
+{
+	((struct emul_ctx *)mc)->p = *p;
+	return 0;
+}
+
+int __wrap_mosrx_set_timing(mosrx_ctx *mc, int on) { (void)mc; (void)on; return 0; }
+int __wrap_mosrx_last_kernel_ms(mosrx_ctx *mc, float *ms) { (void)mc; (void)ms; return -ENODATA; }
+int __wrap_mosrx_host_alloc(mosrx_ctx *mc, size_t bytes, void **p)
+{
+	(void)mc;
+	*p = calloc(1, bytes ? bytes : 1);
+	return *p ? 0 : -ENOMEM;
+}
+int __wrap_mosrx_host_free(mosrx_ctx *mc, void *p) { (void)mc; free(p); return 0; }
+int __wrap_mosrx_classify_host_wait(mosrx_ctx *mc, int slot) { (void)mc; (void)slot; return 0; }
+
+int __wrap_mosrx_bpf_set(mosrx_ctx *mc, const mosrx_bpf_prog *progs, uint32_t nprog)
+{
+	struct emul_ctx *c = (struct emul_ctx *)mc;
+	uint32_t i;
+	if (nprog > MOSRX_BPF_MAX_PROGS)
+		return -EINVAL;
+	for (i = 0; i < nprog; i++)
+		if (progs[i].len && mo_bpf_validate(progs[i].insns, (int)progs[i].len) != 1)
+			return -EINVAL;
+	drop_progs(c);
+	for (i = 0; i < nprog; i++) {
+		c->progs[i] = progs[i];
+		c->insns[i] = NULL;
+		if (progs[i].len) {
+			c->insns[i] = malloc(progs[i].len * sizeof(mosrx_bpf_insn));
+			if (!c->insns[i])
+				return -ENOMEM;
+			memcpy(c->insns[i], progs[i].insns, progs[i].len * sizeof(mosrx_bpf_insn));
+			c->progs[i].insns = c->insns[i];
+		}
+	}
+	c->nprog = nprog;
+	return 0;
+}
+
+int __wrap_mosrx_classify_host_submit_ex(mosrx_ctx *mc, int slot, const mosrx_batch *b, mosrx_result *out,
+                                         mosrx_tcpinfo *ti)
+{
+	struct emul_ctx *c = (struct emul_ctx *)mc;
+	(void)slot;
+	return mo_classify_ex(&c->p, b->frames, b->frames_bytes, b->off, b->len, b->n, out, NULL, ti);
+}
+
+int __wrap_mosrx_classify_host_group_submit(mosrx_ctx *mc, int slot, const mosrx_batch *b, uint32_t nb,
+                                            mosrx_result *const *out, mosrx_tcpinfo *const *ti)
+{
+	uint32_t i;
+	int rc;
+	for (i = 0; i < nb; i++)
+		if ((rc = __wrap_mosrx_classify_host_submit_ex(mc, slot, &b[i], out[i], ti ? ti[i] : NULL)))
+			return rc;
+	return 0;
+}
+
+int __wrap_mosrx_classify_bpf_host_submit(mosrx_ctx *mc, int slot, const mosrx_batch *b, mosrx_result *out,
+                                          uint32_t *match)
+{
+	struct emul_ctx *c = (struct emul_ctx *)mc;
+	int rc = __wrap_mosrx_classify_host_submit_ex(mc, slot, b, out, NULL);
+	if (rc)
+		return rc;
+	return mo_bpf_eval(c->progs, c->nprog, b->frames, b->frames_bytes, b->off, b->len, b->n, match);
+}

@@ -1,0 +1,390 @@
+/*
+ * mos_app.c — TEST INFRASTRUCTURE ONLY (tests/test_mos_consumer.py).
+ *
+ * mOS itself, running: mtcp_init from a mos.conf, one mTCP thread
+ * (mtcp_create_context -> MTCPRunThread -> RunMainLoop, core.c:1282-1349,
+ * 851-1047), monitor sockets with callbacks and BPF filters, an optional
+ * end-host listener -- with gpu_module_func as its I/O module (set before
+ * mtcp_init: core.c is compiled without an ENABLE_* backend, so
+ * core.c:1725-1733 leaves the choice alone, exactly what the ENABLE_GPU
+ * branch of INTEGRATION.md §2 does).  The frames of a trace come in through
+ * the backend from an in-memory source; everything mOS sends (forwarded
+ * frames, RSTs, ICMP replies) goes out through the backend's TX into a pcap
+ * dump.
+ *
+ * RunMainLoop's per-frame call (core.c:906) is routed, at link time
+ * (-Wl,--wrap=ProcessPacket), to
+ *   mode "pp":  mOS's own ProcessPacket (eth_in.c:27-87), checks on the CPU;
+ *   mode "gpu": mosrx_mos_process_packet (csrc/mos_rx.c), the checks' outcome
+ *               taken from the GPU records.
+ * Everything observable is written out for the test to compare between the
+ * two modes: each frame's return value, NETSTAT, every callback with the
+ * packet it saw (mtcp_getlastpkt), the streams in the flow table after the
+ * last frame, and the TX dump.  Per-frame CPU time of the rx loop is timed
+ * per batch (index 0 .. n-1 of RunMainLoop's loop).
+ *
+ * Usage: mos_app <mode> <mos.conf> <trace.mrxt> <outdir>
+ *   env MOSAPP_MONITORS=k        stream monitor sockets (default 1)
+ *   env MOSAPP_RAW="bpf expr"    a raw monitor socket with this filter
+ *   env MOSAPP_RAW_NOFILTER=1    a raw monitor socket without a filter
+ *   env MOSAPP_SYN="bpf expr"    stream SYN filter of the first stream monitor
+ *   env MOSAPP_ORPHAN="bpf expr" its orphan filter
+ *   env MOSAPP_LISTEN=port       an end-host socket listening on that port
+ *   env MOSAPP_BATCH=n           frames per recv_pkts (default 4096)
+ *   env MOSAPP_GROUP=g           batches per launch (default 0 = auto)
+ *   env MOSAPP_LATE_RAW_AT=k     create the raw monitor (MOSAPP_RAW's filter) just before
+ *                                frame k, on the mTCP thread (a filter bound mid-batch)
+ *   env MOSAPP_LATE_MON_AT=k     create one more stream monitor just before frame k (the
+ *                                checksum gate of ip_in.c:67 turning on mid-batch when
+ *                                MOSAPP_MONITORS=0)
+ *   env MOSAPP_LOOPS=l           replay the trace l times (timing runs)
+ *   env MOSAPP_QUIET=1           no callback log (timing runs)
+ */
+#define _GNU_SOURCE
+#include <arpa/inet.h>
+#include <errno.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "mtcp_api.h"
+#include "mos_api.h"
+#include "mtcp.h"
+#include "config.h"
+#include "fhash.h"
+#include "tcp_stream.h"
+#include "io_module.h"
+#include "mosrx_io_module.h"
+#include "mosrx_mos_rx.h"
+
+int __real_ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index, uint32_t cur_ts,
+                         unsigned char *pkt_data, int len);
+extern mtcp_manager_t g_mtcp[];
+
+static int g_mode_gpu;
+static uint64_t g_total;                 /* frames the run will process */
+static _Atomic uint64_t g_done;          /* frames processed so far */
+static int8_t *g_ret;
+static uint32_t g_batch_n;               /* frames of the batch being walked */
+static struct timespec g_t0;
+static double g_rx_ns;                   /* CPU time of the per-frame loop, summed per batch */
+static uint64_t g_rx_frames;
+static FILE *g_cb;
+static int g_quiet;
+static char g_snap[1 << 20];             /* flow table + NETSTAT after the last frame */
+static size_t g_snap_len;
+static mctx_t g_mctx;
+static _Atomic int g_go;                  /* the application's sockets are set up */
+static io_module_func g_gated;           /* gpu_module_func, receiving nothing before g_go */
+
+static uint64_t g_late_raw, g_late_mon;
+static int raw_monitor(void);
+static int stream_monitor(int with_filters);
+
+static int32_t gated_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
+{
+	return atomic_load(&g_go) ? gpu_module_func.recv_pkts(ctx, ifidx) : 0;
+}
+
+static double ns_between(const struct timespec *a, const struct timespec *b)
+{
+	return (b->tv_sec - a->tv_sec) * 1e9 + (b->tv_nsec - a->tv_nsec);
+}
+
+int __wrap_GetNumCPUs(void)   /* core.c sizes per-cpu arrays of MAX_CPUS by it (core.c:1711-1716) */
+{
+	long n = sysconf(_SC_NPROCESSORS_ONLN);
+	return n < MAX_CPUS ? (int)n : MAX_CPUS;
+}
+
+static int stream_cmp(const void *a, const void *b)
+{
+	return memcmp(a, b, 16);
+}
+
+/* The flow table as the test compares it: each stream's tuple, type, state,
+ * side and whether it has a pair, sorted; then NETSTAT. */
+static void snapshot(mtcp_manager_t mtcp)
+{
+	struct hashtable *ht = mtcp->tcp_flow_table;
+	uint8_t (*rows)[16] = calloc(200000, 16);
+	size_t nrow = 0, i;
+	int b;
+	for (b = 0; rows && b < NUM_BINS; b++) {
+		tcp_stream *w;
+		TAILQ_FOREACH(w, &ht->ht_table[b], rcvvar->he_link) {
+			if (nrow == 200000)
+				break;
+			memcpy(rows[nrow], &w->saddr, 4);
+			memcpy(rows[nrow] + 4, &w->daddr, 4);
+			memcpy(rows[nrow] + 8, &w->sport, 2);
+			memcpy(rows[nrow] + 10, &w->dport, 2);
+			rows[nrow][12] = (uint8_t)w->stream_type;
+			rows[nrow][13] = (uint8_t)w->state;
+			rows[nrow][14] = (uint8_t)w->side;
+			rows[nrow][15] = w->pair_stream != NULL;
+			nrow++;
+		}
+	}
+	if (rows)
+		qsort(rows, nrow, 16, stream_cmp);
+	g_snap_len = (size_t)snprintf(g_snap, sizeof(g_snap), "streams %zu flow_cnt %u\n", nrow, mtcp->flow_cnt);
+	for (i = 0; i < nrow && g_snap_len < sizeof(g_snap) - 64; i++) {
+		int k;
+		for (k = 0; k < 16; k++)
+			g_snap_len += (size_t)snprintf(g_snap + g_snap_len, sizeof(g_snap) - g_snap_len, "%02x", rows[i][k]);
+		g_snap[g_snap_len++] = '\n';
+	}
+	g_snap_len += (size_t)snprintf(g_snap + g_snap_len, sizeof(g_snap) - g_snap_len,
+	                               "nstat rx_packets %lu rx_bytes %lu rx_errors %lu\n",
+	                               (unsigned long)mtcp->nstat.rx_packets[0], (unsigned long)mtcp->nstat.rx_bytes[0],
+	                               (unsigned long)mtcp->nstat.rx_errors[0]);
+	free(rows);
+}
+
+/* core.c:906's call, routed to the mode's receive step. */
+int __wrap_ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index, uint32_t cur_ts,
+                         unsigned char *pkt_data, int len)
+{
+	int ret;
+	uint64_t k = atomic_load(&g_done);
+	/* sockets that appear in the middle of a batch, at a fixed frame (on the
+	 * mTCP thread, so both modes see them at the same point) */
+	if (g_late_raw && k + 1 == g_late_raw)
+		raw_monitor();
+	if (g_late_mon && k + 1 == g_late_mon)
+		stream_monitor(0);
+	if (index == 0) {
+		mosrx_rx_state st;
+		g_batch_n = mtcp->iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_STATE, &st) ? 0 : st.n;
+		clock_gettime(CLOCK_MONOTONIC, &g_t0);
+	}
+	ret = g_mode_gpu ? mosrx_mos_process_packet(mtcp, ifidx, index, cur_ts, pkt_data, len)
+	                 : __real_ProcessPacket(mtcp, ifidx, index, cur_ts, pkt_data, len);
+	if ((uint32_t)index + 1 == g_batch_n) {
+		struct timespec t1;
+		clock_gettime(CLOCK_MONOTONIC, &t1);
+		g_rx_ns += ns_between(&g_t0, &t1);
+		g_rx_frames += g_batch_n;
+	}
+	if (g_ret && k < g_total)
+		g_ret[k] = (int8_t)ret;
+	if (k + 1 == g_total)
+		snapshot(mtcp);
+	atomic_store(&g_done, k + 1);
+	return ret;
+}
+
+/* Every callback with the packet it was raised for. */
+static void on_event(mctx_t mctx, int sock, int side, event_t ev, filter_arg_t *arg)
+{
+	struct pkt_info p;
+	(void)arg;
+	if (g_quiet)
+		return;
+	memset(&p, 0, sizeof(p));
+	if (mtcp_getlastpkt(mctx, sock, side, &p) != 0)
+		memset(&p, 0, sizeof(p));
+	fprintf(g_cb, "f %lu ev %lx sock %d side %d eth %u ip %u plen %u seq %u ack %u win %u off %lu\n",
+	        (unsigned long)atomic_load(&g_done), (unsigned long)ev, sock, side, p.eth_len, p.ip_len, p.payloadlen,
+	        p.seq, p.ack_seq, p.window, (unsigned long)p.offset);
+}
+
+static int rd(FILE *f, void *p, size_t n) { return fread(p, 1, n, f) == n ? 0 : -1; }
+
+static void die(const char *m)
+{
+	fprintf(stderr, "mos_app: %s (errno %d)\n", m, errno);
+	exit(2);
+}
+
+static int raw_monitor(void)
+{
+	int s = mtcp_socket(g_mctx, AF_INET, MOS_SOCK_MONITOR_RAW, 0);
+	if (s < 0)
+		die("raw monitor socket");
+	if (getenv("MOSAPP_RAW")) {
+		union monitor_filter ft = {.raw_pkt_filter = getenv("MOSAPP_RAW")};
+		if (mtcp_bind_monitor_filter(g_mctx, s, &ft))
+			die("raw filter");
+	}
+	if (mtcp_register_callback(g_mctx, s, MOS_ON_PKT_IN, MOS_NULL, on_event))
+		die("raw callback");
+	return s;
+}
+
+/* A MOS_SOCK_MONITOR_STREAM socket (num_msp++, socket.c:77-78) with every
+ * stream event's callback; the first one takes MOSAPP_SYN / MOSAPP_ORPHAN. */
+static int stream_monitor(int with_filters)
+{
+	int s = mtcp_socket(g_mctx, AF_INET, MOS_SOCK_MONITOR_STREAM, 0);
+	if (s < 0)
+		die("monitor socket");
+	if (with_filters && (getenv("MOSAPP_SYN") || getenv("MOSAPP_ORPHAN"))) {
+		union monitor_filter ft;
+		memset(&ft, 0, sizeof(ft));
+		ft.stream_syn_filter = getenv("MOSAPP_SYN");
+		ft.stream_orphan_filter = getenv("MOSAPP_ORPHAN");
+		if (mtcp_bind_monitor_filter(g_mctx, s, &ft))
+			die("stream filters");
+	}
+	if (mtcp_register_callback(g_mctx, s, MOS_ON_PKT_IN, MOS_HK_SND, on_event) ||
+	    mtcp_register_callback(g_mctx, s, MOS_ON_PKT_IN, MOS_HK_RCV, on_event) ||
+	    mtcp_register_callback(g_mctx, s, MOS_ON_CONN_START, MOS_HK_SND, on_event) ||
+	    mtcp_register_callback(g_mctx, s, MOS_ON_TCP_STATE_CHANGE, MOS_HK_RCV, on_event) ||
+	    mtcp_register_callback(g_mctx, s, MOS_ON_CONN_END, MOS_HK_RCV, on_event) ||
+	    mtcp_register_callback(g_mctx, s, MOS_ON_ORPHAN, MOS_NULL, on_event))
+		die("stream callbacks");
+	return s;
+}
+
+int main(int argc, char **argv)
+{
+	FILE *in;
+	char magic[4], path[4096];
+	uint32_t ver, n, nlocal = 0, local_ip[16], num_msp, num_esp, i;
+	uint64_t fb;
+	int32_t forward, nq, qmode;
+	uint32_t *off;
+	uint16_t *len;
+	uint8_t *frames;
+	mosrx_source *src;
+	mosrx_gpu_module_cfg cfg;
+	struct mtcp_conf mcfg;
+	int monitors = getenv("MOSAPP_MONITORS") ? atoi(getenv("MOSAPP_MONITORS")) : 1;
+	uint32_t loops = getenv("MOSAPP_LOOPS") ? (uint32_t)atoi(getenv("MOSAPP_LOOPS")) : 1;
+	uint64_t late_raw = getenv("MOSAPP_LATE_RAW_AT") ? strtoull(getenv("MOSAPP_LATE_RAW_AT"), NULL, 10) : 0;
+	int mon0 = -1, m;
+	FILE *f;
+
+	if (argc != 5 || (strcmp(argv[1], "pp") && strcmp(argv[1], "gpu"))) {
+		fprintf(stderr, "usage: %s pp|gpu mos.conf trace.mrxt outdir\n", argv[0]);
+		return 2;
+	}
+	g_mode_gpu = !strcmp(argv[1], "gpu");
+	g_quiet = getenv("MOSAPP_QUIET") != NULL;
+	in = fopen(argv[3], "rb");
+	if (!in || rd(in, magic, 4) || memcmp(magic, "MRXT", 4) || rd(in, &ver, 4) || (ver != 1 && ver != 2) ||
+	    rd(in, &n, 4) || rd(in, &fb, 8) || rd(in, &num_msp, 4) || rd(in, &num_esp, 4) ||
+	    rd(in, &forward, 4) || rd(in, &nq, 4) || rd(in, &qmode, 4) ||
+	    (ver == 2 && (rd(in, &nlocal, 4) || nlocal > 16 || rd(in, local_ip, sizeof(local_ip)))))
+		die("bad trace header");
+	off = malloc((size_t)n * 4 + 4);
+	len = malloc((size_t)n * 2 + 2);
+	frames = calloc(fb + 64, 1);
+	if (!off || !len || !frames || rd(in, off, (size_t)n * 4) || rd(in, len, (size_t)n * 2) || rd(in, frames, fb))
+		die("short trace");
+	fclose(in);
+	g_total = (uint64_t)n * loops;
+	g_ret = calloc(g_total, 1);
+	snprintf(path, sizeof(path), "%s/callbacks.txt", argv[4]);
+	g_cb = fopen(path, "w");
+	if (!g_cb)
+		die("callbacks file");
+
+	/* the backend: frames from memory, TX into a pcap dump, mOS's I/O module */
+	src = mosrx_source_mem(frames, off, len, n, loops);
+	if (!src)
+		die("source");
+	mosrx_source_mem_set_mode(src, 1);   /* copied in runs: frames stay writable for mOS (forward rewrites) */
+	snprintf(path, sizeof(path), "%s/tx.pcap", argv[4]);
+	if (mosrx_source_tx_pcap(src, path))
+		die("tx dump");
+	mosrx_gpu_module_cfg_default(&cfg);
+	cfg.num_ifs = 1;
+	strncpy(cfg.if_names[0], "lo", IFNAMSIZ - 1);
+	cfg.src[0] = src;
+	cfg.batch = getenv("MOSAPP_BATCH") ? (uint32_t)atoi(getenv("MOSAPP_BATCH")) : 4096;
+	cfg.group = getenv("MOSAPP_GROUP") ? (uint32_t)atoi(getenv("MOSAPP_GROUP")) : MOSRX_GROUP_AUTO;
+	cfg.params.num_queues = nq;
+	cfg.params.queue_mode = qmode;
+	cfg.params.num_msp = 0;                       /* followed from mOS's manager (mos_state) */
+	cfg.params.num_esp = 0;
+	if (mosrx_gpu_module_configure(&cfg))
+		die("configure");
+	/* the ENABLE_GPU branch of core.c:1725-1733; frames are held back until the
+	 * application's sockets exist, so both modes see the same stack state */
+	g_gated = gpu_module_func;
+	g_gated.recv_pkts = gated_recv_pkts;
+	current_iomodule_func = &g_gated;
+
+	if (mtcp_init(argv[2]))
+		die("mtcp_init");
+	mtcp_getconf(&mcfg);
+	mcfg.num_cores = 1;
+	mtcp_setconf(&mcfg);
+	g_mctx = mtcp_create_context(0);
+	if (!g_mctx)
+		die("mtcp_create_context");
+
+	/* the application's sockets (simple_firewall.c:383-395 and friends) */
+	for (m = 0; m < monitors; m++) {
+		int s = stream_monitor(m == 0);
+		if (m == 0)
+			mon0 = s;
+	}
+	if ((getenv("MOSAPP_RAW") || getenv("MOSAPP_RAW_NOFILTER")) && !late_raw)
+		raw_monitor();
+	g_late_raw = late_raw;
+	g_late_mon = getenv("MOSAPP_LATE_MON_AT") ? strtoull(getenv("MOSAPP_LATE_MON_AT"), NULL, 10) : 0;
+	if (getenv("MOSAPP_LISTEN")) {
+		struct sockaddr_in a;
+		int s = mtcp_socket(g_mctx, AF_INET, SOCK_STREAM, 0);   /* num_esp++ (socket.c:96) */
+		memset(&a, 0, sizeof(a));
+		a.sin_family = AF_INET;
+		a.sin_addr.s_addr = INADDR_ANY;
+		a.sin_port = htons((uint16_t)atoi(getenv("MOSAPP_LISTEN")));
+		if (s < 0)
+			die("listener socket");
+		if (mtcp_bind(g_mctx, s, (struct sockaddr *)&a, sizeof(a)))
+			die("listener bind");
+		if (mtcp_listen(g_mctx, s, 128))
+			die("listener listen");
+	}
+	atomic_store(&g_go, 1);
+	(void)mon0;
+	(void)num_msp;
+	(void)num_esp;
+	(void)forward;
+	(void)nlocal;
+
+	/* the frames go through; a late raw monitor appears mid-trace (the app
+	 * thread creating a socket while the mTCP thread receives, as
+	 * simple_firewall's threads do) */
+	while (atomic_load(&g_done) < g_total)
+		usleep(200);
+	usleep(100000);                       /* the last round's send_pkts */
+	mtcp_destroy_context(g_mctx);
+	mosrx_source_tx_flush(src);
+	mosrx_source_tx_pcap(src, NULL);
+
+	snprintf(path, sizeof(path), "%s/returns.bin", argv[4]);
+	f = fopen(path, "wb");
+	if (!f || fwrite(g_ret, 1, g_total, f) != g_total)
+		die("returns");
+	fclose(f);
+	snprintf(path, sizeof(path), "%s/state.txt", argv[4]);
+	f = fopen(path, "w");
+	if (!f || fwrite(g_snap, 1, g_snap_len, f) != g_snap_len)
+		die("state");
+	fclose(f);
+	fclose(g_cb);
+	{
+		mosrx_mos_rx_stats cs;
+		mosrx_mos_rx_stats_of(0, &cs);
+		printf("{\"mode\": \"%s\", \"frames\": %lu, \"rx_frames_timed\": %lu, \"rx_ns_per_frame\": %.2f, "
+		       "\"consumer_frames\": %lu, \"stream_step\": %lu, \"reclassified\": %lu, \"filter_installs\": %lu, "
+		       "\"filters_gpu\": %lu, \"filters_cpu\": %lu}\n",
+		       argv[1], (unsigned long)g_total, (unsigned long)g_rx_frames,
+		       g_rx_frames ? g_rx_ns / (double)g_rx_frames : 0.0, (unsigned long)cs.frames,
+		       (unsigned long)cs.stream_step, (unsigned long)cs.reclassified, (unsigned long)cs.filter_installs,
+		       (unsigned long)cs.filters_gpu, (unsigned long)cs.filters_cpu);
+	}
+	mosrx_source_close(src);
+	return 0;
+}

@@ -142,3 +142,82 @@ def read_ref_results(path, n):
     rec = np.frombuffer(raw[: n * sz], REF_DTYPE)
     stats = struct.unpack("<QQQ", raw[n * sz: n * sz + 24])
     return rec, dict(rx_packets=stats[0], rx_bytes=stats[1], rx_errors=stats[2])
+
+
+def conversation_frames(nflows: int = 64, seed: int = 7, *, listen_port: int = 0, local_ip: str = "127.0.0.1"):
+    """Frames of TCP conversations interleaved the way a monitored link carries
+    them -- handshake, data both ways, FIN or RST teardown, retransmissions --
+    plus the traffic around them a stack sees: orphan segments, bad IP / TCP
+    checksums, ARP, IPv6, UDP, ICMP to and past the local address, IP options.
+    Per-flow order is kept; flows interleave pseudo-randomly (seeded).  With
+    listen_port, some flows go to local_ip:listen_port (an end host's listener)."""
+    import random
+    rnd = random.Random(seed)
+    flows = []
+    for f in range(nflows):
+        cli = f"10.{1 + f % 7}.{(f * 37) % 250}.{1 + (f * 11) % 250}"
+        srv = f"192.168.{f % 5}.{1 + (f * 13) % 250}"
+        cp, sp = 20000 + f * 7 % 40000, (80, 443, 8080)[f % 3]
+        if listen_port and f % 4 == 3:
+            srv, sp = local_ip, listen_port
+        ic, is_ = rnd.getrandbits(32), rnd.getrandbits(32)
+        mss = struct.pack("!BBH", 2, 4, 1460)
+        pk = []
+
+        def c2s(flags, seq, ack, pl=b"", opts=b""):
+            pk.append(tcp_frame(cli, srv, cp, sp, pl, flags=flags, seq=seq & 0xFFFFFFFF, ack=ack & 0xFFFFFFFF,
+                                doff=5 + len(opts) // 4, tcp_opts=opts, ip_id=len(pk)))
+
+        def s2c(flags, seq, ack, pl=b"", opts=b""):
+            pk.append(tcp_frame(srv, cli, sp, cp, pl, flags=flags, seq=seq & 0xFFFFFFFF, ack=ack & 0xFFFFFFFF,
+                                doff=5 + len(opts) // 4, tcp_opts=opts, ip_id=len(pk)))
+
+        c2s(0x02, ic, 0, opts=mss)                       # SYN
+        s2c(0x12, is_, ic + 1, opts=mss)                 # SYN-ACK
+        c2s(0x10, ic + 1, is_ + 1)                       # ACK
+        cs, ss = ic + 1, is_ + 1
+        for r in range(rnd.randint(1, 4)):
+            pl = bytes(rnd.getrandbits(8) for _ in range(rnd.choice((1, 100, 536, 1400))))
+            c2s(0x18, cs, ss, pl)
+            if rnd.random() < 0.2:
+                c2s(0x18, cs, ss, pl)                    # retransmission
+            cs += len(pl)
+            pl = bytes(rnd.getrandbits(8) for _ in range(rnd.choice((0, 64, 1000))))
+            s2c(0x18 if pl else 0x10, ss, cs, pl)
+            ss += len(pl)
+        if f % 5 == 4:
+            c2s(0x14, cs, ss)                            # RST
+        else:
+            c2s(0x11, cs, ss)                            # FIN
+            s2c(0x11, ss, cs + 1)
+            c2s(0x10, cs + 1, ss + 1)
+        flows.append(pk)
+    extra = [
+        tcp_frame("10.9.9.9", "192.168.9.9", 5555, 80, b"orphan", flags=0x18, seq=99),
+        tcp_frame("10.9.9.8", "192.168.9.9", 5556, 80, b"orphan", flags=0x10, seq=7),
+        tcp_frame("10.9.9.7", "192.168.9.9", 5557, 80, b"x" * 300, flags=0x18, ip_csum=0x1234),
+        tcp_frame("10.9.9.6", "192.168.9.9", 5558, 80, b"y" * 301, flags=0x18, tcp_csum=0x4321),
+        tcp_frame("10.9.9.6", "192.168.9.9", 5558, 80, b"syn", flags=0x02, tcp_csum=0x4322),
+        tcp_frame("10.9.9.5", "192.168.9.9", 5559, 80, b"z" * 64, flags=0x18, ihl=7),
+        tcp_frame("10.9.9.4", "192.168.9.9", 5560, 80, b"", flags=0x10, doff=4, tot_len=36),
+        tcp_frame("10.9.9.3", "192.168.9.9", 5561, 80, b"", flags=0x10, tot_len=19, pad_to=60),
+        tcp_frame("10.9.9.2", "192.168.9.9", 5562, 80, b"v6", flags=0x10, version=6),
+        tcp_frame("10.9.9.2", "192.168.9.9", 5562, 80, b"arp", ethertype=ETH_ARP, pad_to=60),
+        tcp_frame("10.9.9.2", "192.168.9.9", 5562, 80, b"ipv6", ethertype=0x86DD, pad_to=60),
+        tcp_frame("10.9.9.1", "192.168.9.9", 5563, 53, b"udp" * 10, proto=17),
+        icmp_frame("10.9.9.1", local_ip, 8),
+        icmp_frame("10.9.9.1", "192.168.9.9", 8),
+        icmp_frame("10.9.9.1", local_ip, 0, ip_csum=0x0101),
+        tcp_frame("10.9.9.0", "192.168.9.8", 5564, 80, b"rst", flags=0x04, seq=5),
+    ]
+    out, cursors = [], [0] * len(flows)
+    live = list(range(len(flows)))
+    while live:
+        i = rnd.choice(live)
+        out.append(flows[i][cursors[i]])
+        cursors[i] += 1
+        if cursors[i] == len(flows[i]):
+            live.remove(i)
+        if extra and rnd.random() < 0.04:
+            out.append(extra.pop(0))
+    return out + extra

@@ -138,15 +138,16 @@ def test_gpu_module_config_validation():
     L = mosrx.lib()
     cfg = mosrx.ModuleCfg()
     L.mosrx_gpu_module_cfg_default(C.byref(cfg))
-    assert (cfg.batch, cfg.tx_batch, cfg.group, cfg.pipeline) == (32768, 64, 1, 1)
+    # group 0 = auto: as many batches per launch as the source has ready, up to group_bytes
+    assert (cfg.batch, cfg.tx_batch, cfg.group, cfg.group_bytes, cfg.pipeline) == (32768, 64, 0, 0, 1)
     cfg.num_ifs = 1
-    for field, bad in [("group", 0), ("group", 257), ("max_frame", 63), ("num_ifs", 17)]:
+    for field, bad in [("group", 257), ("max_frame", 63), ("num_ifs", 17), ("bpf_nprog", 33)]:
         c2 = mosrx.ModuleCfg.from_buffer_copy(cfg)
         setattr(c2, field, bad)
         assert L.mosrx_gpu_module_configure(C.byref(c2)) == -22, field
     c2 = mosrx.ModuleCfg.from_buffer_copy(cfg)
-    c2.group, c2.bpf_nprog = 4, 1                          # monitor filters need one batch per launch
-    assert L.mosrx_gpu_module_configure(C.byref(c2)) == -22
+    c2.group, c2.bpf_nprog = 4, 1                          # with filters a launch takes one batch
+    assert L.mosrx_gpu_module_configure(C.byref(c2)) == 0
 
 
 def test_gpu_module_thread_slots_are_reused():

@@ -1,0 +1,161 @@
+"""mOS running with the GPU verdicts: csrc/mos_rx.c against mOS's own ProcessPacket.
+
+oracle/_ref/mos_app is mOS itself -- mtcp_init from a mos.conf, an mTCP thread
+in RunMainLoop, monitor sockets with callbacks and BPF filters, an end-host
+listener -- with gpu_module_func as its I/O module and everything it sends
+going out through the backend's TX into a pcap dump.  RunMainLoop's per-frame
+call (core.c:906) goes either to mOS's ProcessPacket ("pp": every check on
+the CPU) or to mosrx_mos_process_packet ("gpu": the checks' outcome from the
+GPU records, eth_in.c / ip_in.c / tcp.c side effects reproduced, then the
+stream step of tcp.c:445-514).  Both runs of a scenario must agree on
+everything mOS does: each frame's return value, NETSTAT, every callback with
+the packet it saw, the flow table after the last frame, and every frame sent
+(forwards, RSTs, ICMP replies).
+
+The CPU leg runs oracle/_ref/mos_app_emul, the same program over a stand-in
+for the GPU (oracle/gpu_emul.c: the oracle makes the records); the GPU leg
+runs the real kernels.  Scenarios cover forward 0/1 (simple_firewall runs
+with 1), stream monitors with and without SYN / orphan filters, raw monitors
+with and without a filter (filters evaluated on the GPU from the match
+masks), an end-host listener (RSTs for orphans), no socket at all (nothing
+verified, everything forwarded), a filter bound and a monitor created in the
+middle of a batch (the batch classified again), and batches of 1..N per
+launch.
+"""
+import os
+import struct
+import subprocess
+
+import pytest
+
+import pktlib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "_ref")
+APP = os.path.join(REF, "mos_app")
+APP_EMUL = os.path.join(REF, "mos_app_emul")
+
+CONF = """mos {{
+	forward = {forward}
+	netdev {{
+		lo 0x0001
+	}}
+	mos_log = {log}/
+	arp_table {{
+		0.0.0.0/0 02:00:00:00:00:aa
+	}}
+	route_table {{
+		0.0.0.0/0 lo
+	}}
+	nic_forward_table {{
+		lo lo
+	}}
+	max_concurrency = 20000
+	tcp_tw_interval = 0
+	tcp_timeout = -1
+}}
+"""
+
+SCENARIOS = {
+    # simple_firewall's stack: one stream monitor, forward = 1 (setup.sh:135)
+    "monitor_fwd": dict(forward=1, env={}),
+    "monitor_nofwd": dict(forward=0, env={}),
+    "filters": dict(forward=1, env={"MOSAPP_RAW": "tcp port 80", "MOSAPP_SYN": "tcp port 80 or tcp port 443",
+                                    "MOSAPP_ORPHAN": "net 10.9.0.0/16"}),
+    "two_monitors_raw": dict(forward=1, env={"MOSAPP_MONITORS": "2", "MOSAPP_RAW_NOFILTER": "1"}),
+    "listener": dict(forward=1, env={"MOSAPP_LISTEN": "8080"}, listen=8080),
+    "no_socket": dict(forward=1, env={"MOSAPP_MONITORS": "0"}),
+    "late_filter": dict(forward=1, env={"MOSAPP_RAW": "tcp[tcpflags] & tcp-syn != 0", "MOSAPP_LATE_RAW_AT": "150"}),
+    "late_monitor": dict(forward=1, env={"MOSAPP_MONITORS": "0", "MOSAPP_LATE_MON_AT": "200"}),
+    "batch_1_per_launch": dict(forward=1, env={"MOSAPP_GROUP": "1", "MOSAPP_BATCH": "97"}),
+    "groups_of_3": dict(forward=1, env={"MOSAPP_GROUP": "3", "MOSAPP_BATCH": "61"}),
+}
+
+
+def pcap_frames(path):
+    """The frames of a classic pcap file (record timestamps are wall time: left out)."""
+    raw = open(path, "rb").read()
+    out, pos = [], 24
+    while pos + 16 <= len(raw):
+        _, _, incl, _ = struct.unpack("<IIII", raw[pos:pos + 16])
+        out.append(raw[pos + 16:pos + 16 + incl])
+        pos += 16 + incl
+    return out
+
+
+def run_app(exe, mode, tmp, name, sc, frames, extra_env=None):
+    d = tmp / f"{name}_{mode}"
+    d.mkdir()
+    log = tmp / f"{name}_{mode}_log"
+    log.mkdir()
+    conf = tmp / f"{name}_{mode}.conf"
+    conf.write_text(CONF.format(forward=sc["forward"], log=log))
+    trace = tmp / f"{name}.mrxt"
+    if not trace.exists():
+        buf, off, ln = pktlib.pack_frames(frames)
+        pktlib.write_ref_trace(str(trace), buf, off, ln, forward=sc["forward"])
+    env = dict(os.environ, **sc["env"], **(extra_env or {}))
+    r = subprocess.run([exe, mode, str(conf), str(trace), str(d)], capture_output=True, text=True, timeout=120,
+                       env=env)
+    assert r.returncode == 0, f"{mode}: rc {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}"
+    import json
+    stats = json.loads(r.stdout.strip().splitlines()[-1])
+    return dict(returns=(d / "returns.bin").read_bytes(), state=(d / "state.txt").read_text(),
+                callbacks=(d / "callbacks.txt").read_text(), tx=pcap_frames(d / "tx.pcap"), stats=stats)
+
+
+def compare_modes(exe, tmp, name, nflows=64):
+    sc = SCENARIOS[name]
+    frames = pktlib.conversation_frames(nflows, seed=11, listen_port=sc.get("listen", 0))
+    pp = run_app(exe, "pp", tmp, name, sc, frames)
+    gpu = run_app(exe, "gpu", tmp, name, sc, frames)
+    assert len(pp["returns"]) == len(frames)
+    assert gpu["returns"] == pp["returns"], "per-frame return values"
+    assert gpu["state"] == pp["state"], "flow table / NETSTAT"
+    assert gpu["callbacks"] == pp["callbacks"], "callbacks"
+    assert gpu["tx"] == pp["tx"], "frames sent"
+    assert gpu["stats"]["consumer_frames"] == len(frames)
+    return pp, gpu
+
+
+def _have(exe):
+    return os.access(exe, os.X_OK)
+
+
+@pytest.mark.skipif(not _have(APP_EMUL), reason="needs oracle/_ref/mos_app_emul (make -C oracle ref)")
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_consumer_matches_processpacket_emulated(tmp_path, name):
+    pp, gpu = compare_modes(APP_EMUL, tmp_path, name)
+    _check_scenario(name, pp, gpu)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have(APP), reason="needs oracle/_ref/mos_app (built by make -C oracle ref)")
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_consumer_matches_processpacket_on_gpu(tmp_path, name):
+    pp, gpu = compare_modes(APP, tmp_path, name)
+    _check_scenario(name, pp, gpu)
+
+
+def _check_scenario(name, pp, gpu):
+    """What each scenario must have exercised (so a scenario cannot pass vacuously)."""
+    st, cb = gpu["stats"], pp["callbacks"]
+    nstat = pp["state"].splitlines()[-1].split()
+    assert int(nstat[6]) > 0                                   # rx_errors: bad checksums etc. were seen
+    if name in ("monitor_fwd", "filters", "two_monitors_raw", "listener", "late_filter", "batch_1_per_launch",
+                "groups_of_3"):
+        assert " ev 4 " in cb and " ev 1 " in cb               # MOS_ON_CONN_START, MOS_ON_PKT_IN
+        assert st["stream_step"] > 0
+    if name == "monitor_nofwd":
+        assert all(f[12:14] == b"\x08\x06" for f in pp["tx"])  # forward = 0: only mOS's own ARP requests leave
+    if name in ("monitor_fwd", "no_socket"):
+        assert len(pp["tx"]) > 0
+    if name == "filters":
+        assert st["filters_gpu"] == 3 and st["filter_installs"] >= 1
+        assert " ev 100 " in cb                                # MOS_ON_ORPHAN through the orphan filter
+    if name == "listener":
+        assert any(f[47] & 0x04 for f in pp["tx"] if len(f) > 47 and f[23] == 6)   # RSTs to orphans
+    if name == "late_filter":
+        assert st["filter_installs"] >= 1 and st["reclassified"] >= 1
+    if name == "late_monitor":
+        assert st["reclassified"] >= 1

@@ -123,6 +123,15 @@ typedef struct mosrx_afpacket_info {
 	uint64_t ring_drops;       /* frames the kernel dropped with every ring block owned by us (ps_drop) */
 } mosrx_afpacket_info;
 int           mosrx_source_afpacket_info(mosrx_source *s, mosrx_afpacket_info *info);
+/* A TPACKET_V3 receive ring (linux/if_packet.h block layout: tpacket_block_desc,
+ * tpacket3_hdr + sockaddr_ll per frame) at `ring`, `nblocks` blocks of
+ * `block_size` bytes (a power of two), mapped by the caller and filled by
+ * someone else -- another process's capture in shared memory, a driver with
+ * the same layout.  Read and lent exactly like the AF_PACKET socket's ring:
+ * blocks whose status has TP_STATUS_USER are taken in order and handed back
+ * with TP_STATUS_KERNEL once their frames are no longer exposed.  The caller
+ * keeps the mapping until mosrx_source_close.  NULL on bad arguments. */
+mosrx_source *mosrx_source_tpacket_v3(void *ring, uint32_t nblocks, uint32_t block_size);
 /* Pull the next frame into dst (at most cap bytes); returns its caplen, 0 when none. */
 int           mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap);
 /* Zero-copy runs (what gpu_module_func lends to the GPU copy): up to max_n

@@ -375,6 +375,8 @@ struct src_afp {
 	uint8_t *ring;
 	uint32_t nblocks;
 	int registered;                 /* ring registered with hipHostRegister: borrow is available */
+	int external;                   /* the ring is the caller's mapping (mosrx_source_tpacket_v3) */
+	uint32_t bsz;                   /* block size */
 	/* cursor: block `blk`, `left` frames not yet taken, next frame at `fp` */
 	uint32_t blk, left;
 	uint8_t *fp;
@@ -389,7 +391,7 @@ struct src_afp {
 
 static struct tpacket_block_desc *afp_block(struct src_afp *s, uint32_t b)
 {
-	return (struct tpacket_block_desc *)(s->ring + (size_t)(b % s->nblocks) * AFP_BLOCK_SIZE);
+	return (struct tpacket_block_desc *)(s->ring + (size_t)(b % s->nblocks) * s->bsz);
 }
 
 static void afp_release_upto(struct src_afp *s, uint32_t upto)
@@ -534,8 +536,8 @@ static void afp_close(struct mosrx_source *s_)
 	struct src_afp *s = (struct src_afp *)s_;
 	if (s->registered)
 		hipHostUnregister(s->ring);
-	if (s->ring && s->ring != MAP_FAILED)
-		munmap(s->ring, (size_t)s->nblocks * AFP_BLOCK_SIZE);
+	if (s->ring && s->ring != MAP_FAILED && !s->external)
+		munmap(s->ring, (size_t)s->nblocks * s->bsz);
 	if (s->fd >= 0)
 		close(s->fd);
 	free(s);
@@ -553,6 +555,7 @@ mosrx_source *mosrx_source_afpacket_ex(const char *ifname, const mosrx_afpacket_
 		return NULL;
 	}
 	s->base.close = afp_close;
+	s->bsz = AFP_BLOCK_SIZE;
 	s->fd = socket(AF_PACKET, SOCK_RAW, htons(ETH_P_ALL));
 	if (s->fd < 0) {
 		free(s);
@@ -602,6 +605,34 @@ mosrx_source *mosrx_source_afpacket_ex(const char *ifname, const mosrx_afpacket_
 	return &s->base;
 }
 
+/* A TPACKET_V3 ring the caller maps and something else fills (a shared-memory
+ * capture, a driver with the same block layout): the same cursor, lending and
+ * give-back as the socket's ring, registered with the HIP runtime the same way
+ * (hipHostRegister of the whole mapping) so runs are lent zero-copy; copying
+ * when the registration fails.  No socket: nothing to send, no statistics. */
+mosrx_source *mosrx_source_tpacket_v3(void *ring, uint32_t nblocks, uint32_t block_size)
+{
+	struct src_afp *s;
+	if (!ring || !nblocks || nblocks > AFP_MAX_BLOCKS || block_size < 4096 || (block_size & (block_size - 1)))
+		return NULL;
+	s = calloc(1, sizeof(*s));
+	if (!s)
+		return NULL;
+	s->base.close = afp_close;
+	s->base.next = afp_next;
+	s->fd = -1;
+	s->ring = ring;
+	s->external = 1;
+	s->nblocks = nblocks;
+	s->bsz = block_size;
+	if (hipHostRegister(s->ring, (size_t)nblocks * block_size, hipHostRegisterDefault) == hipSuccess) {
+		s->registered = 1;
+		s->base.borrow = afp_borrow;
+		s->base.give_back = afp_give_back;
+	}
+	return &s->base;
+}
+
 mosrx_source *mosrx_source_afpacket(const char *ifname)
 {
 	return mosrx_source_afpacket_ex(ifname, NULL);
@@ -615,12 +646,12 @@ int mosrx_source_afpacket_info(mosrx_source *s_, mosrx_afpacket_info *info)
 	struct tpacket_stats_v3 st;
 	socklen_t sl = sizeof(st);
 	memset(&st, 0, sizeof(st));
-	if (getsockopt(s->fd, SOL_PACKET, PACKET_STATISTICS, &st, &sl) == 0) {   /* pcap_stats' source */
+	if (s->fd >= 0 && getsockopt(s->fd, SOL_PACKET, PACKET_STATISTICS, &st, &sl) == 0) {   /* pcap_stats' source */
 		s->ring_packets += st.tp_packets;
 		s->ring_drops += st.tp_drops;
 	}
 	info->zero_copy = s->registered;
-	info->ring_bytes = (uint64_t)s->nblocks * AFP_BLOCK_SIZE;
+	info->ring_bytes = (uint64_t)s->nblocks * s->bsz;
 	info->dropped_outgoing = s->dropped_outgoing;
 	info->ring_packets = s->ring_packets;
 	info->ring_drops = s->ring_drops;

@@ -229,6 +229,7 @@ def lib():
             "mosrx_last_kernel_ms": (I, [P, C.POINTER(C.c_float)]),
             "mosrx_source_afpacket_ex": (P, [C.c_char_p, C.POINTER(AfpOpts)]),
             "mosrx_source_afpacket_info": (I, [P, C.POINTER(AfpInfo)]),
+            "mosrx_source_tpacket_v3": (P, [P, U32, U32]),
             "mosrx_source_send": (I, [P, P, U32]),
             "mosrx_source_tx_pcap": (I, [P, C.c_char_p]),
             "mosrx_source_tx_flush": (I, [P]),

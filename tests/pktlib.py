@@ -221,3 +221,52 @@ def conversation_frames(nflows: int = 64, seed: int = 7, *, listen_port: int = 0
         if extra and rnd.random() < 0.04:
             out.append(extra.pop(0))
     return out + extra
+
+
+class TpacketRing:
+    """A TPACKET_V3 receive ring in a shared memfd mapping, filled the way the
+    kernel fills an AF_PACKET PACKET_RX_RING (linux/if_packet.h): each block a
+    tpacket_block_desc (48 B) then frames, each frame a tpacket3_hdr (48 B) +
+    sockaddr_ll, its Ethernet header at offset 82 (network header 16-byte
+    aligned, TPACKET3_HDRLEN + 16 rounded), block_status TP_STATUS_USER (1) when
+    handed to the reader, TP_STATUS_KERNEL (0) when given back."""
+
+    def __init__(self, nblocks: int, block_size: int):
+        import mmap
+        import os
+        self.nb, self.bsz = nblocks, block_size
+        self.fd = os.memfd_create("mosrx-tpacket-ring")
+        os.ftruncate(self.fd, nblocks * block_size)
+        self.m = mmap.mmap(self.fd, nblocks * block_size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        import ctypes
+        self._anchor = ctypes.c_char.from_buffer(self.m)
+        self.addr = ctypes.addressof(self._anchor)
+        self.seq = 0
+
+    def status(self, b: int) -> int:
+        return struct.unpack_from("<I", self.m, b * self.bsz + 8)[0]
+
+    def fill(self, b: int, frames: list[bytes]) -> int:
+        """Write as many of `frames` as fit into block b and hand it over; returns the count."""
+        base, pos, k = b * self.bsz, 48, 0
+        for f in frames:
+            rec = (82 + len(f) + 15) & ~15
+            if pos + rec > self.bsz:
+                break
+            hdr = struct.pack("<IIIIIIHH", rec, 0, 0, len(f), len(f), 1, 82, 96) + b"\0" * 20
+            sll = struct.pack("<HHiHBB8s", 17, 0x0300, 1, 1, 0, 6, b"")          # sll_pkttype 0: PACKET_HOST
+            self.m[base + pos:base + pos + 48] = hdr
+            self.m[base + pos + 48:base + pos + 68] = sll
+            self.m[base + pos + 82:base + pos + 82 + len(f)] = f
+            pos += rec
+            k += 1
+        self.seq += 1
+        struct.pack_into("<IIIIIIQ", self.m, base, 3, 0, 0, k, 48, pos, self.seq)
+        struct.pack_into("<I", self.m, base + 8, 1)                              # TP_STATUS_USER, last
+        return k
+
+    def close(self):
+        import os
+        del self._anchor
+        self.m.close()
+        os.close(self.fd)

@@ -191,3 +191,33 @@ def test_pcap_source_replays_and_stops_at_a_truncated_record():
         src = mosrx.lib().mosrx_source_pcap(empty.encode(), 5)
         assert _drain(src) == []
         mosrx.lib().mosrx_source_close(src)
+
+
+def test_module_struct_layouts_match_the_header(tmp_path):
+    """The ctypes mirrors of the backend's structs have the C sizes and offsets."""
+    import subprocess
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mosrx_io_module.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(mosrx_gpu_module_cfg),'
+                   ' offsetof(mosrx_gpu_module_cfg, group_bytes), sizeof(mosrx_gpu_module_stats),'
+                   ' offsetof(mosrx_gpu_module_stats, device), sizeof(mosrx_rx_state), sizeof(mosrx_bpf_set_arg));'
+                   'return 0;}\n')
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", "-I" + os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
+    assert got == [C.sizeof(mosrx.ModuleCfg), mosrx.ModuleCfg.group_bytes.offset, C.sizeof(mosrx.ModuleStats),
+                   mosrx.ModuleStats.device.offset, 20, 16]
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "mos_rx_mos.o")),
+                    reason="needs oracle/_ref (make -C oracle ref)")
+def test_mos_rx_consumer_exports_its_header():
+    """include/mosrx_mos_rx.h's functions are defined by csrc/mos_rx.c as built inside
+    mOS's tree (the object a maintainer links into libmtcp)."""
+    import subprocess
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "mosrx_mos_rx.h")).read(), flags=re.S)
+    want = set(re.findall(r"\b(mosrx_[a-z0-9_]+)\s*\(", txt))
+    nm = subprocess.run(["nm", "-g", "--defined-only", os.path.join(ROOT, "oracle", "_ref", "mos_rx_mos.o")],
+                        capture_output=True, text=True, check=True).stdout
+    have = {ln.split()[-1] for ln in nm.splitlines() if ln.strip()}
+    assert want and want <= have, want - have

@@ -430,6 +430,67 @@ def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
             "sample": f"{reps} passes over one {tr.n}-frame batch ({el:.1f} s), oracle {fn}, 1 thread"}
 
 
+MOS_CONF = """mos {{
+	forward = 1
+	netdev {{
+		lo 0x0001
+	}}
+	mos_log = {log}/
+	arp_table {{
+		0.0.0.0/0 02:00:00:00:00:aa
+	}}
+	route_table {{
+		0.0.0.0/0 lo
+	}}
+	nic_forward_table {{
+		lo lo
+	}}
+	max_concurrency = 20000
+	tcp_tw_interval = 0
+	tcp_timeout = -1
+}}
+"""
+
+
+def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, timeout: float = 60.0):
+    """mOS's own rx loop on one host core (oracle/_ref/mos_app: mtcp_init, an
+    mTCP thread in RunMainLoop, simple_firewall's stack -- one stream monitor,
+    forward = 1 -- with gpu_module_func as the I/O module), its per-frame CPU
+    time (core.c:902-907, timed per batch) with mOS's ProcessPacket on every
+    frame ("pp") and with csrc/mos_rx.c taking the checks from the GPU records
+    ("gpu"), on the same frames.  The difference is the CPU time per frame the
+    GPU saves inside mOS.  A reported baseline; None when the binary did not
+    travel with the tree."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "mos_app")
+    if not os.access(exe, os.X_OK):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import tempfile
+    import pktlib
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        trace = os.path.join(td, "t.mrxt")
+        pktlib.write_ref_trace(trace, tr.frames[:tr.frames_bytes], tr.off, tr.len, forward=1)
+        for mode in ("pp", "gpu"):
+            d = os.path.join(td, mode)
+            os.makedirs(os.path.join(d, "log"))
+            conf = os.path.join(d, "mos.conf")
+            with open(conf, "w") as fh:
+                fh.write(MOS_CONF.format(log=os.path.join(d, "log")))
+            env = dict(os.environ, MOSAPP_QUIET="1", MOSAPP_LOOPS=str(loops), MOSAPP_BATCH="8192")
+            try:
+                r = subprocess.run([exe, mode, conf, trace, d], capture_output=True, text=True, timeout=timeout,
+                                   env=env)
+                out[mode] = json.loads(r.stdout.strip().splitlines()[-1])
+            except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+                return None
+    pp, gp = out["pp"]["rx_ns_per_frame"], out["gpu"]["rx_ns_per_frame"]
+    return {"processpacket_ns_per_frame": round(pp, 1), "gpu_records_ns_per_frame": round(gp, 1),
+            "saved_ns_per_frame": round(pp - gp, 1), "frames": out["pp"]["rx_frames_timed"],
+            "sample": f"{tr.n} frames x {loops} through mOS's RunMainLoop on one core, simple_firewall stack "
+                      f"(1 stream monitor, forward=1), oracle/_ref/mos_app pp vs gpu"}
+
+
 def measure_fw64(ctx, seconds: float):
     """BASELINE config #1: simple_firewall's rx path on ONE core, 10 000 x 60 B
     frames of one flow, the firewall's stack state (num_msp=1, forward=1,
@@ -693,6 +754,13 @@ def main():
         ref = cpu_reference(traces[head], head, 5.0, process_packet=True)
         if ref:
             cpu["reference_processpacket"] = ref
+        # mOS's whole rx loop with and without the GPU records (the CPU the GPU saves inside mOS)
+        rx = cpu_rx_loop_leg(mosrx.Trace(mosrx.TRACE_M1500, 16384), 24)
+        if rx:
+            cpu["mos_rx_loop_M1500"] = rx
+        rx = cpu_rx_loop_leg(mosrx.Trace(mosrx.TRACE_FW64, 10_000), 40)
+        if rx:
+            cpu["mos_rx_loop_FW64"] = rx
         for k in keys:
             if k != head:
                 results[k]["cpu_baseline"] = cpu_baseline(traces[k], k, min_s=2.0)
@@ -780,6 +848,10 @@ def headline_line(detail, h, head, results, e2e):
         for leg in ("all_cores", "reference", "reference_processpacket"):
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("value", "unit", "cores", "kind", "mpkts") if k in cpu[leg]}
+        for leg in ("mos_rx_loop_M1500", "mos_rx_loop_FW64"):
+            if cpu.get(leg):
+                cpu_line[leg] = {k: cpu[leg][k] for k in ("processpacket_ns_per_frame", "gpu_records_ns_per_frame",
+                                                          "saved_ns_per_frame")}
     sec = {}
     for k, r in results.items():
         if k == head:

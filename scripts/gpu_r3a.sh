@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out/r3a
 timeout -k 10 420 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
-    tests/test_mos_consumer.py tests/test_backend_gpu.py > gpurun_out/r3a/pytest.log 2>&1
+    tests/test_mos_consumer.py tests/test_tpacket_ring.py tests/test_backend_gpu.py > gpurun_out/r3a/pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

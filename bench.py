@@ -589,17 +589,20 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     consumed.  The kernels are timed with HIP events (device time per batch);
     the host loop's rate is reported beside it.  Never the bench value."""
     ctx_batch = {"S64": 32_768, "M1500": 65_536, "IMIX": 262_144}[key]
-    if group > 1:
+    if group != 1:
         # a group's batches must be distinct frames: replaying one batch would let
         # the group's copy carry it once and the kernel re-read it from cache
+        # (group 0 = the module's default, auto: as many batches per launch as are
+        # ready, up to MOSRX_GROUP_AUTO_BYTES of frames -- ~58 of 64 B, 1 of 1500 B)
+        nb = group or {"S64": 64, "M1500": 4, "IMIX": 4}[key]
         tr = mosrx.Trace({"S64": mosrx.TRACE_S64, "M1500": mosrx.TRACE_M1500,
-                          "IMIX": mosrx.TRACE_IMIX}[key], ctx_batch * group)
+                          "IMIX": mosrx.TRACE_IMIX}[key], ctx_batch * nb)
     loops = max(1, frames_target // tr.n)
     src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
     be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
                           group=group, timing=True)
     try:
-        be.run_loop(max_pkts=2 * ctx_batch * group)    # warm-up: staging sized, module loaded
+        be.run_loop(max_pkts=2 * ctx_batch * max(group, 64 if key == "S64" else 4))    # warm-up: staging sized, module loaded
         st0 = be.stats()
         t0 = time.perf_counter()
         st = be.run_loop()
@@ -616,7 +619,8 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     ab = algo_bytes(tr) * (ctx_batch / tr.n)
     return {"mpkts": n / dt / 1e6, "gbps": nb * algo_bytes(tr) / dt / 1e9, "frames": n, "seconds": round(dt, 3),
             "distinct_frames": tr.n,
-            "group": group, "kernel_launches": int(launches), "batches": int(batches),
+            "group": group if group else "auto", "batches_per_launch": round(batches / max(launches, 1), 2),
+            "kernel_launches": int(launches), "batches": int(batches),
             "device_us_per_batch": round(dev_us, 3),
             "device_roofline_frac": round(ab / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if dev_us > 0 else None,
             "method": f"mosrx_rx_loop over gpu_module_func (pipelined, {group} batch(es) per launch), "
@@ -729,12 +733,15 @@ def main():
     if not args.no_e2e and "M1500" in traces:
         e2e = {k: measure_e2e(ctx, traces[k], {"M1500": 60, "S64": 800}[k]) for k in ("M1500", "S64") if k in traces}
         # the gpu_module_func backend itself (host thread = this rank)
-        e2e["backend"] = {k: measure_backend(traces[k], k, {"S64": 16_000_000, "M1500": 2_000_000}.get(k, 4_000_000),
-                                             device)
+        # the module's default configuration (cfg.group auto: batches per launch sized to what is ready)
+        e2e["backend"] = {k: measure_backend(traces[k], k, {"S64": 32_000_000, "M1500": 2_000_000}.get(k, 4_000_000),
+                                             device, group=0)
                           for k in ("M1500", "S64", "IMIX") if k in traces}
-        # the launch-amortised rx ring: a group of batches per launch (cfg.group)
+        # one launch per batch, and explicit rings (cfg.group)
         if "S64" in traces:
+            e2e["backend"]["S64_group1"] = measure_backend(traces["S64"], "S64", 16_000_000, device, group=1)
             e2e["backend"]["S64_group128"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=128)
+        e2e["backend"]["M1500_group1"] = measure_backend(traces["M1500"], "M1500", 2_000_000, device, group=1)
         e2e["backend"]["M1500_group8"] = measure_backend(traces["M1500"], "M1500", 4_000_000, device, group=8)
         # one mTCP thread per core, each with its own context / source / rx loop
         # (one GPU's host side: single-rank runs only)

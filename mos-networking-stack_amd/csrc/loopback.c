@@ -147,8 +147,10 @@ static uint32_t mem_borrow(struct mosrx_source *s_, uint32_t max_n, uint32_t max
 static void mem_close(struct mosrx_source *s_)
 {
 	struct src_mem *s = (struct src_mem *)s_;
-	if (s->pinned)
+	if (s->pinned) {
+		mosrx__host_range_del(s->frames);
 		hipHostFree(s->frames);
+	}
 	else
 		free(s->frames);
 	free(s->off);
@@ -168,8 +170,10 @@ mosrx_source *mosrx_source_mem(const uint8_t *frames, const uint32_t *off, const
 		total += ((uint64_t)len[i] + 15) & ~15ull;
 	total += 16;
 	/* pinned when a HIP device is present (zero-copy batches), else plain */
-	if (hipHostMalloc((void **)&s->frames, total, hipHostMallocPortable) == hipSuccess)
+	if (hipHostMalloc((void **)&s->frames, total, hipHostMallocPortable) == hipSuccess) {
 		s->pinned = 1;
+		mosrx__host_range_add(s->frames, total);
+	}
 	else
 		s->frames = malloc(total);
 	s->off = malloc((size_t)(n ? n : 1) * 4);
@@ -534,8 +538,10 @@ static int afp_send(struct mosrx_source *s_, const uint8_t *frame, uint32_t len)
 static void afp_close(struct mosrx_source *s_)
 {
 	struct src_afp *s = (struct src_afp *)s_;
-	if (s->registered)
+	if (s->registered) {
+		mosrx__host_range_del(s->ring);
 		hipHostUnregister(s->ring);
+	}
 	if (s->ring && s->ring != MAP_FAILED && !s->external)
 		munmap(s->ring, (size_t)s->nblocks * s->bsz);
 	if (s->fd >= 0)
@@ -599,6 +605,7 @@ mosrx_source *mosrx_source_afpacket_ex(const char *ifname, const mosrx_afpacket_
 	if (!(o && o->copy) &&
 	    hipHostRegister(s->ring, (size_t)nb * AFP_BLOCK_SIZE, hipHostRegisterDefault) == hipSuccess) {
 		s->registered = 1;
+		mosrx__host_range_add(s->ring, (uint64_t)nb * AFP_BLOCK_SIZE);
 		s->base.borrow = afp_borrow;
 		s->base.give_back = afp_give_back;
 	}
@@ -627,6 +634,7 @@ mosrx_source *mosrx_source_tpacket_v3(void *ring, uint32_t nblocks, uint32_t blo
 	s->bsz = block_size;
 	if (hipHostRegister(s->ring, (size_t)nblocks * block_size, hipHostRegisterDefault) == hipSuccess) {
 		s->registered = 1;
+		mosrx__host_range_add(s->ring, (uint64_t)nblocks * block_size);
 		s->base.borrow = afp_borrow;
 		s->base.give_back = afp_give_back;
 	}

@@ -11,6 +11,9 @@
 #include <string.h>
 
 #include "mosrx_ctx.h"
+#include "mosrx_source.h"
+
+#include <pthread.h>
 
 /* Default cache policy per access class (bit 0: header windows non-temporal,
  * bit 1: tail stream non-temporal), chosen from measurements on MI355X. */
@@ -500,6 +503,8 @@ static uint64_t batch_span(const mosrx_batch *b, const uint8_t **lo_out)
 		return 0;
 	if ((uint64_t)(hi - lo) > span_limit(b->frames_bytes, b->n))
 		return 0;
+	if (!mosrx__host_range_of(lo, (uint64_t)(hi - lo)))   /* the span must lie in one pinned allocation */
+		return 0;
 	*lo_out = lo;
 	return (uint64_t)(hi - lo);
 }
@@ -714,14 +719,16 @@ int mosrx_last_kernel_ms(mosrx_ctx *c, float *ms)
 }
 
 /* ---- a group of host batches in one launch (gpu_module_func's rx ring) ---- */
-struct region { const uint8_t *lo; uint64_t len; int own; uint8_t *dev; };
+struct region { const uint8_t *lo; uint64_t len; int own; uint8_t *dev; uint64_t alloc; };
 
 /* Device copies of every region of the group: regions in address order are
  * gathered into copy runs wherever the gap to the next one is under an eighth
- * of the run + 4 KiB (packed stages, or consecutive runs lent by one source),
- * and each run keeps its host address modulo 256 on the device, so a frame
- * buffer stays 16-byte aligned.  A frame buffer that is not 16-byte aligned on
- * the host is copied on its own to an aligned device address. */
+ * of the run + 4 KiB (packed stages, or consecutive runs lent by one source)
+ * and both lie in the same known pinned allocation (so no copy spans two
+ * allocations or an unmapped gap between them), and each run keeps its host
+ * address modulo 256 on the device, so a frame buffer stays 16-byte aligned.
+ * A frame buffer that is not 16-byte aligned on the host is copied on its own
+ * to an aligned device address. */
 static int group_copy(struct slot *s, struct region *r, uint32_t nr, uint64_t *dev_bytes, int issue)
 {
 	uint32_t i, j;
@@ -736,8 +743,8 @@ static int group_copy(struct slot *s, struct region *r, uint32_t nr, uint64_t *d
 		const uint8_t *lo = ord[i]->lo, *hi = lo + ord[i]->len;
 		uint64_t base;
 		j = i + 1;
-		if (!ord[i]->own)
-			while (j < nr && !ord[j]->own &&
+		if (!ord[i]->own && ord[i]->alloc)
+			while (j < nr && !ord[j]->own && ord[j]->alloc == ord[i]->alloc &&
 			       (uint64_t)(ord[j]->lo > hi ? ord[j]->lo - hi : 0) <= ((uint64_t)(hi - lo) >> 3) + 4096) {
 				if (ord[j]->lo + ord[j]->len > hi)
 					hi = ord[j]->lo + ord[j]->len;
@@ -782,9 +789,12 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 		ntot += b[i].n;
 		if (!b[i].n)
 			continue;
-		r[nr++] = (struct region){b[i].frames, b[i].frames_bytes, ((uintptr_t)b[i].frames & 15) != 0, NULL};
-		r[nr++] = (struct region){(const uint8_t *)b[i].off, (uint64_t)b[i].n * 4, 0, NULL};
-		r[nr++] = (struct region){(const uint8_t *)b[i].len, (uint64_t)b[i].n * 2, 0, NULL};
+		r[nr++] = (struct region){b[i].frames, b[i].frames_bytes, ((uintptr_t)b[i].frames & 15) != 0, NULL,
+		                          mosrx__host_range_of(b[i].frames, b[i].frames_bytes)};
+		r[nr++] = (struct region){(const uint8_t *)b[i].off, (uint64_t)b[i].n * 4, 0, NULL,
+		                          mosrx__host_range_of(b[i].off, (uint64_t)b[i].n * 4)};
+		r[nr++] = (struct region){(const uint8_t *)b[i].len, (uint64_t)b[i].n * 2, 0, NULL,
+		                          mosrx__host_range_of(b[i].len, (uint64_t)b[i].n * 2)};
 	}
 	if (ntot == 0) {
 		memset(s->h_cnt, 0, MOSRX_CNT_WORDS * 4);
@@ -916,12 +926,59 @@ int mosrx_dev_free(mosrx_ctx *c, void *dptr)
 	return 0;
 }
 
+/* ---- pinned host ranges (mosrx_source.h) ---------------------------------- */
+#define MAX_RANGES 4096
+static struct { uintptr_t lo, hi; uint64_t id; } g_ranges[MAX_RANGES];
+static uint32_t g_nranges;
+static uint64_t g_range_seq;
+static pthread_mutex_t g_range_lock = PTHREAD_MUTEX_INITIALIZER;
+
+void mosrx__host_range_add(const void *p, uint64_t len)
+{
+	pthread_mutex_lock(&g_range_lock);
+	if (p && len && g_nranges < MAX_RANGES) {
+		g_ranges[g_nranges].lo = (uintptr_t)p;
+		g_ranges[g_nranges].hi = (uintptr_t)p + len;
+		g_ranges[g_nranges].id = ++g_range_seq;
+		g_nranges++;
+	}
+	pthread_mutex_unlock(&g_range_lock);
+}
+
+void mosrx__host_range_del(const void *p)
+{
+	uint32_t i;
+	pthread_mutex_lock(&g_range_lock);
+	for (i = 0; i < g_nranges; i++)
+		if (g_ranges[i].lo == (uintptr_t)p) {
+			g_ranges[i] = g_ranges[--g_nranges];
+			break;
+		}
+	pthread_mutex_unlock(&g_range_lock);
+}
+
+uint64_t mosrx__host_range_of(const void *p, uint64_t len)
+{
+	const uintptr_t a = (uintptr_t)p, b = a + len;
+	uint64_t id = 0;
+	uint32_t i;
+	pthread_mutex_lock(&g_range_lock);
+	for (i = 0; i < g_nranges; i++)
+		if (a >= g_ranges[i].lo && b <= g_ranges[i].hi && b >= a) {
+			id = g_ranges[i].id;
+			break;
+		}
+	pthread_mutex_unlock(&g_range_lock);
+	return id;
+}
+
 int mosrx_host_alloc(mosrx_ctx *c, size_t bytes, void **hptr)
 {
 	if (!c || !hptr)
 		return -EINVAL;
 	if (hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
 		return -ENOMEM;
+	mosrx__host_range_add(*hptr, bytes ? bytes : 1);
 	return 0;
 }
 
@@ -929,6 +986,7 @@ int mosrx_host_free(mosrx_ctx *c, void *hptr)
 {
 	if (!c)
 		return -EINVAL;
+	mosrx__host_range_del(hptr);
 	HIPCHK(hipHostFree(hptr));
 	return 0;
 }

@@ -37,4 +37,14 @@ struct mosrx_source {
 	uint64_t tx_packets, tx_bytes, tx_errors;
 };
 
+/* Pinned host ranges the library knows (mosrx_host_alloc, the sources' pinned
+ * replay buffers and registered rings): host regions are merged into one
+ * PCIe copy only when one known range holds them all, so a copy never spans
+ * two allocations or the gap between them (mosrx_api.c group_copy /
+ * batch_span).  range_of: the range's id, 0 when no known range holds
+ * [p, p + len). */
+void     mosrx__host_range_add(const void *p, uint64_t len);
+void     mosrx__host_range_del(const void *p);
+uint64_t mosrx__host_range_of(const void *p, uint64_t len);
+
 #endif

@@ -221,3 +221,25 @@ def test_mos_rx_consumer_exports_its_header():
                         capture_output=True, text=True, check=True).stdout
     have = {ln.split()[-1] for ln in nm.splitlines() if ln.strip()}
     assert want and want <= have, want - have
+
+
+def test_pinned_range_registry():
+    """Host regions are merged into one PCIe copy only inside one known pinned
+    allocation (a borrowed run next to the staging block must not be
+    copied together with it): the registry answers which allocation holds a span."""
+    L = mosrx.lib()
+    add, dele, of = L.mosrx__host_range_add, L.mosrx__host_range_del, L.mosrx__host_range_of
+    add.argtypes, dele.argtypes, of.argtypes = [C.c_void_p, C.c_uint64], [C.c_void_p], [C.c_void_p, C.c_uint64]
+    add.restype, dele.restype, of.restype = None, None, C.c_uint64
+    a, b = 0x7F0000000000, 0x7F0000100000            # two adjacent "allocations" of 1 MiB
+    add(a, 1 << 20)
+    add(b, 1 << 20)
+    try:
+        ia, ib = of(a, 1 << 20), of(b + 4096, 4096)
+        assert ia and ib and ia != ib
+        assert of(a + (1 << 20) - 16, 32) == 0          # spans the boundary between the two
+        assert of(a - 1, 2) == 0 and of(b + (1 << 20), 1) == 0
+    finally:
+        dele(a)
+        dele(b)
+    assert of(a, 16) == 0 and of(b, 16) == 0

@@ -411,7 +411,11 @@ def _raw_ip(s):
     ("edge", "msp1", 128, 0, 1), ("edge", "noverify_local", 128, 0, 1), ("rand_small", "msp1_local", 64, 0, 1),
     ("rand_mid", "q4_i40e", 100, 2, 1), ("imix_full", "msp1", 32768, 0, 1),
     # several batches per launch (cfg.group), the stack state changing between groups
-    ("rand_mid", "msp1", 32, (0, 8), 1), ("imix_full", "msp1_local", 4096, (16, 4), 0)])
+    ("rand_mid", "msp1", 32, (0, 8), 1), ("imix_full", "msp1_local", 4096, (16, 4), 0),
+    # ... and inside a group (period not a multiple of group: the rest of the group
+    # is classified again before its next batch is handed out); group 0 = auto
+    ("edge", "msp1_local", 32, (1, 8), 0), ("rand_mid", "msp1", 16, (3, 8), 1),
+    ("imix_full", "msp1", 4096, (5, 0), 1), ("edge", "q3_ixgbe", 16, (0, 0), 0)])
 def test_backend_inside_mos_checked_by_processpacket(tmp_path, fix, state, batch, period, forward):
     """gpu_module_func compiled inside mOS's tree (its own io_module.h /
     config.h) and registered as core.c:1725-1736 does, fed from a trace, with
@@ -489,9 +493,11 @@ def _inside_mos(tmp_path, fix, state, batch, period, forward, listen=False):
     assert d["num_queues"] == nq and d["nstat_ok"] == 1
     assert d["compared"] + d["skipped"] == len(off) and d["compared"] > 0.5 * len(off)
     assert d["batches"] == -(-len(off) // batch)
-    if period:                                    # every change caught a group in flight (changes fall on
-        assert period % group == 0                # group boundaries: a group is classified under one state)
+    if period and group and period % group == 0:  # every change caught a group in flight (changes fall on
+        # group boundaries: a group is classified under one state)
         assert d["reclassified"] == (d["batches"] - 1) // period * group
+    elif period:                                  # changes inside groups: the rest of the group again
+        assert d["reclassified"] >= (d["batches"] - 1) // period
     assert d["forward_diff"] == 0
     # with forwarding on, mOS forwards something unless only end-host sockets exist (msp 0, esp > 0)
     assert (d["forwarded_by_mos"] > 0) == bool(forward and (msp or not esp))

@@ -431,7 +431,7 @@ def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
 
 
 MOS_CONF = """mos {{
-	forward = 1
+	forward = {forward}
 	netdev {{
 		lo 0x0001
 	}}
@@ -452,43 +452,65 @@ MOS_CONF = """mos {{
 """
 
 
-def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, timeout: float = 60.0):
+def orphan_segments(n: int, size: int = 1460, seed: int = 3) -> mosrx.Trace:
+    """`n` TCP data segments (ACK|PSH, `size` payload bytes) of 256 flows that
+    never opened a connection: every one takes mOS's orphan path, so the
+    per-frame cost left after the checks is small (no stream to track)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import pktlib
+    rng = np.random.default_rng(seed)
+    pay = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+    frames = [pktlib.tcp_frame(f"10.1.{i % 256}.7", "192.168.7.7", 2000 + i % 256, 80, pay, flags=0x18,
+                               seq=i * size) for i in range(n)]
+    buf, off, ln = pktlib.pack_frames(frames)
+    t = mosrx.Trace.__new__(mosrx.Trace)
+    t.frames, t.off, t.len, t.n = buf, off, ln, n
+    t.frames_bytes = int(off[-1]) + int(ln[-1])
+    return t
+
+
+def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 3, timeout: float = 60.0):
     """mOS's own rx loop on one host core (oracle/_ref/mos_app: mtcp_init, an
-    mTCP thread in RunMainLoop, simple_firewall's stack -- one stream monitor,
-    forward = 1 -- with gpu_module_func as the I/O module), its per-frame CPU
-    time (core.c:902-907, timed per batch) with mOS's ProcessPacket on every
-    frame ("pp") and with csrc/mos_rx.c taking the checks from the GPU records
-    ("gpu"), on the same frames.  The difference is the CPU time per frame the
-    GPU saves inside mOS.  A reported baseline; None when the binary did not
-    travel with the tree."""
+    mTCP thread in RunMainLoop, one stream monitor socket, gpu_module_func as
+    the I/O module): the per-frame CPU time of core.c:902-907 (timed per batch)
+    with mOS's ProcessPacket on every frame ("pp") and with csrc/mos_rx.c
+    taking the checks from the GPU records ("gpu"), on the same frames,
+    alternated `reps` times (medians).  The difference is the CPU time per
+    frame the GPU saves inside mOS.  A reported baseline; None when the binary
+    did not travel with the tree."""
     exe = os.path.join(ROOT, "oracle", "_ref", "mos_app")
     if not os.access(exe, os.X_OK):
         return None
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import tempfile
     import pktlib
-    out = {}
+    ns = {"pp": [], "gpu": []}
+    frames = 0
     with tempfile.TemporaryDirectory() as td:
         trace = os.path.join(td, "t.mrxt")
-        pktlib.write_ref_trace(trace, tr.frames[:tr.frames_bytes], tr.off, tr.len, forward=1)
-        for mode in ("pp", "gpu"):
-            d = os.path.join(td, mode)
-            os.makedirs(os.path.join(d, "log"))
-            conf = os.path.join(d, "mos.conf")
-            with open(conf, "w") as fh:
-                fh.write(MOS_CONF.format(log=os.path.join(d, "log")))
-            env = dict(os.environ, MOSAPP_QUIET="1", MOSAPP_LOOPS=str(loops), MOSAPP_BATCH="8192")
-            try:
-                r = subprocess.run([exe, mode, conf, trace, d], capture_output=True, text=True, timeout=timeout,
-                                   env=env)
-                out[mode] = json.loads(r.stdout.strip().splitlines()[-1])
-            except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
-                return None
-    pp, gp = out["pp"]["rx_ns_per_frame"], out["gpu"]["rx_ns_per_frame"]
+        pktlib.write_ref_trace(trace, tr.frames[:tr.frames_bytes], tr.off, tr.len, forward=forward)
+        for rep in range(reps):
+            for mode in ("pp", "gpu"):
+                d = os.path.join(td, f"{mode}{rep}")
+                os.makedirs(os.path.join(d, "log"))
+                conf = os.path.join(d, "mos.conf")
+                with open(conf, "w") as fh:
+                    fh.write(MOS_CONF.format(log=os.path.join(d, "log"), forward=forward))
+                env = dict(os.environ, MOSAPP_QUIET="1", MOSAPP_LOOPS=str(loops), MOSAPP_BATCH="8192")
+                try:
+                    r = subprocess.run([exe, mode, conf, trace, d], capture_output=True, text=True, timeout=timeout,
+                                       env=env)
+                    st = json.loads(r.stdout.strip().splitlines()[-1])
+                except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+                    return None
+                ns[mode].append(st["rx_ns_per_frame"])
+                frames = st["rx_frames_timed"]
+    pp, gp = float(np.median(ns["pp"])), float(np.median(ns["gpu"]))
     return {"processpacket_ns_per_frame": round(pp, 1), "gpu_records_ns_per_frame": round(gp, 1),
-            "saved_ns_per_frame": round(pp - gp, 1), "frames": out["pp"]["rx_frames_timed"],
-            "sample": f"{tr.n} frames x {loops} through mOS's RunMainLoop on one core, simple_firewall stack "
-                      f"(1 stream monitor, forward=1), oracle/_ref/mos_app pp vs gpu"}
+            "saved_ns_per_frame": round(pp - gp, 1), "frames": frames,
+            "runs_ns": {k: [round(x, 1) for x in v] for k, v in ns.items()},
+            "sample": f"{tr.n} frames x {loops} through mOS's RunMainLoop on one core (1 stream monitor, "
+                      f"forward={forward}), oracle/_ref/mos_app pp vs gpu, {reps} alternated runs each, medians"}
 
 
 def measure_fw64(ctx, seconds: float):
@@ -593,8 +615,9 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
         # a group's batches must be distinct frames: replaying one batch would let
         # the group's copy carry it once and the kernel re-read it from cache
         # (group 0 = the module's default, auto: as many batches per launch as are
-        # ready, up to MOSRX_GROUP_AUTO_BYTES of frames -- ~58 of 64 B, 1 of 1500 B)
-        nb = group or {"S64": 64, "M1500": 4, "IMIX": 4}[key]
+        # ready, up to MOSRX_GROUP_AUTO_BYTES of frames -- ~120 of 64 B, 2 of 1500 B; more
+        # distinct batches than a launch takes, so no launch holds the same frames twice)
+        nb = group or {"S64": 160, "M1500": 6, "IMIX": 6}[key]
         tr = mosrx.Trace({"S64": mosrx.TRACE_S64, "M1500": mosrx.TRACE_M1500,
                           "IMIX": mosrx.TRACE_IMIX}[key], ctx_batch * nb)
     loops = max(1, frames_target // tr.n)
@@ -602,7 +625,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
                           group=group, timing=True)
     try:
-        be.run_loop(max_pkts=2 * ctx_batch * max(group, 64 if key == "S64" else 4))    # warm-up: staging sized, module loaded
+        be.run_loop(max_pkts=2 * ctx_batch * max(group, 128 if key == "S64" else 4))    # warm-up: staging sized, module loaded
         st0 = be.stats()
         t0 = time.perf_counter()
         st = be.run_loop()
@@ -762,10 +785,12 @@ def main():
         if ref:
             cpu["reference_processpacket"] = ref
         # mOS's whole rx loop with and without the GPU records (the CPU the GPU saves inside mOS)
-        rx = cpu_rx_loop_leg(mosrx.Trace(mosrx.TRACE_M1500, 16384), 24)
+        # 1500 B orphans under a monitor that forwards nothing: little besides the checks per frame
+        rx = cpu_rx_loop_leg(orphan_segments(8192), 16, forward=0)
         if rx:
             cpu["mos_rx_loop_M1500"] = rx
-        rx = cpu_rx_loop_leg(mosrx.Trace(mosrx.TRACE_FW64, 10_000), 40)
+        # config #1: simple_firewall's state (forward = 1), its one flow tracked as a stream
+        rx = cpu_rx_loop_leg(mosrx.Trace(mosrx.TRACE_FW64, 10_000), 20, forward=1)
         if rx:
             cpu["mos_rx_loop_FW64"] = rx
         for k in keys:

@@ -187,7 +187,8 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * (0 = MOSRX_GROUP_AUTO_BYTES) */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
-#define MOSRX_GROUP_AUTO_BYTES  (128ull << 20)   /* 64 B frames: ~55 batches of 32K per launch */
+#define MOSRX_GROUP_AUTO_BYTES  (256ull << 20)   /* per pipeline slot; 64 B frames: ~120 batches of 32K
+                                                   * per launch, 1500 B: 2 of 64K */
 
 void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg);
 int  mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg);

@@ -337,15 +337,16 @@ static uint64_t auto_bytes(void)
 }
 
 /* Explicit groups reserve `group` worst-case stages.  Auto groups hold up to
- * MOSRX_MAX_GROUP stages in a block of auto_bytes() + one worst-case stage
- * (a stage is started only while the frames so far are under auto_bytes()),
- * with records for the frames that can fit (>= 48 bytes of block per frame). */
+ * MOSRX_MAX_GROUP stages in a block of auto_bytes(): stages are packed by the
+ * bytes their frames really take, the last one stops where the block is full
+ * (a short batch, which ends the group), and records are there for the
+ * frames that can fit (a staged frame takes >= 64 bytes of block). */
 static int group_alloc(mosrx_ctx *mc, struct group *g)
 {
 	if (g_cfg.group == MOSRX_GROUP_AUTO) {
 		g->cap_st = MOSRX_MAX_GROUP;
-		g->blk_bytes = auto_bytes() + stage_bytes();
-		g->rec_cap = auto_bytes() / 48 + g_cfg.batch;
+		g->blk_bytes = auto_bytes();
+		g->rec_cap = auto_bytes() / 64 + g_cfg.batch;
 		if (g->rec_cap > (uint64_t)g_cfg.batch * MOSRX_MAX_GROUP)
 			g->rec_cap = (uint64_t)g_cfg.batch * MOSRX_MAX_GROUP;
 	} else {
@@ -492,7 +493,12 @@ static void group_fill(struct if_state *is, struct group *g)
 	g->nst = 0;
 	for (i = 0; i < cap; i++) {
 		struct stage *s = &g->st[i];
-		if (pos + stage_bytes() > g->blk_bytes || recs + g_cfg.batch > g->rec_cap)
+		/* room for this stage: a worst-case one (explicit groups), or its
+		 * descriptors and one largest frame (auto: it stops where the block ends) */
+		const uint64_t need = g_cfg.group == MOSRX_GROUP_AUTO
+		                          ? (((uint64_t)g_cfg.batch * 6 + 15) & ~15ull) + 256 + g_cfg.max_frame + 32
+		                          : stage_bytes();
+		if (pos + need > g->blk_bytes || recs + g_cfg.batch > g->rec_cap)
 			break;
 		stage_fill(g, s, is->src, &pos);
 		s->res = g->res + recs;

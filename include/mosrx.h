@@ -232,6 +232,11 @@ int  mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b,
 #define MOSRX_MAX_GROUP 256
 int  mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
                                       mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo);
+/* The same, plus the flow-table hash of every frame into h_fhash[i] (NULL: none;
+ * see mosrx_classify_dev_fh): the bucket FindStream / HTSearch would compute. */
+int  mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                         mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo,
+                                         uint32_t *const *h_fhash);
 
 /* Kernel timing on the end-to-end path: with timing on, every submit records
  * HIP events around its kernel on the slot's stream, and after the wait

@@ -76,6 +76,9 @@ typedef struct {
 #define MOSRX_PKT_RX_STATE   0x14   /* argp: mosrx_rx_state * -- what the exposed batch was classified under */
 #define MOSRX_PKT_RX_RECLASSIFY 0x15 /* argp: unused (non-NULL) -- classify the exposed batch again now,
                                      * under mOS's current state and BPF set (blocking) */
+#define MOSRX_PKT_RX_FHASH   0x17   /* argp: const uint32_t ** (whole batch): HashFlow of FindStream's tuple
+                                     * before the NUM_BINS mask (cfg.flowhash set; -1 for a batch
+                                     * classified with BPF filters) */
 #define MOSRX_PKT_SET_BPF    0x16   /* argp: const mosrx_bpf_set_arg * -- the monitor filters to evaluate in
                                      * the classify pass from now on (nprog 0: none); batches not yet
                                      * handed out are classified again with them */
@@ -185,6 +188,8 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * launch classifies one batch. */
 	uint64_t      group_bytes;                      /* MOSRX_GROUP_AUTO: frame bytes per launch aimed at
 	                                                 * (0 = MOSRX_GROUP_AUTO_BYTES) */
+	int32_t       flowhash;                         /* 1: also the flow-table hash of every frame
+	                                                 * (dev_ioctl(MOSRX_PKT_RX_FHASH)); not with BPF filters */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
 #define MOSRX_GROUP_AUTO_BYTES  (256ull << 20)   /* per pipeline slot; 64 B frames: ~120 batches of 32K

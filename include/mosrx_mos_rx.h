@@ -52,6 +52,7 @@ int mosrx_mos_process_packet(struct mtcp_manager *mtcp, const int ifidx, const i
 typedef struct mosrx_mos_rx_stats {
 	uint64_t frames;            /* frames taken from records */
 	uint64_t stream_step;       /* of them, TCP segments that entered the stream step (tcp.c:445) */
+	uint64_t gpu_flow_hash;     /* of those, flow-table lookups on the GPU's bucket (cfg.flowhash) */
 	uint64_t reclassified;      /* batches classified again mid-batch (state / filter change) */
 	uint64_t filter_installs;   /* BPF sets installed on the GPU */
 	uint64_t filters_gpu;       /* filters in the installed set */

@@ -61,12 +61,14 @@ struct stage {
 	mosrx_result *res;        /* pinned, in the group's record array */
 	mosrx_tcpinfo *ti;        /* pinned, pkt_info TCP fields (cfg.tcpinfo) */
 	uint32_t *match;          /* pinned, BPF match masks (a filter set installed) */
+	uint32_t *fh;             /* pinned, flow-table hashes (cfg.flowhash) */
 	uint32_t n, max_len;
 	uint64_t bytes;
 	int borrowed;             /* frames lent by the source: give them back when the group is recycled */
 	/* what its records were made under: mOS's socket counts, the netdev's
-	 * parameter / filter generation, the programs behind its masks */
-	uint32_t msp, esp, gen, nprog;
+	 * parameter / filter generation, the programs behind its masks, and
+	 * whether the flow hashes were made (not in a BPF pass) */
+	uint32_t msp, esp, gen, nprog, has_fh;
 };
 
 struct group {
@@ -75,6 +77,7 @@ struct group {
 	mosrx_result *res;        /* pinned, rec_cap records */
 	mosrx_tcpinfo *ti;
 	uint32_t *match;
+	uint32_t *fh;
 	uint64_t rec_cap;         /* frames the record arrays hold */
 	struct stage *st;         /* cap_st stages */
 	uint32_t cap_st;
@@ -320,6 +323,7 @@ static void group_free(mosrx_ctx *mc, struct group *g)
 	if (g->res) mosrx_host_free(mc, g->res);
 	if (g->ti) mosrx_host_free(mc, g->ti);
 	if (g->match) mosrx_host_free(mc, g->match);
+	if (g->fh) mosrx_host_free(mc, g->fh);
 	free(g->st);
 	memset(g, 0, sizeof(*g));
 }
@@ -358,7 +362,8 @@ static int group_alloc(mosrx_ctx *mc, struct group *g)
 	if (!g->st || mosrx_host_alloc(mc, g->blk_bytes, (void **)&g->blk) ||
 	    mosrx_host_alloc(mc, g->rec_cap * sizeof(mosrx_result), (void **)&g->res) ||
 	    (g_cfg.tcpinfo && mosrx_host_alloc(mc, g->rec_cap * sizeof(mosrx_tcpinfo), (void **)&g->ti)) ||
-	    (g_cfg.bpf_nprog && mosrx_host_alloc(mc, g->rec_cap * 4, (void **)&g->match)))
+	    (g_cfg.bpf_nprog && mosrx_host_alloc(mc, g->rec_cap * 4, (void **)&g->match)) ||
+	    (g_cfg.flowhash && mosrx_host_alloc(mc, g->rec_cap * 4, (void **)&g->fh)))
 		return -ENOMEM;
 	return 0;
 }
@@ -504,6 +509,7 @@ static void group_fill(struct if_state *is, struct group *g)
 		s->res = g->res + recs;
 		s->ti = g->ti ? g->ti + recs : NULL;
 		s->match = g->match ? g->match + recs : NULL;
+		s->fh = g->fh ? g->fh + recs : NULL;
 		if (!s->n)
 			break;
 		g->nst++;
@@ -556,6 +562,7 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 	mosrx_batch b[MOSRX_MAX_GROUP];
 	mosrx_result *out[MOSRX_MAX_GROUP];
 	mosrx_tcpinfo *ti[MOSRX_MAX_GROUP];
+	uint32_t *fh[MOSRX_MAX_GROUP];
 	uint32_t i, nb = g->nst - first;
 	if (follow_mos_state(pv, is))
 		return -1;
@@ -564,10 +571,12 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 		stage_batch(s, &b[i - first]);
 		out[i - first] = s->res;
 		ti[i - first] = s->ti;
+		fh[i - first] = s->fh;
 		s->msp = is->params.num_msp;
 		s->esp = is->params.num_esp;
 		s->gen = is->gen;
 		s->nprog = is->nprog;
+		s->has_fh = s->fh && !is->nprog;
 	}
 	if (is->nprog) {
 		for (i = first; i < g->nst; i++) {
@@ -578,9 +587,10 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 		}
 		return 0;
 	}
-	if (nb == 1)
+	if (nb == 1 && !g_cfg.flowhash)
 		return mosrx_classify_host_submit_ex(is->mc, k, &b[0], out[0], ti[0]);
-	return mosrx_classify_host_group_submit(is->mc, k, b, nb, out, g_cfg.tcpinfo ? ti : NULL);
+	return mosrx_classify_host_group_submit_ex(is->mc, k, b, nb, out, g_cfg.tcpinfo ? ti : NULL,
+	                                           g_cfg.flowhash ? fh : NULL);
 }
 
 static int group_wait(struct gpu_priv *pv, struct if_state *is, int k, int count)
@@ -813,6 +823,11 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
 		if (!s || !s->match || !s->nprog)
 			return -1;
 		*(const uint32_t **)argp = s->match;
+		return 0;
+	case MOSRX_PKT_RX_FHASH:
+		if (!s || !s->has_fh)
+			return -1;
+		*(const uint32_t **)argp = s->fh;
 		return 0;
 	case MOSRX_PKT_RX_TCPINFO:
 		if (!s || !s->ti)

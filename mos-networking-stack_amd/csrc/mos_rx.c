@@ -74,6 +74,7 @@ struct rx_view {
 	int ifidx;
 	const mosrx_result *res;
 	const uint32_t *match;       /* NULL: no masks for this batch */
+	const uint32_t *fhash;       /* NULL: no flow-table hashes for this batch */
 	mosrx_rx_state state;
 	/* the filter set installed on this thread's netdevs */
 	struct filt filt[2 * MOSRX_BPF_MAX_PROGS + 64];
@@ -113,11 +114,33 @@ static void view_fetch(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx)
 	v->ifidx = ifidx;
 	v->res = NULL;
 	v->match = NULL;
+	v->fhash = NULL;
 	if (!iom->dev_ioctl || iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_RESULTS, (void *)&v->res) || !v->res ||
 	    iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_STATE, &v->state))
 		fatal("no GPU records for the batch", ifidx);
 	if (v->state.bpf_nprog && iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_MATCH, (void *)&v->match))
 		v->match = NULL;
+	if (iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_FHASH, (void *)&v->fhash))
+		v->fhash = NULL;
+}
+
+/* FindStream (tcp.c:181-191) -> HTSearch (fhash.c:184-214) with the bucket the
+ * GPU computed (HashFlow of the reversed tuple, mosrx_classify_dev_fh) instead
+ * of hashing on the CPU; the bucket's list is walked as HTSearch walks it. */
+static tcp_stream *find_stream(struct rx_view *v, int index, mtcp_manager_t mtcp, const tcp_stream *key,
+                               unsigned int *hash)
+{
+	tcp_stream *w;
+	unsigned int idx;
+	if (!v->fhash)
+		return HTSearch(mtcp->tcp_flow_table, key, hash);
+	idx = v->fhash[index] & (NUM_BINS - 1);
+	*hash = idx;
+	stats_of(mtcp)->gpu_flow_hash++;
+	TAILQ_FOREACH(w, &mtcp->tcp_flow_table->ht_table[idx], rcvvar->he_link)
+		if (w->saddr == key->saddr && w->sport == key->sport && w->daddr == key->daddr && w->dport == key->dport)
+			return w;
+	return NULL;
 }
 
 /* Classify the rest of the exposed batch again (the stack state or the filter
@@ -331,7 +354,7 @@ static int stream_step(struct rx_view *v, int index, mtcp_manager_t mtcp, struct
 	key.sport = tcph->dest;
 	key.daddr = iph->saddr;
 	key.dport = tcph->source;
-	cur = HTSearch(mtcp->tcp_flow_table, &key, &hash);
+	cur = find_stream(v, index, mtcp, &key, &hash);
 	if (!cur) {
 		if (mtcp->listener == NULL && mtcp->num_msp == 0)
 			return TRUE;                  /* a client-only end host: nothing to do (tcp.c:454-458) */

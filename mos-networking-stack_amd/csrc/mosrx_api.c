@@ -767,6 +767,13 @@ static int group_copy(struct slot *s, struct region *r, uint32_t nr, uint64_t *d
 int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
                                      mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo)
 {
+	return mosrx_classify_host_group_submit_ex(c, slot, b, nb, h_out, h_tcpinfo, NULL);
+}
+
+int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                        mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo,
+                                        uint32_t *const *h_fhash)
+{
 	struct region r[3 * MOSRX_MAX_GROUP];
 	uint32_t i, nr = 0, tiles = 0, maxl = 0, ntot = 0, tile;
 	uint64_t dev_bytes = 0, pre = 0;
@@ -781,7 +788,7 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 	for (i = 0; i < nb; i++) {
 		if ((rc = mosrx__check_batch(&b[i], 0)))
 			return rc;
-		if (b[i].n && (!h_out[i] || (h_tcpinfo && !h_tcpinfo[i])))
+		if (b[i].n && (!h_out[i] || (h_tcpinfo && !h_tcpinfo[i]) || (h_fhash && !h_fhash[i])))
 			return -EINVAL;
 		if (!b[i].max_len)
 			unknown = 1;
@@ -815,6 +822,7 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 		d->tile_base = tiles;
 		d->out = s->d_res + pre;
 		d->tinfo = h_tcpinfo ? s->d_ti + pre : NULL;
+		d->fhash = h_fhash ? s->d_fh + pre : NULL;
 		if (b[i].n) {
 			d->frames = r[nr].dev;
 			d->off = (const uint32_t *)r[nr + 1].dev;
@@ -849,7 +857,8 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 		uint32_t j = i + 1;
 		uint64_t n = b[i].n;
 		while (j < nb && h_out[j] == h_out[j - 1] + b[j - 1].n &&
-		       (!h_tcpinfo || h_tcpinfo[j] == h_tcpinfo[j - 1] + b[j - 1].n))
+		       (!h_tcpinfo || h_tcpinfo[j] == h_tcpinfo[j - 1] + b[j - 1].n) &&
+		       (!h_fhash || h_fhash[j] == h_fhash[j - 1] + b[j - 1].n))
 			n += b[j++].n;
 		if (n) {
 			HIPCHK(hipMemcpyAsync(h_out[i], s->d_res + pre, (size_t)n * sizeof(mosrx_result),
@@ -857,6 +866,8 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 			if (h_tcpinfo)
 				HIPCHK(hipMemcpyAsync(h_tcpinfo[i], s->d_ti + pre, (size_t)n * sizeof(mosrx_tcpinfo),
 				                      hipMemcpyDeviceToHost, s->stream));
+			if (h_fhash)
+				HIPCHK(hipMemcpyAsync(h_fhash[i], s->d_fh + pre, (size_t)n * 4, hipMemcpyDeviceToHost, s->stream));
 		}
 		pre += n;
 		i = j;

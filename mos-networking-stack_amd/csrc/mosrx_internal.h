@@ -86,10 +86,11 @@ typedef struct mosrx_qdesc {
 	const uint16_t *len;
 	mosrx_result   *out;
 	mosrx_tcpinfo  *tinfo;       /* NULL unless the queue was launched with pkt_info fields */
+	uint32_t       *fhash;       /* flow-table hashes, or NULL */
 	uint32_t        frames_bytes;
 	uint32_t        n;
 	uint32_t        tile_base;   /* first workgroup of this batch in the launch */
-	uint32_t        pad[3];
+	uint32_t        pad;
 } mosrx_qdesc;
 
 typedef struct mosrx_qparams {

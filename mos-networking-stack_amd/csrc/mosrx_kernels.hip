@@ -54,6 +54,7 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 static_assert(2 + 4 * WIN_DW == MOSRX_WINDOW_END_FULL, "window end");
 static_assert(WIN_NLOAD(MOSRX_WINDOW_END_SMALL) == 5 && WIN_NLOAD(MOSRX_WINDOW_END_STREAM) == 4, "window loads");
 static_assert(sizeof(mosrx_result) == 16, "record size");
+static_assert(sizeof(mosrx_qdesc) == 64, "queue descriptor size");
 // small: 4 waves, one frame per lane; stream: 1 header wave + MOSRX_STREAMERS streamer waves
 #define SMALL_THREADS (MOSRX_SMALL_FRAMES < 256u ? MOSRX_SMALL_FRAMES : 256u)
 #define WG_THREADS(kind) ((kind) == MOSRX_KIND_SMALL ? SMALL_THREADS : 64 * (1 + MOSRX_STREAMERS))
@@ -1176,7 +1177,7 @@ void mosrx_classify_queue_kernel(mosrx_qparams qp)
 	kp.out = d->out;
 	kp.tables = qp.tables;
 	kp.counters = qp.counters;
-	kp.fhash = nullptr;
+	kp.fhash = d->fhash;
 	kp.bmatch = nullptr;
 	kp.tinfo = d->tinfo;
 	kp.frames_bytes = d->frames_bytes;

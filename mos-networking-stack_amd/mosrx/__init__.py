@@ -100,7 +100,7 @@ class ModuleCfg(C.Structure):
                 ("gpu_base", C.c_int32), ("ngpu", C.c_int32), ("pipeline", C.c_int32),
                 ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32),
                 ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32),
-                ("group_bytes", C.c_uint64)]
+                ("group_bytes", C.c_uint64), ("flowhash", C.c_int32)]
 
 
 class ModuleStats(C.Structure):
@@ -225,6 +225,8 @@ def lib():
             "mosrx_device_count": (I, []),
             "mosrx_classify_host_submit_ex": (I, [P, I, C.POINTER(Batch), P, P]),
             "mosrx_classify_host_group_submit": (I, [P, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
+            "mosrx_classify_host_group_submit_ex": (I, [P, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P),
+                                                        C.POINTER(P)]),
             "mosrx_set_timing": (I, [P, I]),
             "mosrx_last_kernel_ms": (I, [P, C.POINTER(C.c_float)]),
             "mosrx_source_afpacket_ex": (P, [C.c_char_p, C.POINTER(AfpOpts)]),
@@ -742,6 +744,7 @@ _PKTFN = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_uint16,
 PKT_TX_IP_CSUM, PKT_TX_TCP_CSUM = 0x01, 0x02
 PKT_RX_RSS, DRV_NAME, PKT_RX_RESULTS, PKT_RX_MATCH = 0x03, 0x08, 0x10, 0x11
 PKT_RX_TCPINFO, PKT_SET_PARAMS = 0x12, 0x13
+PKT_RX_STATE, PKT_RX_RECLASSIFY, PKT_SET_BPF, PKT_RX_FHASH = 0x14, 0x15, 0x16, 0x17
 
 
 class IoModuleFunc(C.Structure):
@@ -766,7 +769,7 @@ class GpuBackend:
     def __init__(self, sources: list[int], params: Params | None = None, batch: int = 32768,
                  max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
                  ngpu: int = 1, bpf=None, group: int = 1, tcpinfo: bool = False, tx_batch: int = 64,
-                 timing: bool = False):
+                 timing: bool = False, flowhash: bool = False):
         cfg = ModuleCfg()
         lib().mosrx_gpu_module_cfg_default(C.byref(cfg))
         cfg.num_ifs = len(sources)
@@ -775,7 +778,7 @@ class GpuBackend:
             cfg.if_names[i].value = f"gpu{i}".encode()
         cfg.batch, cfg.max_frame, cfg.pipeline = batch, max_frame, int(pipeline)
         cfg.gpu_base, cfg.ngpu = gpu_base, ngpu
-        cfg.group, cfg.tcpinfo, cfg.tx_batch = group, int(tcpinfo), tx_batch
+        cfg.group, cfg.tcpinfo, cfg.tx_batch, cfg.flowhash = group, int(tcpinfo), tx_batch, int(flowhash)
         if params is not None:
             cfg.params = params
         self.params = Params.from_buffer_copy(cfg.params)
@@ -820,6 +823,13 @@ class GpuBackend:
         p = C.c_void_p()
         if self._ioctl(self.ctx, ifidx, PKT_RX_MATCH, C.byref(p)):
             raise MosrxError(5, "dev_ioctl(MOSRX_PKT_RX_MATCH)")
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint32)), (n,)).copy()
+
+    def fhashes(self, ifidx: int, n: int) -> np.ndarray:
+        """dev_ioctl(MOSRX_PKT_RX_FHASH): the batch's flow-table hashes (cfg.flowhash)."""
+        p = C.c_void_p()
+        if self._ioctl(self.ctx, ifidx, PKT_RX_FHASH, C.byref(p)):
+            raise MosrxError(5, "dev_ioctl(MOSRX_PKT_RX_FHASH)")
         return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint32)), (n,)).copy()
 
     def tcpinfo(self, ifidx: int, n: int) -> np.ndarray:

@@ -121,6 +121,21 @@ int __wrap_mosrx_classify_host_group_submit(mosrx_ctx *mc, int slot, const mosrx
 	return 0;
 }
 
+int __wrap_mosrx_classify_host_group_submit_ex(mosrx_ctx *mc, int slot, const mosrx_batch *b, uint32_t nb,
+                                               mosrx_result *const *out, mosrx_tcpinfo *const *ti,
+                                               uint32_t *const *fh)
+{
+	struct emul_ctx *c = (struct emul_ctx *)mc;
+	uint32_t i;
+	int rc;
+	(void)slot;
+	for (i = 0; i < nb; i++)
+		if ((rc = mo_classify_ex(&c->p, b[i].frames, b[i].frames_bytes, b[i].off, b[i].len, b[i].n, out[i],
+		                         fh ? fh[i] : NULL, ti ? ti[i] : NULL)))
+			return rc;
+	return 0;
+}
+
 int __wrap_mosrx_classify_bpf_host_submit(mosrx_ctx *mc, int slot, const mosrx_batch *b, mosrx_result *out,
                                           uint32_t *match)
 {

@@ -32,6 +32,7 @@
  *   env MOSAPP_LISTEN=port       an end-host socket listening on that port
  *   env MOSAPP_BATCH=n           frames per recv_pkts (default 4096)
  *   env MOSAPP_GROUP=g           batches per launch (default 0 = auto)
+ *   env MOSAPP_FLOWHASH=0        no flow-table hashes from the GPU (the consumer hashes on the CPU)
  *   env MOSAPP_LATE_RAW_AT=k     create the raw monitor (MOSAPP_RAW's filter) just before
  *                                frame k, on the mTCP thread (a filter bound mid-batch)
  *   env MOSAPP_LATE_MON_AT=k     create one more stream monitor just before frame k (the
@@ -301,6 +302,7 @@ int main(int argc, char **argv)
 	cfg.src[0] = src;
 	cfg.batch = getenv("MOSAPP_BATCH") ? (uint32_t)atoi(getenv("MOSAPP_BATCH")) : 4096;
 	cfg.group = getenv("MOSAPP_GROUP") ? (uint32_t)atoi(getenv("MOSAPP_GROUP")) : MOSRX_GROUP_AUTO;
+	cfg.flowhash = getenv("MOSAPP_FLOWHASH") ? atoi(getenv("MOSAPP_FLOWHASH")) : 1;   /* FindStream's bucket too */
 	cfg.params.num_queues = nq;
 	cfg.params.queue_mode = qmode;
 	cfg.params.num_msp = 0;                       /* followed from mOS's manager (mos_state) */
@@ -378,11 +380,13 @@ int main(int argc, char **argv)
 		mosrx_mos_rx_stats cs;
 		mosrx_mos_rx_stats_of(0, &cs);
 		printf("{\"mode\": \"%s\", \"frames\": %lu, \"rx_frames_timed\": %lu, \"rx_ns_per_frame\": %.2f, "
-		       "\"consumer_frames\": %lu, \"stream_step\": %lu, \"reclassified\": %lu, \"filter_installs\": %lu, "
+		       "\"consumer_frames\": %lu, \"stream_step\": %lu, \"gpu_flow_hash\": %lu, \"reclassified\": %lu, "
+		       "\"filter_installs\": %lu, "
 		       "\"filters_gpu\": %lu, \"filters_cpu\": %lu}\n",
 		       argv[1], (unsigned long)g_total, (unsigned long)g_rx_frames,
 		       g_rx_frames ? g_rx_ns / (double)g_rx_frames : 0.0, (unsigned long)cs.frames,
-		       (unsigned long)cs.stream_step, (unsigned long)cs.reclassified, (unsigned long)cs.filter_installs,
+		       (unsigned long)cs.stream_step, (unsigned long)cs.gpu_flow_hash, (unsigned long)cs.reclassified,
+		       (unsigned long)cs.filter_installs,
 		       (unsigned long)cs.filters_gpu, (unsigned long)cs.filters_cpu);
 	}
 	mosrx_source_close(src);

@@ -107,6 +107,27 @@ def test_tcpinfo_through_the_backend(group):
         be.close()
 
 
+@pytest.mark.parametrize("group,tcpinfo", [(1, False), (4, True), (0, False)])
+def test_flow_hash_through_the_backend(group, tcpinfo):
+    """cfg.flowhash: every batch carries FindStream's flow-table hash per frame
+    (dev_ioctl(MOSRX_PKT_RX_FHASH)), equal to the oracle's HashFlow restatement
+    (pinned to mOS's own in test_flow_hash_golden), whatever the batches per
+    launch (1, 4, auto) and with the pkt_info fields beside it."""
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 9000, nflows=700)
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=1)
+    be = mosrx.GpuBackend([src], batch=1500, cpu=6, group=group, tcpinfo=tcpinfo, flowhash=True)
+    try:
+        ora, ofh = O.classify_fh(t.frames, t.off, t.len, O.params())
+        seen = 0
+        while (n := be.recv_pkts(0)) > 0:
+            assert_records_equal(be.results(0, n), ora[seen:seen + n], "records")
+            np.testing.assert_array_equal(be.fhashes(0, n), ofh[seen:seen + n])
+            seen += n
+        assert seen == t.n
+    finally:
+        be.close()
+
+
 def test_backend_fed_from_a_pcap_file(tmp_path):
     """mosrx_source_pcap (the libpcap-free pcap_next, pcap_module.c:41) behind the
     backend: the trace written to a pcap file classifies exactly as the oracle

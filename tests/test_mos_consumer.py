@@ -69,6 +69,8 @@ SCENARIOS = {
     "late_monitor": dict(forward=1, env={"MOSAPP_MONITORS": "0", "MOSAPP_LATE_MON_AT": "200"}),
     "batch_1_per_launch": dict(forward=1, env={"MOSAPP_GROUP": "1", "MOSAPP_BATCH": "97"}),
     "groups_of_3": dict(forward=1, env={"MOSAPP_GROUP": "3", "MOSAPP_BATCH": "61"}),
+    # FindStream through HTSearch's own hash instead of the GPU's bucket (the default)
+    "cpu_flow_hash": dict(forward=1, env={"MOSAPP_FLOWHASH": "0"}),
 }
 
 
@@ -143,9 +145,13 @@ def _check_scenario(name, pp, gpu):
     nstat = pp["state"].splitlines()[-1].split()
     assert int(nstat[6]) > 0                                   # rx_errors: bad checksums etc. were seen
     if name in ("monitor_fwd", "filters", "two_monitors_raw", "listener", "late_filter", "batch_1_per_launch",
-                "groups_of_3"):
+                "groups_of_3", "cpu_flow_hash"):
         assert " ev 4 " in cb and " ev 1 " in cb               # MOS_ON_CONN_START, MOS_ON_PKT_IN
         assert st["stream_step"] > 0
+    if name == "cpu_flow_hash":
+        assert st["gpu_flow_hash"] == 0
+    elif st["stream_step"] and name not in ("filters", "late_filter"):
+        assert st["gpu_flow_hash"] == st["stream_step"]        # every lookup on the GPU's bucket
     if name == "monitor_nofwd":
         assert all(f[12:14] == b"\x08\x06" for f in pp["tx"])  # forward = 0: only mOS's own ARP requests leave
     if name in ("monitor_fwd", "no_socket"):

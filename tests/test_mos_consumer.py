@@ -71,6 +71,8 @@ SCENARIOS = {
     "groups_of_3": dict(forward=1, env={"MOSAPP_GROUP": "3", "MOSAPP_BATCH": "61"}),
     # FindStream through HTSearch's own hash instead of the GPU's bucket (the default)
     "cpu_flow_hash": dict(forward=1, env={"MOSAPP_FLOWHASH": "0"}),
+    # 600 conversations (~6K frames) in batches of 512, automatic groups of several batches
+    "many_flows": dict(forward=1, env={"MOSAPP_BATCH": "512", "MOSAPP_RAW": "tcp and ip[8] > 32"}, nflows=600),
 }
 
 
@@ -106,8 +108,9 @@ def run_app(exe, mode, tmp, name, sc, frames, extra_env=None):
                 callbacks=(d / "callbacks.txt").read_text(), tx=pcap_frames(d / "tx.pcap"), stats=stats)
 
 
-def compare_modes(exe, tmp, name, nflows=64):
+def compare_modes(exe, tmp, name):
     sc = SCENARIOS[name]
+    nflows = sc.get("nflows", 64)
     frames = pktlib.conversation_frames(nflows, seed=11, listen_port=sc.get("listen", 0))
     pp = run_app(exe, "pp", tmp, name, sc, frames)
     gpu = run_app(exe, "gpu", tmp, name, sc, frames)
@@ -145,12 +148,12 @@ def _check_scenario(name, pp, gpu):
     nstat = pp["state"].splitlines()[-1].split()
     assert int(nstat[6]) > 0                                   # rx_errors: bad checksums etc. were seen
     if name in ("monitor_fwd", "filters", "two_monitors_raw", "listener", "late_filter", "batch_1_per_launch",
-                "groups_of_3", "cpu_flow_hash"):
+                "groups_of_3", "cpu_flow_hash", "many_flows"):
         assert " ev 4 " in cb and " ev 1 " in cb               # MOS_ON_CONN_START, MOS_ON_PKT_IN
         assert st["stream_step"] > 0
     if name == "cpu_flow_hash":
         assert st["gpu_flow_hash"] == 0
-    elif st["stream_step"] and name not in ("filters", "late_filter"):
+    elif st["stream_step"] and name not in ("filters", "late_filter", "many_flows"):
         assert st["gpu_flow_hash"] == st["stream_step"]        # every lookup on the GPU's bucket
     if name == "monitor_nofwd":
         assert all(f[12:14] == b"\x08\x06" for f in pp["tx"])  # forward = 0: only mOS's own ARP requests leave

@@ -646,7 +646,8 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
             "kernel_launches": int(launches), "batches": int(batches),
             "device_us_per_batch": round(dev_us, 3),
             "device_roofline_frac": round(ab / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if dev_us > 0 else None,
-            "method": f"mosrx_rx_loop over gpu_module_func (pipelined, {group} batch(es) per launch), "
+            "method": f"mosrx_rx_loop over gpu_module_func (pipelined, "
+                      f"{group if group else 'auto (MOSRX_GROUP_AUTO)'} batch(es) per launch), "
                       f"in-memory source replaying {tr.n} distinct frames; every batch crosses PCIe; device "
                       f"time = HIP events around each kernel (its frames were just copied in)"}
 

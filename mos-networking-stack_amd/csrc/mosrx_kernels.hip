@@ -264,7 +264,12 @@ static_assert(MOSRX_R_COUNT <= 16, "verdict table holds 16 codes");
 // ProcessInTCPPacket prefix (tcp.c:408-445); see oracle/mosrx_oracle.c.
 // WEND: the window end of the tile (MOSRX_WINDOW_END_*); `win` holds
 // WIN_NLOAD(WEND) chunks, the rest are read here for a wave with IP options.
-template <int VAR, int WEND>
+// RSS (probe builds only, the library uses 0): 0 the 24 nibble tables in LDS,
+// 1 no Toeplitz at all (wrong hashes: the bound of any faster form), 2 twelve
+// byte tables (12 KiB) in LDS after the library's words, 3 the same twelve
+// read from global memory (kp.tables + MOSRX_TAB8_OFF) without staging.
+#define MOSRX_TAB8_OFF 1024
+template <int VAR, int WEND, int RSS = 0>
 __device__ __forceinline__ hdr_t hdr_parse(hdr_win_t win, uint32_t o, uint32_t cap, bool active, uint32_t kflags,
                                            const uint32_t *s_tab, const uint32_t *g_tab, __amdgpu_buffer_rsrc_t rs,
                                            uint32_t nbytes)
@@ -314,7 +319,17 @@ __device__ __forceinline__ hdr_t hdr_parse(hdr_win_t win, uint32_t o, uint32_t c
 
 	// Toeplitz over saddr|daddr|sport|dport in wire order (util.c:61-99, host-order args)
 	uint32_t rss = 0;
-	{
+	if constexpr (RSS == 1) {
+		rss = saddr ^ daddr ^ (is_tcp ? th0 : 0u);
+	} else if constexpr (RSS >= 2) {
+		const uint32_t tup[3] = {saddr, daddr, is_tcp ? th0 : 0u};
+		const uint32_t *t8 = RSS == 2 ? s_tab + MOSRX_TAB_WORDS : g_tab + MOSRX_TAB8_OFF;
+#pragma unroll
+		for (int d = 0; d < 3; d++)
+#pragma unroll
+			for (int b = 0; b < 4; b++)
+				rss ^= t8[(4 * d + b) * 256 + ((tup[d] >> (8 * b)) & 0xFFu)];
+	} else {
 		const uint32_t tup[3] = {saddr, daddr, is_tcp ? th0 : 0u};
 		const char *tb = reinterpret_cast<const char *>(s_tab);
 #pragma unroll
@@ -723,12 +738,22 @@ __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffe
 // The header wave's LDS state: the RSS nibble tables + queue map, and zeroed
 // reason counts (a wave's LDS accesses are ordered: no barrier needed for its
 // own use).
+template <int RSS = 0>
 __device__ __forceinline__ void tab_fill(const mosrx_kparams &kp, uint32_t *s_tab, uint32_t *s_cnt, uint32_t lane)
 {
 	const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
 	const u32x4 a = tg[lane], b = tg[lane + 64];
 	reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
 	reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
+	if constexpr (RSS == 2) {   // probe: the byte tables after the library's words
+		u32x4 v[12];
+#pragma unroll
+		for (int i = 0; i < 12; i++)
+			v[i] = tg[MOSRX_TAB8_OFF / 4 + 64 * i + lane];
+#pragma unroll
+		for (int i = 0; i < 12; i++)
+			reinterpret_cast<u32x4 *>(s_tab + MOSRX_TAB_WORDS)[64 * i + lane] = v[i];
+	}
 	if (lane <= MOSRX_R_COUNT)
 		s_cnt[lane] = 0;
 }
@@ -978,7 +1003,9 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 	// DBG 2048: the full 96-byte window (the round-1 form, 4 % slower)
 	constexpr int WEND = (DBG & 2048) ? MOSRX_WINDOW_END_FULL : MOSRX_WINDOW_END_STREAM;
 	constexpr int NLOAD = (VAR & VAR_BPF) ? WIN_RAW / 4 : WIN_NLOAD(WEND);
-	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
+	// DBG 16384 / 32768 / 65536: RSS form 1 / 2 / 3 of hdr_parse (probe builds)
+	constexpr int RSS = (DBG & 16384) ? 1 : (DBG & 32768) ? 2 : (DBG & 65536) ? 3 : 0;
+	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS + (RSS == 2 ? 12 * 256 : 0)];
 	__shared__ uint32_t s_part[S][64];   // streamer s's tail sums
 	__shared__ uint32_t s_cnt[MOSRX_R_COUNT + 1];
 
@@ -1025,7 +1052,7 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		// 17.68 vs 17.90 us).  DBG 4096 flips the order (probe builds).
 		constexpr bool TAB_FIRST = (TAIL_AUX(VAR) == 0) != ((DBG & 4096) != 0);
 		if constexpr (TAB_FIRST)
-			tab_fill(kp, s_tab, s_cnt, lane);
+			tab_fill<RSS>(kp, s_tab, s_cnt, lane);
 		hdr_win_t win;
 		if constexpr (DBG & 2) {
 #pragma unroll
@@ -1038,7 +1065,7 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		const bool cand = hi_l > lo_l;
 		const u32x4 ov = load16<WIN_AUX(VAR)>(rs, sorted && cand ? (hi_l - 1u) & ~15u : ZERO_OFF, 0);
 		if constexpr (!TAB_FIRST)
-			tab_fill(kp, s_tab, s_cnt, lane);
+			tab_fill<RSS>(kp, s_tab, s_cnt, lane);
 		if constexpr (DBG & 1) {
 			uint32_t x = 0;
 #pragma unroll
@@ -1049,7 +1076,7 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 				kp.out[p].rss = x;
 		} else {
 			TILE_STAMP(2);
-			const hdr_t h = hdr_parse<VAR, WEND>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
+			const hdr_t h = hdr_parse<VAR, WEND, RSS>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
 			if constexpr (IS_TX(VAR) || (DBG & 8192) != 0) {   // DBG 8192: the whole record after the barrier
 				TILE_STAMP(3);
 				__syncthreads();   // B: s_part ready

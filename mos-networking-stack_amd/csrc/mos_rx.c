@@ -79,7 +79,6 @@ struct rx_view {
 	/* the filter set installed on this thread's netdevs */
 	struct filt filt[2 * MOSRX_BPF_MAX_PROGS + 64];
 	uint32_t nfilt, ngpu;
-	uint32_t gen[MOSRX_MAX_DEVICES];   /* netdev generation right after the install */
 };
 
 static __thread struct rx_view t_view;
@@ -227,7 +226,9 @@ static void filters_sync(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx
 static int filter_eval(struct rx_view *v, int index, const struct sfbpf_program *fc, int mode, uint8_t *p, int l)
 {
 	struct filt *f = filt_find(v, fc, mode);
-	if (!f) {   /* bound since the last install */
+	/* bound since the last install (a full table keeps the rest on the CPU
+	 * rather than installing again for every frame) */
+	if (!f && v->nfilt < sizeof(v->filt) / sizeof(v->filt[0])) {
 		filters_sync(v, v->mtcp, v->ifidx);
 		f = filt_find(v, fc, mode);
 	}

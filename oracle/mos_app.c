@@ -44,7 +44,9 @@
 #define _GNU_SOURCE
 #include <arpa/inet.h>
 #include <errno.h>
+#include <execinfo.h>
 #include <pthread.h>
+#include <signal.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -244,6 +246,18 @@ static int stream_monitor(int with_filters)
 	return s;
 }
 
+/* An abort (a fortified copy, an assert in mOS) prints where it came from:
+ * the harness links with -rdynamic, so the frames have names. */
+static void on_abort(int sig)
+{
+	void *fr[48];
+	int n = backtrace(fr, 48);
+	(void)sig;
+	backtrace_symbols_fd(fr, n, 2);
+	signal(SIGABRT, SIG_DFL);
+	abort();
+}
+
 int main(int argc, char **argv)
 {
 	FILE *in;
@@ -262,6 +276,7 @@ int main(int argc, char **argv)
 	uint64_t late_raw = getenv("MOSAPP_LATE_RAW_AT") ? strtoull(getenv("MOSAPP_LATE_RAW_AT"), NULL, 10) : 0;
 	int mon0 = -1, m;
 	FILE *f;
+	signal(SIGABRT, on_abort);
 
 	if (argc != 5 || (strcmp(argv[1], "pp") && strcmp(argv[1], "gpu"))) {
 		fprintf(stderr, "usage: %s pp|gpu mos.conf trace.mrxt outdir\n", argv[0]);

@@ -996,8 +996,11 @@ __device__ __forceinline__ void stream_frames(__amdgpu_buffer_rsrc_t rs, uint32_
 				kp.bmatch[tile * 16u + (i)] = (uint32_t)__builtin_amdgcn_s_memrealtime();         \
 		}                                                                                         \
 	} while (0)
+// One stream tile over frames [first, first + cnt), cnt <= T <= 64 (`tile`
+// only numbers the timeline stamps); the library's tiles are classify_tile_stream.
 template <int S, int VAR, int DBG = 0, int U = STREAM_U, uint32_t T = 64>
-__device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, uint32_t tile)
+__device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, uint32_t tile, uint32_t first,
+                                                     uint32_t cnt)
 {
 	constexpr int AUX = TAIL_AUX(VAR);
 	// DBG 2048: the full 96-byte window (the round-1 form, 4 % slower)
@@ -1012,12 +1015,12 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 	const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
 	const __amdgpu_buffer_rsrc_t rs = frame_rsrc(kp.frames, kp.frames_bytes);
 	const uint32_t nbytes = kp.frames_bytes;
-	const uint32_t nact = min(T, kp.n - tile * T);
+	const uint32_t nact = cnt;
 
 	if (wave == 0)
 		TILE_STAMP(0);
 	// every wave reads the tile's descriptors (lane = frame)
-	const uint32_t p = tile * T + lane;
+	const uint32_t p = first + lane;
 	const bool active = lane < nact;
 	uint32_t o = 0, cap = 0;
 	if (active) {
@@ -1156,6 +1159,12 @@ __device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, ui
 		TILE_STAMP(7 + sidx);
 		__syncthreads();   // B
 	}
+}
+
+template <int S, int VAR, int DBG = 0, int U = STREAM_U, uint32_t T = 64>
+__device__ __forceinline__ void classify_tile_stream(const mosrx_kparams &kp, uint32_t tile)
+{
+	classify_span_stream<S, VAR, DBG, U, T>(kp, tile, tile * T, min(T, kp.n - tile * T));
 }
 
 template <int KIND, int VAR>

@@ -578,6 +578,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	constexpr int AUX = TAIL_AUX(VAR);
 	// the fused BPF hook reads the whole 96-byte window
 	constexpr int NLOAD = (VAR & VAR_BPF) ? WIN_RAW / 4 : WIN_NLOAD(WEND);
+	constexpr int RSS = (DBG & 16384) ? 1 : 0;   // probe builds: no Toeplitz (hdr_parse RSS form 1)
 	// DBG 2 skips the window loads, DBG 4 the record stores (probe builds only).  Tried and slower:
 	// windows staged through LDS from contiguous wave loads (64 B config 192 vs
 	// 125 us per 8M frames).
@@ -633,7 +634,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	const uint32_t p = pv[fi], o = ov[fi], cap = capv[fi];
 	const bool active = actv[fi];
 	const hdr_win_t &win = winv[fi];
-	const hdr_t h = hdr_parse<VAR, WEND>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
+	const hdr_t h = hdr_parse<VAR, WEND, RSS>(win, o, cap, active, kp.flags, s_tab, kp.tables, rs, nbytes);
 	uint32_t tail = 0;
 	for (uint64_t m = __ballot(h.has_tail); m; m &= m - 1) {
 		const uint32_t f = (uint32_t)__builtin_ctzll(m);

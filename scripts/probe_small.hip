@@ -1,0 +1,149 @@
+// probe_small.hip — where the 64 B ring's time goes (diagnostic only).
+//
+// The 64 B ring (256 x 32K frames per launch) runs at 0.93 of the box's read +
+// write rate at its 4:1 mix and its SQ counters show VALU busy ~48 %
+// (DESIGN §4.4).  One launch of the library's SMALL tile over 8M frames (the
+// ring's work in one batch; 3 resident copies, > 1.5 GB) runs here as
+//   library, the batch queue over 256 x 32K batches of the same frames (the
+//   ring as the library launches it), no Toeplitz (RSS form 1: the bound of
+//   any cheaper hash),
+//   no record stores (DBG 4), no window loads (DBG 2), neither (DBG 6),
+// interleaved, 3 rounds.  The library form's records are checked against the
+// oracle-free invariant that every frame got a record (verdict 1: valid frames)
+// and against a second run; the others are timing bounds only.
+#include "../mos-networking-stack_amd/csrc/mosrx_kernels.hip"
+#include "../include/mosrx_trace.h"
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#define CHK(x) do { if ((x) != hipSuccess) { printf("HIP error %s line %d\n", #x, __LINE__); return 1; } } while (0)
+
+template <int DBG>
+__global__ __launch_bounds__(SMALL_THREADS) void k_small(mosrx_kparams kp)
+{
+	classify_tile_small<0, MOSRX_SMALL_FRAMES, DBG>(kp, blockIdx.x);
+}
+
+// the ring as the library launches it: the batch queue over 256 x 32K batches
+// slicing the same frames (one descriptor table per resident copy)
+static mosrx_qparams g_qp[3];
+static uint32_t g_qtiles;
+static void launch_queue(const mosrx_kparams &kp, hipStream_t st)
+{
+	for (int i = 0; i < 3; i++)
+		if (g_qp[i].tables && g_qp[i].counters == (uint32_t *)kp.off) {   // copy i (key: its off array)
+			mosrx_qparams q = g_qp[i];
+			q.counters = nullptr;
+			hipLaunchKernelGGL((mosrx_classify_queue_kernel<MOSRX_KIND_SMALL, 0>), dim3(g_qtiles),
+			                   dim3(SMALL_THREADS), 0, st, q);
+		}
+}
+
+typedef void (*launch_fn)(const mosrx_kparams &, hipStream_t);
+template <int DBG>
+static void launch(const mosrx_kparams &kp, hipStream_t st)
+{
+	hipLaunchKernelGGL((k_small<DBG>), dim3((kp.n + MOSRX_SMALL_FRAMES - 1) / MOSRX_SMALL_FRAMES),
+	                   dim3(SMALL_THREADS), 0, st, kp);
+}
+
+int main(int argc, char **argv)
+{
+	const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 256u * 32768u;
+	const int nb = 3;
+	mosrx_trace t;
+	if (mosrx_trace_gen(MOSRX_TRACE_S64, n, 1000000, 0, &t)) {
+		printf("trace_gen failed\n");
+		return 1;
+	}
+	mosrx_params p;
+	mosrx_params_default(&p);
+	std::vector<uint32_t> tab(MOSRX_TAB_ALLOC_WORDS, 0);
+	mosrx_rss_tables(p.rss_key, p.rss_key_len, tab.data());
+	uint32_t *tables;
+	CHK(hipMalloc((void **)&tables, tab.size() * 4));
+	CHK(hipMemcpy(tables, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+	mosrx_kparams kps[nb];
+	for (int i = 0; i < nb; i++) {
+		uint8_t *f; uint32_t *o; uint16_t *l; mosrx_result *r;
+		CHK(hipMalloc((void **)&f, t.frames_bytes + 64));
+		CHK(hipMemcpy(f, t.frames, t.frames_bytes + 64, hipMemcpyHostToDevice));
+		CHK(hipMalloc((void **)&o, (size_t)n * 4));
+		CHK(hipMemcpy(o, t.off, (size_t)n * 4, hipMemcpyHostToDevice));
+		CHK(hipMalloc((void **)&l, (size_t)n * 2));
+		CHK(hipMemcpy(l, t.len, (size_t)n * 2, hipMemcpyHostToDevice));
+		CHK(hipMalloc((void **)&r, (size_t)n * 16));
+		kps[i] = (mosrx_kparams){f, o, l, r, tables, NULL, NULL, NULL, NULL, (uint32_t)t.frames_bytes, n,
+		                         MOSRX_KF_VERIFY};
+	}
+	const uint32_t bn = 32768u, nbat = n / bn;
+	g_qtiles = nbat * (bn / MOSRX_SMALL_FRAMES);
+	for (int i = 0; i < nb; i++) {
+		std::vector<mosrx_qdesc> qd(nbat);
+		for (uint32_t k = 0; k < nbat; k++) {
+			memset(&qd[k], 0, sizeof(qd[k]));
+			qd[k].frames = kps[i].frames;
+			qd[k].off = kps[i].off + (size_t)k * bn;
+			qd[k].len = kps[i].len + (size_t)k * bn;
+			qd[k].out = kps[i].out + (size_t)k * bn;
+			qd[k].frames_bytes = kps[i].frames_bytes;
+			qd[k].n = bn;
+			qd[k].tile_base = k * (bn / MOSRX_SMALL_FRAMES);
+		}
+		mosrx_qdesc *dq;
+		CHK(hipMalloc((void **)&dq, nbat * sizeof(mosrx_qdesc)));
+		CHK(hipMemcpy(dq, qd.data(), nbat * sizeof(mosrx_qdesc), hipMemcpyHostToDevice));
+		memset(&g_qp[i], 0, sizeof(g_qp[i]));
+		g_qp[i].desc = dq;
+		g_qp[i].tables = tables;
+		g_qp[i].counters = (uint32_t *)kps[i].off;   // lookup key only (cleared at launch)
+		g_qp[i].nb = nbat;
+		g_qp[i].flags = MOSRX_KF_VERIFY;
+		g_qp[i].tpb = bn / MOSRX_SMALL_FRAMES;
+	}
+	const double bytes = (double)t.caplen_sum + 22.0 * n;
+	printf("S64 n %u: %.2f MB algorithmic in one launch\n", n, bytes / 1e6);
+	struct { const char *name; launch_fn fn; } forms[] = {
+	    {"library", launch<0>},          {"queue 256 x 32K", launch_queue}, {"no Toeplitz", launch<16384>},
+	    {"no record stores", launch<4>}, {"no window loads", launch<2>},    {"neither", launch<6>}};
+	// the library's records: deterministic, and the census of the trace
+	std::vector<mosrx_result> a(n), b(n);
+	for (int k = 0; k < 2; k++) {
+		CHK(hipMemset(kps[k].out, 0xEE, (size_t)n * 16));
+		launch<0>(kps[k], 0);
+		CHK(hipDeviceSynchronize());
+	}
+	CHK(hipMemcpy(a.data(), kps[0].out, (size_t)n * 16, hipMemcpyDeviceToHost));
+	CHK(hipMemcpy(b.data(), kps[1].out, (size_t)n * 16, hipMemcpyDeviceToHost));
+	uint64_t ok = 0;
+	for (uint32_t i = 0; i < n; i++)
+		ok += a[i].verdict == 1;
+	printf("library records: %s across runs, %lu of %u frames verdict 1\n",
+	       memcmp(a.data(), b.data(), (size_t)n * 16) ? "DIFFER" : "equal", (unsigned long)ok, n);
+	CHK(hipMemset(kps[1].out, 0xEE, (size_t)n * 16));
+	launch_queue(kps[1], 0);
+	CHK(hipDeviceSynchronize());
+	CHK(hipMemcpy(b.data(), kps[1].out, (size_t)n * 16, hipMemcpyDeviceToHost));
+	printf("queue records: %s to the single launch's\n", memcmp(a.data(), b.data(), (size_t)n * 16) ? "DIFFER" : "equal");
+	hipEvent_t e0, e1;
+	CHK(hipEventCreate(&e0));
+	CHK(hipEventCreate(&e1));
+	const int iters = 30;
+	for (int rep = 0; rep < 3; rep++) {
+		for (auto &f : forms) {
+			CHK(hipDeviceSynchronize());
+			CHK(hipEventRecord(e0, 0));
+			for (int i = 0; i < iters; i++)
+				f.fn(kps[i % nb], 0);
+			CHK(hipEventRecord(e1, 0));
+			CHK(hipEventSynchronize(e1));
+			float ms;
+			CHK(hipEventElapsedTime(&ms, e0, e1));
+			printf("rep %d %-18s %8.2f us per launch (%.3f of 8 TB/s, %.1f Gpkt/s)\n", rep, f.name, ms * 1e3 / iters,
+			       bytes / (ms * 1e-3 / iters) / 8e12, n / (ms * 1e-3 / iters) / 1e9);
+		}
+	}
+	return 0;
+}

@@ -219,7 +219,11 @@ def measure(ctx, dist, key, steps, warmup, rank):
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         kk = 500
-        kern_ms = median_of(lambda: step_fn(kk, 1) / kk)
+        # the kernel's own duration (each launch stamped by its dispatch, as
+        # rocprofv3 reports it); ops of more than one launch: back to back
+        kern_b2b = median_of(lambda: step_fn(kk, 1) / kk)
+        kern_ms = (median_of(lambda: ctx.time_op_dispatch(op, dbs, kk, arg))
+                   if ctx.time_op_dispatch(op, dbs, 8, arg) is not None else kern_b2b)
         kern_iso = None
         frames_per_step, ab_step = batch, ab
         method = f"one launch per batch, batch i on stream i % {STREAMS}"
@@ -240,7 +244,8 @@ def measure(ctx, dist, key, steps, warmup, rank):
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         kk = max(16, 4 * len(qs))
-        kern_ms = median_of(lambda: qs[0].time(kk, qs[1:], kernels=False)[0] / kk)
+        kern_b2b = median_of(lambda: qs[0].time(kk, qs[1:], kernels=False)[0] / kk)
+        kern_ms = median_of(lambda: qs[0].time_dispatch(kk, qs[1:]))
         _, kern_iso = qs[0].time(min(kk, 32), qs[1:])
         for q in qs:
             q.destroy()
@@ -260,12 +265,14 @@ def measure(ctx, dist, key, steps, warmup, rank):
         dist.barrier()
         wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
-        # roofline: average launch duration on ONE stream, HIP events around
-        # 500 back-to-back launches on the launch stream (the figure rocprofv3's
-        # kernel trace reports), median of 5 such runs; the isolated figure
-        # (events around each single launch, dispatch included) is kept beside it
+        # roofline: the kernel's own duration over 500 back-to-back launches on
+        # ONE stream, each launch stamped by its dispatch (hipExtLaunchKernel: the
+        # figure rocprofv3's kernel trace reports), median of 5 such runs; kept
+        # beside it: events around the 500 launches (dispatch gaps included) and
+        # around each single launch (dispatch included)
         kk = 500
-        kern_ms = median_of(lambda: ctx.time_dev_streams(dbs, kk, 1) / kk)
+        kern_b2b = median_of(lambda: ctx.time_dev_streams(dbs, kk, 1) / kk)
+        kern_ms = median_of(lambda: ctx.time_op_dispatch(mosrx.OP_CLASSIFY, dbs, kk))
         kern_iso = ctx.time_dev_kernels(dbs, kk)
         frames_per_step, ab_step = batch, ab
         method = f"one launch per batch, batch i on stream i % {STREAMS}"
@@ -288,6 +295,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         "mpkts": n * frames_per_step * steps / wall_max / 1e6,
         "device_ms_per_step": dev_ms / steps,
         "kernel_ms": kern_ms,
+        "kernel_ms_back_to_back": kern_b2b,
         "kernel_ms_isolated": kern_iso,
     }
     achieved = ab_step / (kern_ms * 1e-3) / 1e9
@@ -299,10 +307,12 @@ def measure(ctx, dist, key, steps, warmup, rank):
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 4),
         "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
-        # the launch duration behind `achieved` (HIP events around back-to-back
-        # launches on the launch stream, median of 5), and the timed region's own
-        # device time per step (HIP events around the K timed steps)
+        # the launch duration behind `achieved` (the kernel's own duration, each
+        # of the back-to-back launches stamped by its dispatch, median of 5), and
+        # the timed region's own device time per step (HIP events around the K
+        # timed steps)
         "launch_us": round(kern_ms * 1e3, 3),
+        "launch_us_back_to_back": round(kern_b2b * 1e3, 3),
         "timed_region_device_us_per_step": round(1e3 * dev_ms / steps, 3),
     }
     if pmc:

@@ -288,6 +288,14 @@ enum { MOSRX_OP_CLASSIFY = 0, MOSRX_OP_CLASSIFY_FH = 1, MOSRX_OP_BPF = 2, MOSRX_
        MOSRX_OP_CLASSIFY_BPF = 4, MOSRX_OP_CLASSIFY_TI = 5 /* aux[i]: mosrx_tcpinfo side arrays */ };
 int  mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
                    void *const *aux, uint32_t iters, uint32_t nstreams, float *total_ms, float *avg_kernel_ms);
+/* The kernel's own duration, averaged over `iters` back-to-back launches on
+ * the context stream: each launch carries a start / stop event pair that the
+ * dispatch itself stamps (hipExtLaunchKernel), so the gap between dispatches
+ * is not counted -- the duration rocprofv3's kernel trace reports.  -ENOTSUP
+ * for an operation that is not one kernel launch (the BPF rows). */
+int  mosrx_time_op_dispatch(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
+                            void *const *aux, uint32_t iters, float *avg_ms);
+int  mosrx_time_queue_dispatch(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq, uint32_t iters, float *avg_ms);
 /* The device's streaming-read ceiling: `iters` coalesced 16-byte-load passes
  * cycling over `nbuf` buffers of `bytes` each (sized past the 256 MiB Infinity
  * Cache), in GB/s.  The roofline figure next to the 8 TB/s spec peak. */

@@ -1182,6 +1182,88 @@ int mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t 
 	return 0;
 }
 
+/* One launch of the operation being timed (launch i). */
+typedef int (*stamped_fn)(mosrx_ctx *c, uint32_t i, void *arg);
+
+/* Average kernel duration over `iters` back-to-back launches on the context
+ * stream, each stamped by its own dispatch (mosrx__stamp_next): -ENOTSUP when
+ * a launch of the operation was not exactly one kernel of mosrx_kernels.hip. */
+static int time_stamped(mosrx_ctx *c, uint32_t iters, stamped_fn run, void *arg, float *avg_ms)
+{
+	hipEvent_t *ev;
+	uint32_t i;
+	int rc = 0;
+	double tot = 0;
+	ev = calloc((size_t)iters * 2, sizeof(*ev));
+	if (!ev)
+		return -ENOMEM;
+	for (i = 0; i < iters * 2 && !rc; i++)
+		if (hipEventCreate(&ev[i]) != hipSuccess)
+			rc = -EIO;
+	for (i = 0; i < iters && !rc; i++) {
+		const uint32_t n0 = mosrx__launch_count();
+		mosrx__stamp_next(ev[2 * i], ev[2 * i + 1]);
+		rc = run(c, i, arg);
+		mosrx__stamp_next(NULL, NULL);
+		if (!rc && mosrx__launch_count() - n0 != 1)
+			rc = -ENOTSUP;
+	}
+	if (hipStreamSynchronize(c->stream) != hipSuccess && !rc)
+		rc = -EIO;
+	for (i = 0; i < iters && !rc; i++) {
+		float ms = 0;
+		if (hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]) != hipSuccess) { rc = -EIO; break; }
+		tot += ms;
+	}
+	for (i = 0; i < iters * 2; i++)
+		if (ev[i])
+			hipEventDestroy(ev[i]);
+	free(ev);
+	if (!rc)
+		*avg_ms = (float)(tot / iters);
+	return rc;
+}
+
+struct op_run { int op, arg; const mosrx_batch *b; uint32_t nb; void *const *out, *const *aux; };
+
+static int op_once(mosrx_ctx *c, uint32_t i, void *a)
+{
+	const struct op_run *r = a;
+	return run_op(c, r->op, r->arg, &r->b[i % r->nb], r->out ? r->out[i % r->nb] : NULL,
+	              r->aux ? r->aux[i % r->nb] : NULL, c->stream);
+}
+
+int mosrx_time_op_dispatch(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
+                           void *const *aux, uint32_t iters, float *avg_ms)
+{
+	struct op_run r = {op, arg, b, nb, out, aux};
+	if (!c || !b || nb == 0 || iters == 0 || !avg_ms || op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_CLASSIFY_TI ||
+	    (op != MOSRX_OP_TX_CSUM && !out) ||
+	    ((op == MOSRX_OP_CLASSIFY_FH || op == MOSRX_OP_CLASSIFY_BPF || op == MOSRX_OP_CLASSIFY_TI) && !aux))
+		return -EINVAL;
+	if (op == MOSRX_OP_BPF || op == MOSRX_OP_CLASSIFY_BPF)   /* the BPF kernels are launched elsewhere */
+		return -ENOTSUP;
+	HIPCHK(hipSetDevice(c->device));
+	return time_stamped(c, iters, op_once, &r, avg_ms);
+}
+
+struct queue_run { mosrx_queue *const *q; uint32_t nq; };
+
+static int queue_once(mosrx_ctx *c, uint32_t i, void *a)
+{
+	const struct queue_run *r = a;
+	return mosrx_queue_run(c, r->q[i % r->nq], c->stream);
+}
+
+int mosrx_time_queue_dispatch(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq, uint32_t iters, float *avg_ms)
+{
+	struct queue_run r = {q, nq};
+	if (!c || !q || nq == 0 || iters == 0 || !avg_ms)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	return time_stamped(c, iters, queue_once, &r, avg_ms);
+}
+
 int mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
                            uint32_t iters, float *avg_ms)
 {

@@ -127,6 +127,12 @@ int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sink, void *st
 /* Launch one classify kernel; returns 0 or -EINVAL / -EIO.  `stream` is a hipStream_t. */
 int mosrx_launch_classify(const mosrx_kparams *kp, int tile, int variant, void *stream);
 
+/* Dispatch-stamped timing hooks (mosrx_kernels.hip): the next classify / queue
+ * launch of the calling thread takes this start / stop event pair; the count
+ * of launches made by the thread so far. */
+void mosrx__stamp_next(void *start, void *stop);
+uint32_t mosrx__launch_count(void);
+
 #ifdef __cplusplus
 }
 #endif

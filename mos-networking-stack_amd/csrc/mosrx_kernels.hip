@@ -38,6 +38,7 @@
 
 #ifndef __HIPCC_RTC__   // hipRTC compiles this file too, for the fused classify + BPF kernel (bpf_jit.c)
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <errno.h>
 #endif
 
@@ -1264,19 +1265,45 @@ extern "C" int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sin
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// Dispatch-stamped timing (mosrx_time_op_dispatch / mosrx_time_queue_dispatch):
+// the next classify or queue launch of this thread carries a start / stop
+// event pair that the runtime stamps at the dispatch's own begin and end
+// (hipExtLaunchKernel) -- the kernel duration rocprofv3's trace reports,
+// without the gap between back-to-back dispatches that events recorded around
+// the launches include.  The count lets the caller check that an operation
+// was exactly one launch.
+static thread_local hipEvent_t t_stamp0, t_stamp1;
+static thread_local uint32_t t_launches;
+extern "C" void mosrx__stamp_next(void *start, void *stop)
+{
+	t_stamp0 = (hipEvent_t)start;
+	t_stamp1 = (hipEvent_t)stop;
+}
+extern "C" uint32_t mosrx__launch_count(void) { return t_launches; }
+
+template <typename P>
+static void launch_one(void (*k)(P), uint32_t grid, uint32_t block, hipStream_t s, const P &p)
+{
+	t_launches++;
+	if (t_stamp0) {
+		hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, t_stamp0, t_stamp1, 0, p);
+		t_stamp0 = t_stamp1 = nullptr;
+	} else {
+		hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, p);
+	}
+}
+
 template <int KIND, int VAR>
 static void launch_queue_v(const mosrx_qparams *qp, uint32_t total_tiles, hipStream_t s)
 {
-	hipLaunchKernelGGL((mosrx_classify_queue_kernel<KIND, VAR>), dim3(total_tiles), dim3(WG_THREADS(KIND)), 0, s,
-	                   *qp);
+	launch_one(mosrx_classify_queue_kernel<KIND, VAR>, total_tiles, WG_THREADS(KIND), s, *qp);
 }
 
 template <int KIND, int VAR>
 static void launch_v(const mosrx_kparams *kp, hipStream_t s)
 {
 	constexpr uint32_t tile = MOSRX_KIND_FRAMES(KIND);
-	hipLaunchKernelGGL((mosrx_classify_kernel<KIND, VAR>), dim3((kp->n + tile - 1) / tile), dim3(WG_THREADS(KIND)),
-	                   0, s, *kp);
+	launch_one(mosrx_classify_kernel<KIND, VAR>, (kp->n + tile - 1) / tile, WG_THREADS(KIND), s, *kp);
 }
 
 // Compiled variants: 0 = default cache policy, 2 = non-temporal tail stream

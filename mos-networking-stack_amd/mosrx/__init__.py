@@ -182,6 +182,9 @@ def lib():
             "mosrx_time_op": (I, [P, I, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P), U32, U32,
                                   C.POINTER(C.c_float), C.POINTER(C.c_float)]),
             "mosrx_time_dev_streams": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, U32, C.POINTER(C.c_float)]),
+            "mosrx_time_op_dispatch": (I, [P, I, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P), U32,
+                                           C.POINTER(C.c_float)]),
+            "mosrx_time_queue_dispatch": (I, [P, C.POINTER(P), U32, U32, C.POINTER(C.c_float)]),
             "mosrx_probe_read_bw": (I, [P, U64, U32, U32, C.POINTER(C.c_float)]),
             "mosrx_queue_create": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
             "mosrx_queue_run": (I, [P, P, P]),
@@ -634,6 +637,23 @@ class Context:
              "mosrx_time_op")
         return (float(tot.value) if total else None), (float(avg.value) if kernels else None)
 
+    def time_op_dispatch(self, op: int, dbs: list[DevBatch], iters: int, arg: int = 0):
+        """mosrx_time_op_dispatch: the kernel's own average duration (ms), each
+        launch stamped by its dispatch; None for an op that is not one kernel."""
+        def ptr(buf):
+            return buf.ptr if buf is not None else None
+        bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
+        outs = (C.c_void_p * len(dbs))(*[(ptr(d.d_match) if op == OP_BPF else d.d_out.ptr) for d in dbs])
+        aux = (C.c_void_p * len(dbs))(*[(ptr(d.d_match) if op == OP_CLASSIFY_BPF else
+                                         ptr(d.d_tinfo) if op == OP_CLASSIFY_TI else
+                                         ptr(d.d_fhash) if op == OP_CLASSIFY_FH else None) for d in dbs])
+        ms = C.c_float()
+        rc = lib().mosrx_time_op_dispatch(self.handle, op, arg, bs, len(dbs), outs, aux, iters, C.byref(ms))
+        if rc == -95:   # -ENOTSUP: more than one launch per operation
+            return None
+        _chk(rc, "mosrx_time_op_dispatch")
+        return float(ms.value)
+
     def time_dev_streams(self, dbs: list[DevBatch], iters: int, nstreams: int) -> float:
         """Total ms for `iters` launches spread round-robin over `nstreams` streams."""
         bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
@@ -706,6 +726,16 @@ class Queue:
         _chk(lib().mosrx_time_queue(self.ctx.handle, arr, len(qs), iters, C.byref(tot),
                                     C.byref(kern) if kernels else None), "mosrx_time_queue")
         return float(tot.value), (float(kern.value) if kernels else None)
+
+    def time_dispatch(self, iters: int, others: list["Queue"] = ()) -> float:
+        """The queue kernel's own average duration (ms) over `iters` back-to-back
+        launches cycling over self + others, each stamped by its dispatch."""
+        qs = [self] + list(others)
+        arr = (C.c_void_p * len(qs))(*[q.handle for q in qs])
+        ms = C.c_float()
+        _chk(lib().mosrx_time_queue_dispatch(self.ctx.handle, arr, len(qs), iters, C.byref(ms)),
+             "mosrx_time_queue_dispatch")
+        return float(ms.value)
 
     def destroy(self):
         if self.handle:

@@ -346,6 +346,32 @@ def test_batch_queue_one_launch(gpu_ctx, kind, n, nb):
         d.free()
 
 
+def test_dispatch_stamped_kernel_timing(gpu_ctx):
+    """The bench's roofline duration (mosrx_time_op_dispatch / _queue_dispatch):
+    every launch stamped by its own dispatch, so never longer than the same
+    launches timed back to back with events around them (dispatch gaps
+    included); BPF rows (not one kernel of mosrx_kernels.hip) are refused; the
+    stamped launches leave the same records."""
+    gpu_ctx.set_params(mosrx.default_params())
+    trs = [mosrx.Trace(mosrx.TRACE_M1500, 4096, nflows=4000, seed=200 + i) for i in range(2)]
+    dbs = [gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len) for t in trs]
+    stamped = gpu_ctx.time_op_dispatch(mosrx.OP_CLASSIFY, dbs, 64)
+    b2b = gpu_ctx.time_dev_streams(dbs, 64, 1) / 64
+    assert 0 < stamped <= b2b * 1.02, (stamped, b2b)
+    for t, d in zip(trs, dbs):
+        assert_records_equal(d.results(), O.classify(t.frames, t.off, t.len, O.params()), "stamped")
+    gpu_ctx.time_op(mosrx.OP_CLASSIFY_FH, dbs, 2, kernels=False)                # side buffers allocated
+    assert gpu_ctx.time_op_dispatch(mosrx.OP_CLASSIFY_FH, dbs, 16) > 0
+    assert gpu_ctx.time_op_dispatch(mosrx.OP_BPF, dbs, 4) is None
+    q = gpu_ctx.queue(dbs)
+    qs = q.time_dispatch(16)
+    qb = q.time(16, kernels=False)[0] / 16
+    assert 0 < qs <= qb * 1.02, (qs, qb)
+    q.destroy()
+    for d in dbs:
+        d.free()
+
+
 # kernel shapes forced through variant bits 2-6 (value - 1: SMALL, S13) with both tail-load
 # cache policies; every shape must be exact on every frame mix
 STREAM_VARIANTS = [mosrx.shape_variant(mosrx.KIND_S13), mosrx.shape_variant(mosrx.KIND_S13, False)]

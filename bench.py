@@ -173,6 +173,18 @@ def median_of(fn, reps: int = 5) -> float:
     return float(np.median([fn() for _ in range(reps)]))
 
 
+def kernel_duration(stamped, back_to_back: float):
+    """(ms, method) of one launch for the roofline: the kernel's own duration
+    from dispatch-stamped events (median of 5) when the operation is one kernel
+    and the runtime stamps it, else the back-to-back figure."""
+    try:
+        if stamped() is not None:
+            return median_of(stamped), "dispatch-stamped (hipExtLaunchKernel events), median of 5"
+    except mosrx.MosrxError as e:
+        print(f"[bench] dispatch-stamped timing unavailable ({e}): back-to-back figure used", file=sys.stderr)
+    return back_to_back, "HIP events around back-to-back launches, median of 5"
+
+
 def resident_batches(ctx, key, world, rank, nres):
     """`nres` resident batches of this rank's share of the job: the contents of its
     first job batches (seeded per job batch; DISTINCT of them for a ring, 2 for the
@@ -222,8 +234,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         # the kernel's own duration (each launch stamped by its dispatch, as
         # rocprofv3 reports it); ops of more than one launch: back to back
         kern_b2b = median_of(lambda: step_fn(kk, 1) / kk)
-        kern_ms = (median_of(lambda: ctx.time_op_dispatch(op, dbs, kk, arg))
-                   if ctx.time_op_dispatch(op, dbs, 8, arg) is not None else kern_b2b)
+        kern_ms, timing = kernel_duration(lambda: ctx.time_op_dispatch(op, dbs, kk, arg), kern_b2b)
         kern_iso = None
         frames_per_step, ab_step = batch, ab
         method = f"one launch per batch, batch i on stream i % {STREAMS}"
@@ -245,7 +256,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         wall_max = dist.max(wall)
         kk = max(16, 4 * len(qs))
         kern_b2b = median_of(lambda: qs[0].time(kk, qs[1:], kernels=False)[0] / kk)
-        kern_ms = median_of(lambda: qs[0].time_dispatch(kk, qs[1:]))
+        kern_ms, timing = kernel_duration(lambda: qs[0].time_dispatch(kk, qs[1:]), kern_b2b)
         _, kern_iso = qs[0].time(min(kk, 32), qs[1:])
         for q in qs:
             q.destroy()
@@ -272,7 +283,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         # around each single launch (dispatch included)
         kk = 500
         kern_b2b = median_of(lambda: ctx.time_dev_streams(dbs, kk, 1) / kk)
-        kern_ms = median_of(lambda: ctx.time_op_dispatch(mosrx.OP_CLASSIFY, dbs, kk))
+        kern_ms, timing = kernel_duration(lambda: ctx.time_op_dispatch(mosrx.OP_CLASSIFY, dbs, kk), kern_b2b)
         kern_iso = ctx.time_dev_kernels(dbs, kk)
         frames_per_step, ab_step = batch, ab
         method = f"one launch per batch, batch i on stream i % {STREAMS}"
@@ -312,6 +323,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         # the timed region's own device time per step (HIP events around the K
         # timed steps)
         "launch_us": round(kern_ms * 1e3, 3),
+        "launch_timing": timing,
         "launch_us_back_to_back": round(kern_b2b * 1e3, 3),
         "timed_region_device_us_per_step": round(1e3 * dev_ms / steps, 3),
     }
@@ -934,7 +946,8 @@ def headline_line(detail, h, head, results, e2e):
         "config": {"workload": h["workload"], "batch": h["batch"], "batches_per_step": h["batches_per_step"],
                    "algo_bytes_per_batch": h["algo_bytes_per_batch"],
                    "parallelism": detail["config"]["parallelism"]},
-        "roofline": {k: rf[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_us")},
+        "roofline": {k: rf[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_us",
+                                         "launch_timing")},
         "read_ceiling_gbps": detail["read_ceiling_gbps"],
         "frac_of_read_ceiling": detail["frac_of_read_ceiling"],
         "cpu_baseline": cpu_line,

@@ -23,7 +23,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t *base
 // Capture length clipped to the batch buffer (a frame never reads past it).
 __device__ __forceinline__ uint32_t eff_caplen(uint32_t o, uint32_t len, uint32_t nbytes)
 {
-	return (o >= nbytes) ? 0u : min(len, nbytes - o);
+	// select form, not a branch: a branch lets the compiler sink the len[]
+	// load behind the off[] load (one more round trip before any frame byte)
+	return min(len, o < nbytes ? nbytes - o : 0u);
 }
 
 #endif

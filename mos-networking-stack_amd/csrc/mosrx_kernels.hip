@@ -601,12 +601,15 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	for (uint32_t i = 0; i < FPL; i++) {
 		pv[i] = tile * TILE + 256u * i + t;
 		actv[i] = pv[i] < kp.n;
-		ov[i] = 0;
-		capv[i] = 0;
-		if (actv[i]) {
-			ov[i] = kp.off[pv[i]];
-			capv[i] = eff_caplen(ov[i], kp.len[pv[i]], nbytes);
-		}
+		// unconditional loads from a clamped index: the descriptor pointers then
+		// come in the kernel's first scalar loads instead of a second, dependent
+		// round trip behind a branch (the ramp of every tile)
+		const uint32_t q = min(pv[i], kp.n - 1u);
+		const uint32_t o = kp.off[q];
+		uint32_t l = kp.len[q];
+		asm volatile("" : "+v"(l));   // keep the len[] load unconditional
+		ov[i] = actv[i] ? o : 0u;
+		capv[i] = actv[i] ? eff_caplen(o, l, nbytes) : 0u;
 	}
 	hdr_win_t winv[FPL];
 #pragma unroll
@@ -1024,11 +1027,13 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 	// every wave reads the tile's descriptors (lane = frame)
 	const uint32_t p = first + lane;
 	const bool active = lane < nact;
-	uint32_t o = 0, cap = 0;
-	if (active) {
-		o = kp.off[p];
-		cap = eff_caplen(o, kp.len[p], nbytes);
-	}
+	// unconditional (clamped to the tile's first frame, cnt >= 1): no branch
+	// between the kernel's scalar loads and the descriptor loads
+	const uint32_t q = active ? p : first;
+	const uint32_t od = kp.off[q];
+	uint32_t ld = kp.len[q];
+	asm volatile("" : "+v"(ld));   // keep the len[] load unconditional (not sunk into a branch)
+	const uint32_t o = active ? od : 0u, cap = active ? eff_caplen(od, ld, nbytes) : 0u;
 	// speculative tail bounds from the capture length: [split, off + caplen)
 	const uint32_t lo_l = (o + (uint32_t)WEND) & ~15u;
 	const uint32_t hi_l = active ? o + cap : 0u;
@@ -1181,10 +1186,23 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 // The stream tiles are held to 64 VGPRs: 8 waves per SIMD.
 #define MIN_WAVES(kind) ((kind) != MOSRX_KIND_SMALL ? 8 : 1)
 
+// The fields every tile needs before its first frame byte lead the argument
+// list as scalars: the build preloads them into SGPRs at dispatch
+// (-amdgpu-kernarg-preload-count, Makefile), so a tile's first memory access is
+// its descriptor load, not a kernarg round trip.  The rest of kp is read from
+// the kernarg segment while the descriptors are on their way.
 template <int KIND, int VAR>
 __global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))
-void mosrx_classify_kernel(mosrx_kparams kp)
+void mosrx_classify_kernel(const uint32_t *off, const uint16_t *len, const uint8_t *frames, const uint32_t *tables,
+                           uint32_t frames_bytes, uint32_t n, uint32_t flags, mosrx_kparams kp)
 {
+	kp.off = off;
+	kp.len = len;
+	kp.frames = frames;
+	kp.tables = tables;
+	kp.frames_bytes = frames_bytes;
+	kp.n = n;
+	kp.flags = flags;
 	classify_tile<KIND, VAR>(kp, blockIdx.x);
 }
 
@@ -1194,8 +1212,11 @@ void mosrx_classify_kernel(mosrx_kparams kp)
 // search of tile_base[] (a chain of dependent scalar loads).
 template <int KIND, int VAR>
 __global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))
-void mosrx_classify_queue_kernel(mosrx_qparams qp)
+void mosrx_classify_queue_kernel(const mosrx_qdesc *desc, uint32_t tpb, uint32_t nb, mosrx_qparams qp)
 {
+	qp.desc = desc;   // preloaded (see mosrx_classify_kernel): the batch lookup starts at dispatch
+	qp.tpb = tpb;
+	qp.nb = nb;
 	const uint32_t b = blockIdx.x;
 	uint32_t lo = 0, hi = qp.nb;               // find k: tile_base[k] <= b < tile_base[k+1]
 	if (qp.tpb)
@@ -1281,29 +1302,31 @@ extern "C" void mosrx__stamp_next(void *start, void *stop)
 }
 extern "C" uint32_t mosrx__launch_count(void) { return t_launches; }
 
-template <typename P>
-static void launch_one(void (*k)(P), uint32_t grid, uint32_t block, hipStream_t s, const P &p)
+template <typename... P, typename... A>
+static void launch_one(void (*k)(P...), uint32_t grid, uint32_t block, hipStream_t s, const A &...a)
 {
 	t_launches++;
 	if (t_stamp0) {
-		hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, t_stamp0, t_stamp1, 0, p);
+		hipExtLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, t_stamp0, t_stamp1, 0, a...);
 		t_stamp0 = t_stamp1 = nullptr;
 	} else {
-		hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, p);
+		hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, a...);
 	}
 }
 
 template <int KIND, int VAR>
 static void launch_queue_v(const mosrx_qparams *qp, uint32_t total_tiles, hipStream_t s)
 {
-	launch_one(mosrx_classify_queue_kernel<KIND, VAR>, total_tiles, WG_THREADS(KIND), s, *qp);
+	launch_one(mosrx_classify_queue_kernel<KIND, VAR>, total_tiles, WG_THREADS(KIND), s, qp->desc, qp->tpb, qp->nb,
+	           *qp);
 }
 
 template <int KIND, int VAR>
 static void launch_v(const mosrx_kparams *kp, hipStream_t s)
 {
 	constexpr uint32_t tile = MOSRX_KIND_FRAMES(KIND);
-	launch_one(mosrx_classify_kernel<KIND, VAR>, (kp->n + tile - 1) / tile, WG_THREADS(KIND), s, *kp);
+	launch_one(mosrx_classify_kernel<KIND, VAR>, (kp->n + tile - 1) / tile, WG_THREADS(KIND), s, kp->off, kp->len,
+	           kp->frames, kp->tables, kp->frames_bytes, kp->n, kp->flags, *kp);
 }
 
 // Compiled variants: 0 = default cache policy, 2 = non-temporal tail stream

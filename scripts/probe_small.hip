@@ -37,7 +37,7 @@ static void launch_queue(const mosrx_kparams &kp, hipStream_t st)
 			mosrx_qparams q = g_qp[i];
 			q.counters = nullptr;
 			hipLaunchKernelGGL((mosrx_classify_queue_kernel<MOSRX_KIND_SMALL, 0>), dim3(g_qtiles),
-			                   dim3(SMALL_THREADS), 0, st, q);
+			                   dim3(SMALL_THREADS), 0, st, q.desc, q.tpb, q.nb, q);
 		}
 }
 

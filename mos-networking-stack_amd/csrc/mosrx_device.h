@@ -20,6 +20,44 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t *base
 	return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)((nbytes + 15u) & ~15u), 0x00020000);
 }
 
+// Stores of the per-frame outputs (records, side arrays): written once, read
+// by the host after the launch.  MOSRX_OUT_AUX (A/B builds) picks the cache
+// policy bits of a buffer store instead (gfx950: 1 sc0, 2 nt, 16 sc1).
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+// out_store(base, i, v): element i of a per-frame output array (`base` is
+// uniform: the kernel's argument).
+#ifdef MOSRX_OUT_AUX
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void *base)
+{
+	return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, 0x7FFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ void out_store(u32x4 *base, uint32_t i, u32x4 v)
+{
+	__builtin_amdgcn_raw_buffer_store_b128(v, out_rsrc(base), 16u * i, 0, MOSRX_OUT_AUX);
+}
+__device__ __forceinline__ void out_store(uint32_t *base, uint32_t i, u32x3 v)   // 12-byte elements
+{
+	__builtin_amdgcn_raw_buffer_store_b96(v, out_rsrc(base), 12u * i, 0, MOSRX_OUT_AUX);
+}
+__device__ __forceinline__ void out_store(uint32_t *base, uint32_t i, uint32_t v)
+{
+	__builtin_amdgcn_raw_buffer_store_b32(v, out_rsrc(base), 4u * i, 0, MOSRX_OUT_AUX);
+}
+#else
+__device__ __forceinline__ void out_store(u32x4 *base, uint32_t i, u32x4 v)
+{
+	__builtin_nontemporal_store(v, base + i);
+}
+__device__ __forceinline__ void out_store(uint32_t *base, uint32_t i, u32x3 v)   // 12-byte elements
+{
+	__builtin_nontemporal_store(v, reinterpret_cast<u32x3 *>(base + 3u * i));
+}
+__device__ __forceinline__ void out_store(uint32_t *base, uint32_t i, uint32_t v)
+{
+	__builtin_nontemporal_store(v, base + i);
+}
+#endif
+
 // Capture length clipped to the batch buffer (a frame never reads past it).
 __device__ __forceinline__ uint32_t eff_caplen(uint32_t o, uint32_t len, uint32_t nbytes)
 {

@@ -476,12 +476,11 @@ __device__ __forceinline__ uint32_t flow_hash(const hdr_t &h)
 __device__ __forceinline__ void store_tcpinfo(mosrx_tcpinfo *ti, uint32_t p, const hdr_t &h)
 {
 	const bool def = h.fields && h.is_tcp;
-	typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 	u32x3 v;
 	v.x = def ? __builtin_bswap32(h.th1) : 0u;
 	v.y = def ? __builtin_bswap32(h.th2) : 0u;
 	v.z = def ? (((h.th3 >> 24) | ((h.th3 >> 8) & 0xFF00u)) | (h.ip_len << 16)) : 0u;   // window = tcph bytes 14,15
-	__builtin_nontemporal_store(v, reinterpret_cast<u32x3 *>(reinterpret_cast<uint32_t *>(ti) + 3u * p));
+	out_store(reinterpret_cast<uint32_t *>(ti), p, v);
 }
 
 // TX: write the fresh checksums into the frame (little-endian u16 stores, as
@@ -540,7 +539,7 @@ __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffe
 // 1500 B 122 -> 119 us, IMIX 141 -> 135 us, 64 B 127 -> 123 us).
 __device__ __forceinline__ void store_record(const mosrx_kparams &kp, uint32_t p, u32x4 rec, uint32_t *s_cnt)
 {
-	__builtin_nontemporal_store(rec, reinterpret_cast<u32x4 *>(kp.out + p));
+	out_store(reinterpret_cast<u32x4 *>(kp.out), p, rec);
 	if (kp.counters) {
 		const uint32_t reason = rec.w & 0xFFu;
 		uint64_t m = __ballot(1);
@@ -671,7 +670,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 		if (active)
 			store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (active && kp.fhash)
-			__builtin_nontemporal_store(flow_hash(h), kp.fhash + p);
+			out_store(kp.fhash, p, flow_hash(h));
 		if constexpr (IS_TI(VAR)) {
 			if (active)
 				store_tcpinfo(kp.tinfo, p, h);
@@ -682,7 +681,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 		__shared__ uint32_t s_bw[25u * 256u];
 		const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * t);
 		if (active)
-			__builtin_nontemporal_store(m, kp.bmatch + p);
+			out_store(kp.bmatch, p, m);
 	}
 #endif
 	}
@@ -734,7 +733,7 @@ __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffe
 	} else if (active) {
 		store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (kp.fhash)
-			__builtin_nontemporal_store(flow_hash(h), kp.fhash + p);
+			out_store(kp.fhash, p, flow_hash(h));
 		if constexpr (IS_TI(VAR))
 			store_tcpinfo(kp.tinfo, p, h);
 	}
@@ -1103,7 +1102,7 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 			} else {
 				// the outputs that do not need the tail sum go out before the barrier
 				if (active && kp.fhash)
-					__builtin_nontemporal_store(flow_hash(h), kp.fhash + p);
+					out_store(kp.fhash, p, flow_hash(h));
 				if constexpr (IS_TI(VAR)) {
 					if (active)
 						store_tcpinfo(kp.tinfo, p, h);
@@ -1113,7 +1112,7 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 					__shared__ uint32_t s_bw[25u * 64u];
 					const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * lane);
 					if (active)
-						__builtin_nontemporal_store(m, kp.bmatch + p);
+						out_store(kp.bmatch, p, m);
 				}
 #endif
 				const hdr_pend_t q =

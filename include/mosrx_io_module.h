@@ -15,7 +15,9 @@
  *     pcap_module.c:37-38) and get_rptr pointers stay valid until the next
  *     recv_pkts on that ifidx (dpdk_module.c:379-382, pcap_module.c:41);
  *   - dev_ioctl(PKT_RX_RSS) fills RssInfo{int8 pktidx, u32 hash_value}
- *     (io_module.h:81-84, dpdk_module.c:568-571); -1 for unsupported commands;
+ *     (io_module.h:81-84, dpdk_module.c:568-571); PKT_TX_IP_CSUM /
+ *     PKT_TX_TCP_CSUM are taken as a NIC offload when cfg.tx_csum is set
+ *     (dpdk_module.c:556-566); -1 for unsupported commands;
  *   - NULL members are "not provided" (select, link_devices, set_wptr).
  * New: dev_ioctl(MOSRX_PKT_RX_RESULTS) returns the batch's mosrx_result array,
  * whose verdicts the rx loop consumes instead of re-running ProcessPacket's checks;
@@ -190,6 +192,12 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * (0 = MOSRX_GROUP_AUTO_BYTES) */
 	int32_t       flowhash;                         /* 1: also the flow-table hash of every frame
 	                                                 * (dev_ioctl(MOSRX_PKT_RX_FHASH)); not with BPF filters */
+	int32_t       tx_csum;                          /* 1: take mOS's TX checksum offload requests
+	                                                 * (dev_ioctl PKT_TX_IP_CSUM / PKT_TX_TCP_CSUM on the frame
+	                                                 * get_wptr returned last, as dpdk_dev_ioctl does,
+	                                                 * dpdk_module.c:556-566) and fill those checks on the GPU
+	                                                 * when send_pkts sends the frames; 0 (default): -1, mOS
+	                                                 * computes them (ip_out.c:169-174, tcp_out.c:207-218) */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
 #define MOSRX_GROUP_AUTO_BYTES  (256ull << 20)   /* per pipeline slot; 64 B frames: ~120 batches of 32K
@@ -221,6 +229,8 @@ typedef struct mosrx_gpu_module_stats {
 	                               num_esp) changed after they were classified (mOS builds) */
 	int32_t  cpu;               /* the mTCP core the context runs as (bind, or ctx->cpu in mOS builds) */
 	int32_t  device;            /* the GPU it drives: gpu_base + cpu % ngpu */
+	uint64_t tx_csum_offloaded; /* TX frames whose requested checks the GPU filled (cfg.tx_csum); frames
+	                               whose pass failed are dropped and counted in tx_errors */
 } mosrx_gpu_module_stats;
 /* Time every kernel this thread's contexts launch (for the stats above). */
 int  mosrx_gpu_module_set_timing(struct mtcp_thread_context *ctx, int on);

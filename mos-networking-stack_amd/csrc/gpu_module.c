@@ -24,7 +24,12 @@
  * buffer; send_pkts (core.c:1004-1006) hands every buffered frame to the
  * netdev's source (AF_PACKET send = pcap_inject, or a pcap dump), as
  * pcap_send_pkts does (pcap_module.c:67-79); a full buffer is flushed by the
- * next get_wptr, like dpdk_get_wptr.
+ * next get_wptr, like dpdk_get_wptr.  With cfg.tx_csum the module takes mOS's
+ * checksum offload requests the way dpdk_dev_ioctl does (PKT_TX_IP_CSUM /
+ * PKT_TX_TCP_CSUM on the frame get_wptr handed out last, dpdk_module.c:556-566;
+ * mOS then skips ip_fast_csum / TCPCalcChecksum, ip_out.c:169-174,
+ * tcp_out.c:207-218) and send_pkts fills those checks on the GPU (the TX
+ * rewrite kernel, mosrx_tx_csum_host) before the frames leave.
  *
  * Threading follows mOS: one context per mTCP thread, every call for a context
  * from that thread (core.c:1282-1349), so the module takes no locks on the fast
@@ -97,8 +102,14 @@ struct if_state {
 	/* TX: frames written through get_wptr, sent by send_pkts */
 	uint8_t *tx_buf;          /* tx_cap x TX_FRAME_LEN */
 	uint16_t *tx_len;
+	uint8_t *tx_fl;           /* per TX frame: checks requested through dev_ioctl (TXF_*) */
+	uint32_t *tx_poff;        /* the TX rewrite's descriptors (tx_cap each) */
+	uint16_t *tx_plen;
 	uint32_t tx_n;
+	mosrx_ctx *mc_tx;         /* the TX rewrite's own context (opened on first use) */
 };
+#define TXF_IP  1u            /* PKT_TX_IP_CSUM */
+#define TXF_TCP 2u            /* PKT_TX_TCP_CSUM */
 
 struct gpu_priv {
 	struct mtcp_thread_context *ctx;
@@ -430,7 +441,10 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 			}
 		is->tx_buf = malloc((size_t)g_cfg.tx_batch * TX_FRAME_LEN);
 		is->tx_len = calloc(g_cfg.tx_batch, sizeof(uint16_t));
-		if (!is->tx_buf || !is->tx_len)
+		is->tx_fl = calloc(g_cfg.tx_batch, 1);
+		is->tx_poff = calloc(g_cfg.tx_batch, sizeof(uint32_t));
+		is->tx_plen = calloc(g_cfg.tx_batch, sizeof(uint16_t));
+		if (!is->tx_buf || !is->tx_len || !is->tx_fl || !is->tx_poff || !is->tx_plen)
 			exit(EXIT_FAILURE);
 	}
 	pthread_mutex_lock(&g_lock);
@@ -723,13 +737,69 @@ static void gpu_release_pkt(struct mtcp_thread_context *ctx, int ifidx, unsigned
 	(void)ctx; (void)ifidx; (void)pkt; (void)len;
 }
 
+/* The checks mOS left to the "NIC" (dev_ioctl PKT_TX_*_CSUM): filled on the
+ * GPU, one TX rewrite pass per distinct request (in practice one: mOS asks for
+ * both on every TCP frame it builds).  A pass that fails leaves its frames
+ * without checksums: they are dropped (TXF bit 7) and counted as TX errors,
+ * as a NIC would, never sent with a stale check. */
+static void tx_csum_fill(struct gpu_priv *pv, struct if_state *is)
+{
+	uint32_t *off = is->tx_poff, i, n, fl;
+	uint16_t *len = is->tx_plen;
+	for (fl = 1; fl <= (TXF_IP | TXF_TCP); fl++) {
+		mosrx_batch b;
+		uint32_t m = 0;
+		int rc;
+		for (i = n = 0; i < is->tx_n; i++)
+			if (is->tx_fl[i] == fl) {
+				off[n] = i * TX_FRAME_LEN;
+				len[n] = is->tx_len[i];
+				m = len[n] > m ? len[n] : m;
+				n++;
+			}
+		if (!n)
+			continue;
+		if (!is->mc_tx) {
+			const int dev = mosrx_gpu_module_device_of(pv->cpu, mosrx_device_count());
+			if (dev < 0 || mosrx_open(dev, &is->params, &is->mc_tx))
+				is->mc_tx = NULL;
+		}
+		b.frames = is->tx_buf;
+		b.frames_bytes = (uint64_t)is->tx_n * TX_FRAME_LEN;
+		b.off = off;
+		b.len = len;
+		b.n = n;
+		b.max_len = m;
+		rc = is->mc_tx ? mosrx_tx_csum_host(is->mc_tx, &b, ((fl & TXF_IP) ? MOSRX_TX_IP_CSUM : 0) |
+		                                                       ((fl & TXF_TCP) ? MOSRX_TX_TCP_CSUM : 0))
+		               : -ENODEV;
+		if (rc) {
+			fprintf(stderr, "[mosrx] gpu_module: TX checksum pass: %s\n", mosrx_strerror(rc));
+			for (i = 0; i < is->tx_n; i++)
+				if (is->tx_fl[i] == fl)
+					is->tx_fl[i] |= 0x80;
+		} else {
+			pv->stats.tx_csum_offloaded += n;
+		}
+	}
+}
+
 /* Hand every buffered TX frame of netdev nif to its source. */
 static int32_t tx_flush(struct gpu_priv *pv, int nif)
 {
 	struct if_state *is = &pv->ifs[nif];
 	uint32_t i;
 	int32_t sent = 0;
+	for (i = 0; i < is->tx_n && g_cfg.tx_csum; i++)
+		if (is->tx_fl[i]) {
+			tx_csum_fill(pv, is);
+			break;
+		}
 	for (i = 0; i < is->tx_n; i++) {
+		if (is->tx_fl[i] & 0x80) {
+			pv->stats.tx_errors++;
+			continue;
+		}
 		if (mosrx_source_send(is->src, is->tx_buf + (size_t)i * TX_FRAME_LEN, is->tx_len[i]) == 0) {
 			sent++;
 			pv->stats.tx_packets++;
@@ -754,6 +824,7 @@ static uint8_t *gpu_get_wptr(struct mtcp_thread_context *ctx, int ifidx, uint16_
 	if (is->tx_n == g_cfg.tx_batch)   /* full: send what is buffered first (dpdk_get_wptr) */
 		tx_flush(pv, ifidx);
 	is->tx_len[is->tx_n] = len;
+	is->tx_fl[is->tx_n] = 0;
 	return is->tx_buf + (size_t)(is->tx_n++) * TX_FRAME_LEN;
 }
 
@@ -866,7 +937,22 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
 	case DRV_NAME:
 		*(const char **)argp = "mosrx_gpu";
 		return 0;
-	default:   /* PKT_TX_*_CSUM: not offloaded, the stack computes them (ip_out.c:169-174) */
+	case PKT_TX_IP_CSUM:
+	case PKT_TX_TCP_CSUM: {
+		/* dpdk_dev_ioctl's offload (dpdk_module.c:556-566): the request is for
+		 * the frame get_wptr handed out last on this netdev, argp its IP header;
+		 * without cfg.tx_csum, or for anything else, -1 and mOS computes it */
+		struct if_state *is = &pv->ifs[nif];
+		const uint8_t *ip = argp, *f;
+		if (!g_cfg.tx_csum || !is->tx_n)
+			return -1;
+		f = is->tx_buf + (size_t)(is->tx_n - 1) * TX_FRAME_LEN;
+		if (ip != f + 14 || is->tx_len[is->tx_n - 1] < 34)
+			return -1;
+		is->tx_fl[is->tx_n - 1] |= cmd == PKT_TX_IP_CSUM ? TXF_IP : TXF_TCP;
+		return 0;
+	}
+	default:
 		return -1;
 	}
 }
@@ -897,6 +983,11 @@ static void gpu_destroy_handle(struct mtcp_thread_context *ctx)
 		}
 		free(is->tx_buf);
 		free(is->tx_len);
+		free(is->tx_fl);
+		free(is->tx_poff);
+		free(is->tx_plen);
+		if (is->mc_tx)
+			mosrx_close(is->mc_tx);
 		mosrx_close(is->mc);
 	}
 	pthread_mutex_lock(&g_lock);

@@ -100,14 +100,15 @@ class ModuleCfg(C.Structure):
                 ("gpu_base", C.c_int32), ("ngpu", C.c_int32), ("pipeline", C.c_int32),
                 ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32),
                 ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32),
-                ("group_bytes", C.c_uint64), ("flowhash", C.c_int32)]
+                ("group_bytes", C.c_uint64), ("flowhash", C.c_int32), ("tx_csum", C.c_int32)]
 
 
 class ModuleStats(C.Structure):
     _fields_ = [("rx_batches", C.c_uint64), ("rx_frames", C.c_uint64), ("tx_packets", C.c_uint64),
                 ("tx_bytes", C.c_uint64), ("tx_errors", C.c_uint64), ("kernel_launches", C.c_uint64),
                 ("kernel_ms", C.c_double), ("rx_drops", C.c_uint64),
-                ("rx_reclassified", C.c_uint64), ("cpu", C.c_int32), ("device", C.c_int32)]
+                ("rx_reclassified", C.c_uint64), ("cpu", C.c_int32), ("device", C.c_int32),
+                ("tx_csum_offloaded", C.c_uint64)]
 
 
 class RxLoopOpts(C.Structure):
@@ -799,7 +800,7 @@ class GpuBackend:
     def __init__(self, sources: list[int], params: Params | None = None, batch: int = 32768,
                  max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
                  ngpu: int = 1, bpf=None, group: int = 1, tcpinfo: bool = False, tx_batch: int = 64,
-                 timing: bool = False, flowhash: bool = False):
+                 timing: bool = False, flowhash: bool = False, tx_csum: bool = False):
         cfg = ModuleCfg()
         lib().mosrx_gpu_module_cfg_default(C.byref(cfg))
         cfg.num_ifs = len(sources)
@@ -809,6 +810,7 @@ class GpuBackend:
         cfg.batch, cfg.max_frame, cfg.pipeline = batch, max_frame, int(pipeline)
         cfg.gpu_base, cfg.ngpu = gpu_base, ngpu
         cfg.group, cfg.tcpinfo, cfg.tx_batch, cfg.flowhash = group, int(tcpinfo), tx_batch, int(flowhash)
+        cfg.tx_csum = int(tx_csum)
         if params is not None:
             cfg.params = params
         self.params = Params.from_buffer_copy(cfg.params)
@@ -882,6 +884,19 @@ class GpuBackend:
         if not p:
             raise MosrxError(5, "get_wptr")
         C.memmove(p, frame, len(frame))
+
+    def send_offloaded(self, ifidx: int, frame: bytes, ip: bool, tcp: bool) -> tuple[int, int]:
+        """get_wptr + copy, then mOS's TX checksum offload requests for the frame
+        (ip_out.c:169-174, tcp_out.c:207-218: dev_ioctl with its IP header):
+        the (PKT_TX_IP_CSUM, PKT_TX_TCP_CSUM) returns, None where not asked."""
+        p = self._wptr(self.ctx, ifidx, len(frame))
+        if not p:
+            raise MosrxError(5, "get_wptr")
+        C.memmove(p, frame, len(frame))
+        iph = C.c_void_p(p + 14)
+        ri = self._ioctl(self.ctx, ifidx, PKT_TX_IP_CSUM, iph) if ip else None
+        rt = self._ioctl(self.ctx, ifidx, PKT_TX_TCP_CSUM, iph) if tcp else None
+        return ri, rt
 
     def send_pkts(self, ifidx: int) -> int:
         return self._send(self.ctx, ifidx)

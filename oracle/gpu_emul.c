@@ -145,3 +145,10 @@ int __wrap_mosrx_classify_bpf_host_submit(mosrx_ctx *mc, int slot, const mosrx_b
 		return rc;
 	return mo_bpf_eval(c->progs, c->nprog, b->frames, b->frames_bytes, b->off, b->len, b->n, match);
 }
+
+/* The TX rewrite (mosrx_tx_csum_host): the oracle's restatement, in place. */
+int __wrap_mosrx_tx_csum_host(mosrx_ctx *mc, const mosrx_batch *b, int flags)
+{
+	(void)mc;
+	return mo_tx_csum((uint8_t *)b->frames, b->frames_bytes, b->off, b->len, b->n, flags);
+}

@@ -52,6 +52,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/time.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -79,6 +80,21 @@ static double g_rx_ns;                   /* CPU time of the per-frame loop, summ
 static uint64_t g_rx_frames;
 static FILE *g_cb;
 static int g_quiet;
+static int g_frozen_clock;
+
+/* MOSAPP_FROZEN_CLOCK: mOS's clock (RunMainLoop's gettimeofday, core.c:887) stands
+ * still, so the frames mOS builds itself carry the same TCP timestamp option in
+ * both runs and can be compared byte for byte (no timer fires either). */
+int __real_gettimeofday(struct timeval *tv, void *tz);
+int __wrap_gettimeofday(struct timeval *tv, void *tz)
+{
+	if (g_frozen_clock) {
+		tv->tv_sec = 1700000000;
+		tv->tv_usec = 0;
+		return 0;
+	}
+	return __real_gettimeofday(tv, tz);
+}
 static char g_snap[1 << 20];             /* flow table + NETSTAT after the last frame */
 static size_t g_snap_len;
 static mctx_t g_mctx;
@@ -92,6 +108,16 @@ static int stream_monitor(int with_filters);
 static int32_t gated_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 {
 	return atomic_load(&g_go) ? gpu_module_func.recv_pkts(ctx, ifidx) : 0;
+}
+
+/* the backend's TX counters after each send_pkts (the context's stats go with
+ * destroy_handle) */
+static mosrx_gpu_module_stats g_tx_stats;
+static int32_t counted_send_pkts(struct mtcp_thread_context *ctx, int nif)
+{
+	const int32_t r = gpu_module_func.send_pkts(ctx, nif);
+	mosrx_gpu_module_stats_of(ctx, &g_tx_stats);
+	return r;
 }
 
 static double ns_between(const struct timespec *a, const struct timespec *b)
@@ -284,6 +310,7 @@ int main(int argc, char **argv)
 	}
 	g_mode_gpu = !strcmp(argv[1], "gpu");
 	g_quiet = getenv("MOSAPP_QUIET") != NULL;
+	g_frozen_clock = getenv("MOSAPP_FROZEN_CLOCK") != NULL;
 	in = fopen(argv[3], "rb");
 	if (!in || rd(in, magic, 4) || memcmp(magic, "MRXT", 4) || rd(in, &ver, 4) || (ver != 1 && ver != 2) ||
 	    rd(in, &n, 4) || rd(in, &fb, 8) || rd(in, &num_msp, 4) || rd(in, &num_esp, 4) ||
@@ -318,6 +345,8 @@ int main(int argc, char **argv)
 	cfg.batch = getenv("MOSAPP_BATCH") ? (uint32_t)atoi(getenv("MOSAPP_BATCH")) : 4096;
 	cfg.group = getenv("MOSAPP_GROUP") ? (uint32_t)atoi(getenv("MOSAPP_GROUP")) : MOSRX_GROUP_AUTO;
 	cfg.flowhash = getenv("MOSAPP_FLOWHASH") ? atoi(getenv("MOSAPP_FLOWHASH")) : 1;   /* FindStream's bucket too */
+	/* mOS's TX checksums on the GPU (dev_ioctl PKT_TX_*_CSUM, as with DPDK's offload) */
+	cfg.tx_csum = getenv("MOSAPP_TX_CSUM") ? atoi(getenv("MOSAPP_TX_CSUM")) : 0;
 	cfg.params.num_queues = nq;
 	cfg.params.queue_mode = qmode;
 	cfg.params.num_msp = 0;                       /* followed from mOS's manager (mos_state) */
@@ -328,6 +357,7 @@ int main(int argc, char **argv)
 	 * application's sockets exist, so both modes see the same stack state */
 	g_gated = gpu_module_func;
 	g_gated.recv_pkts = gated_recv_pkts;
+	g_gated.send_pkts = counted_send_pkts;
 	current_iomodule_func = &g_gated;
 
 	if (mtcp_init(argv[2]))
@@ -397,12 +427,14 @@ int main(int argc, char **argv)
 		printf("{\"mode\": \"%s\", \"frames\": %lu, \"rx_frames_timed\": %lu, \"rx_ns_per_frame\": %.2f, "
 		       "\"consumer_frames\": %lu, \"stream_step\": %lu, \"gpu_flow_hash\": %lu, \"reclassified\": %lu, "
 		       "\"filter_installs\": %lu, "
-		       "\"filters_gpu\": %lu, \"filters_cpu\": %lu}\n",
+		       "\"filters_gpu\": %lu, \"filters_cpu\": %lu, \"tx_packets\": %lu, \"tx_csum_offloaded\": %lu, "
+		       "\"tx_errors\": %lu}\n",
 		       argv[1], (unsigned long)g_total, (unsigned long)g_rx_frames,
 		       g_rx_frames ? g_rx_ns / (double)g_rx_frames : 0.0, (unsigned long)cs.frames,
 		       (unsigned long)cs.stream_step, (unsigned long)cs.gpu_flow_hash, (unsigned long)cs.reclassified,
 		       (unsigned long)cs.filter_installs,
-		       (unsigned long)cs.filters_gpu, (unsigned long)cs.filters_cpu);
+		       (unsigned long)cs.filters_gpu, (unsigned long)cs.filters_cpu, (unsigned long)g_tx_stats.tx_packets,
+		       (unsigned long)g_tx_stats.tx_csum_offloaded, (unsigned long)g_tx_stats.tx_errors);
 	}
 	mosrx_source_close(src);
 	return 0;

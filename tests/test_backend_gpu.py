@@ -4,6 +4,7 @@ oracle for every way a batch reaches the GPU (per-frame, runs, zero-copy,
 groups of batches in one launch, a pcap file), pkt_info fields through
 dev_ioctl, stack-state updates, and TX (get_wptr / send_pkts) reaching the
 source."""
+import ctypes as C
 import os
 import socket
 import struct
@@ -227,6 +228,59 @@ def test_tx_reaches_the_source(tmp_path):
     keep = np.nonzero(mos_forwarded(ora))[0]
     assert sent[:40] == mine
     assert sent[40:] == [bytes(t.frames[t.off[i]:t.off[i] + t.len[i]]) for i in keep]
+
+
+def _zero_checks(f: bytes) -> bytes:
+    """mOS builds its frames with iph->check = 0 (ip_out.c:167) and leaves the TCP
+    check to the offload; zero both as it does."""
+    b = bytearray(f)
+    b[24:26] = b"\0\0"
+    ihl = (b[14] & 15) * 4
+    if b[23] == 6 and len(b) >= 14 + ihl + 18:
+        b[14 + ihl + 16:14 + ihl + 18] = b"\0\0"
+    return bytes(b)
+
+
+def test_tx_checksum_offload(tmp_path):
+    """cfg.tx_csum: dev_ioctl(PKT_TX_IP_CSUM / PKT_TX_TCP_CSUM) on the frame get_wptr
+    returned last is taken as a NIC offload (dpdk_dev_ioctl, dpdk_module.c:556-566) and
+    send_pkts fills those checks on the GPU before the frames leave: each frame as
+    the oracle's TX rewrite (= mOS's ip_fast_csum / TCPCalcChecksum, test_tx_csum.py)
+    makes it for the checks it asked for; frames that asked for nothing leave as
+    written.  Without cfg.tx_csum, or for a pointer that is not the last frame's IP
+    header, the ioctl returns -1 (mOS computes the checksum itself)."""
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 300, nflows=40)
+    frames = [_zero_checks(bytes(t.frames[t.off[i]:t.off[i] + t.len[i]])) for i in range(t.n)]
+    frames += [_zero_checks(tcp_frame(payload=bytes(range(256)) * 5 + b"x" * i, seq=i)) for i in range(7)]
+    asks = [(i % 4 != 3, i % 4 in (0, 2)) for i in range(len(frames))]   # (IP, TCP): both, IP, both, none
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=1)
+    path = str(tmp_path / "tx.pcap")
+    mosrx.source_tx_pcap(src, path)
+    be = mosrx.GpuBackend([src], batch=1024, cpu=3, tx_batch=64, tx_csum=True)
+    try:
+        for f, (ip, tcp) in zip(frames, asks):
+            assert be.send_offloaded(0, f, ip, tcp) == ((0 if ip else None), (0 if tcp else None))
+        # not the last frame's IP header: refused, mOS would compute it
+        assert be.ioctl_raw(0, mosrx.PKT_TX_IP_CSUM, C.c_void_p(0x1000)) == -1
+        be.send_pkts(0)
+        st = be.stats()
+        assert st.tx_packets == len(frames) and st.tx_errors == 0
+        assert st.tx_csum_offloaded == sum(1 for a in asks if any(a))
+    finally:
+        be.close()
+    want = []
+    for f, (ip, tcp) in zip(frames, asks):
+        fl = (mosrx.TX_IP_CSUM if ip else 0) | (mosrx.TX_TCP_CSUM if tcp else 0)
+        buf = np.frombuffer(f, np.uint8)
+        want.append(bytes(O.tx_csum(buf, [0], [len(f)], fl)) if fl else f)
+    assert mosrx.read_pcap(path) == want
+
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=1)
+    be = mosrx.GpuBackend([src], batch=1024, cpu=3, tx_csum=False)
+    try:
+        assert be.send_offloaded(0, frames[0], True, True) == (-1, -1)
+    finally:
+        be.close()
 
 
 def _have_raw():

@@ -43,7 +43,7 @@ CONF = """mos {{
 	}}
 	mos_log = {log}/
 	arp_table {{
-		0.0.0.0/0 02:00:00:00:00:aa
+{arp}
 	}}
 	route_table {{
 		0.0.0.0/0 lo
@@ -57,6 +57,13 @@ CONF = """mos {{
 }}
 """
 
+# mOS's GetDestinationHWaddr (arp.c:89-119) never picks a /0 entry (it wants a prefix
+# longer than 0) and reads prefix 1 as an exact address, so the default table
+# resolves nothing: frames mOS builds itself wait for ARP and only forwarded ones
+# leave.  Four /2 entries resolve every address, so mOS sends its own RSTs / ACKs.
+ARP_NONE = "\t\t0.0.0.0/0 02:00:00:00:00:aa"
+ARP_ALL = "\n".join(f"\t\t{a}.0.0.0/2 02:00:00:00:00:aa" for a in (0, 64, 128, 192))
+
 SCENARIOS = {
     # simple_firewall's stack: one stream monitor, forward = 1 (setup.sh:135)
     "monitor_fwd": dict(forward=1, env={}),
@@ -65,6 +72,14 @@ SCENARIOS = {
                                     "MOSAPP_ORPHAN": "net 10.9.0.0/16"}),
     "two_monitors_raw": dict(forward=1, env={"MOSAPP_MONITORS": "2", "MOSAPP_RAW_NOFILTER": "1"}),
     "listener": dict(forward=1, env={"MOSAPP_LISTEN": "8080"}, listen=8080),
+    # mOS's TX checksums taken by the backend as a NIC offload (dev_ioctl PKT_TX_*_CSUM,
+    # dpdk_module.c:556-566) and filled on the GPU at send_pkts, in the GPU run only: the
+    # frames sent must equal those of the ProcessPacket run, whose checksums mOS computed
+    "listener_tx_csum": dict(forward=1, env={"MOSAPP_LISTEN": "8080", "MOSAPP_FROZEN_CLOCK": "1"}, listen=8080,
+                             arp_all=True,
+                             gpu_env={"MOSAPP_TX_CSUM": "1"}),
+    "listener_arp": dict(forward=1, env={"MOSAPP_LISTEN": "8080", "MOSAPP_FROZEN_CLOCK": "1"}, listen=8080,
+                         arp_all=True),
     "no_socket": dict(forward=1, env={"MOSAPP_MONITORS": "0"}),
     "late_filter": dict(forward=1, env={"MOSAPP_RAW": "tcp[tcpflags] & tcp-syn != 0", "MOSAPP_LATE_RAW_AT": "150"}),
     "late_monitor": dict(forward=1, env={"MOSAPP_MONITORS": "0", "MOSAPP_LATE_MON_AT": "200"}),
@@ -79,6 +94,9 @@ SCENARIOS = {
     "golden_edge_fwd": dict(forward=1, env={"MOSAPP_RAW_NOFILTER": "1"}, fixture="edge"),
     "golden_edge_nofwd": dict(forward=0, env={}, fixture="edge"),
     "golden_edge_listener": dict(forward=1, env={"MOSAPP_LISTEN": "80"}, fixture="edge"),
+    "golden_edge_listener_tx_csum": dict(forward=1, env={"MOSAPP_LISTEN": "80", "MOSAPP_FROZEN_CLOCK": "1"},
+                                         fixture="edge", arp_all=True,
+                                         gpu_env={"MOSAPP_TX_CSUM": "1"}),
     "golden_rand_small_fwd": dict(forward=1, env={"MOSAPP_ORPHAN": "src net 10.0.0.0/8"}, fixture="rand_small"),
     "golden_rand_mid_fwd": dict(forward=1, env={"MOSAPP_BATCH": "37", "MOSAPP_GROUP": "2"}, fixture="rand_mid"),
     "golden_rand_large_nofwd": dict(forward=0, env={}, fixture="rand_large"),
@@ -119,7 +137,7 @@ def run_app(exe, mode, tmp, name, sc, frames, extra_env=None):
     log = tmp / f"{name}_{mode}_log"
     log.mkdir()
     conf = tmp / f"{name}_{mode}.conf"
-    conf.write_text(CONF.format(forward=sc["forward"], log=log))
+    conf.write_text(CONF.format(forward=sc["forward"], log=log, arp=ARP_ALL if sc.get("arp_all") else ARP_NONE))
     trace = tmp / f"{name}.mrxt"
     if not trace.exists():
         buf, off, ln = pktlib.pack_frames(frames)
@@ -141,7 +159,7 @@ def compare_modes(exe, tmp, name):
     else:
         frames = pktlib.conversation_frames(sc.get("nflows", 64), seed=11, listen_port=sc.get("listen", 0))
     pp = run_app(exe, "pp", tmp, name, sc, frames)
-    gpu = run_app(exe, "gpu", tmp, name, sc, frames)
+    gpu = run_app(exe, "gpu", tmp, name, sc, frames, sc.get("gpu_env"))
     assert len(pp["returns"]) == len(frames)
     assert gpu["returns"] == pp["returns"], "per-frame return values"
     assert gpu["state"] == pp["state"], "flow table / NETSTAT"
@@ -192,8 +210,18 @@ def _check_scenario(name, pp, gpu):
     if name == "filters":
         assert st["filters_gpu"] == 3 and st["filter_installs"] >= 1
         assert " ev 100 " in cb                                # MOS_ON_ORPHAN through the orphan filter
-    if name == "listener":
+    if name.startswith("listener"):
         assert any(f[47] & 0x04 for f in pp["tx"] if len(f) > 47 and f[23] == 6)   # RSTs to orphans
+    if name.endswith("_tx_csum"):
+        # the GPU filled the checks of every TCP frame mOS built (SYN-ACKs, ACKs, RSTs);
+        # forwarded frames keep theirs and ask for nothing
+        # (at least the RSTs SendTCPPacketStandalone builds for orphans, tcp.c:503-506: IP id 0,
+        # TCP window 0); the frames themselves were compared above, checks included
+        built = sum(1 for f in gpu["tx"] if len(f) > 47 and f[12:14] == b"\x08\x00" and f[23] == 6
+                    and f[18:20] == b"\x00\x00" and f[48:50] == b"\x00\x00")
+        assert built > 0
+        assert gpu["stats"]["tx_csum_offloaded"] >= built and gpu["stats"]["tx_errors"] == 0
+        assert pp["stats"]["tx_csum_offloaded"] == 0
     if name == "late_filter":
         assert st["filter_installs"] >= 1 and st["reclassified"] >= 1
     if name == "late_monitor":

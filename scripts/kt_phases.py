@@ -1,3 +1,7 @@
+"""Per-dispatch kernel durations of rocprofv3 --kernel-trace runs of bench.py
+rows (gpurun_out/prof3/kt_<row>/), split into the bench's phases: a new phase
+where two dispatches are more than 300 us apart.  Prints n / median / gap per
+phase.  Usage: python3 scripts/kt_phases.py M1500_1 IMIX_1 ..."""
 import csv, statistics as st, sys
 for W in sys.argv[1:]:
     rows = [r for r in csv.DictReader(open(f'gpurun_out/prof3/kt_{W}/kt_kernel_trace.csv')) if 'classify' in r['Kernel_Name']]

@@ -439,7 +439,11 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 				fprintf(stderr, "[mosrx] gpu_module: pinned staging allocation failed\n");
 				exit(EXIT_FAILURE);
 			}
-		is->tx_buf = malloc((size_t)g_cfg.tx_batch * TX_FRAME_LEN);
+		/* pinned when the TX rewrite copies it to the GPU and back (cfg.tx_csum) */
+		if (!g_cfg.tx_csum)
+			is->tx_buf = malloc((size_t)g_cfg.tx_batch * TX_FRAME_LEN);
+		else if (mosrx_host_alloc(is->mc, (size_t)g_cfg.tx_batch * TX_FRAME_LEN, (void **)&is->tx_buf))
+			is->tx_buf = NULL;
 		is->tx_len = calloc(g_cfg.tx_batch, sizeof(uint16_t));
 		is->tx_fl = calloc(g_cfg.tx_batch, 1);
 		is->tx_poff = calloc(g_cfg.tx_batch, sizeof(uint32_t));
@@ -749,12 +753,14 @@ static void tx_csum_fill(struct gpu_priv *pv, struct if_state *is)
 	for (fl = 1; fl <= (TXF_IP | TXF_TCP); fl++) {
 		mosrx_batch b;
 		uint32_t m = 0;
+		uint64_t end = 0;
 		int rc;
 		for (i = n = 0; i < is->tx_n; i++)
 			if (is->tx_fl[i] == fl) {
 				off[n] = i * TX_FRAME_LEN;
 				len[n] = is->tx_len[i];
 				m = len[n] > m ? len[n] : m;
+				end = (uint64_t)off[n] + len[n];
 				n++;
 			}
 		if (!n)
@@ -765,7 +771,7 @@ static void tx_csum_fill(struct gpu_priv *pv, struct if_state *is)
 				is->mc_tx = NULL;
 		}
 		b.frames = is->tx_buf;
-		b.frames_bytes = (uint64_t)is->tx_n * TX_FRAME_LEN;
+		b.frames_bytes = end;         /* up to the last frame of the pass: what crosses PCIe */
 		b.off = off;
 		b.len = len;
 		b.n = n;
@@ -981,7 +987,10 @@ static void gpu_destroy_handle(struct mtcp_thread_context *ctx)
 			group_recycle(&is->g[k], is->src);
 			group_free(is->mc, &is->g[k]);
 		}
-		free(is->tx_buf);
+		if (g_cfg.tx_csum)
+			mosrx_host_free(is->mc, is->tx_buf);
+		else
+			free(is->tx_buf);
 		free(is->tx_len);
 		free(is->tx_fl);
 		free(is->tx_poff);

@@ -82,9 +82,17 @@ static FILE *g_cb;
 static int g_quiet;
 static int g_frozen_clock;
 
-/* MOSAPP_FROZEN_CLOCK: mOS's clock (RunMainLoop's gettimeofday, core.c:887) stands
- * still, so the frames mOS builds itself carry the same TCP timestamp option in
- * both runs and can be compared byte for byte (no timer fires either). */
+/* MOSAPP_FROZEN_CLOCK: the frames mOS builds itself come out the same in both
+ * runs, so they can be compared byte for byte: mOS's clock (RunMainLoop's
+ * gettimeofday, core.c:887) stands still -- the same TCP timestamp option, and
+ * no timer fires -- and the initial sequence numbers of its streams
+ * (posix_seq_rand, tcp_stream.c:526) start from a fixed seed instead of the
+ * mTCP thread's pthread_self (core.c:1085), which ASLR moves from run to run. */
+void __real_posix_seq_srand(unsigned seed);
+void __wrap_posix_seq_srand(unsigned seed)
+{
+	__real_posix_seq_srand(g_frozen_clock ? 1u : seed);
+}
 int __real_gettimeofday(struct timeval *tv, void *tz);
 int __wrap_gettimeofday(struct timeval *tv, void *tz)
 {

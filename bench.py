@@ -491,7 +491,8 @@ def orphan_segments(n: int, size: int = 1460, seed: int = 3) -> mosrx.Trace:
     return t
 
 
-def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 3, timeout: float = 60.0):
+def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 3, timeout: float = 60.0,
+                    exe: str | None = None):
     """mOS's own rx loop on one host core (oracle/_ref/mos_app: mtcp_init, an
     mTCP thread in RunMainLoop, one stream monitor socket, gpu_module_func as
     the I/O module): the per-frame CPU time of core.c:902-907 (timed per batch)
@@ -500,7 +501,7 @@ def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 3, ti
     alternated `reps` times (medians).  The difference is the CPU time per
     frame the GPU saves inside mOS.  A reported baseline; None when the binary
     did not travel with the tree."""
-    exe = os.path.join(ROOT, "oracle", "_ref", "mos_app")
+    exe = exe or os.path.join(ROOT, "oracle", "_ref", "mos_app")
     if not os.access(exe, os.X_OK):
         return None
     sys.path.insert(0, os.path.join(ROOT, "tests"))

@@ -513,7 +513,12 @@ __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffe
 		}
 		s = (s >> 16) + (s & 0xFFFFu);
 		s += s >> 16;                                   // low 16 bits in [1, 0xFFFF], == S mod 0xFFFF
-		uint32_t v = (s & 0xFFFFu) + (0xFFFFu - h.tcw); // - old check word
+		// - the old check word, as far as it lies inside the summed segment: a
+		// short tot_len (doff < 5 is accepted, tcp.c:429) can leave tcph->check
+		// past the ip_len - ihl*4 bytes TCPCalcChecksum covers, wholly or by its
+		// second byte (the odd tail keeps the first, tcp_util.c:175-176)
+		const uint32_t tcw_in = seglen >= 18u ? h.tcw : seglen == 17u ? (h.tcw & 0xFFu) : 0u;
+		uint32_t v = (s & 0xFFFFu) + (0xFFFFu - tcw_in);
 		v = (v & 0xFFFFu) + (v >> 16);
 		const uint32_t c = (~v) & 0xFFFFu;
 		const uint32_t at = h.o + 30u + 4u * h.ihl;

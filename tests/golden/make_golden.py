@@ -213,6 +213,25 @@ def tx_fixture(frames: list[bytes], name: str, phase: int):
     print(f"{name}: {len(frames)} frames, {ip_w.sum()} IP / {tcp_w.sum()} TCP rewrites")
 
 
+def short_segment_frames():
+    """TCP frames whose tot_len leaves the segment shorter than a TCP header
+    (doff < 5 passes mOS's length check, tcp.c:429-430): tcph->check then lies
+    past the ip_len - ihl*4 bytes TCPCalcChecksum covers, wholly (segment <= 16
+    bytes) or by its second byte (17).  Captures run past tot_len, so the check
+    field itself is captured and written."""
+    rng = random.Random(0x5E6)
+    frames = []
+    for seglen in range(12, 24):
+        for doff in range(0, 6):
+            if (5 + doff) * 4 > 20 + seglen:
+                continue
+            for odd in (0, 1):
+                pl = bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 7, 30])))
+                frames.append(tcp_frame(payload=pl, doff=doff, tot_len=20 + seglen, seq=rng.getrandbits(32),
+                                        flags=rng.getrandbits(8), pad_to=60 + 3 * odd))
+    return frames
+
+
 def main():
     if not O.have_ref():
         sys.exit("oracle/_ref/mosref missing: run `make -C oracle ref` first (needs /root/reference)")
@@ -224,6 +243,7 @@ def main():
     txr = random.Random(0x7C5)
     tx_fixture(edge_frames() + random_frames(txr, 200, 0) + random_frames(txr, 100, 1), "tx_mixed", phase=2)
     tx_fixture(random_frames(txr, 120, 2) + random_frames(txr, 60, 0), "tx_odd", phase=7)
+    tx_fixture(short_segment_frames(), "tx_short", phase=3)   # round 3: check field past the segment
     # MSDN Toeplitz vectors (util/rss.c:177-193), Microsoft key (util/rss.c:75-81)
     kat = np.array([
         (0x420995bb, 0xa18e6450, 2794, 1766, 0x51ccc178),

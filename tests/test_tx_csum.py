@@ -15,7 +15,7 @@ import mosrx
 import oracle_py as O
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-FIXTURES = ["tx_mixed", "tx_odd"]
+FIXTURES = ["tx_mixed", "tx_odd", "tx_short"]
 IP, TCP = mosrx.TX_IP_CSUM, mosrx.TX_TCP_CSUM
 FLAGS = [IP | TCP, IP, TCP]
 
@@ -45,6 +45,15 @@ def test_tx_fixture_coverage():
     assert 0 < z["tcp_w"].sum() < z["ip_w"].sum() < len(z["off"])
     after = O.tx_csum(z["frames"], z["off"], z["len"], IP | TCP)
     assert (after != z["frames"]).any()
+
+
+def test_tx_short_segments_fixture():
+    """tx_short: segments shorter than a TCP header (doff < 5, short tot_len), so
+    tcph->check lies past the bytes TCPCalcChecksum sums -- wholly, or by its
+    second byte -- and its old value must not count (found by the round-3 soak)."""
+    z = np.load(os.path.join(GOLDEN, "tx_short.npz"))
+    seg = np.array([((int(z["frames"][o + 16]) << 8) | int(z["frames"][o + 17])) - 20 for o in z["off"].tolist()])
+    assert z["tcp_w"].all() and (seg <= 16).any() and (seg == 17).any() and (seg >= 18).any()
 
 
 def test_tx_rewritten_frames_verify():

@@ -18,7 +18,7 @@ from pktlib import pack_frames  # noqa: E402
 s = int(sys.argv[1])
 rng = random.Random(s)
 fr = [S.rand_frame(rng) for _ in range(rng.choice([1, 2, 63, 64, 65, 255, 256, 257, rng.randint(1, 3000)]))]
-assert rng.random() < 0.8
+assert rng.random() < 0.8   # the packed branch (the only one with the TX rewrite)
 buf, off, ln = pack_frames(fr, align=rng.choice([1, 2, 4, 16]), phase=rng.randint(0, 15), gap=rng.choice([0, 0, 3, 64]))
 ln = ln.copy()
 for i in rng.sample(range(len(ln)), k=min(len(ln), rng.randint(0, 5))):

@@ -1,6 +1,6 @@
 """Soak of the classify kernels against the oracle (diagnostic, not a test).
 
-    python3 scripts/soak_classify.py [seconds=240] [seed=1]
+    python3 scripts/soak_classify.py [seconds=240] [seed=1] [queue]
 
 Random batches until the time is up: TCP frames with IP / TCP options of every
 length, payloads from 0 to ~1500 B, corrupted bytes, bad checksums, wrong
@@ -27,7 +27,7 @@ import numpy as np  # noqa: E402
 import mosrx  # noqa: E402
 import oracle_py as O  # noqa: E402
 from pktlib import icmp_frame, pack_frames, tcp_frame  # noqa: E402
-from test_parity_gpu import ALL_VARIANTS, run_both  # noqa: E402
+from test_parity_gpu import ALL_VARIANTS, oparams, run_both  # noqa: E402
 
 LOCAL = ["10.0.0.2", "192.168.1.1", "172.16.0.9"]
 
@@ -88,9 +88,65 @@ def rand_params(rng):
     return mosrx.default_params(**kw)
 
 
+def rand_batch(rng):
+    """(buf, off, len, packed) of one random batch."""
+    fr = [rand_frame(rng) for _ in range(rng.choice([1, 2, 63, 64, 65, 255, 256, 257, rng.randint(1, 3000)]))]
+    packed = rng.random() < 0.8
+    if packed:
+        buf, off, ln = pack_frames(fr, align=rng.choice([1, 2, 4, 16]), phase=rng.randint(0, 15),
+                                   gap=rng.choice([0, 0, 3, 64]))
+        ln = ln.copy()
+        for i in rng.sample(range(len(ln)), k=min(len(ln), rng.randint(0, 5))):
+            ln[i] = rng.randint(0, int(ln[i]))                      # captures cut short
+    else:                                                           # unsorted / overlapping offsets
+        buf, off, ln = pack_frames(fr)
+        perm = list(range(len(fr)))
+        rng.shuffle(perm)
+        off, ln = off[perm].copy(), ln[perm].copy()
+        for i in rng.sample(range(len(off)), k=min(len(off), rng.randint(0, 8))):
+            off[i] = rng.randint(0, max(0, len(buf) - 1))
+    return buf, off, ln, packed
+
+
+def queue_soak(ctx, rnd, budget):
+    """`queue` mode: random batch queues (mosrx_queue_*: one launch over 1-40
+    resident batches of different sizes, layouts and frame mixes) against the
+    oracle, batch by batch."""
+    t0 = last = time.time()
+    queues = frames = 0
+    while time.time() - t0 < budget:
+        s = rnd.getrandbits(31)
+        rng = random.Random(s)
+        p = rand_params(rng)
+        variant = rng.choice(ALL_VARIANTS)
+        ctx.set_variant(variant)
+        ctx.set_params(p)
+        batches = [rand_batch(rng) for _ in range(rng.choice([1, 2, 3, 8, rng.randint(1, 40)]))]
+        dbs = [ctx.upload(b, o, l, frames_bytes=len(b)) for b, o, l, _ in batches]
+        q = ctx.queue(dbs)
+        q.run()
+        for k, ((b, o, l, _), db) in enumerate(zip(batches, dbs)):
+            want = O.classify(b, o, l, oparams(p))
+            if db.results().tobytes() != want.tobytes():
+                print(f"FAIL queue seed {s} variant {variant}: batch {k} of {len(dbs)} differs", flush=True)
+                sys.exit(1)
+            frames += len(o)
+        q.destroy()
+        for db in dbs:
+            db.free()
+        queues += 1
+        if time.time() - last > 10:
+            last = time.time()
+            print(f"[soak] {queues} queues, {frames} frames, {last - t0:.0f} s", flush=True)
+    ctx.set_variant(2)
+    print(f"[soak] OK: {queues} random batch queues, {frames} frames in {time.time() - t0:.0f} s", flush=True)
+
+
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 240.0
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    if len(sys.argv) > 3 and sys.argv[3] == "queue":
+        return queue_soak(mosrx.Context(0), random.Random(seed), budget)
     rnd = random.Random(seed)
     ctx = mosrx.Context(0)
     t0 = last = time.time()

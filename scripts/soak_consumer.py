@@ -5,8 +5,8 @@
 Random setups of tests/test_mos_consumer.py's harness (oracle/_ref/mos_app:
 mOS itself, mtcp_init + RunMainLoop over gpu_module_func) until the time is
 up: conversation traces of random size and seed (with or without flows to a
-local listener), forward 0/1, 0-2 stream monitors, raw / SYN / orphan BPF
-filters, a listener, a monitor or raw filter appearing mid-trace, frames per
+local listener; some with the reference's golden fixture frames mixed in),
+forward 0/1, 0-2 stream monitors, raw / SYN / orphan BPF filters, a listener, a monitor or raw filter appearing mid-trace, frames per
 batch and batches per launch, resolving ARP with mOS's own TX checksums taken
 by the GPU (cfg.tx_csum, clock frozen), the flow lookup on the GPU hash or on
 mOS's.  Each setup runs mOS twice -- ProcessPacket, then the consumer on the
@@ -66,6 +66,7 @@ def main():
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     exe = T.APP if len(sys.argv) > 3 and sys.argv[3] == "gpu" else T.APP_EMUL
     rnd = random.Random(seed)
+    fixtures = {fix: T.fixture_frames(fix) for fix in ("edge", "rand_small", "rand_mid")}
     t0 = last = time.time()
     count = frames = 0
     while time.time() - t0 < budget:
@@ -73,6 +74,10 @@ def main():
         name = f"s{count}"
         T.SCENARIOS[name] = sc
         fr = pktlib.conversation_frames(sc["nflows"], seed=sc["seed"], listen_port=sc["listen"])
+        if rnd.random() < 0.3:     # the reference's golden fixture frames mixed in at random places
+            extra = [f for fix in ("edge", "rand_small", "rand_mid") for f in fixtures[fix]]
+            for f in rnd.sample(extra, k=rnd.randint(1, 60)):
+                fr.insert(rnd.randint(0, len(fr)), f)
         with tempfile.TemporaryDirectory() as td:
             tmp = pathlib.Path(td)
             try:

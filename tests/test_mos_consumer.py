@@ -142,7 +142,13 @@ def run_app(exe, mode, tmp, name, sc, frames, extra_env=None):
     if not trace.exists():
         buf, off, ln = pktlib.pack_frames(frames)
         pktlib.write_ref_trace(str(trace), buf, off, ln, forward=sc["forward"])
-    env = dict(os.environ, **sc["env"], **(extra_env or {}))
+    # mOS's clock frozen in both runs unless the scenario asks for the real one: ARPTimer
+    # (arp.c:313-327) drops a pending request after 1 s of wall time and the next frame to
+    # that address asks again, so a run slower than 1 s (a fresh GPU's first launches)
+    # would send more ARP requests than the other; the TCP timestamps and ISNs mOS puts
+    # in the frames it builds would differ too
+    env = dict(os.environ, **({} if sc.get("real_clock") else {"MOSAPP_FROZEN_CLOCK": "1"}))
+    env.update(sc["env"], **(extra_env or {}))
     r = subprocess.run([exe, mode, str(conf), str(trace), str(d)], capture_output=True, text=True, timeout=120,
                        env=env)
     assert r.returncode == 0, f"{mode}: rc {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-2000:]}"

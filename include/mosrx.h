@@ -84,6 +84,20 @@ typedef struct mosrx_result {
 	uint8_t  ihl_doff;    /* (ihl << 4) | doff; doff 0 if not TCP */
 } mosrx_result;
 
+/* Compact 8-byte record (opt-in, mosrx_classify_dev_compact / MOSRX_QUEUE_COMPACT):
+ * what an rx loop that keeps no per-frame checksum values reads of a record --
+ * the hash and queue (GetRSSHash / GetRSSCPUCore), the reason code and verdict
+ * (ProcessPacket's return), the TCP flags byte.  Field for field equal to the
+ * same fields of the 16-byte record; half the bytes written per frame, which
+ * is a tenth of the HBM traffic of a 64 B frame (BASELINE config #2). */
+typedef struct mosrx_result8 {
+	uint32_t rss;
+	uint8_t  reason;
+	uint8_t  queue;
+	int8_t   verdict;
+	uint8_t  tcp_flags;
+} mosrx_result8;
+
 /* pkt_info's TCP fields (mos_api.h:122-152) as FillPacketContextTCPInfo
  * (tcp.c:258-270) fills them, for FindStream and the flow engine after it
  * (tcp.c:448): host order.  12 bytes per frame, an optional side array of the
@@ -177,6 +191,9 @@ int  mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_o
 int  mosrx_classify_dev_ex(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,
                            mosrx_tcpinfo *d_tcpinfo, void *stream);
 
+/* Same with 8-byte records into device memory d_out8[n] (8-byte aligned). */
+int  mosrx_classify_dev_compact(mosrx_ctx *c, const mosrx_batch *b, mosrx_result8 *d_out8, void *stream);
+
 /* Device-resident classification of `nb` batches in one launch sequence. */
 int  mosrx_classify_dev_many(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
                              mosrx_result *const *d_out, void *stream);
@@ -190,6 +207,16 @@ int  mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
                         mosrx_result *const *d_out, mosrx_queue **q);
 int  mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream);
 void mosrx_queue_destroy(mosrx_ctx *c, mosrx_queue *q);
+/* The batch queue with its options: d_out[i] points at 16-byte records, or at
+ * 8-byte ones (mosrx_result8) with MOSRX_QUEUE_COMPACT; d_fhash[i] (NULL: none)
+ * the flow-table hashes; d_match[i] (NULL: none) the match masks of the BPF set
+ * installed when the queue runs -- one launch of the fused classify + BPF
+ * queue kernel when the set has its compiled form, else the classify launch
+ * followed by the set's kernel per batch (same results).  Compact records go
+ * with neither side array (-EINVAL). */
+enum { MOSRX_QUEUE_COMPACT = 1 };
+int  mosrx_queue_create_ex(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, void *const *d_out,
+                           uint32_t *const *d_fhash, uint32_t *const *d_match, int flags, mosrx_queue **q);
 /* `iters` back-to-back launches cycling over `nq` queues; HIP events on the
  * kernel stream (total, and per launch for the average kernel duration). */
 int  mosrx_time_queue(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq, uint32_t iters,
@@ -237,6 +264,15 @@ int  mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch 
 int  mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
                                          mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo,
                                          uint32_t *const *h_fhash);
+/* The same for a context with a BPF set installed: the records, the flow
+ * hashes (h_fhash, NULL: none) and the set's match masks into h_match[i] from
+ * ONE launch of the fused classify + BPF queue kernel (the set's compiled
+ * form); while the set is still compiling (mosrx_bpf_set_async) or has no
+ * compiled form, the classify launch and the set's interpreter kernel per
+ * batch, on the slot's stream, same results.  No pkt_info fields with masks. */
+int  mosrx_classify_host_group_submit_bpf(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                          mosrx_result *const *h_out, uint32_t *const *h_fhash,
+                                          uint32_t *const *h_match);
 
 /* Kernel timing on the end-to-end path: with timing on, every submit records
  * HIP events around its kernel on the slot's stream, and after the wait
@@ -259,6 +295,14 @@ int  mosrx_dev_free(mosrx_ctx *c, void *dptr);
  * so H2D copies run at full PCIe rate. */
 int  mosrx_host_alloc(mosrx_ctx *c, size_t bytes, void **hptr);
 int  mosrx_host_free(mosrx_ctx *c, void *hptr);
+/* Host memory the caller owns, made known to the library: pinned here
+ * (hipHostRegister), or, with MOSRX_HOST_PINNED, already pinned by the caller
+ * (hipHostMalloc / hipHostRegister of its own) and only recorded.  Batches and
+ * groups whose frames and descriptors lie in one known range cross PCIe in one
+ * copy (mosrx_classify_host, the group submits).  Unregister before freeing. */
+enum { MOSRX_HOST_PINNED = 1 };
+int  mosrx_host_register(mosrx_ctx *c, void *hptr, size_t bytes, int flags);
+int  mosrx_host_unregister(mosrx_ctx *c, void *hptr);
 int  mosrx_memcpy_h2d(mosrx_ctx *c, void *dst, const void *src, size_t bytes);
 int  mosrx_memcpy_d2h(mosrx_ctx *c, void *dst, const void *src, size_t bytes);
 void *mosrx_stream(mosrx_ctx *c);
@@ -352,6 +396,17 @@ int  mosrx_bpf_check(const mosrx_bpf_insn *insns, uint32_t len);
  * SET_BPFFILTER failing makes mtcp_bind_monitor_filter return EINVAL
  * (mos_api.c:127-155).  nprog = 0 clears the set. */
 int  mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog);
+/* The same without waiting for the compiled form: the set is admitted,
+ * staged and in effect when this returns (microseconds; no device-wide
+ * synchronisation), evaluated by the interpreter kernel until the context's
+ * compile thread has built and loaded its kernels with hipRTC, which replace
+ * it at the next launch (a set seen before is taken from the cache at once).
+ * Results are the same on either engine.  mosrx_bpf_wait blocks until the
+ * installed set's compiled form is in (or failed: the interpreter stays);
+ * mosrx_bpf_pending is 1 while its compile is outstanding. */
+int  mosrx_bpf_set_async(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog);
+int  mosrx_bpf_wait(mosrx_ctx *c);
+int  mosrx_bpf_pending(mosrx_ctx *c);
 /* Evaluation engine of the next mosrx_bpf_set.  JIT (default): the set is
  * translated to one straight-line gfx950 kernel and compiled with hipRTC at
  * set time (cached per context); INTERP: the uniform-pc interpreter kernel.

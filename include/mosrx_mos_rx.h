@@ -33,7 +33,13 @@
  * not hold yet, the monitors' filters are installed on every netdev
  * (MOSRX_PKT_SET_BPF, bit j = filter j) and the batch classified again.
  * Filters past the 32 the GPU evaluates in one pass are evaluated by mOS's
- * own EVAL_BPFFILTER.
+ * own EVAL_BPFFILTER.  Filters are known by their instructions (a closed
+ * monitor's program can be freed and another's allocated at its address), and
+ * the installed set is checked against the monitors' at every batch start.
+ *
+ * GPU errors: a batch whose records cannot be had (a failed reclassification,
+ * no records handed out) loses its remaining frames -- counted in rx_packets
+ * and rx_errors, released, -1 -- and mOS runs on (gpu_errors / gpu_dropped).
  */
 #ifndef MOSRX_MOS_RX_H
 #define MOSRX_MOS_RX_H
@@ -57,6 +63,9 @@ typedef struct mosrx_mos_rx_stats {
 	uint64_t filter_installs;   /* BPF sets installed on the GPU */
 	uint64_t filters_gpu;       /* filters in the installed set */
 	uint64_t filters_cpu;       /* filters evaluated by mOS's EVAL_BPFFILTER (past the GPU's 32) */
+	uint64_t max_filter_sync_ns;/* longest filter install (the rx loop's stall: set + reclassify) */
+	uint64_t gpu_errors;        /* batches (or their rest) left without records: the backend failed */
+	uint64_t gpu_dropped;       /* frames of those batches, dropped and counted in rx_errors */
 } mosrx_mos_rx_stats;
 
 /* Counters of the mTCP thread running core `cpu` (mtcp->ctx->cpu). */

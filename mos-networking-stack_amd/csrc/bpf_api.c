@@ -158,7 +158,7 @@ int mosrx_bpf_jit_compile_fused(const mosrx_bpf_prog *progs, uint32_t nprog, cha
 
 int mosrx_bpf_fused(const mosrx_ctx *c)
 {
-	return c && c->bpf_fs && c->bpf_fm ? 1 : 0;
+	return c && c->bpf_fu[FU_S] && c->bpf_fu[FU_M] ? 1 : 0;
 }
 
 int mosrx_bpf_set_engine(mosrx_ctx *c, int engine)
@@ -181,48 +181,110 @@ const char *mosrx_bpf_jit_log(const mosrx_ctx *c)
 	return c ? c->bpf_jit_log : "";
 }
 
-int mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
+/* The interpreter reads the installed instructions from device memory while
+ * earlier launches may still be in flight on the context's streams (a group
+ * classified behind the rx loop), so each set goes to the next buffer of a
+ * pool: a buffer is written again only after the context's streams drained,
+ * and only if a launch may have read it since its last write.  The compiled
+ * kernels carry their programs in their code. */
+static int stage_insns(mosrx_ctx *c, const mosrx_bpf_insn *staged, uint32_t total)
+{
+	const uint32_t i = c->bpf_pool_next;
+	if (!c->d_bpf_pool[i] &&
+	    hipMalloc((void **)&c->d_bpf_pool[i], MOSRX_BPF_MAX_INSNS * sizeof(mosrx_bpf_insn)) != hipSuccess)
+		return -ENOMEM;
+	if (c->bpf_pool_used[i]) {
+		uint32_t k;
+		HIPCHK(hipStreamSynchronize(c->stream));
+		for (k = 0; k < NSLOT; k++)
+			HIPCHK(hipStreamSynchronize(c->slot[k].stream));
+		for (k = 0; k < c->nxs; k++)
+			HIPCHK(hipStreamSynchronize(c->xs[k]));
+		memset(c->bpf_pool_used, 0, sizeof(c->bpf_pool_used));
+	}
+	if (total)
+		HIPCHK(hipMemcpy(c->d_bpf_pool[i], staged, (size_t)total * sizeof(mosrx_bpf_insn), hipMemcpyHostToDevice));
+	c->d_bpf = c->d_bpf_pool[i];
+	c->bpf_pool_next = (i + 1) % MOSRX_BPF_POOL;
+	return 0;
+}
+
+int mosrx_bpf_set_async(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
 {
 	mosrx_bparams t;
-	mosrx_bpf_insn staged[MOSRX_BPF_MAX_INSNS];
+	mosrx_bpf_insn *staged;
 	uint32_t total = 0;
 	int rc;
 	if (!c)
 		return -EINVAL;
-	if ((rc = stage_set(progs, nprog, &t, staged, &total)))
+	if (!(staged = malloc(MOSRX_BPF_MAX_INSNS * sizeof(*staged))))
+		return -ENOMEM;
+	if ((rc = stage_set(progs, nprog, &t, staged, &total))) {
+		free(staged);
 		return rc;
-	HIPCHK(hipSetDevice(c->device));
-	if (!c->d_bpf)
-		HIPCHK(hipMalloc((void **)&c->d_bpf, MOSRX_BPF_MAX_INSNS * sizeof(mosrx_bpf_insn)));
-	/* the previous set may still be in use by enqueued launches */
-	HIPCHK(hipStreamSynchronize(c->stream));
-	HIPCHK(hipDeviceSynchronize());
-	if (total)
-		HIPCHK(hipMemcpy(c->d_bpf, staged, (size_t)total * sizeof(mosrx_bpf_insn), hipMemcpyHostToDevice));
+	}
+	if (hipSetDevice(c->device) != hipSuccess || (rc = stage_insns(c, staged, total))) {
+		free(staged);
+		return rc ? rc : -EIO;
+	}
 	c->bpf = t;
 	c->bpf_fn = NULL;   /* the compiled kernels of the previous set no longer apply */
-	c->bpf_fs = NULL;
-	c->bpf_fm = NULL;
-	c->bpf_fr = NULL;
+	memset(c->bpf_fu, 0, sizeof(c->bpf_fu));
+	c->bpf_pending = 0;
 	if (c->bpf_engine_req == MOSRX_BPF_ENGINE_JIT && nprog)
-		mosrx__bpf_jit_build(c, staged);   /* on failure the interpreter runs the set */
+		mosrx__bpf_jit_request(c, staged);   /* cached: installed now; else compiled behind, interpreter meanwhile */
+	free(staged);
 	return 0;
 }
 
-static int bpf_launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
-                      const uint16_t *len, uint32_t *match, hipStream_t s)
+int mosrx_bpf_wait(mosrx_ctx *c)
+{
+	if (!c)
+		return -EINVAL;
+	return mosrx__bpf_jit_wait(c);
+}
+
+int mosrx_bpf_pending(mosrx_ctx *c)
+{
+	if (!c)
+		return -EINVAL;
+	mosrx__bpf_poll(c);
+	return c->bpf_pending;
+}
+
+int mosrx_bpf_set(mosrx_ctx *c, const mosrx_bpf_prog *progs, uint32_t nprog)
+{
+	int rc = mosrx_bpf_set_async(c, progs, nprog);
+	return rc ? rc : mosrx_bpf_wait(c);
+}
+
+int mosrx__bpf_launch_dev(mosrx_ctx *c, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
+                          const uint16_t *len, uint32_t n, uint32_t *match, hipStream_t s)
 {
 	mosrx_bparams bp = c->bpf;
+	if (!n)
+		return 0;
+	mosrx__bpf_poll(c);
 	bp.frames = frames;
 	bp.off = off;
 	bp.len = len;
 	bp.match = match;
 	bp.insns = c->d_bpf;
-	bp.frames_bytes = (uint32_t)b->frames_bytes;
-	bp.n = b->n;
+	bp.frames_bytes = (uint32_t)frames_bytes;
+	bp.n = n;
 	if (c->bpf_fn)
 		return mosrx__bpf_jit_launch(c, &bp, s);
+	if (!c->d_bpf && bp.nprog)
+		return -EINVAL;
+	if (c->d_bpf)
+		c->bpf_pool_used[(c->bpf_pool_next + MOSRX_BPF_POOL - 1) % MOSRX_BPF_POOL] = 1;
 	return mosrx_launch_bpf(&bp, (void *)s);
+}
+
+static int bpf_launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,
+                      const uint16_t *len, uint32_t *match, hipStream_t s)
+{
+	return mosrx__bpf_launch_dev(c, frames, b->frames_bytes, off, len, b->n, match, s);
 }
 
 int mosrx_bpf_dev(mosrx_ctx *c, const mosrx_batch *b, uint32_t *d_match, void *stream)

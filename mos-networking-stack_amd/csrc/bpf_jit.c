@@ -20,6 +20,7 @@
  * interpreter (mosrx_bpf_engine() reports which engine is installed).
  */
 #include <errno.h>
+#include <pthread.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -404,15 +405,34 @@ static const char k_hook_pre[] =
 	"  }\n"
 	"  u32 match = 0;\n";
 
+/* Entry points of the fused module: one batch (kp), and the batch queue (a
+ * descriptor table of resident batches, one launch; gpu_module_func's groups),
+ * each as the stream tile with non-temporal tails, the stream tile with cached
+ * tails (batches of small frames) and the SMALL tile. */
 static const char k_fused_main[] =
 	"#define MOSRX_RTC_BPF 1\n"
 	"#include \"mosrx_kernels.hip\"\n"
-	"extern \"C\" __global__ __launch_bounds__(WG_THREADS(MOSRX_KIND_S13)) void mosrx_classify_bpf_stream(mosrx_kparams kp)\n"
+	"#define WGS __launch_bounds__(WG_THREADS(MOSRX_KIND_S13)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(MOSRX_KIND_S13))))\n"
+	"#define WGM __launch_bounds__(WG_THREADS(MOSRX_KIND_SMALL))\n"
+	"extern \"C\" __global__ WGS void mosrx_classify_bpf_stream(mosrx_kparams kp)\n"
 	"{ classify_tile<MOSRX_KIND_S13, 2 | VAR_BPF>(kp, blockIdx.x); }\n"
-	"extern \"C\" __global__ __launch_bounds__(WG_THREADS(MOSRX_KIND_S13)) void mosrx_classify_bpf_stream_rt(mosrx_kparams kp)\n"
+	"extern \"C\" __global__ WGS void mosrx_classify_bpf_stream_rt(mosrx_kparams kp)\n"
 	"{ classify_tile<MOSRX_KIND_S13, VAR_BPF>(kp, blockIdx.x); }\n"
-	"extern \"C\" __global__ __launch_bounds__(WG_THREADS(MOSRX_KIND_SMALL)) void mosrx_classify_bpf_small(mosrx_kparams kp)\n"
-	"{ classify_tile<MOSRX_KIND_SMALL, 2 | VAR_BPF>(kp, blockIdx.x); }\n";
+	"extern \"C\" __global__ WGM void mosrx_classify_bpf_small(mosrx_kparams kp)\n"
+	"{ classify_tile<MOSRX_KIND_SMALL, 2 | VAR_BPF>(kp, blockIdx.x); }\n"
+	"extern \"C\" __global__ WGS void mosrx_classify_bpf_queue_stream(const mosrx_qdesc *desc, uint32_t tpb, uint32_t nb,\n"
+	"    mosrx_qparams qp)\n"
+	"{ queue_tile<MOSRX_KIND_S13, 2 | VAR_BPF>(desc, tpb, nb, qp); }\n"
+	"extern \"C\" __global__ WGS void mosrx_classify_bpf_queue_stream_rt(const mosrx_qdesc *desc, uint32_t tpb,\n"
+	"    uint32_t nb, mosrx_qparams qp)\n"
+	"{ queue_tile<MOSRX_KIND_S13, VAR_BPF>(desc, tpb, nb, qp); }\n"
+	"extern \"C\" __global__ WGM void mosrx_classify_bpf_queue_small(const mosrx_qdesc *desc, uint32_t tpb, uint32_t nb,\n"
+	"    mosrx_qparams qp)\n"
+	"{ queue_tile<MOSRX_KIND_SMALL, 2 | VAR_BPF>(desc, tpb, nb, qp); }\n";
+
+static const char *const k_fused_names[MOSRX_BPF_NFUSED] = {
+	"mosrx_classify_bpf_stream", "mosrx_classify_bpf_stream_rt", "mosrx_classify_bpf_small",
+	"mosrx_classify_bpf_queue_stream", "mosrx_classify_bpf_queue_stream_rt", "mosrx_classify_bpf_queue_small"};
 
 int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out)
 {
@@ -436,6 +456,10 @@ int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams 
 	return 0;
 }
 
+/* hipRTC compiles are serialised process-wide: every mTCP thread's context has
+ * its own compile thread, and the compiles are rare (a filter set change). */
+static pthread_mutex_t g_rtc_lock = PTHREAD_MUTEX_INITIALIZER;
+
 /* hipRTC: source -> gfx950 code object (malloc'd into *code). */
 static int compile_code_h(const char *src, int nh, const char *const *htexts, const char *const *hnames,
                           char **code, size_t *size, char *log, size_t logsz)
@@ -445,9 +469,12 @@ static int compile_code_h(const char *src, int nh, const char *const *htexts, co
 	size_t sz = 0;
 	int rc = 0;
 	*code = NULL;
+	pthread_mutex_lock(&g_rtc_lock);
 	if (hiprtcCreateProgram(&prog, src, "mosrx_bpf_jit.hip", nh, (const char **)htexts, (const char **)hnames) !=
-	    HIPRTC_SUCCESS)
+	    HIPRTC_SUCCESS) {
+		pthread_mutex_unlock(&g_rtc_lock);
 		return -EIO;
+	}
 	if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
 		size_t ls = 0;
 		if (log && logsz && hiprtcGetProgramLogSize(prog, &ls) == HIPRTC_SUCCESS && ls) {
@@ -459,6 +486,7 @@ static int compile_code_h(const char *src, int nh, const char *const *htexts, co
 			free(l);
 		}
 		hiprtcDestroyProgram(&prog);
+		pthread_mutex_unlock(&g_rtc_lock);
 		return -EIO;
 	}
 	if (hiprtcGetCodeSize(prog, &sz) != HIPRTC_SUCCESS || !sz || !(*code = malloc(sz)))
@@ -466,6 +494,7 @@ static int compile_code_h(const char *src, int nh, const char *const *htexts, co
 	else if (hiprtcGetCode(prog, *code) != HIPRTC_SUCCESS)
 		rc = -EIO;
 	hiprtcDestroyProgram(&prog);
+	pthread_mutex_unlock(&g_rtc_lock);
 	if (rc) {
 		free(*code);
 		*code = NULL;
@@ -484,8 +513,8 @@ extern const char *const mosrx__src_names[];
 extern const char *const mosrx__src_texts[];
 
 /* The fused classify + BPF module: the embedded kernel sources + the hook. */
-static int compile_fused(const char *hook, hipModule_t *mod, hipFunction_t *fs, hipFunction_t *fm,
-                         hipFunction_t *fr, char *log, size_t logsz, size_t *code_size)
+static int compile_fused(const char *hook, hipModule_t *mod, hipFunction_t *fu, char *log, size_t logsz,
+                         size_t *code_size)
 {
 	const char *names[8], *texts[8];
 	char *code;
@@ -504,11 +533,17 @@ static int compile_fused(const char *hook, hipModule_t *mod, hipFunction_t *fs, 
 		free(code);
 		return rc;
 	}
-	if (hipModuleLoadData(mod, code) != hipSuccess ||
-	    hipModuleGetFunction(fs, *mod, "mosrx_classify_bpf_stream") != hipSuccess ||
-	    hipModuleGetFunction(fr, *mod, "mosrx_classify_bpf_stream_rt") != hipSuccess ||
-	    hipModuleGetFunction(fm, *mod, "mosrx_classify_bpf_small") != hipSuccess)
+	if (hipModuleLoadData(mod, code) != hipSuccess) {
 		rc = -EIO;
+	} else {
+		for (i = 0; i < MOSRX_BPF_NFUSED && !rc; i++)
+			if (hipModuleGetFunction(&fu[i], *mod, k_fused_names[i]) != hipSuccess)
+				rc = -EIO;
+		if (rc) {
+			hipModuleUnload(*mod);
+			*mod = NULL;
+		}
+	}
 	free(code);
 	return rc;
 }
@@ -532,7 +567,7 @@ int mosrx__bpf_jit_compile_fused(const mosrx_bpf_insn *insns, const mosrx_bparam
 	char *hook = NULL;
 	int rc = mosrx__bpf_jit_hook_source(insns, t, &hook);
 	if (!rc)
-		rc = compile_fused(hook, NULL, NULL, NULL, NULL, log, logsz, code_size);
+		rc = compile_fused(hook, NULL, NULL, log, logsz, code_size);
 	free(hook);
 	return rc;
 }
@@ -548,67 +583,288 @@ int mosrx__bpf_jit_compile(const char *src, char *log, size_t logsz, size_t *cod
 	return rc;
 }
 
-/* Install the compiled form of the set (c->bpf must already hold its table):
- * 0 with c->bpf_fn set, or -errno with the interpreter left in charge. */
-int mosrx__bpf_jit_build(mosrx_ctx *c, const mosrx_bpf_insn *insns)
+/* Build both modules of a set (on the compile thread): e->fn NULL when the
+ * standalone kernel failed (the interpreter keeps the set), e->fu[] NULL when
+ * only the fused one did (two launches then). */
+static void build_entry(const mosrx_bpf_insn *insns, const mosrx_bparams *t, struct mosrx_jit_entry *e, char *log,
+                        size_t logsz)
+{
+	char *src = NULL, *hook = NULL;
+	memset(e, 0, sizeof(*e));
+	e->key = set_hash(insns, t);
+	if (mosrx__bpf_jit_source(insns, t, &src) || compile_module(src, &e->mod, &e->fn, log, logsz)) {
+		e->mod = NULL;
+		e->fn = NULL;
+		free(src);
+		return;
+	}
+	free(src);
+	if (mosrx__bpf_jit_hook_source(insns, t, &hook) || compile_fused(hook, &e->fmod, e->fu, log, logsz, NULL)) {
+		e->fmod = NULL;
+		memset(e->fu, 0, sizeof(e->fu));
+	}
+	free(hook);
+}
+
+static void entry_unload(struct mosrx_jit_entry *e)
+{
+	if (e->mod)
+		hipModuleUnload(e->mod);
+	if (e->fmod)
+		hipModuleUnload(e->fmod);
+	memset(e, 0, sizeof(*e));
+}
+
+/* ---- the context's compile thread ------------------------------------------
+ * mosrx_bpf_set_async hands the set to it and returns; the thread compiles
+ * (hipRTC) and loads (hipModuleLoadData) the set's kernels and leaves the
+ * entry in `done`; the context's own thread takes finished entries into its
+ * cache at its next launch or call (mosrx__bpf_poll) -- so the kernels in use
+ * only ever change on the thread that launches them, between launches. */
+#define WORKER_DONE 8
+struct mosrx_bpf_worker {
+	pthread_t th;
+	pthread_mutex_t mu;
+	pthread_cond_t cv;          /* work for the thread, or stop */
+	pthread_cond_t done_cv;     /* a compile finished */
+	int device, stop, started;
+	int have_want;              /* `want` holds a set to compile */
+	mosrx_bparams want_t;
+	mosrx_bpf_insn *want_insns; /* MOSRX_BPF_MAX_INSNS */
+	uint64_t want_key;
+	int busy;                   /* compiling busy_key */
+	uint64_t busy_key;
+	struct mosrx_jit_entry done[WORKER_DONE];
+	char done_log[WORKER_DONE][512];
+	uint32_t ndone;
+};
+
+static void *worker_main(void *arg)
+{
+	struct mosrx_bpf_worker *w = arg;
+	mosrx_bpf_insn *insns = malloc(MOSRX_BPF_MAX_INSNS * sizeof(*insns));
+	hipSetDevice(w->device);
+	pthread_mutex_lock(&w->mu);
+	for (;;) {
+		struct mosrx_jit_entry e;
+		mosrx_bparams t;
+		char log[512];
+		uint32_t total = 0, j;
+		while (!w->stop && !w->have_want)
+			pthread_cond_wait(&w->cv, &w->mu);
+		if (w->stop || !insns)
+			break;
+		t = w->want_t;
+		for (j = 0; j < t.nprog; j++)
+			total += t.prog_len[j];
+		memcpy(insns, w->want_insns, (size_t)total * sizeof(*insns));
+		w->have_want = 0;
+		w->busy = 1;
+		w->busy_key = w->want_key;
+		pthread_mutex_unlock(&w->mu);
+		log[0] = 0;
+		build_entry(insns, &t, &e, log, sizeof(log));
+		pthread_mutex_lock(&w->mu);
+		if (w->ndone == WORKER_DONE) {   /* nobody collected them: drop the oldest */
+			entry_unload(&w->done[0]);
+			memmove(&w->done[0], &w->done[1], sizeof(w->done[0]) * (WORKER_DONE - 1));
+			memmove(&w->done_log[0], &w->done_log[1], sizeof(w->done_log[0]) * (WORKER_DONE - 1));
+			w->ndone--;
+		}
+		w->done[w->ndone] = e;
+		memcpy(w->done_log[w->ndone], log, sizeof(log));
+		w->ndone++;
+		w->busy = 0;
+		pthread_cond_broadcast(&w->done_cv);
+	}
+	w->busy = 0;
+	pthread_cond_broadcast(&w->done_cv);
+	pthread_mutex_unlock(&w->mu);
+	free(insns);
+	return NULL;
+}
+
+static struct mosrx_bpf_worker *worker_get(mosrx_ctx *c)
+{
+	struct mosrx_bpf_worker *w = c->bw;
+	if (w)
+		return w;
+	w = calloc(1, sizeof(*w));
+	if (!w)
+		return NULL;
+	w->want_insns = malloc(MOSRX_BPF_MAX_INSNS * sizeof(*w->want_insns));
+	w->device = c->device;
+	pthread_mutex_init(&w->mu, NULL);
+	pthread_cond_init(&w->cv, NULL);
+	pthread_cond_init(&w->done_cv, NULL);
+	if (!w->want_insns || pthread_create(&w->th, NULL, worker_main, w)) {
+		free(w->want_insns);
+		free(w);
+		return NULL;
+	}
+	w->started = 1;
+	c->bw = w;
+	return w;
+}
+
+static void sync_own_streams(mosrx_ctx *c)
+{
+	uint32_t i;
+	hipSetDevice(c->device);
+	hipStreamSynchronize(c->stream);
+	for (i = 0; i < NSLOT; i++)
+		hipStreamSynchronize(c->slot[i].stream);
+	for (i = 0; i < c->nxs; i++)
+		hipStreamSynchronize(c->xs[i]);
+}
+
+static void install(mosrx_ctx *c, const struct mosrx_jit_entry *e)
+{
+	c->bpf_fn = e ? e->fn : NULL;
+	if (e && e->fn)
+		memcpy(c->bpf_fu, e->fu, sizeof(c->bpf_fu));
+	else
+		memset(c->bpf_fu, 0, sizeof(c->bpf_fu));
+}
+
+/* Into the cache, evicting the oldest entry that is not the installed set's
+ * (its kernels may be in use; launches still in flight on the context's
+ * streams are drained before a module goes). */
+static void cache_put(mosrx_ctx *c, const struct mosrx_jit_entry *e)
+{
+	uint32_t i;
+	for (i = 0; i < c->njit; i++)
+		if (c->jit[i].key == e->key) {   /* compiled twice (a set re-requested while compiling) */
+			struct mosrx_jit_entry dup = *e;
+			entry_unload(&dup);
+			return;
+		}
+	if (c->njit == MOSRX_BPF_JIT_CACHE) {
+		uint32_t v = 0;
+		while (v < c->njit && c->jit[v].key == c->bpf_key)
+			v++;
+		if (v == c->njit)
+			v = 0;
+		sync_own_streams(c);
+		entry_unload(&c->jit[v]);
+		memmove(&c->jit[v], &c->jit[v + 1], sizeof(c->jit[0]) * (MOSRX_BPF_JIT_CACHE - 1 - v));
+		c->njit--;
+	}
+	c->jit[c->njit++] = *e;
+}
+
+static const struct mosrx_jit_entry *cache_find(const mosrx_ctx *c, uint64_t key)
+{
+	uint32_t i;
+	for (i = 0; i < c->njit; i++)
+		if (c->jit[i].key == key)
+			return &c->jit[i];
+	return NULL;
+}
+
+/* Take the compiles the thread finished into the cache.  On the context's own
+ * thread only. */
+static void collect(mosrx_ctx *c)
+{
+	struct mosrx_bpf_worker *w = c->bw;
+	struct mosrx_jit_entry got[WORKER_DONE];
+	char logs[WORKER_DONE][512];
+	uint32_t i, n;
+	if (!w)
+		return;
+	pthread_mutex_lock(&w->mu);
+	n = w->ndone;
+	memcpy(got, w->done, sizeof(got[0]) * n);
+	memcpy(logs, w->done_log, sizeof(logs[0]) * n);
+	w->ndone = 0;
+	pthread_mutex_unlock(&w->mu);
+	for (i = 0; i < n; i++) {
+		cache_put(c, &got[i]);
+		if (got[i].key == c->bpf_key) {
+			memcpy(c->bpf_jit_log, logs[i], sizeof(c->bpf_jit_log));
+			c->bpf_jit_log[sizeof(c->bpf_jit_log) - 1] = 0;
+		}
+	}
+}
+
+/* Install the installed set's compiled form once its compile is in (called
+ * before every launch that runs the set). */
+void mosrx__bpf_poll(mosrx_ctx *c)
+{
+	const struct mosrx_jit_entry *e;
+	if (!c->bw || !c->bpf_pending)
+		return;
+	collect(c);
+	if ((e = cache_find(c, c->bpf_key))) {
+		install(c, e);
+		c->bpf_pending = 0;
+	}
+}
+
+/* The installed set (c->bpf, staged `insns`) gets its compiled form: from the
+ * cache at once, else asynchronously (c->bpf_pending until mosrx__bpf_poll
+ * installs it); the interpreter runs the set meanwhile.  0, or -errno when no
+ * compile thread could be started (the interpreter keeps the set). */
+int mosrx__bpf_jit_request(mosrx_ctx *c, const mosrx_bpf_insn *insns)
 {
 	const mosrx_bparams *t = &c->bpf;
-	const uint64_t key = set_hash(insns, t);
-	char *src = NULL;
-	uint32_t i;
-	int rc;
-	c->bpf_fn = NULL;
-	c->bpf_fs = NULL;
-	c->bpf_fm = NULL;
-	c->bpf_fr = NULL;
+	const struct mosrx_jit_entry *e;
+	struct mosrx_bpf_worker *w;
+	uint32_t j, total = 0;
+	c->bpf_key = set_hash(insns, t);
+	c->bpf_pending = 0;
 	c->bpf_jit_log[0] = 0;
-	for (i = 0; i < c->njit; i++)
-		if (c->jit[i].key == key) {
-			c->bpf_fn = c->jit[i].fn;
-			c->bpf_fs = c->jit[i].fs;
-			c->bpf_fm = c->jit[i].fm;
-			c->bpf_fr = c->jit[i].fr;
+	install(c, NULL);
+	collect(c);   /* compiles the thread finished (this set's among them, perhaps) */
+	if ((e = cache_find(c, c->bpf_key))) {
+		install(c, e);
+		return 0;
+	}
+	if (!(w = worker_get(c)))
+		return -EAGAIN;
+	for (j = 0; j < t->nprog; j++)
+		total += t->prog_len[j];
+	pthread_mutex_lock(&w->mu);
+	if (!(w->busy && w->busy_key == c->bpf_key)) {   /* (being compiled already: wait for that one) */
+		w->want_t = *t;
+		w->want_key = c->bpf_key;
+		memcpy(w->want_insns, insns, (size_t)total * sizeof(*insns));
+		w->have_want = 1;
+		pthread_cond_signal(&w->cv);
+	}
+	pthread_mutex_unlock(&w->mu);
+	c->bpf_pending = 1;
+	return 0;
+}
+
+/* Block until the installed set's compile is collected (or the thread has
+ * nothing left for it: the interpreter stays). */
+int mosrx__bpf_jit_wait(mosrx_ctx *c)
+{
+	struct mosrx_bpf_worker *w = c->bw;
+	if (!w || !c->bpf_pending)
+		return 0;
+	for (;;) {
+		uint32_t i;
+		int found = 0, idle;
+		pthread_mutex_lock(&w->mu);
+		for (;;) {
+			for (i = 0; i < w->ndone; i++)
+				found |= w->done[i].key == c->bpf_key;
+			idle = !w->busy && !w->have_want;
+			if (found || idle || w->stop)
+				break;
+			pthread_cond_wait(&w->done_cv, &w->mu);
+		}
+		pthread_mutex_unlock(&w->mu);
+		mosrx__bpf_poll(c);
+		if (!c->bpf_pending)
+			return 0;
+		if (idle || w->stop) {   /* nothing for this set in flight: stay on the interpreter */
+			c->bpf_pending = 0;
 			return 0;
 		}
-	if ((rc = mosrx__bpf_jit_source(insns, t, &src)))
-		return rc;
-	{
-		hipModule_t mod;
-		hipFunction_t fn;
-		rc = compile_module(src, &mod, &fn, c->bpf_jit_log, sizeof(c->bpf_jit_log));
-		free(src);
-		if (rc)
-			return rc;
-		hipModule_t fmod = NULL;
-		hipFunction_t fs = NULL, fm = NULL, fr = NULL;
-		char *hook = NULL;
-		if (mosrx__bpf_jit_hook_source(insns, t, &hook) ||
-		    compile_fused(hook, &fmod, &fs, &fm, &fr, c->bpf_jit_log, sizeof(c->bpf_jit_log), NULL)) {
-			fmod = NULL;   /* no fused kernel: mosrx_classify_bpf_dev runs two launches */
-			fs = fm = fr = NULL;
-		}
-		free(hook);
-		if (c->njit == MOSRX_BPF_JIT_CACHE) {   /* evict the oldest */
-			hipModuleUnload(c->jit[0].mod);
-			if (c->jit[0].fmod)
-				hipModuleUnload(c->jit[0].fmod);
-			memmove(&c->jit[0], &c->jit[1], sizeof(c->jit[0]) * (MOSRX_BPF_JIT_CACHE - 1));
-			c->njit--;
-		}
-		c->jit[c->njit].key = key;
-		c->jit[c->njit].mod = mod;
-		c->jit[c->njit].fn = fn;
-		c->jit[c->njit].fmod = fmod;
-		c->jit[c->njit].fs = fs;
-		c->jit[c->njit].fm = fm;
-		c->jit[c->njit].fr = fr;
-		c->njit++;
-		c->bpf_fn = fn;
-		c->bpf_fs = fs;
-		c->bpf_fm = fm;
-		c->bpf_fr = fr;
 	}
-	return 0;
 }
 
 /* Fused classify + BPF launch (kp carries bmatch). */
@@ -616,7 +872,7 @@ int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hi
 {
 	/* the library's tail policy: cached tail loads for batches of small frames */
 	const int cached = !(mosrx__tail_variant(c, kp->frames_bytes, kp->n) & 2);
-	hipFunction_t f = small ? c->bpf_fm : cached && c->bpf_fr ? c->bpf_fr : c->bpf_fs;
+	hipFunction_t f = small ? c->bpf_fu[FU_M] : cached && c->bpf_fu[FU_SR] ? c->bpf_fu[FU_SR] : c->bpf_fu[FU_S];
 	const unsigned tile = small ? MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL) : MOSRX_KIND_FRAMES(MOSRX_KIND_S13);
 	const unsigned threads = small ? 256u : 64u * (1u + MOSRX_STREAMERS);
 	mosrx_kparams k = *kp;
@@ -624,6 +880,26 @@ int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hi
 	if (!f)
 		return -EINVAL;
 	if (hipModuleLaunchKernel(f, (kp->n + tile - 1) / tile, 1, 1, threads, 1, 1, 0, s, args, NULL) != hipSuccess)
+		return -EIO;
+	return 0;
+}
+
+/* The fused kernel over a batch queue (qp's descriptors carry the masks). */
+int mosrx__bpf_fused_queue_launch(mosrx_ctx *c, const mosrx_qparams *qp, uint32_t total_tiles, int small,
+                                  int variant, hipStream_t s)
+{
+	hipFunction_t f = small ? c->bpf_fu[FU_QM] : !(variant & 2) && c->bpf_fu[FU_QSR] ? c->bpf_fu[FU_QSR]
+	                                                                                : c->bpf_fu[FU_QS];
+	const unsigned threads = small ? 256u : 64u * (1u + MOSRX_STREAMERS);
+	const mosrx_qdesc *desc = qp->desc;
+	uint32_t tpb = qp->tpb, nb = qp->nb;
+	mosrx_qparams q = *qp;
+	void *args[] = {&desc, &tpb, &nb, &q};
+	if (!f)
+		return -EINVAL;
+	if (!total_tiles)
+		return 0;
+	if (hipModuleLaunchKernel(f, total_tiles, 1, 1, threads, 1, 1, 0, s, args, NULL) != hipSuccess)
 		return -EIO;
 	return 0;
 }
@@ -647,14 +923,26 @@ int mosrx__bpf_jit_launch(mosrx_ctx *c, const mosrx_bparams *bp, hipStream_t s)
 void mosrx__bpf_jit_free(mosrx_ctx *c)
 {
 	uint32_t i;
-	for (i = 0; i < c->njit; i++) {
-		hipModuleUnload(c->jit[i].mod);
-		if (c->jit[i].fmod)
-			hipModuleUnload(c->jit[i].fmod);
+	struct mosrx_bpf_worker *w = c->bw;
+	if (w) {
+		pthread_mutex_lock(&w->mu);
+		w->stop = 1;
+		pthread_cond_broadcast(&w->cv);
+		pthread_mutex_unlock(&w->mu);
+		if (w->started)
+			pthread_join(w->th, NULL);
+		for (i = 0; i < w->ndone; i++)
+			entry_unload(&w->done[i]);
+		pthread_mutex_destroy(&w->mu);
+		pthread_cond_destroy(&w->cv);
+		pthread_cond_destroy(&w->done_cv);
+		free(w->want_insns);
+		free(w);
+		c->bw = NULL;
 	}
+	for (i = 0; i < c->njit; i++)
+		entry_unload(&c->jit[i]);
 	c->njit = 0;
-	c->bpf_fn = NULL;
-	c->bpf_fs = NULL;
-	c->bpf_fm = NULL;
-	c->bpf_fr = NULL;
+	c->bpf_pending = 0;
+	install(c, NULL);
 }

@@ -72,8 +72,9 @@ struct stage {
 	int borrowed;             /* frames lent by the source: give them back when the group is recycled */
 	/* what its records were made under: mOS's socket counts, the netdev's
 	 * parameter / filter generation, the programs behind its masks, and
-	 * whether the flow hashes were made (not in a BPF pass) */
-	uint32_t msp, esp, gen, nprog, has_fh;
+	 * which side arrays the launch filled (pkt_info fields are not made in a
+	 * BPF pass) */
+	uint32_t msp, esp, gen, nprog, has_fh, has_ti;
 };
 
 struct group {
@@ -346,28 +347,49 @@ static uint64_t stage_bytes(void)
 	return dsc + (uint64_t)g_cfg.batch * ((g_cfg.max_frame + 15u + 16u) & ~15u) + 512;
 }
 
+/* Frame bytes an auto group's block holds.  cfg.group_bytes, else
+ * MOSRX_GROUP_AUTO_BYTES; inside mOS, where every mTCP thread holds two such
+ * blocks per netdev (pinned), the default is scaled so that all of them
+ * together stay near MOSRX_PINNED_BUDGET (mos.conf's num_cores x netdevs),
+ * never under MOSRX_GROUP_AUTO_MIN_BYTES.  INTEGRATION.md §5 gives the
+ * footprint. */
+#define MOSRX_PINNED_BUDGET        (4ull << 30)
+#define MOSRX_GROUP_AUTO_MIN_BYTES (32ull << 20)
 static uint64_t auto_bytes(void)
 {
-	return g_cfg.group_bytes ? g_cfg.group_bytes : MOSRX_GROUP_AUTO_BYTES;
+	uint64_t b = MOSRX_GROUP_AUTO_BYTES;
+	if (g_cfg.group_bytes)
+		return g_cfg.group_bytes;
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+	if (g_config.mos && g_config.mos->num_cores > 0) {
+		const uint64_t per = MOSRX_PINNED_BUDGET / ((uint64_t)g_config.mos->num_cores * g_cfg.num_ifs * MOSRX_NSLOT);
+		if (per < b)
+			b = per < MOSRX_GROUP_AUTO_MIN_BYTES ? MOSRX_GROUP_AUTO_MIN_BYTES : per;
+	}
+#endif
+	return b;
 }
 
 /* Explicit groups reserve `group` worst-case stages.  Auto groups hold up to
  * MOSRX_MAX_GROUP stages in a block of auto_bytes(): stages are packed by the
  * bytes their frames really take, the last one stops where the block is full
  * (a short batch, which ends the group), and records are there for the
- * frames that can fit (a staged frame takes >= 64 bytes of block). */
-static int group_alloc(mosrx_ctx *mc, struct group *g)
+ * frames that can fit (a staged frame takes >= 64 bytes of block).  When the
+ * host cannot pin that much, the block is halved until it can, down to one
+ * worst-case batch: smaller groups, not a dead mTCP thread. */
+static int group_alloc_sized(mosrx_ctx *mc, struct group *g, uint64_t bytes)
 {
+	memset(g, 0, sizeof(*g));
 	if (g_cfg.group == MOSRX_GROUP_AUTO) {
 		g->cap_st = MOSRX_MAX_GROUP;
-		g->blk_bytes = auto_bytes();
-		g->rec_cap = auto_bytes() / 64 + g_cfg.batch;
+		g->blk_bytes = bytes;
+		g->rec_cap = bytes / 64 + g_cfg.batch;
 		if (g->rec_cap > (uint64_t)g_cfg.batch * MOSRX_MAX_GROUP)
 			g->rec_cap = (uint64_t)g_cfg.batch * MOSRX_MAX_GROUP;
 	} else {
-		g->cap_st = g_cfg.group;
-		g->blk_bytes = stage_bytes() * g_cfg.group;
-		g->rec_cap = (uint64_t)g_cfg.batch * g_cfg.group;
+		g->cap_st = (uint32_t)(bytes / stage_bytes());
+		g->blk_bytes = stage_bytes() * g->cap_st;
+		g->rec_cap = (uint64_t)g_cfg.batch * g->cap_st;
 	}
 	g->st = calloc(g->cap_st, sizeof(*g->st));
 	if (!g->st || mosrx_host_alloc(mc, g->blk_bytes, (void **)&g->blk) ||
@@ -377,6 +399,24 @@ static int group_alloc(mosrx_ctx *mc, struct group *g)
 	    (g_cfg.flowhash && mosrx_host_alloc(mc, g->rec_cap * 4, (void **)&g->fh)))
 		return -ENOMEM;
 	return 0;
+}
+
+static int group_alloc(mosrx_ctx *mc, struct group *g)
+{
+	const uint64_t floor = stage_bytes();
+	uint64_t want = g_cfg.group == MOSRX_GROUP_AUTO ? auto_bytes() : stage_bytes() * g_cfg.group;
+	if (want < floor)
+		want = floor;
+	for (;;) {
+		if (!group_alloc_sized(mc, g, want))
+			return 0;
+		group_free(mc, g);
+		if (want <= floor)
+			return -ENOMEM;
+		want = want / 2 > floor ? want / 2 : floor;
+		fprintf(stderr, "[mosrx] gpu_module: pinned staging short: group block reduced to %llu MiB\n",
+		        (unsigned long long)(want >> 20));
+	}
 }
 
 static void gpu_destroy_handle(struct mtcp_thread_context *ctx);
@@ -504,13 +544,14 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
 	*pos = at + fpos;
 }
 
-/* Receive a group: up to cap_st batches (auto: until auto_bytes() of frames),
- * stopping early when the source runs dry -- a batch that comes back short
- * ends the group, so nothing waits for frames that are not there yet.  With a
- * BPF set installed a group is one batch (the filters run in a per-batch pass). */
+/* Receive a group: up to cap_st batches (auto: until the block's bytes of
+ * frames), stopping early when the source runs dry -- a batch that comes back
+ * short ends the group, so nothing waits for frames that are not there yet.
+ * Filters or not, the group is one launch (the fused classify + BPF queue
+ * kernel when a set is installed). */
 static void group_fill(struct if_state *is, struct group *g)
 {
-	const uint32_t cap = is->nprog ? 1 : g->cap_st;
+	const uint32_t cap = g->cap_st;
 	uint64_t pos = 0, recs = 0, fbytes = 0;
 	uint32_t i;
 	g->nst = 0;
@@ -535,7 +576,7 @@ static void group_fill(struct if_state *is, struct group *g)
 		fbytes += s->bytes;
 		if (s->n < g_cfg.batch)
 			break;
-		if (g_cfg.group == MOSRX_GROUP_AUTO && fbytes >= auto_bytes())
+		if (g_cfg.group == MOSRX_GROUP_AUTO && fbytes >= g->blk_bytes)
 			break;
 	}
 }
@@ -572,15 +613,15 @@ static void stage_batch(const struct stage *s, mosrx_batch *b)
 
 /* Classify stages [first, nst) of group k on pipeline slot k, under mOS's
  * current stack state and the installed filter set: one launch for all of
- * them (the batch queue); with filters, one classify + BPF pass per batch,
- * all but the last waited here. */
+ * them (the batch queue; with filters the fused classify + BPF queue kernel,
+ * which also makes the flow hashes). */
 static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_t first)
 {
 	struct group *g = &is->g[k];
 	mosrx_batch b[MOSRX_MAX_GROUP];
 	mosrx_result *out[MOSRX_MAX_GROUP];
 	mosrx_tcpinfo *ti[MOSRX_MAX_GROUP];
-	uint32_t *fh[MOSRX_MAX_GROUP];
+	uint32_t *fh[MOSRX_MAX_GROUP], *mt[MOSRX_MAX_GROUP];
 	uint32_t i, nb = g->nst - first;
 	if (follow_mos_state(pv, is))
 		return -1;
@@ -590,21 +631,16 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 		out[i - first] = s->res;
 		ti[i - first] = s->ti;
 		fh[i - first] = s->fh;
+		mt[i - first] = s->match;
 		s->msp = is->params.num_msp;
 		s->esp = is->params.num_esp;
 		s->gen = is->gen;
 		s->nprog = is->nprog;
-		s->has_fh = s->fh && !is->nprog;
+		s->has_fh = s->fh != NULL;
+		s->has_ti = s->ti != NULL && !is->nprog;
 	}
-	if (is->nprog) {
-		for (i = first; i < g->nst; i++) {
-			if (mosrx_classify_bpf_host_submit(is->mc, k, &b[i - first], g->st[i].res, g->st[i].match))
-				return -1;
-			if (i + 1 < g->nst && mosrx_classify_host_wait(is->mc, k))
-				return -1;
-		}
-		return 0;
-	}
+	if (is->nprog)
+		return mosrx_classify_host_group_submit_bpf(is->mc, k, b, nb, out, g_cfg.flowhash ? fh : NULL, mt);
 	if (nb == 1 && !g_cfg.flowhash)
 		return mosrx_classify_host_submit_ex(is->mc, k, &b[0], out[0], ti[0]);
 	return mosrx_classify_host_group_submit_ex(is->mc, k, b, nb, out, g_cfg.tcpinfo ? ti : NULL,
@@ -856,13 +892,16 @@ static int gpu_get_nif(struct ifreq *ifr)
 /* Install a BPF program set on netdev is (the monitors' filters, bit j =
  * program j): the match arrays are allocated the first time, the stages of
  * both groups pointed at them, and the generation bumped so every batch not
- * yet handed out is classified again with the set. */
+ * yet handed out is classified again with the set.  The set is in effect at
+ * once (mosrx_bpf_set_async: the interpreter kernel until the compile thread
+ * has its hipRTC kernels loaded), so the mTCP thread never waits for a
+ * compile. */
 static int32_t set_bpf(struct gpu_priv *pv, struct if_state *is, const mosrx_bpf_set_arg *a)
 {
 	int k;
 	uint32_t i;
 	(void)pv;
-	if (!a || a->nprog > MOSRX_BPF_MAX_PROGS || mosrx_bpf_set(is->mc, a->progs, a->nprog))
+	if (!a || a->nprog > MOSRX_BPF_MAX_PROGS || mosrx_bpf_set_async(is->mc, a->progs, a->nprog))
 		return -1;
 	for (k = 0; k < MOSRX_NSLOT && a->nprog; k++) {
 		struct group *g = &is->g[k];
@@ -907,7 +946,7 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
 		*(const uint32_t **)argp = s->fh;
 		return 0;
 	case MOSRX_PKT_RX_TCPINFO:
-		if (!s || !s->ti)
+		if (!s || !s->has_ti)
 			return -1;
 		*(const mosrx_tcpinfo **)argp = s->ti;
 		return 0;

@@ -29,11 +29,18 @@
  *
  * TRUNCATED frames (headers claiming bytes past the capture; the reference
  * reads past its buffer there) are dropped with -1.
+ *
+ * A batch whose records cannot be had (the backend could not classify it
+ * again after a state or filter change, or handed out no records) is dropped
+ * from that frame on, the way a NIC drops what it could not receive: each
+ * frame is counted in rx_packets and rx_errors and released, -1, and mOS runs
+ * on (the backend's own policy for a failed group, gpu_module.c group_drop).
  */
 #include <assert.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "mtcp.h"
 #include "arp.h"
@@ -59,12 +66,18 @@
 #define MAX_CORES 64
 #define NO_BIT    (-1)
 
-/* A filter program mOS holds for a monitor, and where its result comes from. */
+/* A filter program mOS holds for a monitor, and where its result comes from.
+ * Keyed by its instructions, not by where mOS keeps them: a monitor that
+ * closes frees its compiled filter (FreeMonListener, socket.c:33-36) and the
+ * next one's can land at the same address with the same length. */
+#define FILT_INSNS 8192              /* instructions the table keeps copies of */
 struct filt {
-	const struct sfbpf_insn *insns;
+	const struct sfbpf_insn *insns;  /* mOS's program (fast path: the same pointer) */
+	const struct sfbpf_insn *copy;   /* its instructions when installed (in t_view.arena) */
 	uint32_t len;
 	int mode;                    /* MOSRX_BPF_LEN_FRAME / _IP: the call site's buffer */
 	int bit;                     /* bit of the GPU match mask, NO_BIT: EVAL_BPFFILTER */
+	int seen;                    /* still bound by a monitor at the last check */
 };
 
 /* The batch the mTCP thread is walking (one view per thread: RunMainLoop
@@ -76,9 +89,12 @@ struct rx_view {
 	const uint32_t *match;       /* NULL: no masks for this batch */
 	const uint32_t *fhash;       /* NULL: no flow-table hashes for this batch */
 	mosrx_rx_state state;
+	int dead_from;               /* >= 0: the batch's frames from this index on have no records (dropped) */
 	/* the filter set installed on this thread's netdevs */
 	struct filt filt[2 * MOSRX_BPF_MAX_PROGS + 64];
 	uint32_t nfilt, ngpu;
+	struct sfbpf_insn arena[FILT_INSNS];
+	uint32_t narena;
 };
 
 static __thread struct rx_view t_view;
@@ -98,11 +114,22 @@ int mosrx_mos_rx_stats_of(int cpu, mosrx_mos_rx_stats *st)
 	return 0;
 }
 
-static void fatal(const char *what, int ifidx)
+static uint64_t now_ns(void)
 {
-	fprintf(stderr, "[mosrx] mosrx_mos_process_packet: netdev %d: %s "
-	        "(is gpu_module_func mOS's I/O module?)\n", ifidx, what);
-	exit(EXIT_FAILURE);
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+/* The batch has no usable records from frame `index` on: those frames are
+ * dropped (counted by the caller), mOS carries on. */
+static void view_lost(struct rx_view *v, struct mtcp_manager *mtcp, int index, const char *what)
+{
+	mosrx_mos_rx_stats *st = stats_of(mtcp);
+	if (!st->gpu_errors++)
+		fprintf(stderr, "[mosrx] mosrx_mos_process_packet: netdev %d: %s; the batch's remaining frames are "
+		        "dropped (rx_errors)\n", v->ifidx, what);
+	v->dead_from = index;
 }
 
 /* The exposed batch's records, masks and classification state. */
@@ -114,9 +141,14 @@ static void view_fetch(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx)
 	v->res = NULL;
 	v->match = NULL;
 	v->fhash = NULL;
+	v->dead_from = -1;
 	if (!iom->dev_ioctl || iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_RESULTS, (void *)&v->res) || !v->res ||
-	    iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_STATE, &v->state))
-		fatal("no GPU records for the batch", ifidx);
+	    iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_STATE, &v->state)) {
+		v->res = NULL;
+		v->state.n = 0x7FFFFFFF;   /* whatever get_rptr hands out goes the dropped way */
+		view_lost(v, mtcp, 0, "no GPU records for the batch (is gpu_module_func mOS's I/O module?)");
+		return;
+	}
 	if (v->state.bpf_nprog && iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_MATCH, (void *)&v->match))
 		v->match = NULL;
 	if (iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_FHASH, (void *)&v->fhash))
@@ -142,38 +174,52 @@ static tcp_stream *find_stream(struct rx_view *v, int index, mtcp_manager_t mtcp
 	return NULL;
 }
 
-/* Classify the rest of the exposed batch again (the stack state or the filter
- * set changed under it) and take the new records. */
-static void view_reclassify(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx)
+/* Classify the rest of the exposed batch (from frame `index`) again -- the
+ * stack state or the filter set changed under it -- and take the new records;
+ * if that fails, the rest of the batch is dropped. */
+static void view_reclassify(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx, int index)
 {
 	static int one = 1;
-	if (mtcp->iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_RECLASSIFY, &one))
-		fatal("reclassification failed", ifidx);
+	if (v->dead_from >= 0)
+		return;
+	if (mtcp->iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_RECLASSIFY, &one)) {
+		view_lost(v, mtcp, index, "reclassification failed");
+		return;
+	}
 	stats_of(mtcp)->reclassified++;
 	view_fetch(v, mtcp, ifidx);
 }
 
+/* The table entry of this program: its instructions, length and call site. */
 static struct filt *filt_find(struct rx_view *v, const struct sfbpf_program *fc, int mode)
 {
 	uint32_t i;
-	for (i = 0; i < v->nfilt; i++)
-		if (v->filt[i].insns == fc->bf_insns && v->filt[i].len == fc->bf_len && v->filt[i].mode == mode)
-			return &v->filt[i];
+	for (i = 0; i < v->nfilt; i++) {
+		struct filt *f = &v->filt[i];
+		if (f->len == fc->bf_len && f->mode == mode &&
+		    !memcmp(f->copy, fc->bf_insns, (size_t)fc->bf_len * sizeof(*fc->bf_insns)))
+			return f;
+	}
 	return NULL;
 }
 
 static void filt_add(struct rx_view *v, const struct sfbpf_program *fc, int mode, mosrx_bpf_prog *progs)
 {
 	struct filt *f;
-	if (!fc->bf_insns || filt_find(v, fc, mode) || v->nfilt == sizeof(v->filt) / sizeof(v->filt[0]))
+	if (!fc->bf_insns || filt_find(v, fc, mode) || v->nfilt == sizeof(v->filt) / sizeof(v->filt[0]) ||
+	    v->narena + fc->bf_len > FILT_INSNS)
 		return;
 	f = &v->filt[v->nfilt++];
 	f->insns = fc->bf_insns;
+	f->copy = v->arena + v->narena;
+	memcpy(v->arena + v->narena, fc->bf_insns, (size_t)fc->bf_len * sizeof(*fc->bf_insns));
+	v->narena += fc->bf_len;
 	f->len = fc->bf_len;
 	f->mode = mode;
 	f->bit = NO_BIT;
+	f->seen = 1;
 	if (v->ngpu < MOSRX_BPF_MAX_PROGS) {
-		progs[v->ngpu].insns = (const mosrx_bpf_insn *)fc->bf_insns;   /* struct sfbpf_insn layout */
+		progs[v->ngpu].insns = (const mosrx_bpf_insn *)f->copy;   /* struct sfbpf_insn layout */
 		progs[v->ngpu].len = fc->bf_len;
 		progs[v->ngpu].len_mode = mode;
 		f->bit = (int)v->ngpu++;
@@ -184,14 +230,16 @@ static void filt_add(struct rx_view *v, const struct sfbpf_program *fc, int mode
  * frame (ip_in.c:58-60: ethh, eth_len), stream SYN / orphan filters over the
  * IP datagram (tcp.c:50-52, :490-492: iph - 14, ip_len + 14), installed on
  * every netdev, then the exposed batch classified again with them. */
-static void filters_sync(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx)
+static void filters_sync(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx, int index)
 {
 	mosrx_bpf_prog progs[MOSRX_BPF_MAX_PROGS];
 	mosrx_bpf_set_arg a;
 	struct mon_listener *walk;
 	mosrx_mos_rx_stats *st = stats_of(mtcp);
+	const uint64_t t0 = now_ns();
 	int nif, ok = 1;
 	v->nfilt = v->ngpu = 0;
+	v->narena = 0;
 	TAILQ_FOREACH(walk, &mtcp->monitors, link) {
 		/* the orphan loop (tcp.c:486-496) reads stream_orphan_fcode of every
 		 * monitor, raw ones included (their union, socket.h:52-60) */
@@ -218,7 +266,48 @@ static void filters_sync(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx
 	st->filter_installs++;
 	st->filters_gpu = v->ngpu;
 	st->filters_cpu = v->nfilt - v->ngpu;
-	view_reclassify(v, mtcp, ifidx);
+	view_reclassify(v, mtcp, ifidx, index);
+	{
+		const uint64_t dt = now_ns() - t0;
+		if (dt > st->max_filter_sync_ns)
+			st->max_filter_sync_ns = dt;
+	}
+}
+
+/* At a batch's first frame: does the installed table still hold exactly the
+ * filters the monitors have bound?  A filter bound since is installed at its
+ * first evaluation anyway; one whose monitor went away (its program freed,
+ * perhaps reused at the same address by another) is dropped from the set
+ * here, so stale programs never hold the GPU's 32 slots. */
+static void filters_check(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx)
+{
+	struct mon_listener *walk;
+	uint32_t i;
+	int stale = 0;
+	if (!v->nfilt)
+		return;
+	for (i = 0; i < v->nfilt; i++)
+		v->filt[i].seen = 0;
+#define SEE(fc, mode)                                                     \
+	do {                                                                  \
+		if ((fc)->bf_insns) {                                             \
+			struct filt *f_ = filt_find(v, (fc), (mode));                 \
+			if (f_)                                                       \
+				f_->seen = 1;                                             \
+		}                                                                 \
+	} while (0)
+	TAILQ_FOREACH(walk, &mtcp->monitors, link) {
+		if (walk->socket->socktype == MOS_SOCK_MONITOR_RAW)
+			SEE(&walk->raw_pkt_fcode, MOSRX_BPF_LEN_FRAME);
+		else
+			SEE(&walk->stream_syn_fcode, MOSRX_BPF_LEN_IP);
+		SEE(&walk->stream_orphan_fcode, MOSRX_BPF_LEN_IP);
+	}
+#undef SEE
+	for (i = 0; i < v->nfilt; i++)
+		stale |= !v->filt[i].seen;
+	if (stale)
+		filters_sync(v, mtcp, ifidx, 0);
 }
 
 /* EVAL_BPFFILTER(*fc, p, l) for frame `index` of the batch (include/bpf/sfbpf.h:84):
@@ -229,10 +318,10 @@ static int filter_eval(struct rx_view *v, int index, const struct sfbpf_program 
 	/* bound since the last install (a full table keeps the rest on the CPU
 	 * rather than installing again for every frame) */
 	if (!f && v->nfilt < sizeof(v->filt) / sizeof(v->filt[0])) {
-		filters_sync(v, v->mtcp, v->ifidx);
+		filters_sync(v, v->mtcp, v->ifidx, index);
 		f = filt_find(v, fc, mode);
 	}
-	if (f && f->bit != NO_BIT && v->match)
+	if (f && f->bit != NO_BIT && v->match && v->dead_from < 0)
 		return (v->match[index] >> f->bit) & 1;
 	return EVAL_BPFFILTER((*fc), p, l);
 }
@@ -427,7 +516,12 @@ static int ipv4(struct rx_view *v, int index, mtcp_manager_t mtcp, struct pkt_ct
 	 * on the other side of it (a socket came or went since the batch was
 	 * classified) are made again first */
 	if (((mtcp->num_msp || mtcp->num_esp) != 0) != ((v->state.num_msp || v->state.num_esp) != 0))
-		view_reclassify(v, mtcp, v->ifidx);
+		view_reclassify(v, mtcp, v->ifidx, index);
+	if (v->dead_from >= 0) {                     /* no records for the rest of the batch: dropped */
+		stats_of(mtcp)->gpu_dropped++;
+		release(mtcp, pctx);
+		return ERROR;
+	}
 	r = &v->res[index];                          /* (a filter install reclassifies the batch too) */
 	if (mtcp->num_msp == 0 && mtcp->num_esp == 0) {
 		if (pctx->forward)
@@ -477,17 +571,29 @@ int mosrx_mos_process_packet(struct mtcp_manager *mtcp, const int ifidx, const i
 	const mosrx_result *r;
 	int ret;
 
-	if (index == 0 || v->mtcp != mtcp || v->ifidx != ifidx || !v->res)
+	if (index == 0 || v->mtcp != mtcp || v->ifidx != ifidx || (!v->res && v->dead_from < 0)) {
 		view_fetch(v, mtcp, ifidx);
-	if (index < 0 || (uint32_t)index >= v->state.n)
-		fatal("frame index past the batch", ifidx);
-	r = &v->res[index];
+		if (index == 0 && v->dead_from < 0)
+			filters_check(v, mtcp, ifidx);
+	}
+	if (v->dead_from < 0 && (index < 0 || (uint32_t)index >= v->state.n))
+		view_lost(v, mtcp, 0, "frame index past the batch's records");
 	stats_of(mtcp)->frames++;
 
 #ifdef NETSTAT
 	mtcp->nstat.rx_packets[ifidx]++;
 	mtcp->nstat.rx_bytes[ifidx] += len + ETHER_OVR;
 #endif
+	if (v->dead_from >= 0 && index >= v->dead_from) {   /* no records: dropped, as a NIC would */
+		stats_of(mtcp)->gpu_dropped++;
+		if (mtcp->iom->release_pkt)
+			mtcp->iom->release_pkt(mtcp->ctx, ifidx, pkt_data, len);
+#ifdef NETSTAT
+		mtcp->nstat.rx_errors[ifidx]++;
+#endif
+		return ERROR;
+	}
+	r = &v->res[index];
 	memset(&pctx, 0, sizeof(pctx));              /* FillInPacketEthContext, eth_in.c:12-25 */
 	pctx.p.cur_ts = cur_ts;
 	pctx.p.in_ifidx = ifidx;

@@ -222,7 +222,9 @@ static void slot_free(struct slot *s)
 	if (s->d_res) hipFree(s->d_res);
 	if (s->d_fh) hipFree(s->d_fh);
 	if (s->d_ti) hipFree(s->d_ti);
+	if (s->d_match) hipFree(s->d_match);
 	s->d_frames = NULL; s->d_off = NULL; s->d_len = NULL; s->d_res = NULL; s->d_fh = NULL; s->d_ti = NULL;
+	s->d_match = NULL;
 	s->cap_frames = 0; s->cap_n = 0;
 }
 
@@ -248,9 +250,11 @@ void mosrx_close(mosrx_ctx *c)
 		if (c->slot[i].h_cnt) hipHostFree(c->slot[i].h_cnt);
 		slot_free(&c->slot[i]);
 	}
+	mosrx__bpf_jit_free(c);   /* (joins the compile thread; launches drained above) */
 	if (c->d_tables) hipFree(c->d_tables);
-	if (c->d_bpf) hipFree(c->d_bpf);
-	mosrx__bpf_jit_free(c);
+	for (i = 0; i < MOSRX_BPF_POOL; i++)
+		if (c->d_bpf_pool[i])
+			hipFree(c->d_bpf_pool[i]);
 	for (i = 0; i < (int)c->nxs; i++) {
 		hipStreamSynchronize(c->xs[i]);
 		hipStreamDestroy(c->xs[i]);
@@ -402,6 +406,19 @@ int mosrx_classify_dev_ex(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_ou
 	              stream ? (hipStream_t)stream : c->stream);
 }
 
+int mosrx_classify_dev_compact(mosrx_ctx *c, const mosrx_batch *b, mosrx_result8 *d_out8, void *stream)
+{
+	int rc;
+	if (!c || (rc = mosrx__check_batch(b, 1)))
+		return c ? rc : -EINVAL;
+	if (b->n == 0)
+		return 0;
+	if (!d_out8 || ((uintptr_t)d_out8 & 7))
+		return -EINVAL;
+	return launch_flags(c, b, b->frames, b->off, b->len, (mosrx_result *)d_out8, NULL, NULL, NULL,
+	                    c->kflags | MOSRX_KF_COMPACT, stream ? (hipStream_t)stream : c->stream);
+}
+
 int mosrx_classify_dev_fh(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *d_out, uint32_t *d_fhash,
                           void *stream)
 {
@@ -422,6 +439,7 @@ static int cls_bpf_launch(mosrx_ctx *c, const mosrx_batch *db, mosrx_result *out
 	mosrx_kparams kp;
 	int rc;
 	const int kind = tile_for(c, db);
+	mosrx__bpf_poll(c);   /* the set's compiled kernels, once its compile is in */
 	if (!mosrx_bpf_fused(c) || (kind != MOSRX_KIND_SMALL && kind != MOSRX_KIND_S13)) {
 		if ((rc = launch(c, db, db->frames, db->off, db->len, out, cnt, NULL, NULL, s)))
 			return rc;
@@ -522,7 +540,8 @@ int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uin
 		    hipMalloc((void **)&s->d_len, (size_t)nn * 2) != hipSuccess ||
 		    hipMalloc((void **)&s->d_res, (size_t)nn * sizeof(mosrx_result)) != hipSuccess ||
 		    hipMalloc((void **)&s->d_fh, (size_t)nn * 4) != hipSuccess ||
-		    hipMalloc((void **)&s->d_ti, (size_t)nn * sizeof(mosrx_tcpinfo)) != hipSuccess) {
+		    hipMalloc((void **)&s->d_ti, (size_t)nn * sizeof(mosrx_tcpinfo)) != hipSuccess ||
+		    hipMalloc((void **)&s->d_match, (size_t)nn * 4) != hipSuccess) {
 			slot_free(s);
 			return -ENOMEM;
 		}
@@ -770,9 +789,12 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
 	return mosrx_classify_host_group_submit_ex(c, slot, b, nb, h_out, h_tcpinfo, NULL);
 }
 
-int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
-                                        mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo,
-                                        uint32_t *const *h_fhash)
+/* One launch over a group of host batches: records, and the side arrays asked
+ * for (pkt_info, flow hashes, and with h_match the installed BPF set's masks:
+ * the fused classify + BPF queue kernel, or the classify queue + the set's
+ * kernel per batch while the set has no compiled form). */
+static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb, mosrx_result *const *h_out,
+                        mosrx_tcpinfo *const *h_tcpinfo, uint32_t *const *h_fhash, uint32_t *const *h_match)
 {
 	struct region r[3 * MOSRX_MAX_GROUP];
 	uint32_t i, nr = 0, tiles = 0, maxl = 0, ntot = 0, tile;
@@ -780,7 +802,9 @@ int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batc
 	mosrx_qparams qp;
 	struct slot *s;
 	int rc, unknown = 0, kind, tpb_ok = 1;
-	if (!c || slot < 0 || slot >= NSLOT || !b || !h_out || nb == 0 || nb > MOSRX_MAX_GROUP)
+	int fused = 0;
+	if (!c || slot < 0 || slot >= NSLOT || !b || !h_out || nb == 0 || nb > MOSRX_MAX_GROUP ||
+	    (h_match && h_tcpinfo))
 		return -EINVAL;
 	s = &c->slot[slot];
 	if (s->busy)
@@ -788,7 +812,8 @@ int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batc
 	for (i = 0; i < nb; i++) {
 		if ((rc = mosrx__check_batch(&b[i], 0)))
 			return rc;
-		if (b[i].n && (!h_out[i] || (h_tcpinfo && !h_tcpinfo[i]) || (h_fhash && !h_fhash[i])))
+		if (b[i].n && (!h_out[i] || (h_tcpinfo && !h_tcpinfo[i]) || (h_fhash && !h_fhash[i]) ||
+		               (h_match && !h_match[i])))
 			return -EINVAL;
 		if (!b[i].max_len)
 			unknown = 1;
@@ -816,12 +841,19 @@ int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batc
 		return rc;
 	kind = kind_of(c, unknown ? 0 : maxl, dev_bytes, ntot);   /* one shape for the whole group */
 	tile = MOSRX_KIND_FRAMES(kind);
+	if (h_match) {
+		mosrx__bpf_poll(c);   /* the set's compiled kernels, once its compile is in */
+		fused = c->bpf_fu[FU_QS] && c->bpf_fu[FU_QM] && (kind == MOSRX_KIND_SMALL || kind == MOSRX_KIND_S13);
+	}
 	for (i = 0, nr = 0; i < nb; i++) {
 		mosrx_qdesc *d = &s->h_qdesc[i];
 		memset(d, 0, sizeof(*d));
 		d->tile_base = tiles;
 		d->out = s->d_res + pre;
-		d->tinfo = h_tcpinfo ? s->d_ti + pre : NULL;
+		if (fused)
+			d->bmatch = s->d_match + pre;
+		else
+			d->tinfo = h_tcpinfo ? s->d_ti + pre : NULL;
 		d->fhash = h_fhash ? s->d_fh + pre : NULL;
 		if (b[i].n) {
 			d->frames = r[nr].dev;
@@ -847,8 +879,18 @@ int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batc
 	qp.tinfo = h_tcpinfo ? 1u : 0u;
 	if (c->timing)
 		HIPCHK(hipEventRecord(s->kev0, s->stream));
-	if ((rc = mosrx_launch_queue(&qp, tiles, kind, mosrx__tail_variant(c, dev_bytes, ntot), s->stream)))
-		return rc;
+	if (fused) {
+		if ((rc = mosrx__bpf_fused_queue_launch(c, &qp, tiles, kind == MOSRX_KIND_SMALL,
+		                                        mosrx__tail_variant(c, dev_bytes, ntot), s->stream)))
+			return rc;
+	} else {
+		if ((rc = mosrx_launch_queue(&qp, tiles, kind, mosrx__tail_variant(c, dev_bytes, ntot), s->stream)))
+			return rc;
+		for (i = 0, pre = 0; h_match && i < nb; pre += b[i].n, i++)   /* the set per batch, same stream */
+			if ((rc = mosrx__bpf_launch_dev(c, s->h_qdesc[i].frames, b[i].frames_bytes, s->h_qdesc[i].off,
+			                                s->h_qdesc[i].len, b[i].n, s->d_match + pre, s->stream)))
+				return rc;
+	}
 	if (c->timing)
 		HIPCHK(hipEventRecord(s->kev1, s->stream));
 	s->timed = c->timing;
@@ -858,7 +900,8 @@ int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batc
 		uint64_t n = b[i].n;
 		while (j < nb && h_out[j] == h_out[j - 1] + b[j - 1].n &&
 		       (!h_tcpinfo || h_tcpinfo[j] == h_tcpinfo[j - 1] + b[j - 1].n) &&
-		       (!h_fhash || h_fhash[j] == h_fhash[j - 1] + b[j - 1].n))
+		       (!h_fhash || h_fhash[j] == h_fhash[j - 1] + b[j - 1].n) &&
+		       (!h_match || h_match[j] == h_match[j - 1] + b[j - 1].n))
 			n += b[j++].n;
 		if (n) {
 			HIPCHK(hipMemcpyAsync(h_out[i], s->d_res + pre, (size_t)n * sizeof(mosrx_result),
@@ -868,6 +911,9 @@ int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batc
 				                      hipMemcpyDeviceToHost, s->stream));
 			if (h_fhash)
 				HIPCHK(hipMemcpyAsync(h_fhash[i], s->d_fh + pre, (size_t)n * 4, hipMemcpyDeviceToHost, s->stream));
+			if (h_match)
+				HIPCHK(hipMemcpyAsync(h_match[i], s->d_match + pre, (size_t)n * 4, hipMemcpyDeviceToHost,
+				                      s->stream));
 		}
 		pre += n;
 		i = j;
@@ -876,6 +922,22 @@ int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batc
 	HIPCHK(hipEventRecord(s->done, s->stream));
 	s->busy = 1;
 	return 0;
+}
+
+int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                        mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo,
+                                        uint32_t *const *h_fhash)
+{
+	return group_submit(c, slot, b, nb, h_out, h_tcpinfo, h_fhash, NULL);
+}
+
+int mosrx_classify_host_group_submit_bpf(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                         mosrx_result *const *h_out, uint32_t *const *h_fhash,
+                                         uint32_t *const *h_match)
+{
+	if (!h_match)
+		return -EINVAL;
+	return group_submit(c, slot, b, nb, h_out, NULL, h_fhash, h_match);
 }
 
 int mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out,
@@ -937,57 +999,139 @@ int mosrx_dev_free(mosrx_ctx *c, void *dptr)
 	return 0;
 }
 
-/* ---- pinned host ranges (mosrx_source.h) ---------------------------------- */
+/* ---- pinned host ranges (mosrx_source.h) ----------------------------------
+ * Every pinned allocation the library knows (its own, the sources', the
+ * caller's registered ones), sorted by address: a submit looks up each of its
+ * regions (3 per batch) by binary search under a read lock, so concurrent rx
+ * threads do not serialise on it. */
 #define MAX_RANGES 4096
-static struct { uintptr_t lo, hi; uint64_t id; } g_ranges[MAX_RANGES];
+static struct range { uintptr_t lo, hi; uint64_t id; int reg; } g_ranges[MAX_RANGES];
 static uint32_t g_nranges;
 static uint64_t g_range_seq;
-static pthread_mutex_t g_range_lock = PTHREAD_MUTEX_INITIALIZER;
+static uint64_t g_range_maxlen;   /* longest range ever added: no range starting further below can hold a */
+static pthread_rwlock_t g_range_lock = PTHREAD_RWLOCK_INITIALIZER;
+
+/* first range whose lo > a */
+static uint32_t range_upper(uintptr_t a)
+{
+	uint32_t lo = 0, hi = g_nranges;
+	while (lo < hi) {
+		const uint32_t mid = (lo + hi) / 2;
+		if (g_ranges[mid].lo <= a)
+			lo = mid + 1;
+		else
+			hi = mid;
+	}
+	return lo;
+}
+
+static int range_add(const void *p, uint64_t len, int reg)
+{
+	int rc = -ENOSPC;
+	pthread_rwlock_wrlock(&g_range_lock);
+	if (p && len && g_nranges < MAX_RANGES) {
+		const uint32_t at = range_upper((uintptr_t)p);
+		memmove(&g_ranges[at + 1], &g_ranges[at], (g_nranges - at) * sizeof(g_ranges[0]));
+		g_ranges[at].lo = (uintptr_t)p;
+		g_ranges[at].hi = (uintptr_t)p + len;
+		g_ranges[at].id = ++g_range_seq;
+		g_ranges[at].reg = reg;
+		g_nranges++;
+		if (len > g_range_maxlen)
+			g_range_maxlen = len;
+		rc = 0;
+	}
+	pthread_rwlock_unlock(&g_range_lock);
+	return rc;
+}
+
+/* Remove the range starting at p; its `reg` flag, or -1 if none. */
+static int range_del(const void *p)
+{
+	int reg = -1;
+	uint32_t at;
+	pthread_rwlock_wrlock(&g_range_lock);
+	at = range_upper((uintptr_t)p);
+	if (at > 0 && g_ranges[at - 1].lo == (uintptr_t)p) {
+		reg = g_ranges[at - 1].reg;
+		memmove(&g_ranges[at - 1], &g_ranges[at], (g_nranges - at) * sizeof(g_ranges[0]));
+		g_nranges--;
+	}
+	pthread_rwlock_unlock(&g_range_lock);
+	return reg;
+}
 
 void mosrx__host_range_add(const void *p, uint64_t len)
 {
-	pthread_mutex_lock(&g_range_lock);
-	if (p && len && g_nranges < MAX_RANGES) {
-		g_ranges[g_nranges].lo = (uintptr_t)p;
-		g_ranges[g_nranges].hi = (uintptr_t)p + len;
-		g_ranges[g_nranges].id = ++g_range_seq;
-		g_nranges++;
-	}
-	pthread_mutex_unlock(&g_range_lock);
+	range_add(p, len, 0);
 }
 
 void mosrx__host_range_del(const void *p)
 {
-	uint32_t i;
-	pthread_mutex_lock(&g_range_lock);
-	for (i = 0; i < g_nranges; i++)
-		if (g_ranges[i].lo == (uintptr_t)p) {
-			g_ranges[i] = g_ranges[--g_nranges];
-			break;
-		}
-	pthread_mutex_unlock(&g_range_lock);
+	range_del(p);
 }
 
+/* The id of the known range holding [p, p + len), 0 if none: the ranges
+ * starting at or below p, nearest first (usually the first one holds it; a
+ * registered sub-range of another allocation can sit in between), back to
+ * where no range is long enough to reach p. */
 uint64_t mosrx__host_range_of(const void *p, uint64_t len)
 {
 	const uintptr_t a = (uintptr_t)p, b = a + len;
 	uint64_t id = 0;
-	uint32_t i;
-	pthread_mutex_lock(&g_range_lock);
-	for (i = 0; i < g_nranges; i++)
-		if (a >= g_ranges[i].lo && b <= g_ranges[i].hi && b >= a) {
-			id = g_ranges[i].id;
+	uint32_t k;
+	if (b < a)
+		return 0;
+	pthread_rwlock_rdlock(&g_range_lock);
+	for (k = range_upper(a); k-- > 0 && a - g_ranges[k].lo < g_range_maxlen;)
+		if (b <= g_ranges[k].hi) {
+			id = g_ranges[k].id;
 			break;
 		}
-	pthread_mutex_unlock(&g_range_lock);
+	pthread_rwlock_unlock(&g_range_lock);
 	return id;
 }
 
+int mosrx_host_register(mosrx_ctx *c, void *hptr, size_t bytes, int flags)
+{
+	int rc;
+	if (!c || !hptr || !bytes || (flags & ~MOSRX_HOST_PINNED))
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	if (!(flags & MOSRX_HOST_PINNED) && hipHostRegister(hptr, bytes, hipHostRegisterDefault) != hipSuccess)
+		return -ENOMEM;
+	if ((rc = range_add(hptr, bytes, !(flags & MOSRX_HOST_PINNED)))) {
+		if (!(flags & MOSRX_HOST_PINNED))
+			hipHostUnregister(hptr);
+		return rc;
+	}
+	return 0;
+}
+
+int mosrx_host_unregister(mosrx_ctx *c, void *hptr)
+{
+	int reg;
+	if (!c || !hptr)
+		return -EINVAL;
+	if ((reg = range_del(hptr)) < 0)
+		return -ENOENT;
+	if (reg) {
+		HIPCHK(hipSetDevice(c->device));
+		HIPCHK(hipHostUnregister(hptr));
+	}
+	return 0;
+}
+
+/* Pinned host memory, NUMA-local: hipHostMallocNumaUser places the pages by
+ * the calling thread's memory policy (mOS binds each mTCP thread to its core
+ * and that core's node before init_handle, core/src/cpu.c:56-87), i.e. on the
+ * node of the thread that stages and consumes the frames. */
 int mosrx_host_alloc(mosrx_ctx *c, size_t bytes, void **hptr)
 {
 	if (!c || !hptr)
 		return -EINVAL;
-	if (hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+	if (hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault | hipHostMallocNumaUser) != hipSuccess &&
+	    hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
 		return -ENOMEM;
 	mosrx__host_range_add(*hptr, bytes ? bytes : 1);
 	return 0;
@@ -1333,28 +1477,35 @@ int mosrx_device_sync(mosrx_ctx *c)
 /* ---- batch queue (one launch over many resident batches) ---- */
 struct mosrx_queue {
 	mosrx_qdesc *d_desc;
+	mosrx_qdesc *h_desc;   /* host copy: the per-batch BPF launches of a queue with masks */
 	uint32_t nb;
 	uint32_t total_tiles;
 	uint32_t tpb;   /* tiles per batch if uniform, else 0 */
 	int tile;
 	uint64_t bytes, n;   /* frame bytes and frames of all batches (tail policy) */
+	int compact;         /* 8-byte records */
+	int match;           /* the descriptors' bmatch: the installed BPF set's masks */
+	uint32_t **d_match;  /* per batch (the non-fused form) */
 };
 
-int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
-                       mosrx_queue **q)
+int mosrx_queue_create_ex(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, void *const *d_out,
+                          uint32_t *const *d_fhash, uint32_t *const *d_match, int flags, mosrx_queue **q)
 {
 	mosrx_qdesc *h;
 	mosrx_queue *qq;
 	uint32_t i, tiles = 0, maxl = 0, tile;
 	uint64_t bytes = 0, frames = 0;
+	const int compact = (flags & MOSRX_QUEUE_COMPACT) != 0;
 	int rc, unknown = 0, kind;
-	if (!c || !b || !d_out || !q || nb == 0)
+	if (!c || !b || !d_out || !q || nb == 0 || (flags & ~MOSRX_QUEUE_COMPACT) || (compact && (d_fhash || d_match)))
 		return -EINVAL;
 	*q = NULL;
 	for (i = 0; i < nb; i++) {
 		if ((rc = mosrx__check_batch(&b[i], 1)))
 			return rc;
-		if (b[i].n && (!d_out[i] || ((uintptr_t)d_out[i] & 15)))
+		if (b[i].n && (!d_out[i] || ((uintptr_t)d_out[i] & (compact ? 7 : 15)) ||
+		               (d_fhash && (!d_fhash[i] || ((uintptr_t)d_fhash[i] & 3))) ||
+		               (d_match && (!d_match[i] || ((uintptr_t)d_match[i] & 3)))))
 			return -EINVAL;
 		if (!b[i].max_len)
 			unknown = 1;
@@ -1367,8 +1518,10 @@ int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_re
 	tile = MOSRX_KIND_FRAMES(kind);
 	h = calloc(nb, sizeof(*h));
 	qq = calloc(1, sizeof(*qq));
-	if (!h || !qq) {
+	if (!h || !qq || (d_match && !(qq->d_match = calloc(nb, sizeof(*qq->d_match))))) {
 		free(h);
+		if (qq)
+			free(qq->d_match);
 		free(qq);
 		return -ENOMEM;
 	}
@@ -1376,7 +1529,12 @@ int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_re
 		h[i].frames = b[i].frames;
 		h[i].off = b[i].off;
 		h[i].len = b[i].len;
-		h[i].out = d_out[i];
+		h[i].out = (mosrx_result *)d_out[i];
+		h[i].fhash = d_fhash ? d_fhash[i] : NULL;
+		if (d_match) {
+			h[i].bmatch = d_match[i];
+			qq->d_match[i] = d_match[i];
+		}
 		h[i].frames_bytes = (uint32_t)b[i].frames_bytes;
 		h[i].n = b[i].n;
 		h[i].tile_base = tiles;
@@ -1388,10 +1546,11 @@ int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_re
 		if (qq->d_desc)
 			hipFree(qq->d_desc);
 		free(h);
+		free(qq->d_match);
 		free(qq);
 		return -ENOMEM;
 	}
-	free(h);
+	qq->h_desc = h;
 	qq->nb = nb;
 	qq->total_tiles = tiles;
 	qq->tpb = tiles % nb == 0 ? tiles / nb : 0u;
@@ -1399,17 +1558,27 @@ int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_re
 		if ((b[i].n + (uint32_t)tile - 1) / (uint32_t)tile != qq->tpb)
 			qq->tpb = 0;
 	qq->tile = kind;
-	for (i = 0; i < nb; i++) {
-		qq->bytes += b[i].frames_bytes;
-		qq->n += b[i].n;
-	}
+	qq->compact = compact;
+	qq->match = d_match != NULL;
+	qq->bytes = bytes;
+	qq->n = frames;
 	*q = qq;
 	return 0;
+}
+
+int mosrx_queue_create(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
+                       mosrx_queue **q)
+{
+	return mosrx_queue_create_ex(c, b, nb, (void *const *)d_out, NULL, NULL, 0, q);
 }
 
 int mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream)
 {
 	mosrx_qparams qp;
+	const hipStream_t s = stream ? (hipStream_t)stream : c ? c->stream : NULL;
+	const int variant = c ? mosrx__tail_variant(c, q ? q->bytes : 0, q ? q->n : 0) : 0;
+	uint32_t i;
+	int rc;
 	if (!c || !q)
 		return -EINVAL;
 	qp.desc = q->d_desc;
@@ -1418,9 +1587,19 @@ int mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream)
 	qp.nb = q->nb;
 	qp.flags = c->kflags;
 	qp.tpb = q->tpb;
-	qp.tinfo = 0;
-	return mosrx_launch_queue(&qp, q->total_tiles, q->tile, mosrx__tail_variant(c, q->bytes, q->n),
-	                          stream ? stream : (void *)c->stream);
+	qp.tinfo = q->compact ? 2u : 0u;
+	if (!q->match)
+		return mosrx_launch_queue(&qp, q->total_tiles, q->tile, variant, s);
+	mosrx__bpf_poll(c);
+	if (c->bpf_fu[FU_QS] && c->bpf_fu[FU_QM])
+		return mosrx__bpf_fused_queue_launch(c, &qp, q->total_tiles, q->tile == MOSRX_KIND_SMALL, variant, s);
+	if ((rc = mosrx_launch_queue(&qp, q->total_tiles, q->tile, variant, s)))
+		return rc;
+	for (i = 0; i < q->nb; i++)
+		if ((rc = mosrx__bpf_launch_dev(c, q->h_desc[i].frames, q->h_desc[i].frames_bytes, q->h_desc[i].off,
+		                                q->h_desc[i].len, q->h_desc[i].n, q->d_match[i], s)))
+			return rc;
+	return 0;
 }
 
 void mosrx_queue_destroy(mosrx_ctx *c, mosrx_queue *q)
@@ -1431,6 +1610,8 @@ void mosrx_queue_destroy(mosrx_ctx *c, mosrx_queue *q)
 		hipSetDevice(c->device);
 	if (q->d_desc)
 		hipFree(q->d_desc);
+	free(q->h_desc);
+	free(q->d_match);
 	free(q);
 }
 

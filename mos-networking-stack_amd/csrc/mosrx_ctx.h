@@ -13,6 +13,20 @@
 #define HIPCHK(x) do { if ((x) != hipSuccess) return -EIO; } while (0)
 
 #define MOSRX_BPF_JIT_CACHE 16   /* compiled program sets kept per context */
+#define MOSRX_BPF_POOL 8         /* device buffers the interpreter's instructions rotate over */
+
+/* The fused classify + BPF kernels of a compiled set (bpf_jit.c k_fused_main):
+ * one batch as the stream tile (non-temporal / cached tails) or the SMALL tile,
+ * and the same three over a batch queue. */
+#define MOSRX_BPF_NFUSED 6
+enum { FU_S = 0, FU_SR = 1, FU_M = 2, FU_QS = 3, FU_QSR = 4, FU_QM = 5 };
+struct mosrx_jit_entry {
+	uint64_t key;                          /* set_hash of the set */
+	hipModule_t mod, fmod;
+	hipFunction_t fn;                      /* the set's own kernel; NULL: the compile failed */
+	hipFunction_t fu[MOSRX_BPF_NFUSED];    /* fused kernels; NULL: none (two launches) */
+};
+struct mosrx_bpf_worker;                   /* the context's compile thread (bpf_jit.c) */
 
 /* pipeline slots for the end-to-end path (double-buffered H2D | kernel | D2H) */
 #define NSLOT MOSRX_NSLOT
@@ -24,6 +38,7 @@ struct slot {
 	mosrx_result *d_res;
 	uint32_t *d_fh;
 	mosrx_tcpinfo *d_ti;
+	uint32_t *d_match;         /* BPF match masks (the group submit with a set installed) */
 	uint32_t *d_cnt;
 	uint64_t cap_frames;
 	uint32_t cap_n;
@@ -47,15 +62,21 @@ struct mosrx_ctx {
 	uint32_t h_cnt[MOSRX_R_COUNT];   /* counters of the last waited batch */
 	hipEvent_t ev0, ev1;
 	int variant;                     /* kernel cache-policy variant (mosrx_set_variant) */
-	mosrx_bpf_insn *d_bpf;           /* installed BPF programs (MOSRX_BPF_MAX_INSNS), NULL until set */
+	mosrx_bpf_insn *d_bpf;           /* installed BPF programs (MOSRX_BPF_MAX_INSNS), NULL until set:
+	                                  * one of the pool's buffers */
+	mosrx_bpf_insn *d_bpf_pool[MOSRX_BPF_POOL];
+	int bpf_pool_used[MOSRX_BPF_POOL];   /* a launch may have read it since it was written */
+	uint32_t bpf_pool_next;
 	mosrx_bparams bpf;               /* program table of the installed set */
 	hipFunction_t bpf_fn;            /* compiled form of the installed set (bpf_jit.c), NULL: interpreter */
 	int bpf_engine_req;              /* MOSRX_BPF_ENGINE_* for the next mosrx_bpf_set */
 	char bpf_jit_log[512];           /* hipRTC log of the last failed compile */
-	hipFunction_t bpf_fs, bpf_fm;    /* fused classify + BPF kernels (S13 / SMALL tiles), NULL: none */
-	hipFunction_t bpf_fr;            /* the S13 one with cached tail loads (batches of small frames) */
-	struct { uint64_t key; hipModule_t mod, fmod; hipFunction_t fn, fs, fm, fr; } jit[MOSRX_BPF_JIT_CACHE];
+	hipFunction_t bpf_fu[MOSRX_BPF_NFUSED];   /* fused classify + BPF kernels, NULL: none */
+	struct mosrx_jit_entry jit[MOSRX_BPF_JIT_CACHE];
 	uint32_t njit;
+	uint64_t bpf_key;                /* set_hash of the installed set */
+	int bpf_pending;                 /* its compile is outstanding (the interpreter runs it meanwhile) */
+	struct mosrx_bpf_worker *bw;
 	hipStream_t xs[MOSRX_MAX_STREAMS];   /* timing streams (mosrx_time_op), created on first use */
 	hipEvent_t xdone[MOSRX_MAX_STREAMS];
 	uint32_t nxs;
@@ -64,7 +85,15 @@ struct mosrx_ctx {
 };
 
 int mosrx__check_batch(const mosrx_batch *b, int dev);
-int mosrx__bpf_jit_build(mosrx_ctx *c, const mosrx_bpf_insn *insns);
+int mosrx__bpf_jit_request(mosrx_ctx *c, const mosrx_bpf_insn *insns);
+int mosrx__bpf_jit_wait(mosrx_ctx *c);
+void mosrx__bpf_poll(mosrx_ctx *c);
+int mosrx__bpf_fused_queue_launch(mosrx_ctx *c, const mosrx_qparams *qp, uint32_t total_tiles, int small,
+                                  int variant, hipStream_t s);
+/* The installed set's standalone kernel (compiled, else the interpreter) over a
+ * device-resident batch, match masks into match[n]. */
+int mosrx__bpf_launch_dev(mosrx_ctx *c, const uint8_t *frames, uint64_t frames_bytes, const uint32_t *off,
+                          const uint16_t *len, uint32_t n, uint32_t *match, hipStream_t s);
 int mosrx__bpf_jit_launch(mosrx_ctx *c, const mosrx_bparams *bp, hipStream_t s);
 int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out);
 void mosrx__bpf_jit_free(mosrx_ctx *c);

@@ -24,6 +24,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t *base
 // by the host after the launch.  MOSRX_OUT_AUX (A/B builds) picks the cache
 // policy bits of a buffer store instead (gfx950: 1 sc0, 2 nt, 16 sc1).
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // out_store(base, i, v): element i of a per-frame output array (`base` is
 // uniform: the kernel's argument).
 #ifdef MOSRX_OUT_AUX
@@ -35,6 +36,10 @@ __device__ __forceinline__ void out_store(u32x4 *base, uint32_t i, u32x4 v)
 {
 	__builtin_amdgcn_raw_buffer_store_b128(v, out_rsrc(base), 16u * i, 0, MOSRX_OUT_AUX);
 }
+__device__ __forceinline__ void out_store(u32x2 *base, uint32_t i, u32x2 v)
+{
+	__builtin_amdgcn_raw_buffer_store_b64(v, out_rsrc(base), 8u * i, 0, MOSRX_OUT_AUX);
+}
 __device__ __forceinline__ void out_store(uint32_t *base, uint32_t i, u32x3 v)   // 12-byte elements
 {
 	__builtin_amdgcn_raw_buffer_store_b96(v, out_rsrc(base), 12u * i, 0, MOSRX_OUT_AUX);
@@ -45,6 +50,10 @@ __device__ __forceinline__ void out_store(uint32_t *base, uint32_t i, uint32_t v
 }
 #else
 __device__ __forceinline__ void out_store(u32x4 *base, uint32_t i, u32x4 v)
+{
+	__builtin_nontemporal_store(v, base + i);
+}
+__device__ __forceinline__ void out_store(u32x2 *base, uint32_t i, u32x2 v)
 {
 	__builtin_nontemporal_store(v, base + i);
 }

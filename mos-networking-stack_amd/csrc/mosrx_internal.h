@@ -30,6 +30,7 @@ enum {
 	MOSRX_KF_SKIP_TCP  = 1u << 2,  /* skip TCPCalcChecksum (BASELINE config #2 mode) */
 	MOSRX_KF_TX_IP     = 1u << 3,  /* TX fill: write iph->check (no records) */
 	MOSRX_KF_TX_TCP    = 1u << 4,  /* TX fill: write tcph->check (no records) */
+	MOSRX_KF_COMPACT   = 1u << 5,  /* host side only: 8-byte records (mosrx_result8) */
 };
 
 typedef struct mosrx_kparams {
@@ -84,8 +85,11 @@ typedef struct mosrx_qdesc {
 	const uint8_t  *frames;
 	const uint32_t *off;
 	const uint16_t *len;
-	mosrx_result   *out;
-	mosrx_tcpinfo  *tinfo;       /* NULL unless the queue was launched with pkt_info fields */
+	mosrx_result   *out;         /* 16-byte records, or 8-byte ones (mosrx_result8) for a compact queue */
+	union {
+		mosrx_tcpinfo *tinfo;    /* the classify kernels: NULL unless launched with pkt_info fields */
+		uint32_t      *bmatch;   /* the fused classify + BPF kernels (they write no pkt_info): match masks */
+	};
 	uint32_t       *fhash;       /* flow-table hashes, or NULL */
 	uint32_t        frames_bytes;
 	uint32_t        n;
@@ -100,7 +104,8 @@ typedef struct mosrx_qparams {
 	uint32_t           nb;
 	uint32_t           flags;
 	uint32_t           tpb;      /* tiles per batch when every batch has the same tile count, else 0 */
-	uint32_t           tinfo;    /* 1: the descriptors carry pkt_info TCP field buffers (VAR_TI) */
+	uint32_t           tinfo;    /* 1: the descriptors carry pkt_info TCP field buffers (VAR_TI);
+	                              * 2: the records are the 8-byte compact form (VAR_C8) */
 } mosrx_qparams;
 
 /* Batched BPF launch: the program table rides in the kernel arguments, the

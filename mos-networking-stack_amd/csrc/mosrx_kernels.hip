@@ -81,6 +81,10 @@ __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t c, ui
 // Variant bit 6: also write pkt_info's TCP fields (mosrx_tcpinfo side array, kp.tinfo).
 #define VAR_TI 64
 #define IS_TI(v) (((v) & VAR_TI) != 0)
+// Variant bit 7: 8-byte records (mosrx_result8) into kp.out instead of 16-byte ones.
+#define VAR_C8 128
+#define IS_C8(v) (((v) & VAR_C8) != 0)
+static_assert(sizeof(mosrx_result8) == 8, "compact record size");
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 __device__ __forceinline__ uint32_t be16hi(uint32_t w) { return ((w >> 8) & 0xFF00u) | (w >> 24); } // bytes 2,3
@@ -542,9 +546,18 @@ __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffe
 // Records and side arrays are written once and read by the host after the
 // launch: non-temporal stores (rings 3-4 % faster than default-policy stores:
 // 1500 B 122 -> 119 us, IMIX 141 -> 135 us, 64 B 127 -> 123 us).
+template <int VAR>
 __device__ __forceinline__ void store_record(const mosrx_kparams &kp, uint32_t p, u32x4 rec, uint32_t *s_cnt)
 {
-	out_store(reinterpret_cast<u32x4 *>(kp.out), p, rec);
+	if constexpr (IS_C8(VAR)) {
+		// mosrx_result8: rss | reason, queue (rec.w bytes 0-1), verdict (rec.z byte 3), tcp_flags (rec.w byte 2)
+		u32x2 c;
+		c.x = rec.x;
+		c.y = (rec.w & 0xFFFFu) | ((rec.z >> 24) << 16) | (((rec.w >> 16) & 0xFFu) << 24);
+		out_store(reinterpret_cast<u32x2 *>(kp.out), p, c);
+	} else {
+		out_store(reinterpret_cast<u32x4 *>(kp.out), p, rec);
+	}
 	if (kp.counters) {
 		const uint32_t reason = rec.w & 0xFFu;
 		uint64_t m = __ballot(1);
@@ -670,10 +683,10 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	} else if constexpr ((DBG & 4) != 0) {   // probe: records kept live, (almost) never stored
 		const u32x4 r = hdr_finish(h, tail, kp.flags);
 		if (active && (r.x ^ r.y ^ r.z ^ r.w) == 0x9E3779B9u)
-			store_record(kp, p, r, s_cnt);
+			store_record<VAR>(kp, p, r, s_cnt);
 	} else {
 		if (active)
-			store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
+			store_record<VAR>(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (active && kp.fhash)
 			out_store(kp.fhash, p, flow_hash(h));
 		if constexpr (IS_TI(VAR)) {
@@ -736,7 +749,7 @@ __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffe
 	if constexpr (IS_TX(VAR)) {
 		tx_store(kp, rs, h, tail);
 	} else if (active) {
-		store_record(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
+		store_record<VAR>(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (kp.fhash)
 			out_store(kp.fhash, p, flow_hash(h));
 		if constexpr (IS_TI(VAR))
@@ -822,6 +835,7 @@ __device__ __forceinline__ u32x4 pend_finish(const hdr_pend_t &q, uint32_t tail)
 // between the datagram end and the capture end (Ethernet padding of a long
 // capture) were summed too and come out here (rare: a wave-wide pass per such
 // frame), then the record.
+template <int VAR>
 __device__ __forceinline__ void pend_emit(const mosrx_kparams &kp, __amdgpu_buffer_rsrc_t rs, uint32_t nbytes,
                                           const hdr_pend_t &q, uint32_t lo_l, uint32_t hi_l, uint32_t tail,
                                           uint32_t p, bool active, uint32_t lane, uint32_t *s_cnt)
@@ -837,7 +851,7 @@ __device__ __forceinline__ void pend_emit(const mosrx_kparams &kp, __amdgpu_buff
 			tail -= sm;
 	}
 	if (active)
-		store_record(kp, p, pend_finish(q, tail), s_cnt);
+		store_record<VAR>(kp, p, pend_finish(q, tail), s_cnt);
 }
 
 // ---------------------------------------------------------------------------
@@ -1133,7 +1147,7 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 						tail += s_part[s][lane];
 					tail -= q.ovs;
 				}
-				pend_emit(kp, rs, nbytes, q, lo_l, hi_l, tail, p, active, lane, s_cnt);
+				pend_emit<VAR>(kp, rs, nbytes, q, lo_l, hi_l, tail, p, active, lane, s_cnt);
 			}
 			TILE_STAMP(5);
 			// only this wave counted (its LDS accesses are ordered): it adds the
@@ -1214,25 +1228,24 @@ void mosrx_classify_kernel(const uint32_t *off, const uint16_t *len, const uint8
 // Workgroup b finds its batch by one scalar division when every batch has the
 // same tile count (the usual rx ring of equal batches), else by a binary
 // search of tile_base[] (a chain of dependent scalar loads).
+// The fused classify + BPF kernels (hipRTC, bpf_jit.c) instantiate the same
+// body with VAR_BPF: their descriptors carry the match masks where the
+// classify kernels carry pkt_info (mosrx_qdesc's union).
 template <int KIND, int VAR>
-__global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))
-void mosrx_classify_queue_kernel(const mosrx_qdesc *desc, uint32_t tpb, uint32_t nb, mosrx_qparams qp)
+__device__ __forceinline__ void queue_tile(const mosrx_qdesc *desc, uint32_t tpb, uint32_t nb, const mosrx_qparams &qp)
 {
-	qp.desc = desc;   // preloaded (see mosrx_classify_kernel): the batch lookup starts at dispatch
-	qp.tpb = tpb;
-	qp.nb = nb;
 	const uint32_t b = blockIdx.x;
-	uint32_t lo = 0, hi = qp.nb;               // find k: tile_base[k] <= b < tile_base[k+1]
-	if (qp.tpb)
-		lo = hi = min(b / qp.tpb, qp.nb - 1u);
+	uint32_t lo = 0, hi = nb;                  // find k: tile_base[k] <= b < tile_base[k+1]
+	if (tpb)
+		lo = hi = min(b / tpb, nb - 1u);
 	while (hi - lo > 1) {
 		const uint32_t mid = (lo + hi) >> 1;
-		if (__builtin_amdgcn_readfirstlane(qp.desc[mid].tile_base) <= b)
+		if (__builtin_amdgcn_readfirstlane(desc[mid].tile_base) <= b)
 			lo = mid;
 		else
 			hi = mid;
 	}
-	const mosrx_qdesc *d = &qp.desc[lo];
+	const mosrx_qdesc *d = &desc[lo];
 	mosrx_kparams kp;
 	kp.frames = d->frames;
 	kp.off = d->off;
@@ -1241,12 +1254,20 @@ void mosrx_classify_queue_kernel(const mosrx_qdesc *desc, uint32_t tpb, uint32_t
 	kp.tables = qp.tables;
 	kp.counters = qp.counters;
 	kp.fhash = d->fhash;
-	kp.bmatch = nullptr;
-	kp.tinfo = d->tinfo;
+	kp.bmatch = (VAR & VAR_BPF) ? d->bmatch : nullptr;
+	kp.tinfo = (VAR & VAR_BPF) ? nullptr : d->tinfo;
 	kp.frames_bytes = d->frames_bytes;
 	kp.n = d->n;
 	kp.flags = qp.flags;
 	classify_tile<KIND, VAR>(kp, b - d->tile_base);
+}
+
+template <int KIND, int VAR>
+__global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))
+void mosrx_classify_queue_kernel(const mosrx_qdesc *desc, uint32_t tpb, uint32_t nb, mosrx_qparams qp)
+{
+	// desc / tpb / nb preloaded (see mosrx_classify_kernel): the batch lookup starts at dispatch
+	queue_tile<KIND, VAR>(desc, tpb, nb, qp);
 }
 
 #ifndef __HIPCC_RTC__
@@ -1343,11 +1364,14 @@ extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles,
 	if (kind < 0 || kind >= MOSRX_KIND_COUNT)
 		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-#define QROW(k) {launch_queue_v<k, 0>, launch_queue_v<k, 2>, launch_queue_v<k, 2 | VAR_TI>}
-	static void (*const tab[MOSRX_KIND_COUNT][3])(const mosrx_qparams *, uint32_t, hipStream_t) = {
+#define QROW(k)                                                                                         \
+	{launch_queue_v<k, 0>, launch_queue_v<k, 2>, launch_queue_v<k, 2 | VAR_TI>, launch_queue_v<k, VAR_C8>, \
+	 launch_queue_v<k, 2 | VAR_C8>}
+	static void (*const tab[MOSRX_KIND_COUNT][5])(const mosrx_qparams *, uint32_t, hipStream_t) = {
 		QROW(MOSRX_KIND_SMALL), QROW(MOSRX_KIND_S13)};
 #undef QROW
-	tab[kind][qp->tinfo ? 2 : (variant >> 1) & 1](qp, total_tiles, s);
+	const int tv = (variant >> 1) & 1;
+	tab[kind][qp->tinfo == 1 ? 2 : qp->tinfo == 2 ? 3 + tv : tv](qp, total_tiles, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -1358,12 +1382,19 @@ extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int vari
 	if (kind < 0 || kind >= MOSRX_KIND_COUNT)
 		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-#define KROW(k) {launch_v<k, 0>, launch_v<k, 2>, launch_v<k, 2 | VAR_TX>, launch_v<k, 2 | VAR_TI>}
-	static void (*const tab[MOSRX_KIND_COUNT][4])(const mosrx_kparams *, hipStream_t) = {
+#define KROW(k)                                                                                    \
+	{launch_v<k, 0>, launch_v<k, 2>, launch_v<k, 2 | VAR_TX>, launch_v<k, 2 | VAR_TI>, launch_v<k, VAR_C8>, \
+	 launch_v<k, 2 | VAR_C8>}
+	static void (*const tab[MOSRX_KIND_COUNT][6])(const mosrx_kparams *, hipStream_t) = {
 		KROW(MOSRX_KIND_SMALL), KROW(MOSRX_KIND_S13)};
 #undef KROW
-	const int v = (kp->flags & (MOSRX_KF_TX_IP | MOSRX_KF_TX_TCP)) ? 2 : kp->tinfo ? 3 : (variant >> 1) & 1;
-	tab[kind][v](kp, s);
+	const int tv = (variant >> 1) & 1;
+	// MOSRX_KF_COMPACT is the host's request for 8-byte records; the kernel's flags never carry it
+	const int v = (kp->flags & (MOSRX_KF_TX_IP | MOSRX_KF_TX_TCP)) ? 2 : kp->tinfo ? 3
+	            : (kp->flags & MOSRX_KF_COMPACT) ? 4 + tv : tv;
+	mosrx_kparams k = *kp;
+	k.flags &= ~(uint32_t)MOSRX_KF_COMPACT;
+	tab[kind][v](&k, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 #endif   // __HIPCC_RTC__

@@ -36,6 +36,12 @@ MAX_LOCAL = 16
 # mosrx_tcpinfo: pkt_info's TCP fields (FillPacketContextTCPInfo, tcp.c:258-270), host order
 TCPINFO_DTYPE = np.dtype([("seq", "<u4"), ("ack_seq", "<u4"), ("window", "<u2"), ("ip_len", "<u2")])
 assert TCPINFO_DTYPE.itemsize == 12
+# mosrx_result8: the compact record (rss, reason, queue, verdict, tcp_flags)
+RESULT8_DTYPE = np.dtype([("rss", "<u4"), ("reason", "u1"), ("queue", "u1"), ("verdict", "i1"),
+                          ("tcp_flags", "u1")])
+assert RESULT8_DTYPE.itemsize == 8
+QUEUE_COMPACT = 1
+HOST_PINNED = 1
 KIND_SMALL, KIND_S13 = 0, 1
 
 
@@ -244,6 +250,16 @@ def lib():
             "mosrx_gpu_module_device_of": (I, [I, I]),
             "mosrx_gpu_module_stats_of": (I, [P, C.POINTER(ModuleStats)]),
             "mosrx_gpu_module_set_timing": (I, [P, I]),
+            "mosrx_bpf_set_async": (I, [P, C.POINTER(BpfProg), U32]),
+            "mosrx_bpf_wait": (I, [P]),
+            "mosrx_bpf_pending": (I, [P]),
+            "mosrx_classify_dev_compact": (I, [P, C.POINTER(Batch), P, P]),
+            "mosrx_queue_create_ex": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P), C.POINTER(P), I,
+                                          C.POINTER(P)]),
+            "mosrx_classify_host_group_submit_bpf": (I, [P, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P),
+                                                         C.POINTER(P)]),
+            "mosrx_host_register": (I, [P, P, C.c_size_t, I]),
+            "mosrx_host_unregister": (I, [P, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -395,6 +411,7 @@ class DevBatch:
         self.d_fhash = None   # allocated on the first classify_dev(..., flow_hash=True)
         self.d_tinfo = None   # allocated on the first classify_dev(..., tcpinfo=True)
         self.d_match = None   # allocated on the first bpf_dev
+        self.d_out8 = None    # compact records, allocated on the first classify_dev_compact
         self.max_len = int(max_len if max_len is not None else (int(ln.max()) if self.n else 0))
         self.caplen_sum = int(ln.astype(np.uint64).sum())
 
@@ -419,6 +436,12 @@ class DevBatch:
             self.d_match.download(out)
         return out
 
+    def results8(self) -> np.ndarray:
+        out = np.zeros(self.n, RESULT8_DTYPE)
+        if self.n:
+            self.d_out8.download(out)
+        return out
+
     def flow_hashes(self) -> np.ndarray:
         out = np.zeros(self.n, np.uint32)
         if self.n:
@@ -432,7 +455,8 @@ class DevBatch:
         return out
 
     def free(self):
-        for b in (self.d_frames, self.d_off, self.d_len, self.d_out, self.d_fhash, self.d_match, self.d_tinfo):
+        for b in (self.d_frames, self.d_off, self.d_len, self.d_out, self.d_fhash, self.d_match, self.d_tinfo,
+                  self.d_out8):
             if b is not None:
                 b.free()
 
@@ -526,6 +550,20 @@ class Context:
         arr, _keep = _bpf_progs(progs)
         _chk(lib().mosrx_bpf_set(self.handle, arr, len(progs)), "mosrx_bpf_set")
 
+    def bpf_set_async(self, progs) -> None:
+        """mosrx_bpf_set_async: in effect at once (interpreter), compiled behind."""
+        arr, _keep = _bpf_progs(progs)
+        _chk(lib().mosrx_bpf_set_async(self.handle, arr, len(progs)), "mosrx_bpf_set_async")
+
+    def bpf_wait(self) -> None:
+        _chk(lib().mosrx_bpf_wait(self.handle), "mosrx_bpf_wait")
+
+    def bpf_pending(self) -> bool:
+        rc = lib().mosrx_bpf_pending(self.handle)
+        if rc < 0:
+            _chk(rc, "mosrx_bpf_pending")
+        return rc == 1
+
     def bpf_set_engine(self, engine: int) -> None:
         """Engine of the next bpf_set: BPF_ENGINE_JIT (hipRTC-compiled set) or BPF_ENGINE_INTERP."""
         _chk(lib().mosrx_bpf_set_engine(self.handle, engine), "mosrx_bpf_set_engine")
@@ -608,6 +646,40 @@ class Context:
             _chk(lib().mosrx_classify_dev(self.handle, C.byref(b), db.d_out.ptr, None), "mosrx_classify_dev")
         if sync:
             _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
+
+    def classify_dev_compact(self, db: DevBatch, sync: bool = True) -> None:
+        """8-byte records (mosrx_result8) into db.d_out8."""
+        if db.d_out8 is None:
+            db.d_out8 = DevBuffer(self, max(db.n * 8, 8))
+        b = db.batch()
+        _chk(lib().mosrx_classify_dev_compact(self.handle, C.byref(b), db.d_out8.ptr, None),
+             "mosrx_classify_dev_compact")
+        if sync:
+            _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
+
+    def group_submit_bpf(self, slot: int, batches: list, outs: list, fhash: list | None, match: list) -> None:
+        """mosrx_classify_host_group_submit_bpf over host batches (Batch structs);
+        outs / fhash / match: lists of host pointers (wait with group_wait)."""
+        n = len(batches)
+        bs = (Batch * n)(*batches)
+        o = (C.c_void_p * n)(*outs)
+        f = (C.c_void_p * n)(*fhash) if fhash is not None else None
+        m = (C.c_void_p * n)(*match)
+        _chk(lib().mosrx_classify_host_group_submit_bpf(self.handle, slot, bs, n, o, f, m),
+             "mosrx_classify_host_group_submit_bpf")
+
+    def group_wait(self, slot: int) -> None:
+        _chk(lib().mosrx_classify_host_wait(self.handle, slot), "mosrx_classify_host_wait")
+
+    def host_register(self, ptr: int, nbytes: int, flags: int = 0) -> None:
+        _chk(lib().mosrx_host_register(self.handle, ptr, nbytes, flags), "mosrx_host_register")
+
+    def host_unregister(self, ptr: int) -> None:
+        _chk(lib().mosrx_host_unregister(self.handle, ptr), "mosrx_host_unregister")
+
+    def queue_ex(self, dbs: list[DevBatch], flow_hash: bool = False, match: bool = False,
+                 compact: bool = False) -> "Queue":
+        return Queue(self, dbs, flow_hash=flow_hash, match=match, compact=compact)
 
     def time_dev(self, dbs: list[DevBatch], iters: int) -> float:
         bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
@@ -705,12 +777,27 @@ class Context:
 class Queue:
     """mosrx_queue: one launch classifies every batch of the queue."""
 
-    def __init__(self, ctx: Context, dbs: list[DevBatch]):
+    def __init__(self, ctx: Context, dbs: list[DevBatch], flow_hash: bool = False, match: bool = False,
+                 compact: bool = False):
         self.ctx = ctx
-        bs = (Batch * len(dbs))(*[d.batch() for d in dbs])
-        outs = (C.c_void_p * len(dbs))(*[d.d_out.ptr for d in dbs])
+        n = len(dbs)
+        for d in dbs:
+            if flow_hash and d.d_fhash is None:
+                d.d_fhash = DevBuffer(ctx, max(d.n * 4, 4))
+            if match and d.d_match is None:
+                d.d_match = DevBuffer(ctx, max(d.n * 4, 4))
+            if compact and d.d_out8 is None:
+                d.d_out8 = DevBuffer(ctx, max(d.n * 8, 8))
+        bs = (Batch * n)(*[d.batch() for d in dbs])
+        outs = (C.c_void_p * n)(*[(d.d_out8.ptr if compact else d.d_out.ptr) for d in dbs])
         h = C.c_void_p()
-        _chk(lib().mosrx_queue_create(ctx.handle, bs, len(dbs), outs, C.byref(h)), "mosrx_queue_create")
+        if not (flow_hash or match or compact):
+            _chk(lib().mosrx_queue_create(ctx.handle, bs, n, outs, C.byref(h)), "mosrx_queue_create")
+        else:
+            fh = (C.c_void_p * n)(*[d.d_fhash.ptr for d in dbs]) if flow_hash else None
+            mt = (C.c_void_p * n)(*[d.d_match.ptr for d in dbs]) if match else None
+            _chk(lib().mosrx_queue_create_ex(ctx.handle, bs, n, outs, fh, mt, QUEUE_COMPACT if compact else 0,
+                                             C.byref(h)), "mosrx_queue_create_ex")
         self.handle = h.value
 
     def run(self, sync: bool = True):

@@ -102,6 +102,12 @@ int __wrap_mosrx_bpf_set(mosrx_ctx *mc, const mosrx_bpf_prog *progs, uint32_t np
 	return 0;
 }
 
+/* The set is in effect at once (the interpreter's results = the compiled ones). */
+int __wrap_mosrx_bpf_set_async(mosrx_ctx *mc, const mosrx_bpf_prog *progs, uint32_t nprog)
+{
+	return __wrap_mosrx_bpf_set(mc, progs, nprog);
+}
+
 int __wrap_mosrx_classify_host_submit_ex(mosrx_ctx *mc, int slot, const mosrx_batch *b, mosrx_result *out,
                                          mosrx_tcpinfo *ti)
 {
@@ -144,6 +150,23 @@ int __wrap_mosrx_classify_bpf_host_submit(mosrx_ctx *mc, int slot, const mosrx_b
 	if (rc)
 		return rc;
 	return mo_bpf_eval(c->progs, c->nprog, b->frames, b->frames_bytes, b->off, b->len, b->n, match);
+}
+
+int __wrap_mosrx_classify_host_group_submit_bpf(mosrx_ctx *mc, int slot, const mosrx_batch *b, uint32_t nb,
+                                                mosrx_result *const *out, uint32_t *const *fh,
+                                                uint32_t *const *match)
+{
+	struct emul_ctx *c = (struct emul_ctx *)mc;
+	uint32_t i;
+	int rc;
+	(void)slot;
+	for (i = 0; i < nb; i++)
+		if ((rc = mo_classify_ex(&c->p, b[i].frames, b[i].frames_bytes, b[i].off, b[i].len, b[i].n, out[i],
+		                         fh ? fh[i] : NULL, NULL)) ||
+		    (rc = mo_bpf_eval(c->progs, c->nprog, b[i].frames, b[i].frames_bytes, b[i].off, b[i].len, b[i].n,
+		                      match[i])))
+			return rc;
+	return 0;
 }
 
 /* The TX rewrite (mosrx_tx_csum_host): the oracle's restatement, in place. */

@@ -40,6 +40,19 @@
  *                                MOSAPP_MONITORS=0)
  *   env MOSAPP_LOOPS=l           replay the trace l times (timing runs)
  *   env MOSAPP_QUIET=1           no callback log (timing runs)
+ *   env MOSAPP_NO_TX=1           no TX dump: what mOS sends is dropped at the source (counted as
+ *                                TX errors), so timing runs do not time pcap writes
+ *   env MOSAPP_REOPEN_RAW_AT=k   just before frame k, the raw monitor's program is replaced by
+ *                                MOSAPP_RAW2's (same length) at the same address: what a freed
+ *                                program (FreeMonListener, socket.c:33-36) reallocated for the
+ *                                next monitor's filter looks like.  (mOS's mtcp_close cannot
+ *                                close a monitor socket -- it looks the id up in smap, monitors
+ *                                live in msmap -- and the allocator need not hand the address
+ *                                back, so the harness writes the new program in place.)
+ *   env MOSAPP_FAIL_RECLASSIFY=k the k-th MOSRX_PKT_RX_RECLASSIFY request fails (a GPU error
+ *                                in the middle of a batch: the consumer drops the rest of it)
+ * The per-frame time is reported as measured and without the time spent in
+ * get_wptr (which flushes the TX buffer to the source every tx_batch frames).
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -65,6 +78,8 @@
 #include "io_module.h"
 #include "mosrx_io_module.h"
 #include "mosrx_mos_rx.h"
+#include "socket.h"
+#include "sfbpf.h"
 
 int __real_ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index, uint32_t cur_ts,
                          unsigned char *pkt_data, int len);
@@ -103,15 +118,46 @@ int __wrap_gettimeofday(struct timeval *tv, void *tz)
 	}
 	return __real_gettimeofday(tv, tz);
 }
+static unsigned long g_arp_sent;         /* ARP frames in the TX dump */
 static char g_snap[1 << 20];             /* flow table + NETSTAT after the last frame */
 static size_t g_snap_len;
 static mctx_t g_mctx;
 static _Atomic int g_go;                  /* the application's sockets are set up */
 static io_module_func g_gated;           /* gpu_module_func, receiving nothing before g_go */
 
-static uint64_t g_late_raw, g_late_mon;
+static uint64_t g_late_raw, g_late_mon, g_reopen_raw;
+static int g_raw_sock = -1;
+static int g_reopen_same_addr;           /* the rebound program took the freed one's address */
 static int raw_monitor(void);
+static int raw_monitor_filter(const char *expr);
+static void die(const char *m);
 static int stream_monitor(int with_filters);
+static int g_in_window;                  /* inside a batch's timed per-frame loop */
+static double g_tx_ns;                   /* of the timed loop, the time spent in get_wptr (TX flushes) */
+static uint64_t g_fail_reclassify, g_reclassify_calls;
+
+/* get_wptr timed inside the rx window: a full TX buffer is flushed to the
+ * source there (the pcap dump), which is the harness's sink, not mOS's work */
+static uint8_t *timed_get_wptr(struct mtcp_thread_context *ctx, int ifidx, uint16_t len)
+{
+	struct timespec a, b;
+	uint8_t *r;
+	if (!g_in_window)
+		return gpu_module_func.get_wptr(ctx, ifidx, len);
+	clock_gettime(CLOCK_MONOTONIC, &a);
+	r = gpu_module_func.get_wptr(ctx, ifidx, len);
+	clock_gettime(CLOCK_MONOTONIC, &b);
+	g_tx_ns += (b.tv_sec - a.tv_sec) * 1e9 + (b.tv_nsec - a.tv_nsec);
+	return r;
+}
+
+/* a GPU error on the k-th reclassification (MOSAPP_FAIL_RECLASSIFY) */
+static int32_t failing_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, void *argp)
+{
+	if (cmd == MOSRX_PKT_RX_RECLASSIFY && ++g_reclassify_calls == g_fail_reclassify)
+		return -1;
+	return gpu_module_func.dev_ioctl(ctx, nif, cmd, argp);
+}
 
 static int32_t gated_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 {
@@ -196,9 +242,19 @@ int __wrap_ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index, 
 		raw_monitor();
 	if (g_late_mon && k + 1 == g_late_mon)
 		stream_monitor(0);
+	if (g_reopen_raw && k + 1 == g_reopen_raw && g_raw_sock >= 0) {
+		struct sfbpf_program *fc = &mtcp->msmap[g_raw_sock].monitor_listener->raw_pkt_fcode, nf;
+		memset(&nf, 0, sizeof(nf));
+		if (SET_BPFFILTER(&nf, getenv("MOSAPP_RAW2")) < 0 || nf.bf_len != fc->bf_len)
+			die("MOSAPP_RAW2: a filter of the same length");
+		memcpy(fc->bf_insns, nf.bf_insns, nf.bf_len * sizeof(*nf.bf_insns));
+		sfbpf_freecode(&nf);
+		g_reopen_same_addr = 1;
+	}
 	if (index == 0) {
 		mosrx_rx_state st;
 		g_batch_n = mtcp->iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_STATE, &st) ? 0 : st.n;
+		g_in_window = 1;
 		clock_gettime(CLOCK_MONOTONIC, &g_t0);
 	}
 	ret = g_mode_gpu ? mosrx_mos_process_packet(mtcp, ifidx, index, cur_ts, pkt_data, len)
@@ -208,6 +264,7 @@ int __wrap_ProcessPacket(mtcp_manager_t mtcp, const int ifidx, const int index, 
 		clock_gettime(CLOCK_MONOTONIC, &t1);
 		g_rx_ns += ns_between(&g_t0, &t1);
 		g_rx_frames += g_batch_n;
+		g_in_window = 0;
 	}
 	if (g_ret && k < g_total)
 		g_ret[k] = (int8_t)ret;
@@ -240,19 +297,49 @@ static void die(const char *m)
 	exit(2);
 }
 
-static int raw_monitor(void)
+static int raw_monitor_filter(const char *expr)
 {
 	int s = mtcp_socket(g_mctx, AF_INET, MOS_SOCK_MONITOR_RAW, 0);
 	if (s < 0)
 		die("raw monitor socket");
-	if (getenv("MOSAPP_RAW")) {
-		union monitor_filter ft = {.raw_pkt_filter = getenv("MOSAPP_RAW")};
+	if (expr) {
+		union monitor_filter ft = {.raw_pkt_filter = (char *)expr};
 		if (mtcp_bind_monitor_filter(g_mctx, s, &ft))
 			die("raw filter");
 	}
 	if (mtcp_register_callback(g_mctx, s, MOS_ON_PKT_IN, MOS_NULL, on_event))
 		die("raw callback");
 	return s;
+}
+
+static int raw_monitor(void)
+{
+	return g_raw_sock = raw_monitor_filter(getenv("MOSAPP_RAW"));
+}
+
+/* ARP frames (ethertype 0x0806) in a classic pcap file: mOS's ARP requests */
+static unsigned long pcap_arp_frames(const char *path)
+{
+	FILE *f = fopen(path, "rb");
+	unsigned char h[24], rec[16], eth[14];
+	unsigned long n = 0;
+	if (!f || fread(h, 1, 24, f) != 24) {
+		if (f)
+			fclose(f);
+		return 0;
+	}
+	while (fread(rec, 1, 16, f) == 16) {
+		uint32_t incl;
+		memcpy(&incl, rec + 8, 4);
+		if (incl >= 14 && fread(eth, 1, 14, f) == 14) {
+			n += eth[12] == 0x08 && eth[13] == 0x06;
+			incl -= 14;
+		}
+		if (fseek(f, incl, SEEK_CUR))
+			break;
+	}
+	fclose(f);
+	return n;
 }
 
 /* A MOS_SOCK_MONITOR_STREAM socket (num_msp++, socket.c:77-78) with every
@@ -344,7 +431,7 @@ int main(int argc, char **argv)
 		die("source");
 	mosrx_source_mem_set_mode(src, 1);   /* copied in runs: frames stay writable for mOS (forward rewrites) */
 	snprintf(path, sizeof(path), "%s/tx.pcap", argv[4]);
-	if (mosrx_source_tx_pcap(src, path))
+	if (!getenv("MOSAPP_NO_TX") && mosrx_source_tx_pcap(src, path))
 		die("tx dump");
 	mosrx_gpu_module_cfg_default(&cfg);
 	cfg.num_ifs = 1;
@@ -366,6 +453,10 @@ int main(int argc, char **argv)
 	g_gated = gpu_module_func;
 	g_gated.recv_pkts = gated_recv_pkts;
 	g_gated.send_pkts = counted_send_pkts;
+	g_gated.get_wptr = timed_get_wptr;
+	g_fail_reclassify = getenv("MOSAPP_FAIL_RECLASSIFY") ? strtoull(getenv("MOSAPP_FAIL_RECLASSIFY"), NULL, 10) : 0;
+	if (g_fail_reclassify)
+		g_gated.dev_ioctl = failing_dev_ioctl;
 	current_iomodule_func = &g_gated;
 
 	if (mtcp_init(argv[2]))
@@ -386,6 +477,7 @@ int main(int argc, char **argv)
 	if ((getenv("MOSAPP_RAW") || getenv("MOSAPP_RAW_NOFILTER")) && !late_raw)
 		raw_monitor();
 	g_late_raw = late_raw;
+	g_reopen_raw = getenv("MOSAPP_REOPEN_RAW_AT") ? strtoull(getenv("MOSAPP_REOPEN_RAW_AT"), NULL, 10) : 0;
 	g_late_mon = getenv("MOSAPP_LATE_MON_AT") ? strtoull(getenv("MOSAPP_LATE_MON_AT"), NULL, 10) : 0;
 	if (getenv("MOSAPP_LISTEN")) {
 		struct sockaddr_in a;
@@ -417,6 +509,11 @@ int main(int argc, char **argv)
 	mtcp_destroy_context(g_mctx);
 	mosrx_source_tx_flush(src);
 	mosrx_source_tx_pcap(src, NULL);
+	snprintf(path, sizeof(path), "%s/tx.pcap", argv[4]);
+	{
+		const unsigned long arp = getenv("MOSAPP_NO_TX") ? 0 : pcap_arp_frames(path);
+		g_arp_sent = arp;
+	}
 
 	snprintf(path, sizeof(path), "%s/returns.bin", argv[4]);
 	f = fopen(path, "wb");
@@ -433,16 +530,20 @@ int main(int argc, char **argv)
 		mosrx_mos_rx_stats cs;
 		mosrx_mos_rx_stats_of(0, &cs);
 		printf("{\"mode\": \"%s\", \"frames\": %lu, \"rx_frames_timed\": %lu, \"rx_ns_per_frame\": %.2f, "
+		       "\"rx_ns_per_frame_excl_tx\": %.2f, "
 		       "\"consumer_frames\": %lu, \"stream_step\": %lu, \"gpu_flow_hash\": %lu, \"reclassified\": %lu, "
-		       "\"filter_installs\": %lu, "
+		       "\"filter_installs\": %lu, \"max_filter_sync_ns\": %lu, \"gpu_errors\": %lu, \"gpu_dropped\": %lu, "
 		       "\"filters_gpu\": %lu, \"filters_cpu\": %lu, \"tx_packets\": %lu, \"tx_csum_offloaded\": %lu, "
-		       "\"tx_errors\": %lu}\n",
+		       "\"tx_errors\": %lu, \"arp_sent\": %lu, \"reopen_same_addr\": %d}\n",
 		       argv[1], (unsigned long)g_total, (unsigned long)g_rx_frames,
-		       g_rx_frames ? g_rx_ns / (double)g_rx_frames : 0.0, (unsigned long)cs.frames,
+		       g_rx_frames ? g_rx_ns / (double)g_rx_frames : 0.0,
+		       g_rx_frames ? (g_rx_ns - g_tx_ns) / (double)g_rx_frames : 0.0, (unsigned long)cs.frames,
 		       (unsigned long)cs.stream_step, (unsigned long)cs.gpu_flow_hash, (unsigned long)cs.reclassified,
-		       (unsigned long)cs.filter_installs,
+		       (unsigned long)cs.filter_installs, (unsigned long)cs.max_filter_sync_ns, (unsigned long)cs.gpu_errors,
+		       (unsigned long)cs.gpu_dropped,
 		       (unsigned long)cs.filters_gpu, (unsigned long)cs.filters_cpu, (unsigned long)g_tx_stats.tx_packets,
-		       (unsigned long)g_tx_stats.tx_csum_offloaded, (unsigned long)g_tx_stats.tx_errors);
+		       (unsigned long)g_tx_stats.tx_csum_offloaded, (unsigned long)g_tx_stats.tx_errors, g_arp_sent,
+		       g_reopen_same_addr);
 	}
 	mosrx_source_close(src);
 	return 0;

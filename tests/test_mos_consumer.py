@@ -100,6 +100,22 @@ SCENARIOS = {
     "golden_rand_small_fwd": dict(forward=1, env={"MOSAPP_ORPHAN": "src net 10.0.0.0/8"}, fixture="rand_small"),
     "golden_rand_mid_fwd": dict(forward=1, env={"MOSAPP_BATCH": "37", "MOSAPP_GROUP": "2"}, fixture="rand_mid"),
     "golden_rand_large_nofwd": dict(forward=0, env={}, fixture="rand_large"),
+    # round 3's consumer soak, seed 7, setup 3 (scripts/soak_consumer.py), with mOS's wall clock
+    # running: forward 0, a listener (RSTs need ARP, unresolved: mOS sends ARP requests, and
+    # ARPTimer, arp.c:313-327, retires a request after 1 s), a raw monitor, SYN and orphan filters
+    # (bound before the first frame: the first filter evaluation installs them on the GPU).  The
+    # ARP requests mOS sends depend on how long the run takes, so the filter install must not
+    # stall the mTCP thread (the set is in effect at once, its hipRTC compile runs behind)
+    "real_clock_seed7_setup3": dict(forward=0, env={"MOSAPP_LISTEN": "80", "MOSAPP_MONITORS": "1",
+                                                    "MOSAPP_RAW_NOFILTER": "1", "MOSAPP_SYN": "tcp port 8080",
+                                                    "MOSAPP_ORPHAN": "net 10.9.0.0/16", "MOSAPP_BATCH": "4096",
+                                                    "MOSAPP_GROUP": "2"},
+                                    listen=80, nflows=64, seed=1000704748, real_clock=True),
+    # a raw monitor's program freed mid-trace (as FreeMonListener does, socket.c:33-36) and a
+    # filter of the same length bound in its place, usually at the same address: the GPU's set
+    # must follow the programs, not their addresses
+    "reopen_filter": dict(forward=1, env={"MOSAPP_RAW": "tcp port 80", "MOSAPP_RAW2": "tcp port 443",
+                                          "MOSAPP_REOPEN_RAW_AT": "333", "MOSAPP_BATCH": "97"}),
 }
 
 
@@ -163,16 +179,28 @@ def compare_modes(exe, tmp, name):
     if "fixture" in sc:
         frames = fixture_frames(sc["fixture"])
     else:
-        frames = pktlib.conversation_frames(sc.get("nflows", 64), seed=11, listen_port=sc.get("listen", 0))
+        frames = pktlib.conversation_frames(sc.get("nflows", 64), seed=sc.get("seed", 11),
+                                            listen_port=sc.get("listen", 0))
     pp = run_app(exe, "pp", tmp, name, sc, frames)
     gpu = run_app(exe, "gpu", tmp, name, sc, frames, sc.get("gpu_env"))
     assert len(pp["returns"]) == len(frames)
     assert gpu["returns"] == pp["returns"], "per-frame return values"
     assert gpu["state"] == pp["state"], "flow table / NETSTAT"
     assert gpu["callbacks"] == pp["callbacks"], "callbacks"
-    assert gpu["tx"] == pp["tx"], "frames sent"
+    assert gpu["tx"] == pp["tx"], (f"frames sent: {len(gpu['tx'])} vs {len(pp['tx'])}, ARP requests "
+                                    f"{gpu['stats']['arp_sent']} vs {pp['stats']['arp_sent']}, first difference at "
+                                    f"{first_diff(gpu['tx'], pp['tx'])}")
     assert gpu["stats"]["consumer_frames"] == len(frames)
+    assert gpu["stats"]["gpu_errors"] == 0 and gpu["stats"]["gpu_dropped"] == 0
     return pp, gpu
+
+
+def first_diff(a, b):
+    """Index and ethertypes of the first frame sent that differs between two runs."""
+    for i, (x, y) in enumerate(zip(a, b)):
+        if x != y:
+            return i, x[12:14].hex(), y[12:14].hex()
+    return min(len(a), len(b)), None, None
 
 
 def _have(exe):
@@ -205,10 +233,12 @@ def _check_scenario(name, pp, gpu):
         assert st["stream_step"] > 0
     if name == "cpu_flow_hash":
         assert st["gpu_flow_hash"] == 0
-    elif st["stream_step"] and not any(k in SCENARIOS[name]["env"] for k in ("MOSAPP_RAW", "MOSAPP_SYN",
-                                                                            "MOSAPP_ORPHAN")):
-        # every lookup on the GPU's bucket (a BPF pass per batch makes no flow hashes: HTSearch then)
+    elif st["stream_step"]:
+        # every lookup on the GPU's bucket, filters or not (the fused classify + BPF pass makes them too)
         assert st["gpu_flow_hash"] == st["stream_step"]
+    # a filter install never stalls the mTCP thread on a compile (the set runs on the interpreter
+    # kernel until its hipRTC kernels are in): the longest install + reclassification
+    assert st["max_filter_sync_ns"] < (10e6 if name.startswith("real_clock") else 50e6), st["max_filter_sync_ns"]
     if name == "monitor_nofwd":
         assert all(f[12:14] == b"\x08\x06" for f in pp["tx"])  # forward = 0: only mOS's own ARP requests leave
     if name in ("monitor_fwd", "no_socket"):
@@ -230,8 +260,50 @@ def _check_scenario(name, pp, gpu):
         assert pp["stats"]["tx_csum_offloaded"] == 0
     if name == "late_filter":
         assert st["filter_installs"] >= 1 and st["reclassified"] >= 1
+    if name == "reopen_filter":
+        assert st["filter_installs"] >= 2 and st["filters_gpu"] == 1   # the freed program's entry went
+        assert st["reopen_same_addr"] == 1 and pp["stats"]["reopen_same_addr"] == 1
+    if name.startswith("real_clock"):
+        assert st["filter_installs"] >= 1 and st["filters_gpu"] == 2
+        assert pp["stats"]["arp_sent"] > 0 and gpu["stats"]["arp_sent"] == pp["stats"]["arp_sent"]
     if name == "late_monitor":
         assert st["reclassified"] >= 1
     if name.startswith("golden_"):
         assert st["stream_step"] > 0
         assert len(set(pp["returns"])) == 3                     # -1, 0 and 1 all reached
+
+
+def _gpu_error_run(exe, tmp_path):
+    """late_monitor with the consumer's first reclassification failing (a GPU error in the
+    middle of a batch, injected by the harness): the rest of that batch is dropped and
+    counted, mOS carries on, and everything else equals ProcessPacket's run."""
+    sc = dict(SCENARIOS["late_monitor"])
+    sc["env"] = dict(sc["env"], MOSAPP_BATCH="97", MOSAPP_GROUP="1")
+    frames = pktlib.conversation_frames(64, seed=11)
+    pp = run_app(exe, "pp", tmp_path, "gpu_error", sc, frames)
+    gpu = run_app(exe, "gpu", tmp_path, "gpu_error", sc, frames, {"MOSAPP_FAIL_RECLASSIFY": "1"})
+    st = gpu["stats"]
+    assert st["consumer_frames"] == len(frames) and st["gpu_errors"] == 1
+    at = int(SCENARIOS["late_monitor"]["env"]["MOSAPP_LATE_MON_AT"]) - 1   # the frame the monitor appears at
+    end = min((at // 97 + 1) * 97, len(frames))                           # the end of its batch
+    # the reclassification comes at the first IPv4 frame from `at` on (the checksum gate, ip_in.c:67)
+    first = end - st["gpu_dropped"]
+    assert at <= first < end
+    r_pp, r_gpu = pp["returns"], gpu["returns"]
+    assert r_gpu[:first] == r_pp[:first] and r_gpu[end:] == r_pp[end:]   # the frames around them: unchanged
+    assert set(r_gpu[first:end]) == {0xFF}                                # dropped: -1
+    n_pp, n_gpu = (x["state"].splitlines()[-1].split() for x in (pp, gpu))
+    assert n_gpu[2] == n_pp[2]                                            # rx_packets: every frame seen
+    neg = sum(1 for x in r_gpu if x == 0xFF)
+    assert int(n_gpu[6]) == neg                                           # rx_errors: the -1 returns, dropped ones in
+
+
+@pytest.mark.skipif(not _have(APP_EMUL), reason="needs oracle/_ref/mos_app_emul (make -C oracle ref)")
+def test_consumer_survives_gpu_error_emulated(tmp_path):
+    _gpu_error_run(APP_EMUL, tmp_path)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have(APP), reason="needs oracle/_ref/mos_app (built by make -C oracle ref)")
+def test_consumer_survives_gpu_error_on_gpu(tmp_path):
+    _gpu_error_run(APP, tmp_path)

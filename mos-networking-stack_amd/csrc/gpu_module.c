@@ -901,7 +901,12 @@ static int32_t set_bpf(struct gpu_priv *pv, struct if_state *is, const mosrx_bpf
 	int k;
 	uint32_t i;
 	(void)pv;
-	if (!a || a->nprog > MOSRX_BPF_MAX_PROGS || mosrx_bpf_set_async(is->mc, a->progs, a->nprog))
+	/* MOSRX_BPF_SYNC=1 (diagnostics): wait for the compile here, as before round 4 */
+	static int sync_set = -1;
+	if (sync_set < 0)
+		sync_set = getenv("MOSRX_BPF_SYNC") && atoi(getenv("MOSRX_BPF_SYNC")) == 1;
+	if (!a || a->nprog > MOSRX_BPF_MAX_PROGS ||
+	    (sync_set ? mosrx_bpf_set(is->mc, a->progs, a->nprog) : mosrx_bpf_set_async(is->mc, a->progs, a->nprog)))
 		return -1;
 	for (k = 0; k < MOSRX_NSLOT && a->nprog; k++) {
 		struct group *g = &is->g[k];

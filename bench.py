@@ -491,16 +491,19 @@ def orphan_segments(n: int, size: int = 1460, seed: int = 3) -> mosrx.Trace:
     return t
 
 
-def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 3, timeout: float = 60.0,
+def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 5, timeout: float = 60.0,
                     exe: str | None = None):
     """mOS's own rx loop on one host core (oracle/_ref/mos_app: mtcp_init, an
     mTCP thread in RunMainLoop, one stream monitor socket, gpu_module_func as
     the I/O module): the per-frame CPU time of core.c:902-907 (timed per batch)
     with mOS's ProcessPacket on every frame ("pp") and with csrc/mos_rx.c
     taking the checks from the GPU records ("gpu"), on the same frames,
-    alternated `reps` times (medians).  The difference is the CPU time per
-    frame the GPU saves inside mOS.  A reported baseline; None when the binary
-    did not travel with the tree."""
+    alternated `reps` times (medians, with min / max).  What mOS sends goes
+    nowhere (MOSAPP_NO_TX: no pcap dump) and the time spent in get_wptr -- the
+    TX buffer's flush to the source every 64 frames, the harness's sink -- is
+    taken out of the figures (`*_excl_tx`; the raw ones are kept beside them).
+    The difference is the CPU time per frame the GPU saves inside mOS.  A
+    reported baseline; None when the binary did not travel with the tree."""
     exe = exe or os.path.join(ROOT, "oracle", "_ref", "mos_app")
     if not os.access(exe, os.X_OK):
         return None
@@ -508,6 +511,7 @@ def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 3, ti
     import tempfile
     import pktlib
     ns = {"pp": [], "gpu": []}
+    raw = {"pp": [], "gpu": []}
     frames = 0
     with tempfile.TemporaryDirectory() as td:
         trace = os.path.join(td, "t.mrxt")
@@ -519,21 +523,30 @@ def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 3, ti
                 conf = os.path.join(d, "mos.conf")
                 with open(conf, "w") as fh:
                     fh.write(MOS_CONF.format(log=os.path.join(d, "log"), forward=forward))
-                env = dict(os.environ, MOSAPP_QUIET="1", MOSAPP_LOOPS=str(loops), MOSAPP_BATCH="8192")
+                env = dict(os.environ, MOSAPP_QUIET="1", MOSAPP_LOOPS=str(loops), MOSAPP_BATCH="8192",
+                           MOSAPP_NO_TX="1")
                 try:
                     r = subprocess.run([exe, mode, conf, trace, d], capture_output=True, text=True, timeout=timeout,
                                        env=env)
                     st = json.loads(r.stdout.strip().splitlines()[-1])
                 except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
                     return None
-                ns[mode].append(st["rx_ns_per_frame"])
+                ns[mode].append(st["rx_ns_per_frame_excl_tx"])
+                raw[mode].append(st["rx_ns_per_frame"])
                 frames = st["rx_frames_timed"]
     pp, gp = float(np.median(ns["pp"])), float(np.median(ns["gpu"]))
+    saved = [a - b for a, b in zip(ns["pp"], ns["gpu"])]           # per alternated pair
     return {"processpacket_ns_per_frame": round(pp, 1), "gpu_records_ns_per_frame": round(gp, 1),
-            "saved_ns_per_frame": round(pp - gp, 1), "frames": frames,
+            "saved_ns_per_frame": round(pp - gp, 1),
+            "saved_ns_per_frame_pairs": {"median": round(float(np.median(saved)), 1),
+                                         "min": round(min(saved), 1), "max": round(max(saved), 1)},
+            "spread_ns": {k: [round(min(v), 1), round(max(v), 1)] for k, v in ns.items()},
+            "frames": frames, "excluded": "get_wptr (TX buffer flushes), no TX dump",
             "runs_ns": {k: [round(x, 1) for x in v] for k, v in ns.items()},
+            "runs_ns_incl_tx": {k: [round(x, 1) for x in v] for k, v in raw.items()},
             "sample": f"{tr.n} frames x {loops} through mOS's RunMainLoop on one core (1 stream monitor, "
-                      f"forward={forward}), oracle/_ref/mos_app pp vs gpu, {reps} alternated runs each, medians"}
+                      f"forward={forward}), oracle/_ref/mos_app pp vs gpu, {reps} alternated runs each, medians; "
+                      f"TX flushes excluded"}
 
 
 def measure_fw64(ctx, seconds: float):
@@ -766,6 +779,10 @@ def main():
     # MOSRX_BENCH_DEVICE pins every rank to one device: a rehearsal of the
     # multi-rank path on a one-GPU box, never a result
     device = int(os.environ.get("MOSRX_BENCH_DEVICE", local))
+    # each rank on its GPU's NUMA node before its first GPU call (mOS binds
+    # every mTCP thread to its core's node, cpu.c:56-87): the host side of the batches it
+    # stages and waits for stays node-local
+    numa = mosrx.bind_to_gpu_node(device)
     ctx = mosrx.Context(device)
     keys = [k for k in args.workloads.split(",") if k]
     results, traces = {}, {}
@@ -861,6 +878,7 @@ def main():
                    "resident_bytes": h["resident_bytes"]},
         "roofline": h["roofline"],
         "read_ceiling_gbps": read_ceiling,
+        "numa": numa,
         # the headline kernel's rate against the box's own streaming-read rate for
         # launches of the ring's size (what the HBM delivers to a read-only kernel)
         "frac_of_read_ceiling": (round(h["roofline"]["achieved"] / read_ceiling["launch_768MiB"], 4)
@@ -907,7 +925,7 @@ def headline_line(detail, h, head, results, e2e):
         for leg in ("mos_rx_loop_M1500", "mos_rx_loop_FW64"):
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("processpacket_ns_per_frame", "gpu_records_ns_per_frame",
-                                                          "saved_ns_per_frame")}
+                                                          "saved_ns_per_frame", "spread_ns")}
     sec = {}
     for k, r in results.items():
         if k == head:

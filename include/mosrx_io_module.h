@@ -198,6 +198,8 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * dpdk_module.c:556-566) and fill those checks on the GPU
 	                                                 * when send_pkts sends the frames; 0 (default): -1, mOS
 	                                                 * computes them (ip_out.c:169-174, tcp_out.c:207-218) */
+	int32_t       numa;                             /* 1 (default): core c drives a GPU on c's NUMA node
+	                                                 * (mosrx_numa_pick); 0: gpu_base + c % ngpu */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
 #define MOSRX_GROUP_AUTO_BYTES  (256ull << 20)   /* per pipeline slot; 64 B frames: ~120 batches of 32K
@@ -216,9 +218,26 @@ int  mosrx_gpu_module_bind(struct mtcp_thread_context *ctx, int cpu);
 /* Give mTCP thread `cpu` its own source for netdev `ifidx` (e.g. one
  * PACKET_FANOUT_HASH socket per thread), instead of cfg.src[ifidx]. */
 int  mosrx_gpu_module_bind_source(int cpu, int ifidx, mosrx_source *src);
-/* The GPU mTCP thread `cpu` runs on: gpu_base + cpu % ngpu (ngpu 0: all visible
- * devices, `ndev`), the per-core sharding of SURVEY.md §8e.  -EINVAL if none. */
+/* The GPU mTCP thread `cpu` runs on, among gpu_base .. gpu_base + ngpu - 1
+ * (ngpu 0: all visible devices, `ndev`), the per-core sharding of SURVEY.md
+ * §8e: with cfg.numa one on cpu's NUMA node (mosrx_numa_pick), else -- or
+ * when the topology does not say -- gpu_base + cpu % ngpu.  -EINVAL if none. */
 int  mosrx_gpu_module_device_of(int cpu, int ndev);
+
+/* ---- NUMA topology (csrc/topology.c; sysfs, like mOS's cpu.c / numa(3)) ---- */
+/* Node of a PCI device ("0000:c1:00.0", /sys/bus/pci/devices/<bdf>/numa_node),
+ * of a core (/sys/devices/system/cpu/cpu<c>/node<n>), of HIP device `device`
+ * (its PCI address from hipDeviceGetPCIBusId); -1 when unknown. */
+int  mosrx_pci_numa_node(const char *bdf);
+int  mosrx_cpu_numa_node(int cpu);
+int  mosrx_gpu_numa_node(int device);
+/* Of `ngpu` candidate GPUs on nodes gpu_node[0..ngpu-1], the one core `cpu`
+ * drives: one on cpu's node, round robin by cpu's rank among the node's cores
+ * (/sys/devices/system/node/node<n>/cpulist); -1 when a node is unknown or
+ * cpu's node has no GPU. */
+int  mosrx_numa_pick(int cpu, const int *gpu_node, int ngpu);
+/* Read sysfs under `root` instead of "/" (tests: a fake tree; NULL or "/": the real one). */
+int  mosrx_topology_set_root(const char *root);
 /* Frames a context sent, received and dropped on TX (per netdev summed). */
 typedef struct mosrx_gpu_module_stats {
 	uint64_t rx_batches, rx_frames, tx_packets, tx_bytes, tx_errors;
@@ -231,6 +250,8 @@ typedef struct mosrx_gpu_module_stats {
 	int32_t  device;            /* the GPU it drives: gpu_base + cpu % ngpu */
 	uint64_t tx_csum_offloaded; /* TX frames whose requested checks the GPU filled (cfg.tx_csum); frames
 	                               whose pass failed are dropped and counted in tx_errors */
+	int32_t  cpu_node;          /* the core's NUMA node, -1 unknown */
+	int32_t  gpu_node;          /* its GPU's, -1 unknown */
 } mosrx_gpu_module_stats;
 /* Time every kernel this thread's contexts launch (for the stats above). */
 int  mosrx_gpu_module_set_timing(struct mtcp_thread_context *ctx, int on);

@@ -137,6 +137,7 @@ void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg)
 	cfg->tx_batch = 64;
 	cfg->group = MOSRX_GROUP_AUTO;
 	cfg->group_bytes = 0;
+	cfg->numa = 1;
 	mosrx_params_default(&cfg->params);
 }
 
@@ -198,14 +199,41 @@ int mosrx_gpu_module_bind_source(int cpu, int ifidx, mosrx_source *src)
 	return 0;
 }
 
-/* Per-core sharding: thread `cpu` drives GPU gpu_base + cpu % ngpu. */
+/* NUMA node of HIP device d, looked up once (-1: unknown or not a device). */
+#define NODE_CACHE 64
+static int g_gpu_node[NODE_CACHE];
+static int g_gpu_node_known[NODE_CACHE];
+static int gpu_node_of(int d)
+{
+	int n;
+	if (d < 0 || d >= NODE_CACHE)
+		return -1;
+	pthread_mutex_lock(&g_lock);
+	if (!g_gpu_node_known[d]) {
+		g_gpu_node[d] = mosrx_gpu_numa_node(d);
+		g_gpu_node_known[d] = 1;
+	}
+	n = g_gpu_node[d];
+	pthread_mutex_unlock(&g_lock);
+	return n;
+}
+
+/* Per-core sharding: thread `cpu` drives a GPU on its NUMA
+ * node (topology.c: round robin over the node's GPUs), else gpu_base + cpu % ngpu. */
 int mosrx_gpu_module_device_of(int cpu, int ndev)
 {
 	const int ngpu = g_cfg.ngpu > 0 ? g_cfg.ngpu : ndev - g_cfg.gpu_base;
-	int dev;
+	int dev, k;
 	if (cpu < 0 || ngpu <= 0)
 		return -EINVAL;
 	dev = g_cfg.gpu_base + cpu % ngpu;
+	if (g_cfg.numa && ngpu <= NODE_CACHE) {
+		int nodes[NODE_CACHE], i;
+		for (i = 0; i < ngpu; i++)
+			nodes[i] = g_cfg.gpu_base + i < ndev ? gpu_node_of(g_cfg.gpu_base + i) : -1;
+		if ((k = mosrx_numa_pick(cpu, nodes, ngpu)) >= 0)
+			dev = g_cfg.gpu_base + k;
+	}
 	return dev < ndev ? dev : -EINVAL;
 }
 
@@ -458,6 +486,8 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 	ndev = mosrx_device_count();
 	pv->stats.cpu = cpu;
 	pv->stats.device = mosrx_gpu_module_device_of(cpu, ndev);
+	pv->stats.cpu_node = mosrx_cpu_numa_node(cpu);
+	pv->stats.gpu_node = pv->stats.device >= 0 ? gpu_node_of(pv->stats.device) : -1;
 	for (i = 0; i < (int)g_cfg.num_ifs; i++) {
 		struct if_state *is = &pv->ifs[i];
 		int dev = mosrx_gpu_module_device_of(cpu, ndev);

@@ -106,7 +106,8 @@ class ModuleCfg(C.Structure):
                 ("gpu_base", C.c_int32), ("ngpu", C.c_int32), ("pipeline", C.c_int32),
                 ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32),
                 ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32),
-                ("group_bytes", C.c_uint64), ("flowhash", C.c_int32), ("tx_csum", C.c_int32)]
+                ("group_bytes", C.c_uint64), ("flowhash", C.c_int32), ("tx_csum", C.c_int32),
+                ("numa", C.c_int32)]
 
 
 class ModuleStats(C.Structure):
@@ -114,7 +115,7 @@ class ModuleStats(C.Structure):
                 ("tx_bytes", C.c_uint64), ("tx_errors", C.c_uint64), ("kernel_launches", C.c_uint64),
                 ("kernel_ms", C.c_double), ("rx_drops", C.c_uint64),
                 ("rx_reclassified", C.c_uint64), ("cpu", C.c_int32), ("device", C.c_int32),
-                ("tx_csum_offloaded", C.c_uint64)]
+                ("tx_csum_offloaded", C.c_uint64), ("cpu_node", C.c_int32), ("gpu_node", C.c_int32)]
 
 
 class RxLoopOpts(C.Structure):
@@ -260,6 +261,11 @@ def lib():
                                                          C.POINTER(P)]),
             "mosrx_host_register": (I, [P, P, C.c_size_t, I]),
             "mosrx_host_unregister": (I, [P, P]),
+            "mosrx_pci_numa_node": (I, [C.c_char_p]),
+            "mosrx_cpu_numa_node": (I, [I]),
+            "mosrx_gpu_numa_node": (I, [I]),
+            "mosrx_numa_pick": (I, [I, C.POINTER(C.c_int), I]),
+            "mosrx_topology_set_root": (I, [C.c_char_p]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -1109,6 +1115,84 @@ def read_pcap(path: str) -> list[bytes]:
             out.append(bytes(buf[:n]))
     finally:
         lib().mosrx_source_close(s)
+
+
+def _sysfs_props(path: str) -> dict:
+    out = {}
+    try:
+        with open(path) as fh:
+            for line in fh:
+                k, _, v = line.strip().partition(" ")
+                if v.strip().lstrip("-").isdigit():
+                    out[k] = int(v)
+    except OSError:
+        pass
+    return out
+
+
+def _parse_cpulist(text: str) -> list[int]:
+    cpus = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        cpus += list(range(int(lo), int(hi or lo) + 1))
+    return cpus
+
+
+def gpu_numa_cpus(device: int, root: str = "/"):
+    """(PCI address, NUMA node, that node's cores) of HIP device `device`, read from
+    sysfs without touching the GPU (so a rank can bind itself before its first HIP
+    call): the KFD topology's GPU nodes in order -- HIP's device order -- less those
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES hide, the GPU's PCI numa_node, the
+    node's cpulist.  None when any of it is unknown."""
+    base = os.path.join(root, "sys", "class", "kfd", "kfd", "topology", "nodes")
+    try:
+        ids = sorted(int(d) for d in os.listdir(base) if d.isdigit())
+    except OSError:
+        return None
+    gpus = []
+    for k in ids:
+        pr = _sysfs_props(os.path.join(base, str(k), "properties"))
+        if pr.get("simd_count", 0) > 0 and "location_id" in pr:
+            loc = pr["location_id"]
+            gpus.append(f"{pr.get('domain', 0):04x}:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 7:x}")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            try:
+                gpus = [gpus[int(x)] for x in v.split(",") if x.strip()]
+            except (ValueError, IndexError):
+                return None
+    if not 0 <= device < len(gpus):
+        return None
+    bdf = gpus[device]
+    try:
+        with open(os.path.join(root, "sys", "bus", "pci", "devices", bdf, "numa_node")) as fh:
+            node = int(fh.read().strip())
+        with open(os.path.join(root, "sys", "devices", "system", "node", f"node{node}", "cpulist")) as fh:
+            cpus = _parse_cpulist(fh.read())
+    except (OSError, ValueError):
+        return None
+    return (bdf, node, cpus) if node >= 0 and cpus else None
+
+
+def bind_to_gpu_node(device: int, root: str = "/") -> dict:
+    """Bind the calling process to the cores of device's NUMA node (those it may
+    run on), as mOS binds each mTCP thread to its core's node (cpu.c:56-87).
+    Call before the first GPU call; never re-execs.  Returns what was done."""
+    info = gpu_numa_cpus(device, root)
+    if not info:
+        return {"device": device, "bound": False, "why": "topology unknown"}
+    bdf, node, cpus = info
+    allowed = os.sched_getaffinity(0)
+    mine = sorted(set(cpus) & allowed)
+    if not mine:
+        return {"device": device, "pci": bdf, "node": node, "bound": False,
+                "why": f"none of node {node}'s cores in this process's affinity"}
+    if set(mine) != allowed:
+        os.sched_setaffinity(0, mine)
+    return {"device": device, "pci": bdf, "node": node, "bound": True, "cpus": len(mine)}
 
 
 def shard_plan(nbatches: int, world: int, rank: int) -> list[int]:

@@ -53,7 +53,9 @@ RESIDENT_BYTES = 1200 << 20    # working set per rank: well past the 256 MiB Inf
 WORKLOADS = {
     "M1500": (mosrx.TRACE_M1500, 65_536, 8, "1xMI355X 1500B MTU TCP segments, 1M distinct 5-tuples, batch=64K (BASELINE config #3)"),
     "S64": (mosrx.TRACE_S64, 32_768, 256, "1xMI355X 64B TCP, 1 flow, batch=32K (BASELINE config #2), full verdict"),
-    "S64_hdr": (mosrx.TRACE_S64, 32_768, 256, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum)"),
+    "S64_hdr": (mosrx.TRACE_S64, 32_768, 256, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum), "
+                                              "8-byte records (mosrx_result8)"),
+    "S64_hdr16": (mosrx.TRACE_S64, 32_768, 256, "config #2 header-only as S64_hdr, 16-byte records"),
     "IMIX": (mosrx.TRACE_IMIX, 262_144, 8, "IMIX 60/590/1514 7:4:1, 1M flows, batch=256K (BASELINE config #4)"),
     # one kernel launch per batch, two batches in flight (two rx queues)
     "M1500_1": (mosrx.TRACE_M1500, 65_536, 0, "config #3, one launch per 64K batch"),
@@ -65,8 +67,14 @@ WORKLOADS = {
     "M1500_tx": (mosrx.TRACE_M1500, 65_536, 0, "config #3 TX checksum rewrite (MOS_UPDATE_IP|TCP_CHKSUM), in place"),
     "IMIX_bpf": (mosrx.TRACE_IMIX, 262_144, 0, "config #4 batched BPF, 8 mOS filter programs (sfbpf_compile output)"),
     "IMIX_cls_bpf": (mosrx.TRACE_IMIX, 262_144, 0, "config #4 classify + the 8 BPF programs fused in one pass"),
+    # the fused pass over a ring (the batch queue: gpu_module_func's groups with filters installed)
+    "IMIX_cls_bpf_ring": (mosrx.TRACE_IMIX, 262_144, 8, "config #4 classify + 8 BPF programs fused, one batch-queue "
+                                                         "launch over 8 batches"),
+    "S64_cls_bpf_ring": (mosrx.TRACE_S64, 32_768, 256, "config #2 classify + 8 BPF programs fused, one batch-queue "
+                                                       "launch over 256 batches"),
 }
-DEFAULT_WORKLOADS = "M1500,S64,S64_hdr,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,M1500_tx,IMIX_bpf,IMIX_cls_bpf"
+DEFAULT_WORKLOADS = ("M1500,S64,S64_hdr,S64_hdr16,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,M1500_tx,IMIX_bpf,"
+                     "IMIX_cls_bpf,IMIX_cls_bpf_ring,S64_cls_bpf_ring")
 OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_ti": mosrx.OP_CLASSIFY_TI, "M1500_tx": mosrx.OP_TX_CSUM,
        "IMIX_bpf": mosrx.OP_BPF, "IMIX_cls_bpf": mosrx.OP_CLASSIFY_BPF}
 # filter expressions whose compiled programs (tests/golden/bpf.npz, mOS's own compiler) the BPF row runs
@@ -131,8 +139,10 @@ def algo_bytes(tr: mosrx.Trace, key: str = "") -> int:
     bytes per frame (the line a filter reads; deeper loads are extra)."""
     if key.endswith("_tx"):
         return tr.caplen_sum + tr.n * (DESC_BYTES + 4)
-    if key.endswith("_cls_bpf"):   # the classify bytes + the 4-byte match mask
+    if "_cls_bpf" in key:          # the classify bytes + the 4-byte match mask
         return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES + 4)
+    if key == "S64_hdr":           # 8-byte compact records
+        return tr.caplen_sum + tr.n * (DESC_BYTES + 8)
     if key.endswith("_bpf"):
         return tr.n * (DESC_BYTES + 4) + int(np.minimum(tr.len, 64).astype(np.int64).sum())
     extra = 4 if key.endswith("_fh") else 12 if key.endswith("_ti") else 0
@@ -201,7 +211,7 @@ def resident_batches(ctx, key, world, rank, nres):
 
 def measure(ctx, dist, key, steps, warmup, rank):
     kind, batch, ring, label = WORKLOADS[key]
-    params = mosrx.default_params(skip_tcp_csum=1 if key == "S64_hdr" else 0)
+    params = mosrx.default_params(skip_tcp_csum=1 if key.startswith("S64_hdr") else 0)
     ctx.set_params(params)
     probe = mosrx.Trace(kind, batch)
     per_batch = max(probe.frames_bytes, 1)
@@ -242,7 +252,10 @@ def measure(ctx, dist, key, steps, warmup, rank):
         # each step = ONE queue launch over `ring` distinct resident batches (an rx
         # ring serviced at once, gpu_module_func cfg.group); several rings over
         # disjoint resident copies cycle so the working set stays past the L3
-        qs = [ctx.queue(dbs[i:i + ring]) for i in range(0, len(dbs), ring)]
+        if "_cls_bpf" in key:
+            ctx.bpf_set(bpf_bench_programs())   # (compiled before the queues run)
+        qs = [ctx.queue_ex(dbs[i:i + ring], match="_cls_bpf" in key, compact=key == "S64_hdr")
+              for i in range(0, len(dbs), ring)]
         prewarm(lambda: qs[0].time(8, qs[1:], kernels=False))
         if warmup:
             qs[0].time(warmup, qs[1:], kernels=False)
@@ -261,7 +274,9 @@ def measure(ctx, dist, key, steps, warmup, rank):
         for q in qs:
             q.destroy()
         frames_per_step, ab_step = batch * ring, ab * ring
-        method = f"one batch-queue launch per step over {ring} resident batches"
+        method = f"one batch-queue launch per step over {ring} resident batches" + (
+            " (fused classify + BPF queue kernel)" if "_cls_bpf" in key else
+            ", 8-byte records" if key == "S64_hdr" else "")
     else:
         prewarm(lambda: ctx.time_dev_streams(dbs, 200, STREAMS))
         if warmup:
@@ -355,10 +370,10 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, all_cores: bool 
     Reported baseline only; never the measured product path."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
-    p = O.params(skip_tcp_csum=1 if key == "S64_hdr" else 0)
+    p = O.params(skip_tcp_csum=1 if key.startswith("S64_hdr") else 0)
     ab = algo_bytes(tr, key)
 
-    if key in OPS:
+    if key in OPS or "_cls_bpf" in key:
         return cpu_baseline_row(tr, key, min_s, O)
 
     def run(nt):
@@ -429,14 +444,14 @@ def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: boo
 def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
     """The oracle for a §8f row (flow hash / pkt_info / TX rewrite / BPF), one thread."""
     ab = algo_bytes(tr, key)
-    progs = bpf_bench_programs() if key.endswith("_bpf") else None
+    progs = bpf_bench_programs() if "_bpf" in key else None
     reps, t0 = 0, time.perf_counter()
     while True:
         if key.endswith("_fh") or key.endswith("_ti"):
             O.classify_ex(tr.frames, tr.off, tr.len, O.params())
         elif key.endswith("_tx"):
             O.tx_csum(tr.frames, tr.off, tr.len, mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM)
-        elif key.endswith("_cls_bpf"):
+        elif "_cls_bpf" in key:
             O.classify(tr.frames, tr.off, tr.len, O.params())
             O.bpf_eval(progs, tr.frames, tr.off, tr.len)
         else:
@@ -445,7 +460,7 @@ def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
         el = time.perf_counter() - t0
         if el >= min_s:
             break
-    fn = ("mo_classify + mo_bpf_eval" if key.endswith("_cls_bpf") else
+    fn = ("mo_classify + mo_bpf_eval" if "_cls_bpf" in key else
           {"_fh": "mo_classify_ex", "_ti": "mo_classify_ex", "_tx": "mo_tx_csum", "bpf": "mo_bpf_eval"}[key[-3:]])
     return {"value": round(reps * ab / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "mpkts": round(reps * tr.n / el / 1e6, 3),
@@ -638,7 +653,7 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
             "method": "pinned hipHostMalloc staging (one block: frames | off | len), one H2D copy, kernel, D2H records; 2 streams"}
 
 
-def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1):
+def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1, bpf=None):
     """The drop-in boundary's own rate: mosrx_rx_loop (RunMainLoop's rx section,
     core.c:897-909) over gpu_module_func (io_module.h:63-78) fed by an in-memory
     source replaying the trace — per group of batches: source -> pinned
@@ -659,7 +674,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     loops = max(1, frames_target // tr.n)
     src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
     be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
-                          group=group, timing=True)
+                          group=group, timing=True, bpf=bpf)
     try:
         be.run_loop(max_pkts=2 * ctx_batch * max(group, 128 if key == "S64" else 4))    # warm-up: staging sized, module loaded
         st0 = be.stats()
@@ -675,15 +690,17 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     kms = st1.kernel_ms - st0.kernel_ms
     batches = st1.rx_batches - st0.rx_batches
     dev_us = 1e3 * kms / max(batches, 1)
-    ab = algo_bytes(tr) * (ctx_batch / tr.n)
-    return {"mpkts": n / dt / 1e6, "gbps": nb * algo_bytes(tr) / dt / 1e9, "frames": n, "seconds": round(dt, 3),
+    ab = (algo_bytes(tr, "_cls_bpf" if bpf else "")) * (ctx_batch / tr.n)
+    return {"mpkts": n / dt / 1e6, "gbps": nb * algo_bytes(tr, "_cls_bpf" if bpf else "") / dt / 1e9, "frames": n,
+            "seconds": round(dt, 3), "filters": len(bpf) if bpf else 0,
             "distinct_frames": tr.n,
             "group": group if group else "auto", "batches_per_launch": round(batches / max(launches, 1), 2),
             "kernel_launches": int(launches), "batches": int(batches),
             "device_us_per_batch": round(dev_us, 3),
             "device_roofline_frac": round(ab / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if dev_us > 0 else None,
             "method": f"mosrx_rx_loop over gpu_module_func (pipelined, "
-                      f"{group if group else 'auto (MOSRX_GROUP_AUTO)'} batch(es) per launch), "
+                      f"{group if group else 'auto (MOSRX_GROUP_AUTO)'} batch(es) per launch"
+                      f"{', ' + str(len(bpf)) + ' monitor filters installed: the fused classify + BPF queue kernel' if bpf else ''}), "
                       f"in-memory source replaying {tr.n} distinct frames; every batch crosses PCIe; device "
                       f"time = HIP events around each kernel (its frames were just copied in)"}
 
@@ -794,7 +811,7 @@ def main():
                   f"kernel {r['kernel_ms']*1e3:.1f} us roofline {r['roofline']['frac']:.3f}",
                   file=sys.stderr, flush=True)
     e2e = None
-    if not args.no_e2e and "M1500" in traces:
+    if not args.no_e2e and any(k in traces for k in ("M1500", "S64", "IMIX")):
         e2e = {k: measure_e2e(ctx, traces[k], {"M1500": 60, "S64": 800}[k]) for k in ("M1500", "S64") if k in traces}
         # the gpu_module_func backend itself (host thread = this rank)
         # the module's default configuration (cfg.group auto: batches per launch sized to what is ready)
@@ -805,15 +822,24 @@ def main():
         if "S64" in traces:
             e2e["backend"]["S64_group1"] = measure_backend(traces["S64"], "S64", 16_000_000, device, group=1)
             e2e["backend"]["S64_group128"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=128)
-        e2e["backend"]["M1500_group1"] = measure_backend(traces["M1500"], "M1500", 2_000_000, device, group=1)
-        e2e["backend"]["M1500_group8"] = measure_backend(traces["M1500"], "M1500", 4_000_000, device, group=8)
+            # 8 monitor filters installed (mtcp_bind_monitor_filter): auto groups through the fused
+            # classify + BPF queue kernel, as without filters
+            e2e["backend"]["S64_bpf"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=0,
+                                                        bpf=bpf_bench_programs())
+        if "IMIX" in traces:
+            e2e["backend"]["IMIX_bpf"] = measure_backend(traces["IMIX"], "IMIX", 4_000_000, device, group=0,
+                                                         bpf=bpf_bench_programs())
+        if "M1500" in traces:
+            e2e["backend"]["M1500_group1"] = measure_backend(traces["M1500"], "M1500", 2_000_000, device, group=1)
+            e2e["backend"]["M1500_group8"] = measure_backend(traces["M1500"], "M1500", 4_000_000, device, group=8)
         # one mTCP thread per core, each with its own context / source / rx loop
         # (one GPU's host side: single-rank runs only)
         if ws == 1:
             mt = {}
             if "S64" in traces:
                 mt["S64"] = [measure_backend_threads("S64", t, 32, 32 * 2 ** 20, device) for t in (1, 2, 4, 8)]
-            mt["M1500"] = [measure_backend_threads("M1500", t, 1, 2_000_000, device) for t in (1, 2, 4)]
+            if "M1500" in traces:
+                mt["M1500"] = [measure_backend_threads("M1500", t, 1, 2_000_000, device) for t in (1, 2, 4)]
             e2e["backend_threads"] = mt
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu:

@@ -29,6 +29,13 @@
 #include "mosrx_ctx.h"
 #include <hip/hiprtc.h>
 
+/* hip/hip_ext.h is C++ only: its C-linkage launcher with dispatch-stamped events */
+hipError_t hipExtModuleLaunchKernel(hipFunction_t f, uint32_t globalWorkSizeX, uint32_t globalWorkSizeY,
+                                    uint32_t globalWorkSizeZ, uint32_t localWorkSizeX, uint32_t localWorkSizeY,
+                                    uint32_t localWorkSizeZ, size_t sharedMemBytes, hipStream_t hStream,
+                                    void **kernelParams, void **extra, hipEvent_t startEvent, hipEvent_t stopEvent,
+                                    uint32_t flags);
+
 enum {
 	LD = 0, LDX = 1, ST = 2, STX = 3, ALU = 4, JMP = 5, RET = 6, MISC = 7,
 	W = 0, H = 8, B = 0x10, IMM = 0, ABS = 0x20, IND = 0x40, MEM = 0x60, LEN = 0x80, MSH = 0xa0,
@@ -867,6 +874,19 @@ int mosrx__bpf_jit_wait(mosrx_ctx *c)
 	}
 }
 
+/* One launch of a hipRTC-built kernel, dispatch-stamped when the timing asks. */
+static int module_launch(hipFunction_t f, unsigned grid, unsigned threads, hipStream_t s, void **args)
+{
+	void *e0, *e1;
+	hipError_t rc;
+	if (mosrx__stamp_take(&e0, &e1))
+		rc = hipExtModuleLaunchKernel(f, grid * threads, 1, 1, threads, 1, 1, 0, s, args, NULL, (hipEvent_t)e0,
+		                              (hipEvent_t)e1, 0);
+	else
+		rc = hipModuleLaunchKernel(f, grid, 1, 1, threads, 1, 1, 0, s, args, NULL);
+	return rc == hipSuccess ? 0 : -EIO;
+}
+
 /* Fused classify + BPF launch (kp carries bmatch). */
 int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hipStream_t s)
 {
@@ -879,9 +899,7 @@ int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hi
 	void *args[] = {&k};
 	if (!f)
 		return -EINVAL;
-	if (hipModuleLaunchKernel(f, (kp->n + tile - 1) / tile, 1, 1, threads, 1, 1, 0, s, args, NULL) != hipSuccess)
-		return -EIO;
-	return 0;
+	return module_launch(f, (kp->n + tile - 1) / tile, threads, s, args);
 }
 
 /* The fused kernel over a batch queue (qp's descriptors carry the masks). */
@@ -899,9 +917,7 @@ int mosrx__bpf_fused_queue_launch(mosrx_ctx *c, const mosrx_qparams *qp, uint32_
 		return -EINVAL;
 	if (!total_tiles)
 		return 0;
-	if (hipModuleLaunchKernel(f, total_tiles, 1, 1, threads, 1, 1, 0, s, args, NULL) != hipSuccess)
-		return -EIO;
-	return 0;
+	return module_launch(f, total_tiles, threads, s, args);
 }
 
 int mosrx__bpf_jit_launch(mosrx_ctx *c, const mosrx_bparams *bp, hipStream_t s)
@@ -915,9 +931,7 @@ int mosrx__bpf_jit_launch(mosrx_ctx *c, const mosrx_bparams *bp, hipStream_t s)
 	const unsigned grid = (n + 255u) / 256u;
 	if (!c->bpf_fn)
 		return -EINVAL;
-	if (hipModuleLaunchKernel(c->bpf_fn, grid, 1, 1, 256, 1, 1, 0, s, args, NULL) != hipSuccess)
-		return -EIO;
-	return 0;
+	return module_launch(c->bpf_fn, grid, 256, s, args);
 }
 
 void mosrx__bpf_jit_free(mosrx_ctx *c)

@@ -1385,8 +1385,8 @@ int mosrx_time_op_dispatch(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, 
 	    (op != MOSRX_OP_TX_CSUM && !out) ||
 	    ((op == MOSRX_OP_CLASSIFY_FH || op == MOSRX_OP_CLASSIFY_BPF || op == MOSRX_OP_CLASSIFY_TI) && !aux))
 		return -EINVAL;
-	if (op == MOSRX_OP_BPF || op == MOSRX_OP_CLASSIFY_BPF)   /* the BPF kernels are launched elsewhere */
-		return -ENOTSUP;
+	/* (the BPF ops are one launch with the fused kernel / the set's own kernel;
+	 * classify + the set's kernel, two, is refused by the launch count) */
 	HIPCHK(hipSetDevice(c->device));
 	return time_stamped(c, iters, op_once, &r, avg_ms);
 }

@@ -21,6 +21,8 @@
 // checked against buflen exactly as the reference does first.
 
 #include <errno.h>
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include "mosrx_device.h"
 
@@ -242,6 +244,11 @@ extern "C" int mosrx_launch_bpf(const mosrx_bparams *bp, void *stream)
 	if (bp->nprog > MOSRX_BPF_MAX_PROGS)
 		return -EINVAL;
 	const uint32_t grid = (bp->n + BPF_TILE - 1u) / BPF_TILE;
-	hipLaunchKernelGGL(mosrx_bpf_kernel, dim3(grid), dim3(BPF_TILE), 0, (hipStream_t)stream, *bp);
+	void *e0, *e1;
+	if (mosrx__stamp_take(&e0, &e1))   // dispatch-stamped timing (mosrx_time_op_dispatch)
+		hipExtLaunchKernelGGL(mosrx_bpf_kernel, dim3(grid), dim3(BPF_TILE), 0, (hipStream_t)stream,
+		                      (hipEvent_t)e0, (hipEvent_t)e1, 0, *bp);
+	else
+		hipLaunchKernelGGL(mosrx_bpf_kernel, dim3(grid), dim3(BPF_TILE), 0, (hipStream_t)stream, *bp);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

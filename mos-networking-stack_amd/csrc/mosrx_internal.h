@@ -137,6 +137,9 @@ int mosrx_launch_classify(const mosrx_kparams *kp, int tile, int variant, void *
  * of launches made by the thread so far. */
 void mosrx__stamp_next(void *start, void *stop);
 uint32_t mosrx__launch_count(void);
+/* A launch made outside mosrx_kernels.hip: counted, and the pending stamp
+ * pair (1) or none (0) handed over for it. */
+int mosrx__stamp_take(void **start, void **stop);
 
 #ifdef __cplusplus
 }

@@ -1326,6 +1326,16 @@ extern "C" void mosrx__stamp_next(void *start, void *stop)
 	t_stamp1 = (hipEvent_t)stop;
 }
 extern "C" uint32_t mosrx__launch_count(void) { return t_launches; }
+// For launches made elsewhere (the hipRTC modules of bpf_jit.c, the interpreter
+// kernel): counts the launch and hands over the pending stamp pair, if any.
+extern "C" int mosrx__stamp_take(void **start, void **stop)
+{
+	t_launches++;
+	*start = t_stamp0;
+	*stop = t_stamp1;
+	t_stamp0 = t_stamp1 = nullptr;
+	return *start != nullptr;
+}
 
 template <typename... P, typename... A>
 static void launch_one(void (*k)(P...), uint32_t grid, uint32_t block, hipStream_t s, const A &...a)

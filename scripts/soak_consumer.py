@@ -61,6 +61,20 @@ def setup(rnd):
     return sc
 
 
+def describe(pp, gpu):
+    """What differs, for the record: per-frame returns, the frames sent (count, ARP
+    requests, ethertypes of the first differing pair), the longest filter install."""
+    rp, rg = pp["returns"], gpu["returns"]
+    bad = [i for i, (a, b) in enumerate(zip(rp, rg)) if a != b]
+    print(f"  returns: {len(bad)} frames differ, first {bad[:8]}", flush=True)
+    tp, tg = pp["tx"], gpu["tx"]
+    arp = lambda fs: sum(1 for f in fs if f[12:14] == b"\x08\x06")  # noqa: E731
+    print(f"  sent: {len(tg)} (gpu) vs {len(tp)} (pp) frames; ARP requests {arp(tg)} vs {arp(tp)}; "
+          f"first difference (index, ethertypes) {T.first_diff(tg, tp)}", flush=True)
+    for k in ("max_filter_sync_ns", "filter_installs", "reclassified", "gpu_errors", "arp_sent"):
+        print(f"  {k}: gpu {gpu['stats'].get(k)} pp {pp['stats'].get(k)}", flush=True)
+
+
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 300.0
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
@@ -90,6 +104,7 @@ def main():
                 assert gpu["stats"]["consumer_frames"] == len(fr)
             except AssertionError as e:
                 print(f"FAIL setup {count}: {sc}: {str(e)[:2000]}", flush=True)
+                describe(pp, gpu)
                 sys.exit(1)
         del T.SCENARIOS[name]
         count += 1

@@ -243,3 +243,46 @@ def test_pinned_range_registry():
         dele(a)
         dele(b)
     assert of(a, 16) == 0 and of(b, 16) == 0
+
+
+def test_pinned_range_registry_nested_and_many():
+    """The sorted registry (binary search under a read lock): a registered
+    sub-range inside another allocation (a NIC ring registered within a larger
+    mapping) does not hide the outer one from spans outside it, and hundreds
+    of ranges added and removed in any order keep every answer right."""
+    import random
+    L = mosrx.lib()
+    add, dele, of = L.mosrx__host_range_add, L.mosrx__host_range_del, L.mosrx__host_range_of
+    add.argtypes, dele.argtypes, of.argtypes = [C.c_void_p, C.c_uint64], [C.c_void_p], [C.c_void_p, C.c_uint64]
+    add.restype, dele.restype, of.restype = None, None, C.c_uint64
+    outer, inner = 0x7E0000000000, 0x7E0000200000
+    add(outer, 8 << 20)
+    add(inner, 1 << 20)
+    try:
+        io, ii = of(outer, 4096), of(inner + 64, 64)
+        assert io and ii and io != ii
+        assert of(inner + (2 << 20), 4096) == io            # past the inner range, still in the outer one
+        assert of(inner - 4096, 8192) == io                 # straddling the inner start: the outer one holds it
+        assert of(outer + (8 << 20) - 8, 16) == 0
+    finally:
+        dele(inner)
+        dele(outer)
+    rnd = random.Random(5)
+    base = 0x7D0000000000
+    slots = list(range(300))
+    rnd.shuffle(slots)
+    for k in slots:
+        add(base + k * (1 << 20), 4096 * (1 + k % 7))
+    try:
+        for k in range(300):
+            a = base + k * (1 << 20)
+            assert of(a, 4096 * (1 + k % 7)) != 0
+            assert of(a + 4096 * (1 + k % 7), 1) == 0       # just past its end: nobody's
+        for k in slots[:150]:
+            dele(base + k * (1 << 20))
+        gone = set(slots[:150])
+        for k in range(300):
+            assert (of(base + k * (1 << 20), 16) == 0) == (k in gone)
+    finally:
+        for k in slots[150:]:
+            dele(base + k * (1 << 20))

@@ -176,13 +176,24 @@ static void gen_ld(struct sbuf *s, uint32_t k, uint32_t size, const struct genop
 	}
 }
 
-/* Load at the run-time offset kk (X + k). */
-static const char *ind_ld(const struct genopt *g, uint32_t size)
+/* Load at the run-time offset kk = X + k (size bytes).  Standalone: the LDS
+ * stage / memory.  Fused: X is 4 * ihl in every filter mOS compiles
+ * (`ldxb 4*([14]&0xf)`) and ihl is 5 in nearly every frame, so kk = k + 20 is
+ * speculated: a constant offset, read from the window's registers; any other
+ * X reads memory (the frame's lines are in L2 behind the header window). */
+static void gen_ind(struct sbuf *s, uint32_t k, uint32_t size, const struct genopt *g)
 {
-	if (g->fused)
-		return size == 4 ? "hk_ind(kk, 4u)" : size == 2 ? "hk_ind(kk, 2u)" : "hk_ind(kk, 1u)";
-	return size == 4 ? "fr_le32(win, sh, rs, o, kk, 4u)" : size == 2 ? "fr_le32(win, sh, rs, o, kk, 2u)"
-	                                                          : "fr_le32(win, sh, rs, o, kk, 1u)";
+	if (!g->fused) {
+		sb_printf(s, "fr_le32(win, sh, rs, o, kk, %uu)", size);
+		return;
+	}
+	if ((uint64_t)k + 20 + 8 <= 94) {
+		sb_printf(s, "(X == 20u ? ");
+		gen_ld(s, k + 20, size, g);
+		sb_printf(s, " : hk_ld_le32(rs, o + kk))");
+	} else {
+		sb_printf(s, "hk_ld_le32(rs, o + kk)");
+	}
 }
 
 static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_t len, int ipm,
@@ -246,16 +257,19 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 		case LD | W | LEN: sb_printf(s, "A = L;"); break;
 		case LDX | W | LEN: sb_printf(s, "X = L;"); break;
 		case LD | W | IND:
-			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 4u > L) goto P%u_R0; A = be32(%s); }",
-			          k, j, ind_ld(g, 4));
+			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 4u > L) goto P%u_R0; A = be32(", k, j);
+			gen_ind(s, k, 4, g);
+			sb_printf(s, "); }");
 			break;
 		case LD | H | IND:
-			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 2u > L) goto P%u_R0; A = be16(%s); }",
-			          k, j, ind_ld(g, 2));
+			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 2u > L) goto P%u_R0; A = be16(", k, j);
+			gen_ind(s, k, 2, g);
+			sb_printf(s, "); }");
 			break;
 		case LD | B | IND:
-			sb_printf(s, "{ const u32 kk = X + %uu; if (kk >= L) goto P%u_R0; A = %s & 0xFFu; }",
-			          k, j, ind_ld(g, 1));
+			sb_printf(s, "{ const u32 kk = X + %uu; if (kk >= L) goto P%u_R0; A = ", k, j);
+			gen_ind(s, k, 1, g);
+			sb_printf(s, " & 0xFFu; }");
 			break;
 		case LDX | MSH | B:
 			gen_abs_check(s, j, k, 1);
@@ -392,19 +406,12 @@ static const char k_hook_pre[] =
 	"/* frame bytes [k, k+4), k constant in [2, 86]: the realigned window registers */\n"
 	"#define RW32(k) (((k) - 2u) % 4u == 0u ? w[((k) - 2u) / 4u] \\\n"
 	"                 : __builtin_amdgcn_alignbyte(w[((k) - 2u) / 4u + 1u], w[((k) - 2u) / 4u], ((k) - 2u) % 4u))\n"
-	"/* frame bytes [kk, kk+4) at a run-time offset: the lane's LDS copy of the window, else memory */\n"
-	"#define hk_ind(kk, size) (((kk) >= 2u && (kk) + (size) <= 94u) \\\n"
-	"  ? __builtin_amdgcn_alignbyte(lw[(((kk) - 2u) >> 2) + 1u], lw[((kk) - 2u) >> 2], ((kk) - 2u) & 3u) \\\n"
-	"  : hk_ld_le32(rs, o + (kk)))\n"
 	"static __device__ __attribute__((always_inline)) inline u32 mosrx_bpf_hook(const hdr_win_t &win, u32 o, u32 cap,\n"
-	"    bool live, __amdgpu_buffer_rsrc_t rs, u32 *lw) {\n"
+	"    bool live, __amdgpu_buffer_rsrc_t rs) {\n"
 	"  u32 w[WIN_DW];\n"
 	"  const u32 rsh = (o + 2u) & 3u;\n"
 	"#pragma unroll\n"
 	"  for (int j = 0; j < WIN_DW; j++) w[j] = __builtin_amdgcn_alignbyte(win.raw[j + 1], win.raw[j], rsh);\n"
-	"#pragma unroll\n"
-	"  for (int j = 0; j < WIN_DW; j++) lw[j] = w[j];\n"
-	"  lw[WIN_DW] = 0u;\n"
 	"  u32 lip = 0;\n"
 	"  if (cap >= 18u && be16hi(w[2]) == 0x0800u) {\n"
 	"    lip = 14u + be16hi(w[3]);\n"
@@ -454,7 +461,7 @@ int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams 
 			free(s.p);
 			return rc;
 		}
-	sb_printf(&s, "  return match;\n}\n#undef RW32\n#undef hk_ind\n");
+	sb_printf(&s, "  return match;\n}\n#undef RW32\n");
 	if (s.err) {
 		free(s.p);
 		return -ENOMEM;

@@ -175,7 +175,7 @@ __device__ __forceinline__ void hdr_load(__amdgpu_buffer_rsrc_t rs, uint32_t nby
 }
 
 #ifdef MOSRX_RTC_BPF
-#include "mosrx_bpf_hook.h"   // generated by bpf_jit.c: mosrx_bpf_hook(win, o, cap, live, rs, lds)
+#include "mosrx_bpf_hook.h"   // generated by bpf_jit.c: mosrx_bpf_hook(win, o, cap, live, rs)
 #endif
 
 // ip_fast_csum (ip_in.h:10-38) over the realigned header (w[3] = IP dword 0):
@@ -696,8 +696,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	}
 #ifdef MOSRX_RTC_BPF
 	if constexpr ((VAR & VAR_BPF) != 0) {
-		__shared__ uint32_t s_bw[25u * 256u];
-		const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * t);
+		const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs);
 		if (active)
 			out_store(kp.bmatch, p, m);
 	}
@@ -1128,8 +1127,7 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 				}
 #ifdef MOSRX_RTC_BPF
 				if constexpr ((VAR & VAR_BPF) != 0) {
-					__shared__ uint32_t s_bw[25u * 64u];
-					const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs, s_bw + 25u * lane);
+					const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs);
 					if (active)
 						out_store(kp.bmatch, p, m);
 				}

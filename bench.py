@@ -56,6 +56,11 @@ WORKLOADS = {
     "S64_hdr": (mosrx.TRACE_S64, 32_768, 256, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum), "
                                               "8-byte records (mosrx_result8)"),
     "S64_hdr16": (mosrx.TRACE_S64, 32_768, 256, "config #2 header-only as S64_hdr, 16-byte records"),
+    # the same frames packed back to back (60-byte stride, every frame at a different
+    # alignment) instead of at 16-byte boundary + 2: the inter-frame pad is the 64 B
+    # rows' only traffic beyond the algorithmic bytes (diagnostic row)
+    "S64_hdr_packed": (mosrx.TRACE_S64, 32_768, 256, "config #2 header-only, 8-byte records, frames packed back to "
+                                                     "back (60 B stride)"),
     "IMIX": (mosrx.TRACE_IMIX, 262_144, 8, "IMIX 60/590/1514 7:4:1, 1M flows, batch=256K (BASELINE config #4)"),
     # one kernel launch per batch, two batches in flight (two rx queues)
     "M1500_1": (mosrx.TRACE_M1500, 65_536, 0, "config #3, one launch per 64K batch"),
@@ -73,8 +78,8 @@ WORKLOADS = {
     "S64_cls_bpf_ring": (mosrx.TRACE_S64, 32_768, 256, "config #2 classify + 8 BPF programs fused, one batch-queue "
                                                        "launch over 256 batches"),
 }
-DEFAULT_WORKLOADS = ("M1500,S64,S64_hdr,S64_hdr16,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,M1500_tx,IMIX_bpf,"
-                     "IMIX_cls_bpf,IMIX_cls_bpf_ring,S64_cls_bpf_ring")
+DEFAULT_WORKLOADS = ("M1500,S64,S64_hdr,S64_hdr16,S64_hdr_packed,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,"
+                     "M1500_tx,IMIX_bpf,IMIX_cls_bpf,IMIX_cls_bpf_ring,S64_cls_bpf_ring")
 OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_ti": mosrx.OP_CLASSIFY_TI, "M1500_tx": mosrx.OP_TX_CSUM,
        "IMIX_bpf": mosrx.OP_BPF, "IMIX_cls_bpf": mosrx.OP_CLASSIFY_BPF}
 # filter expressions whose compiled programs (tests/golden/bpf.npz, mOS's own compiler) the BPF row runs
@@ -141,7 +146,7 @@ def algo_bytes(tr: mosrx.Trace, key: str = "") -> int:
         return tr.caplen_sum + tr.n * (DESC_BYTES + 4)
     if "_cls_bpf" in key:          # the classify bytes + the 4-byte match mask
         return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES + 4)
-    if key == "S64_hdr":           # 8-byte compact records
+    if key in ("S64_hdr", "S64_hdr_packed"):   # 8-byte compact records
         return tr.caplen_sum + tr.n * (DESC_BYTES + 8)
     if key.endswith("_bpf"):
         return tr.n * (DESC_BYTES + 4) + int(np.minimum(tr.len, 64).astype(np.int64).sum())
@@ -195,6 +200,24 @@ def kernel_duration(stamped, back_to_back: float):
     return back_to_back, "HIP events around back-to-back launches, median of 5"
 
 
+def pack_uniform(t: mosrx.Trace) -> mosrx.Trace:
+    """Trace t with its frames packed back to back (all frames one length, as in the
+    64 B traces): frame i at 2 + i * len instead of at a 16-byte boundary + 2."""
+    ln = int(t.len[0])
+    assert (t.len == ln).all() and (np.diff(t.off.astype(np.int64)) == int(t.off[1]) - int(t.off[0])).all()
+    stride = int(t.off[1]) - int(t.off[0])
+    rows = t.frames[int(t.off[0]):int(t.off[0]) + stride * t.n].reshape(t.n, stride)[:, :ln]
+    p = mosrx.Trace.__new__(mosrx.Trace)
+    p.n = t.n
+    p.frames = np.zeros(2 + ln * t.n + 64, np.uint8)
+    p.frames[2:2 + ln * t.n] = rows.reshape(-1)
+    p.off = (2 + ln * np.arange(t.n, dtype=np.uint64)).astype(np.uint32)
+    p.len = t.len.copy()
+    p.frames_bytes = 2 + ln * t.n
+    p.max_len, p.caplen_sum = t.max_len, t.caplen_sum
+    return p
+
+
 def resident_batches(ctx, key, world, rank, nres):
     """`nres` resident batches of this rank's share of the job: the contents of its
     first job batches (seeded per job batch; DISTINCT of them for a ring, 2 for the
@@ -204,6 +227,8 @@ def resident_batches(ctx, key, world, rank, nres):
     nd = min(DISTINCT, ring) if ring else 2
     mine = job_batches(world * nd, world, rank)[:nd]
     trs = [mosrx.Trace(kind, batch, seed=job_seed(kind, b)) for b in mine]
+    if key.endswith("_packed"):
+        trs = [pack_uniform(t) for t in trs]
     dbs = [ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len)
            for t in (trs[i % len(trs)] for i in range(nres))]
     return dbs, trs, mine
@@ -254,7 +279,8 @@ def measure(ctx, dist, key, steps, warmup, rank):
         # disjoint resident copies cycle so the working set stays past the L3
         if "_cls_bpf" in key:
             ctx.bpf_set(bpf_bench_programs())   # (compiled before the queues run)
-        qs = [ctx.queue_ex(dbs[i:i + ring], match="_cls_bpf" in key, compact=key == "S64_hdr")
+        compact = key in ("S64_hdr", "S64_hdr_packed")
+        qs = [ctx.queue_ex(dbs[i:i + ring], match="_cls_bpf" in key, compact=compact)
               for i in range(0, len(dbs), ring)]
         prewarm(lambda: qs[0].time(8, qs[1:], kernels=False))
         if warmup:
@@ -276,7 +302,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         frames_per_step, ab_step = batch * ring, ab * ring
         method = f"one batch-queue launch per step over {ring} resident batches" + (
             " (fused classify + BPF queue kernel)" if "_cls_bpf" in key else
-            ", 8-byte records" if key == "S64_hdr" else "")
+            ", 8-byte records" if compact else "")
     else:
         prewarm(lambda: ctx.time_dev_streams(dbs, 200, STREAMS))
         if warmup:

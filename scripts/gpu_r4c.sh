@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 out=gpurun_out/r4c
 mkdir -p $out
-timeout -k 10 600 python -u bench.py --workloads S64,S64_hdr,S64_hdr16,IMIX,IMIX_cls_bpf,IMIX_cls_bpf_ring,S64_cls_bpf_ring \
+timeout -k 10 600 python -u bench.py --workloads S64,S64_hdr,S64_hdr16,S64_hdr_packed,IMIX,IMIX_cls_bpf,IMIX_cls_bpf_ring,S64_cls_bpf_ring \
     --no-cpu --steps 20 --warmup 5 --detail $out/bench_detail.json > $out/bench.out 2> $out/bench.err
 rc=$?; echo "bench rc=$rc"; grep "^\[bench\]" $out/bench.err
 python3 - <<'PY'

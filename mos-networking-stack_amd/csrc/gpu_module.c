@@ -405,6 +405,15 @@ static uint64_t auto_bytes(void)
  * frames that can fit (a staged frame takes >= 64 bytes of block).  When the
  * host cannot pin that much, the block is halved until it can, down to one
  * worst-case batch: smaller groups, not a dead mTCP thread. */
+/* The BPF match arrays: with the group when filters are configured, and
+ * always inside mOS, where a monitor can bind a filter at any time -- pinning
+ * them at the first bind would stall the mTCP thread for milliseconds. */
+#ifdef MOSRX_HAVE_MOS_IO_MODULE
+#define MATCH_UP_FRONT 1
+#else
+#define MATCH_UP_FRONT (g_cfg.bpf_nprog != 0)
+#endif
+
 static int group_alloc_sized(mosrx_ctx *mc, struct group *g, uint64_t bytes)
 {
 	memset(g, 0, sizeof(*g));
@@ -423,7 +432,7 @@ static int group_alloc_sized(mosrx_ctx *mc, struct group *g, uint64_t bytes)
 	if (!g->st || mosrx_host_alloc(mc, g->blk_bytes, (void **)&g->blk) ||
 	    mosrx_host_alloc(mc, g->rec_cap * sizeof(mosrx_result), (void **)&g->res) ||
 	    (g_cfg.tcpinfo && mosrx_host_alloc(mc, g->rec_cap * sizeof(mosrx_tcpinfo), (void **)&g->ti)) ||
-	    (g_cfg.bpf_nprog && mosrx_host_alloc(mc, g->rec_cap * 4, (void **)&g->match)) ||
+	    (MATCH_UP_FRONT && mosrx_host_alloc(mc, g->rec_cap * 4, (void **)&g->match)) ||
 	    (g_cfg.flowhash && mosrx_host_alloc(mc, g->rec_cap * 4, (void **)&g->fh)))
 		return -ENOMEM;
 	return 0;

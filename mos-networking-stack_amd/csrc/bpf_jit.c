@@ -509,6 +509,15 @@ static int compile_code_h(const char *src, int nh, const char *const *htexts, co
 		rc = -EIO;
 	hiprtcDestroyProgram(&prog);
 	pthread_mutex_unlock(&g_rtc_lock);
+	if (!rc && getenv("MOSRX_BPF_DUMP")) {   /* diagnostics: the code object, for llvm-readelf --notes */
+		char path[512];
+		FILE *f;
+		snprintf(path, sizeof(path), "%s.%s.co", getenv("MOSRX_BPF_DUMP"), nh ? "fused" : "set");
+		if ((f = fopen(path, "wb"))) {
+			fwrite(*code, 1, sz, f);
+			fclose(f);
+		}
+	}
 	if (rc) {
 		free(*code);
 		*code = NULL;

@@ -841,8 +841,10 @@ def main():
         e2e = {k: measure_e2e(ctx, traces[k], {"M1500": 60, "S64": 800}[k]) for k in ("M1500", "S64") if k in traces}
         # the gpu_module_func backend itself (host thread = this rank)
         # the module's default configuration (cfg.group auto: batches per launch sized to what is ready)
-        e2e["backend"] = {k: measure_backend(traces[k], k, {"S64": 32_000_000, "M1500": 2_000_000}.get(k, 4_000_000),
-                                             device, group=0)
+        # (frames through each leg: enough that the timed part holds several launches after the
+        # warm-up's pipelined group -- an IMIX auto group is 3 batches of 100 MB)
+        target = {"S64": 32_000_000, "M1500": 2_000_000, "IMIX": 12_000_000}
+        e2e["backend"] = {k: measure_backend(traces[k], k, target[k], device, group=0)
                           for k in ("M1500", "S64", "IMIX") if k in traces}
         # one launch per batch, and explicit rings (cfg.group)
         if "S64" in traces:
@@ -853,7 +855,7 @@ def main():
             e2e["backend"]["S64_bpf"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=0,
                                                         bpf=bpf_bench_programs())
         if "IMIX" in traces:
-            e2e["backend"]["IMIX_bpf"] = measure_backend(traces["IMIX"], "IMIX", 4_000_000, device, group=0,
+            e2e["backend"]["IMIX_bpf"] = measure_backend(traces["IMIX"], "IMIX", 12_000_000, device, group=0,
                                                          bpf=bpf_bench_programs())
         if "M1500" in traces:
             e2e["backend"]["M1500_group1"] = measure_backend(traces["M1500"], "M1500", 2_000_000, device, group=1)

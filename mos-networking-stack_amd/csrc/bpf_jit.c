@@ -157,6 +157,7 @@ static void gen_abs_check(struct sbuf *s, unsigned j, uint32_t k, uint32_t size)
 struct genopt {
 	int fused;          /* 0: standalone kernel (staged bytes); 1: classify header wave (its window) */
 	uint32_t stage_w;   /* standalone: realigned staged dwords in w[] */
+	uint32_t wend;      /* fused: the header window the tiles load for the set ends at frame byte wend */
 };
 
 /* Constant-offset load expression.  Standalone: registers when frame bytes
@@ -165,7 +166,7 @@ struct genopt {
 static void gen_ld(struct sbuf *s, uint32_t k, uint32_t size, const struct genopt *g)
 {
 	if (g->fused) {
-		if (k >= 2 && (uint64_t)k + 8 <= 94)
+		if (k >= 2 && (uint64_t)k + 8 <= g->wend)
 			sb_printf(s, "RW32(%uu)", k);
 		else
 			sb_printf(s, "hk_ld_le32(rs, o + %uu)", k);
@@ -187,7 +188,7 @@ static void gen_ind(struct sbuf *s, uint32_t k, uint32_t size, const struct geno
 		sb_printf(s, "fr_le32(win, sh, rs, o, kk, %uu)", size);
 		return;
 	}
-	if ((uint64_t)k + 20 + 8 <= 94) {
+	if ((uint64_t)k + 20 + 8 <= g->wend) {
 		sb_printf(s, "(X == 20u ? ");
 		gen_ld(s, k + 20, size, g);
 		sb_printf(s, " : hk_ld_le32(rs, o + kk))");
@@ -369,7 +370,7 @@ int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, c
 {
 	struct sbuf s = {0};
 	const uint32_t v = stage_pieces(insns, t);
-	const struct genopt g = {0, 4 * v - 1};
+	const struct genopt g = {0, 4 * v - 1, 0};
 	uint32_t j;
 	int rc;
 	*out = NULL;
@@ -448,14 +449,41 @@ static const char *const k_fused_names[MOSRX_BPF_NFUSED] = {
 	"mosrx_classify_bpf_stream", "mosrx_classify_bpf_stream_rt", "mosrx_classify_bpf_small",
 	"mosrx_classify_bpf_queue_stream", "mosrx_classify_bpf_queue_stream_rt", "mosrx_classify_bpf_queue_small"};
 
+/* The header window a fused set needs: every constant-offset load at frame
+ * bytes [k, k + 8) with k >= 2 -- and every indexed load at its speculated
+ * offset k + 20 -- inside it is read from the window's registers, anything
+ * else from memory.  The smallest of the tiles' windows (62 / 78 / 94 bytes:
+ * 4 / 5 / 6 chunks) that holds them, so the fused tiles load no more than the
+ * classify tiles for the filters mOS compiles (they read Ethernet, IP and
+ * TCP header fields). */
+static uint32_t hook_wend(const mosrx_bpf_insn *insns, const mosrx_bparams *t)
+{
+	uint64_t need = 18;   /* the datagram-length probe reads frame bytes 12..17 */
+	uint32_t j, i;
+	for (j = 0; j < t->nprog; j++)
+		for (i = 0; i < t->prog_len[j]; i++) {
+			const mosrx_bpf_insn *f = &insns[t->prog_off[j] + i];
+			const uint16_t c = f->code;
+			uint64_t end = 0;
+			if (c == (LD | W | ABS) || c == (LD | H | ABS) || c == (LD | B | ABS) || c == (LDX | MSH | B))
+				end = f->k >= 2 ? (uint64_t)f->k + 8 : 0;
+			else if (c == (LD | W | IND) || c == (LD | H | IND) || c == (LD | B | IND))
+				end = (uint64_t)f->k + 20 + 8;
+			if (end > need && end <= MOSRX_WINDOW_END_FULL)
+				need = end;
+		}
+	return need <= MOSRX_WINDOW_END_STREAM ? MOSRX_WINDOW_END_STREAM
+	     : need <= MOSRX_WINDOW_END_SMALL ? MOSRX_WINDOW_END_SMALL : MOSRX_WINDOW_END_FULL;
+}
+
 int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out)
 {
 	struct sbuf s = {0};
-	const struct genopt g = {1, 0};
+	const struct genopt g = {1, 0, hook_wend(insns, t)};
 	uint32_t j;
 	int rc;
 	*out = NULL;
-	sb_printf(&s, "/* generated by bpf_jit.c */\n%s", k_hook_pre);
+	sb_printf(&s, "/* generated by bpf_jit.c */\n#define MOSRX_BPF_WEND %u\n%s", g.wend, k_hook_pre);
 	for (j = 0; j < t->nprog; j++)
 		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u, &g))) {
 			free(s.p);

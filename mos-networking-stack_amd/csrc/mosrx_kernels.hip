@@ -175,8 +175,14 @@ __device__ __forceinline__ void hdr_load(__amdgpu_buffer_rsrc_t rs, uint32_t nby
 }
 
 #ifdef MOSRX_RTC_BPF
-#include "mosrx_bpf_hook.h"   // generated by bpf_jit.c: mosrx_bpf_hook(win, o, cap, live, rs)
+#include "mosrx_bpf_hook.h"   // generated by bpf_jit.c: mosrx_bpf_hook(win, o, cap, live, rs), MOSRX_BPF_WEND
 #endif
+// The window a fused set reads from registers (bpf_jit.c hook_wend): the BPF
+// tiles load at least up to it.
+#ifndef MOSRX_BPF_WEND
+#define MOSRX_BPF_WEND MOSRX_WINDOW_END_FULL
+#endif
+#define BPF_NLOAD(wend) (WIN_NLOAD(wend) > WIN_NLOAD(MOSRX_BPF_WEND) ? WIN_NLOAD(wend) : WIN_NLOAD(MOSRX_BPF_WEND))
 
 // ip_fast_csum (ip_in.h:10-38) over the realigned header (w[3] = IP dword 0):
 // 32-bit adc chain, the final carry added once (its own carry lost), fold, not.
@@ -594,8 +600,8 @@ template <int VAR, uint32_t TILE = MOSRX_KIND_FRAMES(MOSRX_KIND_SMALL), int DBG 
 __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uint32_t tile)
 {
 	constexpr int AUX = TAIL_AUX(VAR);
-	// the fused BPF hook reads the whole 96-byte window
-	constexpr int NLOAD = (VAR & VAR_BPF) ? WIN_RAW / 4 : WIN_NLOAD(WEND);
+	// the fused BPF hook reads the window up to MOSRX_BPF_WEND
+	constexpr int NLOAD = (VAR & VAR_BPF) ? BPF_NLOAD(WEND) : WIN_NLOAD(WEND);
 	constexpr int RSS = (DBG & 16384) ? 1 : 0;   // probe builds: no Toeplitz (hdr_parse RSS form 1)
 	// DBG 2 skips the window loads, DBG 4 the record stores (probe builds only).  Tried and slower:
 	// windows staged through LDS from contiguous wave loads (64 B config 192 vs
@@ -1027,7 +1033,7 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 	constexpr int AUX = TAIL_AUX(VAR);
 	// DBG 2048: the full 96-byte window (the round-1 form, 4 % slower)
 	constexpr int WEND = (DBG & 2048) ? MOSRX_WINDOW_END_FULL : MOSRX_WINDOW_END_STREAM;
-	constexpr int NLOAD = (VAR & VAR_BPF) ? WIN_RAW / 4 : WIN_NLOAD(WEND);
+	constexpr int NLOAD = (VAR & VAR_BPF) ? BPF_NLOAD(WEND) : WIN_NLOAD(WEND);
 	// DBG 16384 / 32768 / 65536: RSS form 1 / 2 / 3 of hdr_parse (probe builds)
 	constexpr int RSS = (DBG & 16384) ? 1 : (DBG & 32768) ? 2 : (DBG & 65536) ? 3 : 0;
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS + (RSS == 2 ? 12 * 256 : 0)];

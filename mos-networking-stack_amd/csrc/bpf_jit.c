@@ -407,12 +407,9 @@ static const char k_hook_pre[] =
 	"/* frame bytes [k, k+4), k constant in [2, 86]: the realigned window registers */\n"
 	"#define RW32(k) (((k) - 2u) % 4u == 0u ? w[((k) - 2u) / 4u] \\\n"
 	"                 : __builtin_amdgcn_alignbyte(w[((k) - 2u) / 4u + 1u], w[((k) - 2u) / 4u], ((k) - 2u) % 4u))\n"
-	"static __device__ __attribute__((always_inline)) inline u32 mosrx_bpf_hook(const hdr_win_t &win, u32 o, u32 cap,\n"
+	"/* w: the header wave's realigned window, frame bytes [4j + 2, 4j + 6) in w[j], valid up to MOSRX_BPF_WEND */\n"
+	"static __device__ __attribute__((always_inline)) inline u32 mosrx_bpf_hook(const u32 *w, u32 o, u32 cap,\n"
 	"    bool live, __amdgpu_buffer_rsrc_t rs) {\n"
-	"  u32 w[WIN_DW];\n"
-	"  const u32 rsh = (o + 2u) & 3u;\n"
-	"#pragma unroll\n"
-	"  for (int j = 0; j < WIN_DW; j++) w[j] = __builtin_amdgcn_alignbyte(win.raw[j + 1], win.raw[j], rsh);\n"
 	"  u32 lip = 0;\n"
 	"  if (cap >= 18u && be16hi(w[2]) == 0x0800u) {\n"
 	"    lip = 14u + be16hi(w[3]);\n"

@@ -153,6 +153,7 @@ struct hdr_t {
 	uint32_t tcw, ipc_tx;          // TX: segment-grid TCP check word, IP checksum with check = 0
 	int verdict;
 	bool fields, need_tcp, has_tail, is_tcp, tx_ip;
+	uint32_t bmatch;               // BPF: the fused set's match mask (VAR_BPF)
 };
 
 struct hdr_win_t {
@@ -175,7 +176,7 @@ __device__ __forceinline__ void hdr_load(__amdgpu_buffer_rsrc_t rs, uint32_t nby
 }
 
 #ifdef MOSRX_RTC_BPF
-#include "mosrx_bpf_hook.h"   // generated by bpf_jit.c: mosrx_bpf_hook(win, o, cap, live, rs), MOSRX_BPF_WEND
+#include "mosrx_bpf_hook.h"   // generated by bpf_jit.c: mosrx_bpf_hook(w, o, cap, live, rs), MOSRX_BPF_WEND
 #endif
 // The window a fused set reads from registers (bpf_jit.c hook_wend): the BPF
 // tiles load at least up to it.
@@ -286,12 +287,21 @@ __device__ __forceinline__ hdr_t hdr_parse(hdr_win_t win, uint32_t o, uint32_t c
                                            uint32_t nbytes)
 {
 	constexpr int NDW = WIN_NDW(WEND), NLOAD = WIN_NLOAD(WEND);
+	// a fused BPF set reads the realigned window up to MOSRX_BPF_WEND (the tile loaded it)
+	constexpr int NDW_R = (VAR & VAR_BPF) && WIN_NDW(MOSRX_BPF_WEND) > NDW ? WIN_NDW(MOSRX_BPF_WEND) : NDW;
 	hdr_t h;
 	uint32_t w[WIN_DW];
 	const uint32_t rsh = (o + 2u) & 3u;
 #pragma unroll
-	for (int j = 0; j < NDW; j++)
+	for (int j = 0; j < NDW_R; j++)
 		w[j] = __builtin_amdgcn_alignbyte(win.raw[j + 1], win.raw[j], rsh);
+	h.bmatch = 0;
+#ifdef MOSRX_RTC_BPF
+	// the set first, on the registers the parse is about to read: no second
+	// realignment, and the raw window is dead from here on
+	if constexpr ((VAR & VAR_BPF) != 0)
+		h.bmatch = mosrx_bpf_hook(w, o, cap, active, rs);
+#endif
 
 	// frame byte f sits in byte (f-2)&3 of w[(f-2)>>2]
 	const uint32_t h_proto = be16hi(w[2]);            // frame bytes 12,13  (eth_in.c:34)
@@ -702,9 +712,8 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	}
 #ifdef MOSRX_RTC_BPF
 	if constexpr ((VAR & VAR_BPF) != 0) {
-		const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs);
 		if (active)
-			out_store(kp.bmatch, p, m);
+			out_store(kp.bmatch, p, h.bmatch);
 	}
 #endif
 	}
@@ -1133,9 +1142,8 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 				}
 #ifdef MOSRX_RTC_BPF
 				if constexpr ((VAR & VAR_BPF) != 0) {
-					const uint32_t m = mosrx_bpf_hook(win, o, cap, active, rs);
 					if (active)
-						out_store(kp.bmatch, p, m);
+						out_store(kp.bmatch, p, h.bmatch);
 				}
 #endif
 				const hdr_pend_t q =

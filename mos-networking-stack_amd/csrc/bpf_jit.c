@@ -144,12 +144,14 @@ static const char k_preamble[] =
 	"  }\n"
 	"  u32 match = 0;\n";
 
-/* bounds test "(u64)off + size > L" for a constant offset: 1 = always out of range */
-static void gen_abs_check(struct sbuf *s, unsigned j, uint32_t k, uint32_t size)
+/* bounds test "(u64)off + size > L" for a constant offset: 1 = always out of range.
+ * In a program's fast copy (`lp` "F") L covers every constant offset: only the
+ * offsets past any length (2^32) remain. */
+static void gen_abs_check(struct sbuf *s, unsigned j, uint32_t k, uint32_t size, const char *lp)
 {
 	if ((uint64_t)k + size > 0xFFFFFFFFull)
 		sb_printf(s, "goto P%u_R0; ", j);
-	else
+	else if (!*lp)
 		sb_printf(s, "if (%uu > L) goto P%u_R0; ", (unsigned)(k + size), j);
 }
 
@@ -197,12 +199,105 @@ static void gen_ind(struct sbuf *s, uint32_t k, uint32_t size, const struct geno
 	}
 }
 
+/* One copy of program j's instructions, labels P<j>_<lp><i>: lp "" checks
+ * every constant-offset load against L as sfbpf_filter does; lp "F" is the
+ * copy for lanes whose L covers all of them (frames long enough for every
+ * header field the program reads -- nearly all), with those checks left out:
+ * half the branches of a typical filter. */
+static int gen_body(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_t len, const uint8_t *tgt,
+                    const char *lp, const struct genopt *g)
+{
+	uint32_t i;
+	for (i = 0; i < len; i++) {
+		const uint16_t c = f[i].code;
+		const uint32_t k = f[i].k;
+		const unsigned jt = i + 1 + f[i].jt, jf = i + 1 + f[i].jf;
+		if (tgt[i])
+			sb_printf(s, "  P%u_%s%u: ", j, lp, (unsigned)i);
+		else
+			sb_printf(s, "    ");
+		switch (c) {
+		case RET | K: sb_printf(s, "ret = %uu; goto P%u_E;", k, j); break;
+		case RET | A: sb_printf(s, "ret = A; goto P%u_E;", j); break;
+		case LD | W | ABS:
+			gen_abs_check(s, j, k, 4, lp); sb_printf(s, "A = be32("); gen_ld(s, k, 4, g); sb_printf(s, ");");
+			break;
+		case LD | H | ABS:
+			gen_abs_check(s, j, k, 2, lp); sb_printf(s, "A = be16("); gen_ld(s, k, 2, g); sb_printf(s, ");");
+			break;
+		case LD | B | ABS:
+			gen_abs_check(s, j, k, 1, lp); sb_printf(s, "A = "); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFFu;");
+			break;
+		case LD | W | LEN: sb_printf(s, "A = L;"); break;
+		case LDX | W | LEN: sb_printf(s, "X = L;"); break;
+		case LD | W | IND:
+			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 4u > L) goto P%u_R0; A = be32(", k, j);
+			gen_ind(s, k, 4, g);
+			sb_printf(s, "); }");
+			break;
+		case LD | H | IND:
+			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 2u > L) goto P%u_R0; A = be16(", k, j);
+			gen_ind(s, k, 2, g);
+			sb_printf(s, "); }");
+			break;
+		case LD | B | IND:
+			sb_printf(s, "{ const u32 kk = X + %uu; if (kk >= L) goto P%u_R0; A = ", k, j);
+			gen_ind(s, k, 1, g);
+			sb_printf(s, " & 0xFFu; }");
+			break;
+		case LDX | MSH | B:
+			gen_abs_check(s, j, k, 1, lp);
+			sb_printf(s, "X = ("); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFu) << 2;");
+			break;
+		case LD | IMM: sb_printf(s, "A = %uu;", k); break;
+		case LDX | IMM: sb_printf(s, "X = %uu;", k); break;
+		case LD | MEM: sb_printf(s, "A = M%u;", k & 15); break;
+		case LDX | MEM: sb_printf(s, "X = M%u;", k & 15); break;
+		case ST: sb_printf(s, "M%u = A;", k & 15); break;
+		case STX: sb_printf(s, "M%u = X;", k & 15); break;
+		case JMP | JA: sb_printf(s, "goto P%u_%s%u;", j, lp, (unsigned)(i + 1 + k)); break;
+		case JMP | JGT | K: sb_printf(s, "if (A > %uu) goto P%u_%s%u; goto P%u_%s%u;", k, j, lp, jt, j, lp, jf); break;
+		case JMP | JGE | K: sb_printf(s, "if (A >= %uu) goto P%u_%s%u; goto P%u_%s%u;", k, j, lp, jt, j, lp, jf); break;
+		case JMP | JEQ | K: sb_printf(s, "if (A == %uu) goto P%u_%s%u; goto P%u_%s%u;", k, j, lp, jt, j, lp, jf); break;
+		case JMP | JSET | K: sb_printf(s, "if (A & %uu) goto P%u_%s%u; goto P%u_%s%u;", k, j, lp, jt, j, lp, jf); break;
+		case JMP | JGT | X: sb_printf(s, "if (A > X) goto P%u_%s%u; goto P%u_%s%u;", j, lp, jt, j, lp, jf); break;
+		case JMP | JGE | X: sb_printf(s, "if (A >= X) goto P%u_%s%u; goto P%u_%s%u;", j, lp, jt, j, lp, jf); break;
+		case JMP | JEQ | X: sb_printf(s, "if (A == X) goto P%u_%s%u; goto P%u_%s%u;", j, lp, jt, j, lp, jf); break;
+		case JMP | JSET | X: sb_printf(s, "if (A & X) goto P%u_%s%u; goto P%u_%s%u;", j, lp, jt, j, lp, jf); break;
+		case ALU | ADD | X: sb_printf(s, "A += X;"); break;
+		case ALU | SUB | X: sb_printf(s, "A -= X;"); break;
+		case ALU | MUL | X: sb_printf(s, "A *= X;"); break;
+		case ALU | DIV | X: sb_printf(s, "if (X == 0u) goto P%u_R0; A /= X;", j); break;
+		case ALU | AND | X: sb_printf(s, "A &= X;"); break;
+		case ALU | OR | X: sb_printf(s, "A |= X;"); break;
+		case ALU | LSH | X: sb_printf(s, "A <<= (X & 31u);"); break;
+		case ALU | RSH | X: sb_printf(s, "A >>= (X & 31u);"); break;
+		case ALU | ADD | K: sb_printf(s, "A += %uu;", k); break;
+		case ALU | SUB | K: sb_printf(s, "A -= %uu;", k); break;
+		case ALU | MUL | K: sb_printf(s, "A *= %uu;", k); break;
+		case ALU | DIV | K: sb_printf(s, "A /= %uu;", k); break;        /* k != 0 (mosrx_bpf_check) */
+		case ALU | AND | K: sb_printf(s, "A &= %uu;", k); break;
+		case ALU | OR | K: sb_printf(s, "A |= %uu;", k); break;
+		case ALU | LSH | K: sb_printf(s, "A <<= %uu;", k & 31u); break;
+		case ALU | RSH | K: sb_printf(s, "A >>= %uu;", k & 31u); break;
+		case ALU | NEG: sb_printf(s, "A = 0u - A;"); break;
+		case MISC | TAX: sb_printf(s, "X = A;"); break;
+		case MISC | TXA: sb_printf(s, "A = X;"); break;
+		default:   /* rejected by mosrx_bpf_check */
+			return -EINVAL;
+		}
+		sb_printf(s, "\n");
+	}
+	return 0;
+}
+
 static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_t len, int ipm,
                        const struct genopt *g)
 {
 	uint8_t *tgt, mem_used[16];
 	uint32_t i, q;
-	int need_r0 = 0;
+	uint64_t maxk = 0;   /* every constant-offset load lies below it */
+	int rc;
 
 	sb_printf(s, "  { /* program %u, %u insns, %s length */\n", j, (unsigned)len, ipm ? "datagram" : "frame");
 	if (len == 0) {
@@ -225,9 +320,12 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 		}
 		if (c == (LD | MEM) || c == (LDX | MEM) || c == ST || c == STX)
 			mem_used[f[i].k & 15] = 1;
-		if (c == (LD | W | ABS) || c == (LD | H | ABS) || c == (LD | B | ABS) || c == (LD | W | IND) ||
-		    c == (LD | H | IND) || c == (LD | B | IND) || c == (LDX | MSH | B) || c == (ALU | DIV | X))
-			need_r0 = 1;
+		{
+			const uint64_t end = c == (LD | W | ABS) ? (uint64_t)f[i].k + 4 : c == (LD | H | ABS) ? (uint64_t)f[i].k + 2
+			                   : c == (LD | B | ABS) || c == (LDX | MSH | B) ? (uint64_t)f[i].k + 1 : 0;
+			if (end <= 0xFFFFFFFFull && end > maxk)
+				maxk = end;
+		}
 	}
 	sb_printf(s, "    u32 A = 0, X = 0, ret = 0;\n");
 	for (q = 0; q < 16; q++)
@@ -235,89 +333,19 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 			sb_printf(s, "    u32 M%u = 0;\n", q);
 	sb_printf(s, "    const u32 L = %s;\n", ipm ? "lip" : "cap");
 	sb_printf(s, "    if (!live%s) goto P%u_E;\n", ipm ? " || lip == 0u" : "", j);
-	for (i = 0; i < len; i++) {
-		const uint16_t c = f[i].code;
-		const uint32_t k = f[i].k;
-		const unsigned jt = i + 1 + f[i].jt, jf = i + 1 + f[i].jf;
-		if (tgt[i])
-			sb_printf(s, "  P%u_%u: ", j, (unsigned)i);
-		else
-			sb_printf(s, "    ");
-		switch (c) {
-		case RET | K: sb_printf(s, "ret = %uu; goto P%u_E;", k, j); break;
-		case RET | A: sb_printf(s, "ret = A; goto P%u_E;", j); break;
-		case LD | W | ABS:
-			gen_abs_check(s, j, k, 4); sb_printf(s, "A = be32("); gen_ld(s, k, 4, g); sb_printf(s, ");");
-			break;
-		case LD | H | ABS:
-			gen_abs_check(s, j, k, 2); sb_printf(s, "A = be16("); gen_ld(s, k, 2, g); sb_printf(s, ");");
-			break;
-		case LD | B | ABS:
-			gen_abs_check(s, j, k, 1); sb_printf(s, "A = "); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFFu;");
-			break;
-		case LD | W | LEN: sb_printf(s, "A = L;"); break;
-		case LDX | W | LEN: sb_printf(s, "X = L;"); break;
-		case LD | W | IND:
-			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 4u > L) goto P%u_R0; A = be32(", k, j);
-			gen_ind(s, k, 4, g);
-			sb_printf(s, "); }");
-			break;
-		case LD | H | IND:
-			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 2u > L) goto P%u_R0; A = be16(", k, j);
-			gen_ind(s, k, 2, g);
-			sb_printf(s, "); }");
-			break;
-		case LD | B | IND:
-			sb_printf(s, "{ const u32 kk = X + %uu; if (kk >= L) goto P%u_R0; A = ", k, j);
-			gen_ind(s, k, 1, g);
-			sb_printf(s, " & 0xFFu; }");
-			break;
-		case LDX | MSH | B:
-			gen_abs_check(s, j, k, 1);
-			sb_printf(s, "X = ("); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFu) << 2;");
-			break;
-		case LD | IMM: sb_printf(s, "A = %uu;", k); break;
-		case LDX | IMM: sb_printf(s, "X = %uu;", k); break;
-		case LD | MEM: sb_printf(s, "A = M%u;", k & 15); break;
-		case LDX | MEM: sb_printf(s, "X = M%u;", k & 15); break;
-		case ST: sb_printf(s, "M%u = A;", k & 15); break;
-		case STX: sb_printf(s, "M%u = X;", k & 15); break;
-		case JMP | JA: sb_printf(s, "goto P%u_%u;", j, (unsigned)(i + 1 + k)); break;
-		case JMP | JGT | K: sb_printf(s, "if (A > %uu) goto P%u_%u; goto P%u_%u;", k, j, jt, j, jf); break;
-		case JMP | JGE | K: sb_printf(s, "if (A >= %uu) goto P%u_%u; goto P%u_%u;", k, j, jt, j, jf); break;
-		case JMP | JEQ | K: sb_printf(s, "if (A == %uu) goto P%u_%u; goto P%u_%u;", k, j, jt, j, jf); break;
-		case JMP | JSET | K: sb_printf(s, "if (A & %uu) goto P%u_%u; goto P%u_%u;", k, j, jt, j, jf); break;
-		case JMP | JGT | X: sb_printf(s, "if (A > X) goto P%u_%u; goto P%u_%u;", j, jt, j, jf); break;
-		case JMP | JGE | X: sb_printf(s, "if (A >= X) goto P%u_%u; goto P%u_%u;", j, jt, j, jf); break;
-		case JMP | JEQ | X: sb_printf(s, "if (A == X) goto P%u_%u; goto P%u_%u;", j, jt, j, jf); break;
-		case JMP | JSET | X: sb_printf(s, "if (A & X) goto P%u_%u; goto P%u_%u;", j, jt, j, jf); break;
-		case ALU | ADD | X: sb_printf(s, "A += X;"); break;
-		case ALU | SUB | X: sb_printf(s, "A -= X;"); break;
-		case ALU | MUL | X: sb_printf(s, "A *= X;"); break;
-		case ALU | DIV | X: sb_printf(s, "if (X == 0u) goto P%u_R0; A /= X;", j); break;
-		case ALU | AND | X: sb_printf(s, "A &= X;"); break;
-		case ALU | OR | X: sb_printf(s, "A |= X;"); break;
-		case ALU | LSH | X: sb_printf(s, "A <<= (X & 31u);"); break;
-		case ALU | RSH | X: sb_printf(s, "A >>= (X & 31u);"); break;
-		case ALU | ADD | K: sb_printf(s, "A += %uu;", k); break;
-		case ALU | SUB | K: sb_printf(s, "A -= %uu;", k); break;
-		case ALU | MUL | K: sb_printf(s, "A *= %uu;", k); break;
-		case ALU | DIV | K: sb_printf(s, "A /= %uu;", k); break;        /* k != 0 (mosrx_bpf_check) */
-		case ALU | AND | K: sb_printf(s, "A &= %uu;", k); break;
-		case ALU | OR | K: sb_printf(s, "A |= %uu;", k); break;
-		case ALU | LSH | K: sb_printf(s, "A <<= %uu;", k & 31u); break;
-		case ALU | RSH | K: sb_printf(s, "A >>= %uu;", k & 31u); break;
-		case ALU | NEG: sb_printf(s, "A = 0u - A;"); break;
-		case MISC | TAX: sb_printf(s, "X = A;"); break;
-		case MISC | TXA: sb_printf(s, "A = X;"); break;
-		default:   /* rejected by mosrx_bpf_check */
+	if (maxk && maxk <= 65535) {   /* lengths are 16-bit: a larger bound never holds */
+		tgt[0] = 1;
+		sb_printf(s, "    if (L >= %uu) goto P%u_F0;\n", (unsigned)maxk, j);
+		if ((rc = gen_body(s, j, f, len, tgt, "", g)) || (rc = gen_body(s, j, f, len, tgt, "F", g))) {
 			free(tgt);
-			return -EINVAL;
+			return rc;
 		}
-		sb_printf(s, "\n");
+	} else if ((rc = gen_body(s, j, f, len, tgt, "", g))) {
+		free(tgt);
+		return rc;
 	}
-	if (need_r0)
-		sb_printf(s, "  P%u_R0: ret = 0;\n", j);
+	/* P<j>_R0 is always emitted (the fast copy's indexed loads and divisions jump there too) */
+	sb_printf(s, "  P%u_R0: ret = 0;\n", j);
 	sb_printf(s, "  P%u_E: if (ret) match |= %uu;\n  }\n", j, 1u << j);
 	free(tgt);
 	return 0;

@@ -160,7 +160,14 @@ struct genopt {
 	int fused;          /* 0: standalone kernel (staged bytes); 1: classify header wave (its window) */
 	uint32_t stage_w;   /* standalone: realigned staged dwords in w[] */
 	uint32_t wend;      /* fused: the header window the tiles load for the set ends at frame byte wend */
+	int pred;           /* if-converted programs (gen_pred); 0: branchy (MOSRX_BPF_PRED=0) */
 };
+
+static int pred_mode(void)
+{
+	const char *e = getenv("MOSRX_BPF_PRED");
+	return !(e && e[0] == '0');
+}
 
 /* Constant-offset load expression.  Standalone: registers when frame bytes
  * [k, k + 8) are in w[], else the LDS stage / memory (fr_le32).  Fused: the
@@ -291,6 +298,129 @@ static int gen_body(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_
 	return 0;
 }
 
+/* Program j if-converted, for the lanes whose L covers every constant-offset
+ * load: no branches.  Each lane's position is a predicate -- `c` for the
+ * instruction being emitted, b<i> for the jump targets not yet reached -- a
+ * jump moves `c` into its targets' predicates, every A / X / scratch update
+ * is a select on `c`, and a return sets the lane's hit flag `h`.  The
+ * branchy form costs the structurizer's exec-mask bookkeeping at every
+ * join (~6 scalar instructions per BPF jump); the mOS filters are short and
+ * IPv4 headers put most lanes of a wave on the same path, so evaluating
+ * every instruction for all lanes is cheaper.  Blocks of 4 or more
+ * instructions no lane reaches are skipped with a uniform branch. */
+static int gen_pred(struct sbuf *s, const mosrx_bpf_insn *f, uint32_t len, const uint8_t *tgt,
+                    const struct genopt *g)
+{
+	uint32_t i, e = 0;
+	int open = 0;
+	for (i = 1; i < len; i++)
+		if (tgt[i])
+			sb_printf(s, "    bool b%u = false;\n", (unsigned)i);
+	for (i = 0; i < len; i++) {
+		const uint16_t c = f[i].code;
+		const uint32_t k = f[i].k;
+		const unsigned jt = i + 1 + f[i].jt, jf = i + 1 + f[i].jf;
+		if (i == 0 || tgt[i]) {
+			if (i > 0)
+				sb_printf(s, "    c = c || b%u;\n", (unsigned)i);
+			/* the block: up to its jump / return, or up to the next jump target */
+			for (e = i; e + 1 < len && (f[e].code & 7) != JMP && (f[e].code & 7) != RET && !tgt[e + 1]; e++)
+				;
+			if (e - i + 1 >= 4) {
+				sb_printf(s, "    if (__any(c)) {\n");
+				open = 1;
+			}
+		}
+		sb_printf(s, "      ");
+		if ((c == (LD | W | ABS) && (uint64_t)k + 4 > 0xFFFFFFFFull) ||
+		    (c == (LD | H | ABS) && (uint64_t)k + 2 > 0xFFFFFFFFull) ||
+		    ((c == (LD | B | ABS) || c == (LDX | MSH | B)) && (uint64_t)k + 1 > 0xFFFFFFFFull)) {
+			sb_printf(s, "c = false;\n");   /* past any length: the lane returns 0 */
+			goto next;
+		}
+		switch (c) {
+		case RET | K: sb_printf(s, k ? "h = h || c; c = false;" : "c = false;"); break;
+		case RET | A: sb_printf(s, "h = h || (c && A != 0u); c = false;"); break;
+		case LD | W | ABS: sb_printf(s, "A = c ? be32("); gen_ld(s, k, 4, g); sb_printf(s, ") : A;"); break;
+		case LD | H | ABS: sb_printf(s, "A = c ? be16("); gen_ld(s, k, 2, g); sb_printf(s, ") : A;"); break;
+		case LD | B | ABS: sb_printf(s, "A = c ? ("); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFFu) : A;"); break;
+		case LD | W | LEN: sb_printf(s, "A = c ? L : A;"); break;
+		case LDX | W | LEN: sb_printf(s, "X = c ? L : X;"); break;
+		case LD | W | IND: case LD | H | IND: case LD | B | IND: {
+			const uint32_t size = (c & 0x18) == W ? 4 : (c & 0x18) == H ? 2 : 1;
+			sb_printf(s, "{ const u32 kk = X + %uu; c = c && (u64)kk + %uu <= L; u32 v; ", k, size);
+			if (g->fused && (uint64_t)k + 20 + 8 <= g->wend) {
+				/* the speculated window read; a wave with any other live X also reads memory */
+				sb_printf(s, "v = ");
+				gen_ld(s, k + 20, size, g);
+				sb_printf(s, "; if (__any(c && X != 20u)) v = X == 20u ? v : hk_ld_le32(rs, o + kk); ");
+			} else if (g->fused) {
+				sb_printf(s, "v = hk_ld_le32(rs, o + kk); ");   /* a buffer load: out-of-range offsets read 0 */
+			} else {   /* lanes off the path read the stage at offset 0, not at their X + k */
+				sb_printf(s, "v = fr_le32(win, sh, rs, o, c ? kk : 0u, %uu); ", size);
+			}
+			sb_printf(s, size == 4 ? "A = c ? be32(v) : A; }" : size == 2 ? "A = c ? be16(v) : A; }"
+			                                                             : "A = c ? (v & 0xFFu) : A; }");
+			break;
+		}
+		case LDX | MSH | B: sb_printf(s, "X = c ? (("); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFu) << 2) : X;"); break;
+		case LD | IMM: sb_printf(s, "A = c ? %uu : A;", k); break;
+		case LDX | IMM: sb_printf(s, "X = c ? %uu : X;", k); break;
+		case LD | MEM: sb_printf(s, "A = c ? M%u : A;", k & 15); break;
+		case LDX | MEM: sb_printf(s, "X = c ? M%u : X;", k & 15); break;
+		case ST: sb_printf(s, "M%u = c ? A : M%u;", k & 15, k & 15); break;
+		case STX: sb_printf(s, "M%u = c ? X : M%u;", k & 15, k & 15); break;
+		case JMP | JA: sb_printf(s, "b%u = b%u || c; c = false;", (unsigned)(i + 1 + k), (unsigned)(i + 1 + k)); break;
+		case JMP | JGT | K: case JMP | JGE | K: case JMP | JEQ | K: case JMP | JSET | K:
+		case JMP | JGT | X: case JMP | JGE | X: case JMP | JEQ | X: case JMP | JSET | X: {
+			const char *rhs = (c & 8) ? "X" : NULL;
+			char kb[16];
+			const char *op = (c & 0xf0) == JGT ? ">" : (c & 0xf0) == JGE ? ">=" : (c & 0xf0) == JEQ ? "==" : "&";
+			if (!rhs) {
+				snprintf(kb, sizeof(kb), "%uu", k);
+				rhs = kb;
+			}
+			if (jt == jf) {
+				sb_printf(s, "b%u = b%u || c; c = false;", jt, jt);
+				break;
+			}
+			sb_printf(s, (c & 0xf0) == JSET ? "{ const bool t_ = (A & %s) != 0u; " : "{ const bool t_ = A %s %s; ",
+			          (c & 0xf0) == JSET ? rhs : op, rhs);
+			sb_printf(s, "b%u = b%u || (c && t_); b%u = b%u || (c && !t_); c = false; }", jt, jt, jf, jf);
+			break;
+		}
+		case ALU | ADD | X: sb_printf(s, "A = c ? A + X : A;"); break;
+		case ALU | SUB | X: sb_printf(s, "A = c ? A - X : A;"); break;
+		case ALU | MUL | X: sb_printf(s, "A = c ? A * X : A;"); break;
+		case ALU | DIV | X: sb_printf(s, "c = c && X != 0u; A = c ? A / (X ? X : 1u) : A;"); break;
+		case ALU | AND | X: sb_printf(s, "A = c ? (A & X) : A;"); break;
+		case ALU | OR | X: sb_printf(s, "A = c ? (A | X) : A;"); break;
+		case ALU | LSH | X: sb_printf(s, "A = c ? A << (X & 31u) : A;"); break;
+		case ALU | RSH | X: sb_printf(s, "A = c ? A >> (X & 31u) : A;"); break;
+		case ALU | ADD | K: sb_printf(s, "A = c ? A + %uu : A;", k); break;
+		case ALU | SUB | K: sb_printf(s, "A = c ? A - %uu : A;", k); break;
+		case ALU | MUL | K: sb_printf(s, "A = c ? A * %uu : A;", k); break;
+		case ALU | DIV | K: sb_printf(s, "A = c ? A / %uu : A;", k); break;   /* k != 0 (mosrx_bpf_check) */
+		case ALU | AND | K: sb_printf(s, "A = c ? (A & %uu) : A;", k); break;
+		case ALU | OR | K: sb_printf(s, "A = c ? (A | %uu) : A;", k); break;
+		case ALU | LSH | K: sb_printf(s, "A = c ? A << %uu : A;", k & 31u); break;
+		case ALU | RSH | K: sb_printf(s, "A = c ? A >> %uu : A;", k & 31u); break;
+		case ALU | NEG: sb_printf(s, "A = c ? 0u - A : A;"); break;
+		case MISC | TAX: sb_printf(s, "X = c ? A : X;"); break;
+		case MISC | TXA: sb_printf(s, "A = c ? X : A;"); break;
+		default:
+			return -EINVAL;
+		}
+		sb_printf(s, "\n");
+	next:
+		if (open && i == e) {
+			sb_printf(s, "    }\n");
+			open = 0;
+		}
+	}
+	return 0;
+}
+
 static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_t len, int ipm,
                        const struct genopt *g)
 {
@@ -332,8 +462,36 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 		if (mem_used[q])
 			sb_printf(s, "    u32 M%u = 0;\n", q);
 	sb_printf(s, "    const u32 L = %s;\n", ipm ? "lip" : "cap");
+	if (g->pred && maxk <= 65535) {   /* lengths are 16-bit: a larger bound never holds */
+		const char *lv = ipm ? "live && lip != 0u" : "live";
+		sb_printf(s, "    bool h = false;\n");
+		if (maxk)
+			sb_printf(s, "    bool c = %s && L >= %uu;\n", lv, (unsigned)maxk);
+		else
+			sb_printf(s, "    bool c = %s;\n", lv);
+		if ((rc = gen_pred(s, f, len, tgt, g))) {
+			free(tgt);
+			return rc;
+		}
+		if (!maxk) {
+			sb_printf(s, "    if (h) match |= %uu;\n  }\n", 1u << j);
+			free(tgt);
+			return 0;
+		}
+		/* frames shorter than the program's furthest constant load: the checked copy */
+		sb_printf(s, "    if (__any(%s && L < %uu)) {\n    if (%s && L < %uu) {\n", lv, (unsigned)maxk, lv,
+		          (unsigned)maxk);
+		if ((rc = gen_body(s, j, f, len, tgt, "", g))) {
+			free(tgt);
+			return rc;
+		}
+		sb_printf(s, "  P%u_R0: ret = 0;\n    }}\n", j);
+		sb_printf(s, "  P%u_E: if (h || ret) match |= %uu;\n  }\n", j, 1u << j);
+		free(tgt);
+		return 0;
+	}
 	sb_printf(s, "    if (!live%s) goto P%u_E;\n", ipm ? " || lip == 0u" : "", j);
-	if (maxk && maxk <= 65535) {   /* lengths are 16-bit: a larger bound never holds */
+	if (maxk && maxk <= 65535) {
 		tgt[0] = 1;
 		sb_printf(s, "    if (L >= %uu) goto P%u_F0;\n", (unsigned)maxk, j);
 		if ((rc = gen_body(s, j, f, len, tgt, "", g)) || (rc = gen_body(s, j, f, len, tgt, "F", g))) {
@@ -398,7 +556,7 @@ int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, c
 {
 	struct sbuf s = {0};
 	const uint32_t v = stage_pieces(insns, t);
-	const struct genopt g = {0, 4 * v - 1, 0};
+	const struct genopt g = {0, 4 * v - 1, 0, pred_mode()};
 	uint32_t j;
 	int rc;
 	*out = NULL;
@@ -504,7 +662,7 @@ static uint32_t hook_wend(const mosrx_bpf_insn *insns, const mosrx_bparams *t)
 int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out)
 {
 	struct sbuf s = {0};
-	const struct genopt g = {1, 0, hook_wend(insns, t)};
+	const struct genopt g = {1, 0, hook_wend(insns, t), pred_mode()};
 	uint32_t j;
 	int rc;
 	*out = NULL;

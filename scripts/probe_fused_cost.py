@@ -4,7 +4,9 @@ programs (`ret #1`: the fused tile's fixed cost, masks stored), and fused with
 the bench's 8 mOS filters; dispatch-stamped medians.  Records and masks are
 checked against the oracle first.
 
-    python3 scripts/probe_fused_cost.py [S64|IMIX]
+    python3 scripts/probe_fused_cost.py [S64|IMIX] [set index 0-2]
+
+PROBE_SHORT=1: no prewarm and a handful of launches (for rocprofv3 --pmc passes).
 """
 import os, sys
 import numpy as np
@@ -22,6 +24,9 @@ dbs = [ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t
        for t in (trs[i % 4] for i in range(nres))]
 trivial = [(np.array([(0x06, 0, 0, 1)], mosrx.BPF_INSN), m % 2) for m in range(8)]
 sets = {"plain": None, "fused, 8 x ret #1": trivial, "fused, 8 mOS filters": bench.bpf_bench_programs()}
+if len(sys.argv) > 2:
+    sets = dict([list(sets.items())[int(sys.argv[2])]])
+short = os.environ.get("PROBE_SHORT") == "1"
 for name, ps in sets.items():
     if ps is not None:
         ctx.bpf_set(ps)
@@ -32,8 +37,9 @@ for name, ps in sets.items():
     assert np.array_equal(d.results().view(np.uint8), O.classify(t.frames, t.off, t.len, O.params()).view(np.uint8))
     if ps is not None:
         np.testing.assert_array_equal(d.matches(), O.bpf_eval(ps, t.frames[:t.frames_bytes], t.off, t.len))
-    bench.prewarm(lambda: qs[0].time(8, qs[1:], kernels=False))
-    us = [1e3 * qs[0].time_dispatch(64, qs[1:]) for _ in range(5)]
+    if not short:
+        bench.prewarm(lambda: qs[0].time(8, qs[1:], kernels=False))
+    us = [1e3 * qs[0].time_dispatch(4 if short else 64, qs[1:]) for _ in range(1 if short else 5)]
     print(f"{key} ring {ring} x {batch}: {name:24s} {np.median(us):8.2f} us per launch "
           f"(min {min(us):.2f}, max {max(us):.2f})", flush=True)
     for q in qs:

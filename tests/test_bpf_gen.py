@@ -1,0 +1,107 @@
+"""The BPF code generator's output, run on the CPU.
+
+csrc/bpf_jit.c turns a program set into gfx950 source.  Its program bodies are
+plain C once the packet-load helpers are defined, so this test compiles the
+generated text with gcc, one frame at a time (a wave with a single lane), and
+checks it against mOS's own sfbpf_filter results (tests/golden/bpf.npz) and the
+oracle.  Both code shapes are covered -- the if-converted programs
+(MOSRX_BPF_PRED, default) and the branchy form -- so a generator error shows
+here, apart from anything the GPU compiler does with the text.  No GPU.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import mosrx
+import oracle_py as O
+from test_bpf import load, program_sets, random_sets
+
+HARNESS = r"""
+#include <stdbool.h>
+#include <stdint.h>
+#include <string.h>
+typedef uint32_t u32; typedef uint64_t u64; typedef uint16_t u16; typedef uint8_t u8;
+static const u8 *g_fr;
+static u32 ld(u64 k) { u32 v; memcpy(&v, g_fr + k, 4); return v; }
+static u32 be32(u32 v) { return __builtin_bswap32(v); }
+static u32 be16(u32 v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }
+#define W32(k) ld(k)
+#define fr_le32(win, sh, rs, o, k, size) ld(k)
+#define __any(x) (x)
+void eval(const u8 *buf, u32 nbytes, const u32 *off, const u16 *len, u32 n, u32 *out)
+{
+  static const u8 zero[1 << 17];
+  for (u32 p = 0; p < n; p++) {
+    const bool live = true;
+    const u32 o = off[p], l = len[p];
+    const u32 cap = (o >= nbytes) ? 0u : (l < nbytes - o ? l : nbytes - o);
+    const int rs = 0, sh = 0; const u32 *win = 0;
+    u32 lip = 0, match = 0;
+    (void)rs; (void)sh; (void)win;
+    g_fr = o >= nbytes ? zero : buf + o;
+    if (cap >= 18u && (ld(12) & 0xFFFFu) == 0x0008u) {
+      lip = 14u + be16(ld(16));
+      if (lip > cap) lip = 0;
+    }
+    BODY
+    out[p] = match;
+  }
+}
+"""
+
+
+def build(tmp_path, ps, pred):
+    os.environ["MOSRX_BPF_PRED"] = str(pred)
+    try:
+        src = mosrx.bpf_jit_source(ps)
+    finally:
+        del os.environ["MOSRX_BPF_PRED"]
+    body = src[src.index("  u32 match = 0;\n") + len("  u32 match = 0;\n"):src.index("  if (live) match_out[p]")]
+    c = tmp_path / f"gen{pred}.c"
+    c.write_text(HARNESS.replace("BODY", body))
+    so = tmp_path / f"gen{pred}.so"
+    r = subprocess.run(["gcc", "-O1", "-shared", "-fPIC", "-w", "-o", str(so), str(c)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return C.CDLL(str(so))
+
+
+def run(lib, buf, off, ln):
+    # the if-converted programs load every constant offset below 65536 (zero padding, as the GPU's
+    # buffer descriptor returns zeros past the end)
+    padded = np.zeros(len(buf) + 70000, np.uint8)
+    padded[:len(buf)] = buf
+    off = np.ascontiguousarray(off, np.uint32)
+    ln = np.ascontiguousarray(ln, np.uint16)
+    out = np.zeros(len(off), np.uint32)
+    lib.eval(padded.ctypes.data_as(C.c_void_p), C.c_uint32(len(buf)), off.ctypes.data_as(C.c_void_p),
+             ln.ctypes.data_as(C.c_void_p), C.c_uint32(len(off)), out.ctypes.data_as(C.c_void_p))
+    return out
+
+
+@pytest.mark.parametrize("pred", [1, 0])
+def test_generated_golden_sets(tmp_path, pred):
+    z, progs = load()
+    for i, (ps, exp) in enumerate(program_sets(z, progs)):
+        d = tmp_path / str(i)
+        d.mkdir()
+        lib = build(d, ps, pred)
+        got = run(lib, z["frames"], z["off"], z["len"])
+        bad = np.nonzero(got != exp)[0]
+        assert not len(bad), (i, bad[:5], hex(int(got[bad[0]] ^ exp[bad[0]])))
+
+
+@pytest.mark.parametrize("pred", [1, 0])
+@pytest.mark.parametrize("seed", [3, 11])
+def test_generated_random_programs(tmp_path, pred, seed):
+    z, _ = load()
+    for i, ps in enumerate(random_sets(seed)):
+        d = tmp_path / str(i)
+        d.mkdir()
+        lib = build(d, ps, pred)
+        got = run(lib, z["frames"], z["off"], z["len"])
+        exp = O.bpf_eval(ps, z["frames"], z["off"], z["len"])
+        bad = np.nonzero(got != exp)[0]
+        assert not len(bad), (i, bad[:5], hex(int(got[bad[0]] ^ exp[bad[0]])))

@@ -419,6 +419,9 @@ int  mosrx_bpf_engine(const mosrx_ctx *c);
 const char *mosrx_bpf_jit_log(const mosrx_ctx *c);
 /* The generated kernel source of a program set (no GPU needed; free() it). */
 int  mosrx_bpf_jit_source(const mosrx_bpf_prog *progs, uint32_t nprog, char **src);
+/* The generated hook of the fused classify + BPF kernel: the set as the
+ * device function the header wave calls on its window (free() it). */
+int  mosrx_bpf_jit_hook_source(const mosrx_bpf_prog *progs, uint32_t nprog, char **src);
 /* Generate and compile a program set with hipRTC for gfx950 without loading
  * it (no GPU needed): 0 and the code-object size, or -errno and the log. */
 int  mosrx_bpf_jit_compile(const mosrx_bpf_prog *progs, uint32_t nprog, char *log, size_t logsz,

@@ -130,6 +130,23 @@ int mosrx_bpf_jit_source(const mosrx_bpf_prog *progs, uint32_t nprog, char **src
 	return rc;
 }
 
+int mosrx_bpf_jit_hook_source(const mosrx_bpf_prog *progs, uint32_t nprog, char **src)
+{
+	mosrx_bpf_insn *staged;
+	mosrx_bparams t;
+	uint32_t total;
+	int rc;
+	if (!src)
+		return -EINVAL;
+	*src = NULL;
+	if (!(staged = malloc(MOSRX_BPF_MAX_INSNS * sizeof(*staged))))
+		return -ENOMEM;
+	if (!(rc = stage_set(progs, nprog, &t, staged, &total)))
+		rc = mosrx__bpf_jit_hook_source(staged, &t, src);
+	free(staged);
+	return rc;
+}
+
 int mosrx_bpf_jit_compile(const mosrx_bpf_prog *progs, uint32_t nprog, char *log, size_t logsz,
                           size_t *code_size)
 {

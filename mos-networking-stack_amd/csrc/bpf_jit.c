@@ -160,13 +160,59 @@ struct genopt {
 	int fused;          /* 0: standalone kernel (staged bytes); 1: classify header wave (its window) */
 	uint32_t stage_w;   /* standalone: realigned staged dwords in w[] */
 	uint32_t wend;      /* fused: the header window the tiles load for the set ends at frame byte wend */
-	int pred;           /* if-converted programs (gen_pred); 0: branchy (MOSRX_BPF_PRED=0) */
+	int pred;           /* 1: if-converted programs (gen_pred, MOSRX_BPF_PRED=1); 0: branchy */
+	int lds;            /* fused: the hook stages the window in LDS for loads at X + k with X not 4 * ihl */
 };
 
+/* Per-instruction flags of a program: a jump target; X holds 4 * ihl (only
+ * `ldxb 4*([k]&0xf)` defines the X that reaches here). */
+enum { TG_TARGET = 1, TG_XMSH = 2 };
+
+/* Which definitions of X reach each instruction (forward over the DAG):
+ * sets TG_XMSH where every one is an MSH load.  Returns 1 if some indexed
+ * load sees any other X. */
+static int x_provenance(const mosrx_bpf_insn *f, uint32_t len, uint8_t *tg)
+{
+	enum { XI = 1, XM = 2, XO = 4 };   /* X still 0, from MSH, from anything else */
+	uint8_t *in = calloc((size_t)len + 1, 1);
+	uint32_t i;
+	int other = 0;
+	if (!in)
+		return 1;
+	in[0] = XI;
+	for (i = 0; i < len; i++) {
+		const uint16_t c = f[i].code;
+		uint8_t out = in[i];
+		if (c == (LDX | MSH | B))
+			out = XM;
+		else if ((c & 7) == LDX || c == (MISC | TAX))
+			out = XO;
+		if ((c & 7) == LD && (c & 0xe0) == IND) {
+			if (in[i] == XM)
+				tg[i] |= TG_XMSH;
+			else
+				other = 1;
+		}
+		if (c == (JMP | JA)) {
+			in[i + 1 + f[i].k] |= out;
+		} else if ((c & 7) == JMP) {
+			in[i + 1 + f[i].jt] |= out;
+			in[i + 1 + f[i].jf] |= out;
+		} else if ((c & 7) != RET && i + 1 < len) {
+			in[i + 1] |= out;
+		}
+	}
+	free(in);
+	return other;
+}
+
+/* The program shape: branchy by default (the 64 B fused ring measured 123.5 us
+ * branchy, 125.3 if-converted; IMIX 139.1 / 138.6: profiles/r04/fused_cost/);
+ * MOSRX_BPF_PRED=1 selects the if-converted form. */
 static int pred_mode(void)
 {
 	const char *e = getenv("MOSRX_BPF_PRED");
-	return !(e && e[0] == '0');
+	return e && e[0] == '1';
 }
 
 /* Constant-offset load expression.  Standalone: registers when frame bytes
@@ -187,20 +233,25 @@ static void gen_ld(struct sbuf *s, uint32_t k, uint32_t size, const struct genop
 }
 
 /* Load at the run-time offset kk = X + k (size bytes).  Standalone: the LDS
- * stage / memory.  Fused: X is 4 * ihl in every filter mOS compiles
- * (`ldxb 4*([14]&0xf)`) and ihl is 5 in nearly every frame, so kk = k + 20 is
- * speculated: a constant offset, read from the window's registers; any other
- * X reads memory (the frame's lines are in L2 behind the header window). */
-static void gen_ind(struct sbuf *s, uint32_t k, uint32_t size, const struct genopt *g)
+ * stage / memory.  Fused: where X is 4 * ihl (`ldxb 4*([14]&0xf)`, every
+ * header filter mOS compiles) ihl is 5 in nearly every frame, so kk = k + 20
+ * is speculated: a constant offset, read from the window's registers, any
+ * other X reads memory.  Any other X (payload offsets such as
+ * `tcp[((tcp[12:1] & 0xf0) >> 2):4]`) reads the hook's LDS copy of the window
+ * (hk_ind_le32), memory past it: a dependent memory read in every wave cost
+ * the 64 B ring 19 us per such program. */
+static void gen_ind(struct sbuf *s, uint32_t k, uint32_t size, int msh, const struct genopt *g)
 {
 	if (!g->fused) {
 		sb_printf(s, "fr_le32(win, sh, rs, o, kk, %uu)", size);
 		return;
 	}
-	if ((uint64_t)k + 20 + 8 <= g->wend) {
+	if (msh && (uint64_t)k + 20 + 8 <= g->wend) {
 		sb_printf(s, "(X == 20u ? ");
 		gen_ld(s, k + 20, size, g);
 		sb_printf(s, " : hk_ld_le32(rs, o + kk))");
+	} else if (!msh && g->lds) {
+		sb_printf(s, "hk_ind_le32(bw, kk, rs, o)");
 	} else {
 		sb_printf(s, "hk_ld_le32(rs, o + kk)");
 	}
@@ -219,7 +270,7 @@ static int gen_body(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_
 		const uint16_t c = f[i].code;
 		const uint32_t k = f[i].k;
 		const unsigned jt = i + 1 + f[i].jt, jf = i + 1 + f[i].jf;
-		if (tgt[i])
+		if (tgt[i] & TG_TARGET)
 			sb_printf(s, "  P%u_%s%u: ", j, lp, (unsigned)i);
 		else
 			sb_printf(s, "    ");
@@ -239,17 +290,17 @@ static int gen_body(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_
 		case LDX | W | LEN: sb_printf(s, "X = L;"); break;
 		case LD | W | IND:
 			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 4u > L) goto P%u_R0; A = be32(", k, j);
-			gen_ind(s, k, 4, g);
+			gen_ind(s, k, 4, tgt[i] & TG_XMSH, g);
 			sb_printf(s, "); }");
 			break;
 		case LD | H | IND:
 			sb_printf(s, "{ const u32 kk = X + %uu; if ((u64)kk + 2u > L) goto P%u_R0; A = be16(", k, j);
-			gen_ind(s, k, 2, g);
+			gen_ind(s, k, 2, tgt[i] & TG_XMSH, g);
 			sb_printf(s, "); }");
 			break;
 		case LD | B | IND:
 			sb_printf(s, "{ const u32 kk = X + %uu; if (kk >= L) goto P%u_R0; A = ", k, j);
-			gen_ind(s, k, 1, g);
+			gen_ind(s, k, 1, tgt[i] & TG_XMSH, g);
 			sb_printf(s, " & 0xFFu; }");
 			break;
 		case LDX | MSH | B:
@@ -298,33 +349,86 @@ static int gen_body(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint32_
 	return 0;
 }
 
+/* Registers of the BPF machine as bits: A, X, the 16 scratch slots. */
+#define RB_A 1u
+#define RB_X 2u
+#define RB_M(k) (4u << ((k) & 15u))
+
+static void insn_use_def(const mosrx_bpf_insn *f, uint32_t *use, uint32_t *def)
+{
+	const uint16_t c = f->code;
+	*use = *def = 0;
+	switch (c & 7) {
+	case LD:
+		*def = RB_A;
+		if ((c & 0xe0) == IND) *use = RB_X;
+		else if ((c & 0xe0) == MEM) *use = RB_M(f->k);
+		break;
+	case LDX:
+		*def = RB_X;
+		if ((c & 0xe0) == MEM) *use = RB_M(f->k);
+		break;
+	case ST: *use = RB_A; *def = RB_M(f->k); break;
+	case STX: *use = RB_X; *def = RB_M(f->k); break;
+	case ALU: *use = RB_A | ((c & 8) && (c & 0xf0) != NEG ? RB_X : 0); *def = RB_A; break;
+	case JMP: if (c != (JMP | JA)) *use = RB_A | ((c & 8) ? RB_X : 0); break;
+	case RET: if ((c & 0x18) == A) *use = RB_A; break;
+	case MISC: if (c == (MISC | TAX)) { *use = RB_A; *def = RB_X; } else { *use = RB_X; *def = RB_A; } break;
+	}
+}
+
 /* Program j if-converted, for the lanes whose L covers every constant-offset
  * load: no branches.  Each lane's position is a predicate -- `c` for the
  * instruction being emitted, b<i> for the jump targets not yet reached -- a
- * jump moves `c` into its targets' predicates, every A / X / scratch update
- * is a select on `c`, and a return sets the lane's hit flag `h`.  The
- * branchy form costs the structurizer's exec-mask bookkeeping at every
- * join (~6 scalar instructions per BPF jump); the mOS filters are short and
- * IPv4 headers put most lanes of a wave on the same path, so evaluating
- * every instruction for all lanes is cheaper.  Blocks of 4 or more
- * instructions no lane reaches are skipped with a uniform branch. */
+ * jump moves `c` into its targets' predicates, a return sets the lane's hit
+ * flag `h`.  A write to A / X / a scratch slot is a select on `c` only when a
+ * lane waiting at a pending jump target still needs the old value (liveness
+ * over the program's DAG); mOS filters reload A after nearly every jump, so
+ * most writes are plain, and the same load in several programs of the set
+ * becomes one value (one compare) for all of them.  The branchy form pays the
+ * structurizer's exec-mask bookkeeping at every join instead.  Blocks of 4 or
+ * more instructions no lane reaches are skipped with a uniform branch. */
 static int gen_pred(struct sbuf *s, const mosrx_bpf_insn *f, uint32_t len, const uint8_t *tgt,
                     const struct genopt *g)
 {
-	uint32_t i, e = 0;
+	uint32_t i, t, e = 0, *live, *need;
 	int open = 0;
+	live = calloc((size_t)len + 1, sizeof(*live));   /* registers live on entry to instruction i */
+	need = calloc((size_t)len + 1, sizeof(*need));   /* of them, those a lane waiting at target i needs */
+	if (!live || !need) {
+		free(live);
+		free(need);
+		return -ENOMEM;
+	}
+	for (i = len; i-- > 0;) {
+		const uint16_t c = f[i].code;
+		uint32_t use, def, out = 0;
+		insn_use_def(&f[i], &use, &def);
+		if (c == (JMP | JA))
+			out = live[i + 1 + f[i].k];
+		else if ((c & 7) == JMP)
+			out = live[i + 1 + f[i].jt] | live[i + 1 + f[i].jf];
+		else if ((c & 7) != RET)
+			out = live[i + 1];
+		live[i] = use | (out & ~def);
+	}
 	for (i = 1; i < len; i++)
-		if (tgt[i])
+		if (tgt[i] & TG_TARGET)
 			sb_printf(s, "    bool b%u = false;\n", (unsigned)i);
 	for (i = 0; i < len; i++) {
 		const uint16_t c = f[i].code;
 		const uint32_t k = f[i].k;
 		const unsigned jt = i + 1 + f[i].jt, jf = i + 1 + f[i].jf;
-		if (i == 0 || tgt[i]) {
+		uint32_t use, def, wait = 0;
+		const char *r;
+		insn_use_def(&f[i], &use, &def);
+		for (t = i + 1; t < len; t++)   /* what the lanes parked at targets past i still read */
+			wait |= need[t];
+		if (i == 0 || (tgt[i] & TG_TARGET)) {
 			if (i > 0)
 				sb_printf(s, "    c = c || b%u;\n", (unsigned)i);
 			/* the block: up to its jump / return, or up to the next jump target */
-			for (e = i; e + 1 < len && (f[e].code & 7) != JMP && (f[e].code & 7) != RET && !tgt[e + 1]; e++)
+			for (e = i; e + 1 < len && (f[e].code & 7) != JMP && (f[e].code & 7) != RET && !(tgt[e + 1] & TG_TARGET); e++)
 				;
 			if (e - i + 1 >= 4) {
 				sb_printf(s, "    if (__any(c)) {\n");
@@ -338,38 +442,47 @@ static int gen_pred(struct sbuf *s, const mosrx_bpf_insn *f, uint32_t len, const
 			sb_printf(s, "c = false;\n");   /* past any length: the lane returns 0 */
 			goto next;
 		}
+		/* "R = (value);" or "R = c ? (value) : R;" */
+		r = def == RB_A ? "A" : def == RB_X ? "X" : NULL;
+#define SET_OPEN(name) do { if (def & wait) sb_printf(s, "%s = c ? (", name); else sb_printf(s, "%s = (", name); } while (0)
+#define SET_CLOSE(name) do { if (def & wait) sb_printf(s, ") : %s;", name); else sb_printf(s, ");"); } while (0)
 		switch (c) {
 		case RET | K: sb_printf(s, k ? "h = h || c; c = false;" : "c = false;"); break;
 		case RET | A: sb_printf(s, "h = h || (c && A != 0u); c = false;"); break;
-		case LD | W | ABS: sb_printf(s, "A = c ? be32("); gen_ld(s, k, 4, g); sb_printf(s, ") : A;"); break;
-		case LD | H | ABS: sb_printf(s, "A = c ? be16("); gen_ld(s, k, 2, g); sb_printf(s, ") : A;"); break;
-		case LD | B | ABS: sb_printf(s, "A = c ? ("); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFFu) : A;"); break;
-		case LD | W | LEN: sb_printf(s, "A = c ? L : A;"); break;
-		case LDX | W | LEN: sb_printf(s, "X = c ? L : X;"); break;
+		case LD | W | ABS: SET_OPEN(r); sb_printf(s, "be32("); gen_ld(s, k, 4, g); sb_printf(s, ")"); SET_CLOSE(r); break;
+		case LD | H | ABS: SET_OPEN(r); sb_printf(s, "be16("); gen_ld(s, k, 2, g); sb_printf(s, ")"); SET_CLOSE(r); break;
+		case LD | B | ABS: SET_OPEN(r); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFFu"); SET_CLOSE(r); break;
+		case LD | W | LEN: case LDX | W | LEN: SET_OPEN(r); sb_printf(s, "L"); SET_CLOSE(r); break;
 		case LD | W | IND: case LD | H | IND: case LD | B | IND: {
 			const uint32_t size = (c & 0x18) == W ? 4 : (c & 0x18) == H ? 2 : 1;
 			sb_printf(s, "{ const u32 kk = X + %uu; c = c && (u64)kk + %uu <= L; u32 v; ", k, size);
-			if (g->fused && (uint64_t)k + 20 + 8 <= g->wend) {
+			if (g->fused && (tgt[i] & TG_XMSH) && (uint64_t)k + 20 + 8 <= g->wend) {
 				/* the speculated window read; a wave with any other live X also reads memory */
 				sb_printf(s, "v = ");
 				gen_ld(s, k + 20, size, g);
 				sb_printf(s, "; if (__any(c && X != 20u)) v = X == 20u ? v : hk_ld_le32(rs, o + kk); ");
+			} else if (g->fused && !(tgt[i] & TG_XMSH) && g->lds) {
+				sb_printf(s, "v = hk_ind_le32(bw, c ? kk : 2u, rs, o); ");
 			} else if (g->fused) {
 				sb_printf(s, "v = hk_ld_le32(rs, o + kk); ");   /* a buffer load: out-of-range offsets read 0 */
 			} else {   /* lanes off the path read the stage at offset 0, not at their X + k */
 				sb_printf(s, "v = fr_le32(win, sh, rs, o, c ? kk : 0u, %uu); ", size);
 			}
-			sb_printf(s, size == 4 ? "A = c ? be32(v) : A; }" : size == 2 ? "A = c ? be16(v) : A; }"
-			                                                             : "A = c ? (v & 0xFFu) : A; }");
+			SET_OPEN(r);
+			sb_printf(s, size == 4 ? "be32(v)" : size == 2 ? "be16(v)" : "v & 0xFFu");
+			SET_CLOSE(r);
+			sb_printf(s, " }");
 			break;
 		}
-		case LDX | MSH | B: sb_printf(s, "X = c ? (("); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFu) << 2) : X;"); break;
-		case LD | IMM: sb_printf(s, "A = c ? %uu : A;", k); break;
-		case LDX | IMM: sb_printf(s, "X = c ? %uu : X;", k); break;
-		case LD | MEM: sb_printf(s, "A = c ? M%u : A;", k & 15); break;
-		case LDX | MEM: sb_printf(s, "X = c ? M%u : X;", k & 15); break;
-		case ST: sb_printf(s, "M%u = c ? A : M%u;", k & 15, k & 15); break;
-		case STX: sb_printf(s, "M%u = c ? X : M%u;", k & 15, k & 15); break;
+		case LDX | MSH | B: SET_OPEN(r); sb_printf(s, "("); gen_ld(s, k, 1, g); sb_printf(s, " & 0xFu) << 2"); SET_CLOSE(r); break;
+		case LD | IMM: case LDX | IMM: SET_OPEN(r); sb_printf(s, "%uu", k); SET_CLOSE(r); break;
+		case LD | MEM: case LDX | MEM: SET_OPEN(r); sb_printf(s, "M%u", k & 15); SET_CLOSE(r); break;
+		case ST: case STX: {
+			char m[8];
+			snprintf(m, sizeof(m), "M%u", k & 15);
+			SET_OPEN(m); sb_printf(s, c == ST ? "A" : "X"); SET_CLOSE(m);
+			break;
+		}
 		case JMP | JA: sb_printf(s, "b%u = b%u || c; c = false;", (unsigned)(i + 1 + k), (unsigned)(i + 1 + k)); break;
 		case JMP | JGT | K: case JMP | JGE | K: case JMP | JEQ | K: case JMP | JSET | K:
 		case JMP | JGT | X: case JMP | JGE | X: case JMP | JEQ | X: case JMP | JSET | X: {
@@ -389,35 +502,50 @@ static int gen_pred(struct sbuf *s, const mosrx_bpf_insn *f, uint32_t len, const
 			sb_printf(s, "b%u = b%u || (c && t_); b%u = b%u || (c && !t_); c = false; }", jt, jt, jf, jf);
 			break;
 		}
-		case ALU | ADD | X: sb_printf(s, "A = c ? A + X : A;"); break;
-		case ALU | SUB | X: sb_printf(s, "A = c ? A - X : A;"); break;
-		case ALU | MUL | X: sb_printf(s, "A = c ? A * X : A;"); break;
-		case ALU | DIV | X: sb_printf(s, "c = c && X != 0u; A = c ? A / (X ? X : 1u) : A;"); break;
-		case ALU | AND | X: sb_printf(s, "A = c ? (A & X) : A;"); break;
-		case ALU | OR | X: sb_printf(s, "A = c ? (A | X) : A;"); break;
-		case ALU | LSH | X: sb_printf(s, "A = c ? A << (X & 31u) : A;"); break;
-		case ALU | RSH | X: sb_printf(s, "A = c ? A >> (X & 31u) : A;"); break;
-		case ALU | ADD | K: sb_printf(s, "A = c ? A + %uu : A;", k); break;
-		case ALU | SUB | K: sb_printf(s, "A = c ? A - %uu : A;", k); break;
-		case ALU | MUL | K: sb_printf(s, "A = c ? A * %uu : A;", k); break;
-		case ALU | DIV | K: sb_printf(s, "A = c ? A / %uu : A;", k); break;   /* k != 0 (mosrx_bpf_check) */
-		case ALU | AND | K: sb_printf(s, "A = c ? (A & %uu) : A;", k); break;
-		case ALU | OR | K: sb_printf(s, "A = c ? (A | %uu) : A;", k); break;
-		case ALU | LSH | K: sb_printf(s, "A = c ? A << %uu : A;", k & 31u); break;
-		case ALU | RSH | K: sb_printf(s, "A = c ? A >> %uu : A;", k & 31u); break;
-		case ALU | NEG: sb_printf(s, "A = c ? 0u - A : A;"); break;
-		case MISC | TAX: sb_printf(s, "X = c ? A : X;"); break;
-		case MISC | TXA: sb_printf(s, "A = c ? X : A;"); break;
+		case ALU | DIV | X:
+			sb_printf(s, "c = c && X != 0u; ");
+			SET_OPEN(r); sb_printf(s, "A / (X ? X : 1u)"); SET_CLOSE(r);
+			break;
+		case ALU | NEG: SET_OPEN(r); sb_printf(s, "0u - A"); SET_CLOSE(r); break;
+		case MISC | TAX: SET_OPEN(r); sb_printf(s, "A"); SET_CLOSE(r); break;
+		case MISC | TXA: SET_OPEN(r); sb_printf(s, "X"); SET_CLOSE(r); break;
 		default:
+			if ((c & 7) == ALU) {
+				static const char *const ops[] = {"+", "-", "*", "/", "|", "&", "<<", ">>"};
+				const unsigned o = (c & 0xf0) >> 4;
+				if (o > 7)
+					goto bad;
+				SET_OPEN(r);
+				if (c & 8)
+					sb_printf(s, o >= 6 ? "A %s (X & 31u)" : "A %s X", ops[o]);
+				else
+					sb_printf(s, "A %s %uu", ops[o], o >= 6 ? k & 31u : k);   /* DIV K: k != 0 (mosrx_bpf_check) */
+				SET_CLOSE(r);
+				break;
+			}
+		bad:
+			free(live);
+			free(need);
 			return -EINVAL;
 		}
+#undef SET_OPEN
+#undef SET_CLOSE
 		sb_printf(s, "\n");
 	next:
+		/* a jump parks its lanes at its targets: they need what is live there */
+		if (c == (JMP | JA))
+			need[i + 1 + k] |= live[i + 1 + k];
+		else if ((c & 7) == JMP) {
+			need[jt] |= live[jt];
+			need[jf] |= live[jf];
+		}
 		if (open && i == e) {
 			sb_printf(s, "    }\n");
 			open = 0;
 		}
 	}
+	free(live);
+	free(need);
 	return 0;
 }
 
@@ -437,15 +565,16 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 	tgt = calloc(len + 1, 1);
 	if (!tgt)
 		return -ENOMEM;
+	x_provenance(f, len, tgt);
 	memset(mem_used, 0, sizeof(mem_used));
 	for (i = 0; i < len; i++) {
 		const uint16_t c = f[i].code;
 		if ((c & 7) == JMP) {
 			if (c == (JMP | JA)) {
-				tgt[i + 1 + f[i].k] = 1;
+				tgt[i + 1 + f[i].k] |= TG_TARGET;
 			} else {
-				tgt[i + 1 + f[i].jt] = 1;
-				tgt[i + 1 + f[i].jf] = 1;
+				tgt[i + 1 + f[i].jt] |= TG_TARGET;
+				tgt[i + 1 + f[i].jf] |= TG_TARGET;
 			}
 		}
 		if (c == (LD | MEM) || c == (LDX | MEM) || c == ST || c == STX)
@@ -481,6 +610,12 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 		/* frames shorter than the program's furthest constant load: the checked copy */
 		sb_printf(s, "    if (__any(%s && L < %uu)) {\n    if (%s && L < %uu) {\n", lv, (unsigned)maxk, lv,
 		          (unsigned)maxk);
+		/* the if-converted code wrote registers of lanes off its path: start afresh */
+		sb_printf(s, "    A = 0u; X = 0u;");
+		for (q = 0; q < 16; q++)
+			if (mem_used[q])
+				sb_printf(s, " M%u = 0u;", q);
+		sb_printf(s, "\n");
 		if ((rc = gen_body(s, j, f, len, tgt, "", g))) {
 			free(tgt);
 			return rc;
@@ -492,7 +627,7 @@ static int gen_program(struct sbuf *s, unsigned j, const mosrx_bpf_insn *f, uint
 	}
 	sb_printf(s, "    if (!live%s) goto P%u_E;\n", ipm ? " || lip == 0u" : "", j);
 	if (maxk && maxk <= 65535) {
-		tgt[0] = 1;
+		tgt[0] |= TG_TARGET;
 		sb_printf(s, "    if (L >= %uu) goto P%u_F0;\n", (unsigned)maxk, j);
 		if ((rc = gen_body(s, j, f, len, tgt, "", g)) || (rc = gen_body(s, j, f, len, tgt, "F", g))) {
 			free(tgt);
@@ -556,7 +691,7 @@ int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, c
 {
 	struct sbuf s = {0};
 	const uint32_t v = stage_pieces(insns, t);
-	const struct genopt g = {0, 4 * v - 1, 0, pred_mode()};
+	const struct genopt g = {0, 4 * v - 1, 0, pred_mode(), 0};
 	uint32_t j;
 	int rc;
 	*out = NULL;
@@ -589,6 +724,15 @@ static const char k_hook_pre[] =
 	"  const u32 lo = __builtin_amdgcn_raw_buffer_load_b32(rs, a4, 0, 0);\n"
 	"  const u32 hi = __builtin_amdgcn_raw_buffer_load_b32(rs, a4 + 4u, 0, 0);\n"
 	"  return __builtin_amdgcn_alignbyte(hi, lo, a & 3u);\n"
+	"}\n"
+	"/* frame bytes [kk, kk+4) at a run-time offset: the hook's LDS copy of the window (column bw[256 j]), memory past it */\n"
+	"static __device__ __attribute__((always_inline)) inline u32 hk_ind_le32(const u32 *bw, u32 kk,\n"
+	"    __amdgpu_buffer_rsrc_t rs, u32 o) {\n"
+	"  if (kk >= 2u && kk + 8u <= MOSRX_BPF_WEND) {\n"
+	"    const u32 a = kk - 2u;\n"
+	"    return __builtin_amdgcn_alignbyte(bw[256u * ((a >> 2) + 1u)], bw[256u * (a >> 2)], a & 3u);\n"
+	"  }\n"
+	"  return hk_ld_le32(rs, o + kk);\n"
 	"}\n"
 	"/* frame bytes [k, k+4), k constant in [2, 86]: the realigned window registers */\n"
 	"#define RW32(k) (((k) - 2u) % 4u == 0u ? w[((k) - 2u) / 4u] \\\n"
@@ -639,22 +783,30 @@ static const char *const k_fused_names[MOSRX_BPF_NFUSED] = {
  * 4 / 5 / 6 chunks) that holds them, so the fused tiles load no more than the
  * classify tiles for the filters mOS compiles (they read Ethernet, IP and
  * TCP header fields). */
-static uint32_t hook_wend(const mosrx_bpf_insn *insns, const mosrx_bparams *t)
+static uint32_t hook_wend(const mosrx_bpf_insn *insns, const mosrx_bparams *t, int *lds)
 {
 	uint64_t need = 18;   /* the datagram-length probe reads frame bytes 12..17 */
 	uint32_t j, i;
-	for (j = 0; j < t->nprog; j++)
+	*lds = 0;
+	for (j = 0; j < t->nprog; j++) {
+		const mosrx_bpf_insn *f = &insns[t->prog_off[j]];
+		uint8_t *tg = calloc((size_t)t->prog_len[j] + 1, 1);
+		if (!tg)
+			return MOSRX_WINDOW_END_FULL;
+		*lds |= x_provenance(f, t->prog_len[j], tg);
 		for (i = 0; i < t->prog_len[j]; i++) {
-			const mosrx_bpf_insn *f = &insns[t->prog_off[j] + i];
-			const uint16_t c = f->code;
+			const uint16_t c = f[i].code;
 			uint64_t end = 0;
 			if (c == (LD | W | ABS) || c == (LD | H | ABS) || c == (LD | B | ABS) || c == (LDX | MSH | B))
-				end = f->k >= 2 ? (uint64_t)f->k + 8 : 0;
+				end = f[i].k >= 2 ? (uint64_t)f[i].k + 8 : 0;
 			else if (c == (LD | W | IND) || c == (LD | H | IND) || c == (LD | B | IND))
-				end = (uint64_t)f->k + 20 + 8;
+				/* X = 4 * ihl: ihl 5; any other X: a payload offset past IPv4 + TCP headers without options */
+				end = (uint64_t)f[i].k + ((tg[i] & TG_XMSH) ? 20 : 40) + 8;
 			if (end > need && end <= MOSRX_WINDOW_END_FULL)
 				need = end;
 		}
+		free(tg);
+	}
 	return need <= MOSRX_WINDOW_END_STREAM ? MOSRX_WINDOW_END_STREAM
 	     : need <= MOSRX_WINDOW_END_SMALL ? MOSRX_WINDOW_END_SMALL : MOSRX_WINDOW_END_FULL;
 }
@@ -662,11 +814,17 @@ static uint32_t hook_wend(const mosrx_bpf_insn *insns, const mosrx_bparams *t)
 int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, char **out)
 {
 	struct sbuf s = {0};
-	const struct genopt g = {1, 0, hook_wend(insns, t), pred_mode()};
+	struct genopt g = {1, 0, 0, pred_mode(), 0};
 	uint32_t j;
 	int rc;
 	*out = NULL;
+	g.wend = hook_wend(insns, t, &g.lds);
 	sb_printf(&s, "/* generated by bpf_jit.c */\n#define MOSRX_BPF_WEND %u\n%s", g.wend, k_hook_pre);
+	if (g.lds)   /* the window, column per lane (conflict-free): loads at X + k index it */
+		sb_printf(&s, "  __shared__ u32 s_bw[(MOSRX_BPF_WEND - 2u) / 4u * 256u];\n"
+		              "  u32 *const bw = s_bw + (threadIdx.x & 255u);\n"
+		              "#pragma unroll\n"
+		              "  for (u32 j = 0; j < (MOSRX_BPF_WEND - 2u) / 4u; j++) bw[256u * j] = w[j];\n");
 	for (j = 0; j < t->nprog; j++)
 		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u, &g))) {
 			free(s.p);

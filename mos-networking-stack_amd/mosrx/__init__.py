@@ -210,6 +210,7 @@ def lib():
             "mosrx_bpf_engine": (I, [P]),
             "mosrx_bpf_jit_log": (C.c_char_p, [P]),
             "mosrx_bpf_jit_source": (I, [C.POINTER(BpfProg), U32, C.POINTER(P)]),
+            "mosrx_bpf_jit_hook_source": (I, [C.POINTER(BpfProg), U32, C.POINTER(P)]),
             "mosrx_bpf_jit_compile": (I, [C.POINTER(BpfProg), U32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
             "mosrx_bpf_jit_compile_fused": (I, [C.POINTER(BpfProg), U32, C.c_char_p, C.c_size_t,
                                                 C.POINTER(C.c_size_t)]),
@@ -322,6 +323,17 @@ def bpf_jit_source(progs) -> str:
     arr, _keep = _bpf_progs(progs)
     out = C.c_void_p()
     _chk(lib().mosrx_bpf_jit_source(arr, len(progs), C.byref(out)), "mosrx_bpf_jit_source")
+    try:
+        return C.string_at(out.value).decode()
+    finally:
+        C.CDLL(None).free(out)
+
+
+def bpf_jit_hook_source(progs) -> str:
+    """mosrx_bpf_jit_hook_source: the fused kernel's generated hook for a program set."""
+    arr, _keep = _bpf_progs(progs)
+    out = C.c_void_p()
+    _chk(lib().mosrx_bpf_jit_hook_source(arr, len(progs), C.byref(out)), "mosrx_bpf_jit_hook_source")
     try:
         return C.string_at(out.value).decode()
     finally:

@@ -5,8 +5,11 @@ plain C once the packet-load helpers are defined, so this test compiles the
 generated text with gcc, one frame at a time (a wave with a single lane), and
 checks it against mOS's own sfbpf_filter results (tests/golden/bpf.npz) and the
 oracle.  Both code shapes are covered -- the if-converted programs
-(MOSRX_BPF_PRED, default) and the branchy form -- so a generator error shows
-here, apart from anything the GPU compiler does with the text.  No GPU.
+(MOSRX_BPF_PRED=1) and the branchy form (default) -- and both consumers: the
+standalone kernel's programs and the fused classify kernel's hook (its
+window registers, the X = 4 * ihl speculation, the LDS window copy for other
+indexed loads).  A generator error shows here, apart from anything the GPU
+compiler does with the text.  No GPU.
 """
 import ctypes as C
 import os
@@ -53,6 +56,53 @@ void eval(const u8 *buf, u32 nbytes, const u32 *off, const u16 *len, u32 n, u32 
 """
 
 
+HOOK_HARNESS = r"""
+#include <stdbool.h>
+#include <string.h>
+static unsigned buf_ld(const unsigned char *rs, unsigned a) { unsigned v; memcpy(&v, rs + a, 4); return v; }
+#define __amdgpu_buffer_rsrc_t const unsigned char *
+#define __builtin_amdgcn_raw_buffer_load_b32(rs, a, x, y) buf_ld(rs, a)
+#define __builtin_amdgcn_alignbyte(h, l, s) \
+  ((unsigned)((((unsigned long long)(h) << 32) | (unsigned)(l)) >> (8u * ((s) & 3u))))
+#define __device__
+#define __shared__ static
+#define __any(x) (x)
+static struct { unsigned x; } threadIdx;
+static unsigned be16hi(unsigned w) { return ((w >> 8) & 0xFF00u) | (w >> 24); }
+HOOK
+void eval(const unsigned char *buf, unsigned nbytes, const unsigned *off, const unsigned short *len, unsigned n,
+          unsigned *out)
+{
+  for (unsigned p = 0; p < n; p++) {
+    const unsigned o = off[p] < nbytes ? off[p] : nbytes, l = len[p];
+    const unsigned cap = (off[p] >= nbytes) ? 0u : (l < nbytes - o ? l : nbytes - o);
+    unsigned w[23];
+    threadIdx.x = p & 255u;
+    for (unsigned j = 0; j < 23; j++) w[j] = buf_ld(buf, o + 2u + 4u * j);
+    out[p] = mosrx_bpf_hook(w, o, cap, true, buf);
+  }
+}
+"""
+
+
+def build_hook(tmp_path, ps, pred):
+    os.environ["MOSRX_BPF_PRED"] = str(pred)
+    try:
+        src = mosrx.bpf_jit_hook_source(ps)
+    finally:
+        del os.environ["MOSRX_BPF_PRED"]
+    return compile_c(tmp_path, f"hook{pred}", HOOK_HARNESS.replace("HOOK", src))
+
+
+def compile_c(tmp_path, name, text):
+    c = tmp_path / f"{name}.c"
+    c.write_text(text)
+    so = tmp_path / f"{name}.so"
+    r = subprocess.run(["gcc", "-O1", "-shared", "-fPIC", "-w", "-o", str(so), str(c)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return C.CDLL(str(so))
+
+
 def build(tmp_path, ps, pred):
     os.environ["MOSRX_BPF_PRED"] = str(pred)
     try:
@@ -60,12 +110,7 @@ def build(tmp_path, ps, pred):
     finally:
         del os.environ["MOSRX_BPF_PRED"]
     body = src[src.index("  u32 match = 0;\n") + len("  u32 match = 0;\n"):src.index("  if (live) match_out[p]")]
-    c = tmp_path / f"gen{pred}.c"
-    c.write_text(HARNESS.replace("BODY", body))
-    so = tmp_path / f"gen{pred}.so"
-    r = subprocess.run(["gcc", "-O1", "-shared", "-fPIC", "-w", "-o", str(so), str(c)], capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr[-2000:]
-    return C.CDLL(str(so))
+    return compile_c(tmp_path, f"gen{pred}", HARNESS.replace("BODY", body))
 
 
 def run(lib, buf, off, ln):
@@ -81,26 +126,28 @@ def run(lib, buf, off, ln):
     return out
 
 
+@pytest.mark.parametrize("fused", [0, 1])
 @pytest.mark.parametrize("pred", [1, 0])
-def test_generated_golden_sets(tmp_path, pred):
+def test_generated_golden_sets(tmp_path, pred, fused):
     z, progs = load()
     for i, (ps, exp) in enumerate(program_sets(z, progs)):
         d = tmp_path / str(i)
         d.mkdir()
-        lib = build(d, ps, pred)
+        lib = (build_hook if fused else build)(d, ps, pred)
         got = run(lib, z["frames"], z["off"], z["len"])
         bad = np.nonzero(got != exp)[0]
         assert not len(bad), (i, bad[:5], hex(int(got[bad[0]] ^ exp[bad[0]])))
 
 
+@pytest.mark.parametrize("fused", [0, 1])
 @pytest.mark.parametrize("pred", [1, 0])
-@pytest.mark.parametrize("seed", [3, 11])
-def test_generated_random_programs(tmp_path, pred, seed):
+@pytest.mark.parametrize("seed", [3, 11, 19, 27])
+def test_generated_random_programs(tmp_path, pred, seed, fused):
     z, _ = load()
     for i, ps in enumerate(random_sets(seed)):
         d = tmp_path / str(i)
         d.mkdir()
-        lib = build(d, ps, pred)
+        lib = (build_hook if fused else build)(d, ps, pred)
         got = run(lib, z["frames"], z["off"], z["len"])
         exp = O.bpf_eval(ps, z["frames"], z["off"], z["len"])
         bad = np.nonzero(got != exp)[0]

@@ -17,7 +17,7 @@ key = sys.argv[1] if len(sys.argv) > 1 else "M1500"
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 kind, batch, ring, _ = bench.WORKLOADS[key]
 ctx = mosrx.Context(0)
-ctx.set_params(mosrx.default_params(skip_tcp_csum=1 if key == "S64_hdr" else 0))
+ctx.set_params(mosrx.default_params(skip_tcp_csum=1 if key.startswith("S64_hdr") else 0))
 probe = mosrx.Trace(kind, batch)
 if ring:
     nres = max(2 * ring, -(-bench.RESIDENT_BYTES // probe.frames_bytes))
@@ -27,8 +27,11 @@ else:
 dbs, trs, _ = bench.resident_batches(ctx, key, 1, 0, nres)
 tr = trs[0]
 ab = bench.algo_bytes(tr, key) * (ring or 1)
-if ring:
-    qs = [ctx.queue(dbs[i:i + ring]) for i in range(0, len(dbs), ring)]
+if ring:   # the queues bench.measure builds for the row
+    if "_cls_bpf" in key:
+        ctx.bpf_set(bench.bpf_bench_programs())
+    qs = [ctx.queue_ex(dbs[i:i + ring], match="_cls_bpf" in key, compact=key in ("S64_hdr", "S64_hdr_packed"))
+          for i in range(0, len(dbs), ring)]
     _, avg = qs[0].time(iters, qs[1:])
     for q in qs:
         q.destroy()

@@ -350,8 +350,9 @@ def test_dispatch_stamped_kernel_timing(gpu_ctx):
     """The bench's roofline duration (mosrx_time_op_dispatch / _queue_dispatch):
     every launch stamped by its own dispatch, so never longer than the same
     launches timed back to back with events around them (dispatch gaps
-    included); BPF rows (not one kernel of mosrx_kernels.hip) are refused; the
-    stamped launches leave the same records."""
+    included); the BPF op (the set's own kernel, or the interpreter) is one
+    launch and is stamped too, with the oracle's masks; the stamped launches
+    leave the same records."""
     gpu_ctx.set_params(mosrx.default_params())
     trs = [mosrx.Trace(mosrx.TRACE_M1500, 4096, nflows=4000, seed=200 + i) for i in range(2)]
     dbs = [gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len) for t in trs]
@@ -362,7 +363,15 @@ def test_dispatch_stamped_kernel_timing(gpu_ctx):
         assert_records_equal(d.results(), O.classify(t.frames, t.off, t.len, O.params()), "stamped")
     gpu_ctx.time_op(mosrx.OP_CLASSIFY_FH, dbs, 2, kernels=False)                # side buffers allocated
     assert gpu_ctx.time_op_dispatch(mosrx.OP_CLASSIFY_FH, dbs, 16) > 0
-    assert gpu_ctx.time_op_dispatch(mosrx.OP_BPF, dbs, 4) is None
+    progs = [(np.array([(0x28, 0, 0, 12), (0x15, 0, 1, 0x800), (0x06, 0, 0, 1), (0x06, 0, 0, 0)],
+                       mosrx.BPF_INSN), 0)]
+    gpu_ctx.bpf_set(progs)
+    for d in dbs:
+        gpu_ctx.bpf_dev(d)                                                   # match buffers allocated
+    assert gpu_ctx.time_op_dispatch(mosrx.OP_BPF, dbs, 4) > 0
+    for t, d in zip(trs, dbs):
+        np.testing.assert_array_equal(d.matches(), O.bpf_eval(progs, t.frames[:t.frames_bytes], t.off, t.len))
+    gpu_ctx.bpf_set([])
     q = gpu_ctx.queue(dbs)
     qs = q.time_dispatch(16)
     qb = q.time(16, kernels=False)[0] / 16

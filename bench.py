@@ -533,7 +533,7 @@ def orphan_segments(n: int, size: int = 1460, seed: int = 3) -> mosrx.Trace:
 
 
 def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 5, timeout: float = 60.0,
-                    exe: str | None = None):
+                    exe: str | None = None, monitors: int = 1):
     """mOS's own rx loop on one host core (oracle/_ref/mos_app: mtcp_init, an
     mTCP thread in RunMainLoop, one stream monitor socket, gpu_module_func as
     the I/O module): the per-frame CPU time of core.c:902-907 (timed per batch)
@@ -543,8 +543,10 @@ def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 5, ti
     nowhere (MOSAPP_NO_TX: no pcap dump) and the time spent in get_wptr -- the
     TX buffer's flush to the source every 64 frames, the harness's sink -- is
     taken out of the figures (`*_excl_tx`; the raw ones are kept beside them).
-    The difference is the CPU time per frame the GPU saves inside mOS.  A
-    reported baseline; None when the binary did not travel with the tree."""
+    The difference is the CPU time per frame the GPU saves inside mOS.
+    `monitors` 0: mOS with no monitor socket (no stream tracking, no
+    callbacks: ProcessPacket plus the loop).  A reported baseline; None when
+    the binary did not travel with the tree."""
     exe = exe or os.path.join(ROOT, "oracle", "_ref", "mos_app")
     if not os.access(exe, os.X_OK):
         return None
@@ -565,7 +567,7 @@ def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 5, ti
                 with open(conf, "w") as fh:
                     fh.write(MOS_CONF.format(log=os.path.join(d, "log"), forward=forward))
                 env = dict(os.environ, MOSAPP_QUIET="1", MOSAPP_LOOPS=str(loops), MOSAPP_BATCH="8192",
-                           MOSAPP_NO_TX="1")
+                           MOSAPP_NO_TX="1", MOSAPP_MONITORS=str(monitors))
                 try:
                     r = subprocess.run([exe, mode, conf, trace, d], capture_output=True, text=True, timeout=timeout,
                                        env=env)
@@ -585,7 +587,7 @@ def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 5, ti
             "frames": frames, "excluded": "get_wptr (TX buffer flushes), no TX dump",
             "runs_ns": {k: [round(x, 1) for x in v] for k, v in ns.items()},
             "runs_ns_incl_tx": {k: [round(x, 1) for x in v] for k, v in raw.items()},
-            "sample": f"{tr.n} frames x {loops} through mOS's RunMainLoop on one core (1 stream monitor, "
+            "sample": f"{tr.n} frames x {loops} through mOS's RunMainLoop on one core ({monitors} stream monitor(s), "
                       f"forward={forward}), oracle/_ref/mos_app pp vs gpu, {reps} alternated runs each, medians; "
                       f"TX flushes excluded"}
 
@@ -888,6 +890,10 @@ def main():
         rx = cpu_rx_loop_leg(mosrx.Trace(mosrx.TRACE_FW64, 10_000), 20, forward=1)
         if rx:
             cpu["mos_rx_loop_FW64"] = rx
+        # the same frames through a bare mOS (no monitor: no stream tracking, no callbacks)
+        rx = cpu_rx_loop_leg(mosrx.Trace(mosrx.TRACE_FW64, 10_000), 20, forward=1, monitors=0)
+        if rx:
+            cpu["mos_rx_loop_FW64_bare"] = rx
         for k in keys:
             if k != head:
                 results[k]["cpu_baseline"] = cpu_baseline(traces[k], k, min_s=2.0)
@@ -976,7 +982,7 @@ def headline_line(detail, h, head, results, e2e):
         for leg in ("all_cores", "reference", "reference_processpacket"):
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("value", "unit", "cores", "kind", "mpkts") if k in cpu[leg]}
-        for leg in ("mos_rx_loop_M1500", "mos_rx_loop_FW64"):
+        for leg in ("mos_rx_loop_M1500", "mos_rx_loop_FW64", "mos_rx_loop_FW64_bare"):
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("processpacket_ns_per_frame", "gpu_records_ns_per_frame",
                                                           "saved_ns_per_frame", "spread_ns")}
@@ -991,15 +997,15 @@ def headline_line(detail, h, head, results, e2e):
                       "cpu_ref_processpacket_mpkts": (cb.get("reference_processpacket") or {}).get("mpkts"),
                       "boundary_mpkts": round(r["e2e_boundary"]["mpkts"], 2)}
             continue
-        sec[k] = {"gbps": round(r["gbps"], 1), "mpkts": round(r["mpkts"], 1),
-                  "launch_us": r["roofline"]["launch_us"], "frac": r["roofline"]["frac"]}
+        sec[k] = {"mpkts": round(r["mpkts"], 1), "launch_us": r["roofline"]["launch_us"],
+                  "frac": r["roofline"]["frac"]}   # (GB/s: the detail record)
     e2e_line = None
     if e2e:
         e2e_line = {k: {"gbps": round(v["gbps"], 1), "mpkts": round(v["mpkts"], 1)}
                     for k, v in e2e.items() if k in ("M1500", "S64")}
         be = e2e.get("backend") or {}
-        e2e_line["backend"] = {k: {"mpkts": round(v["mpkts"], 1), "group": v["group"],
-                                   "dev_frac": v.get("device_roofline_frac")} for k, v in be.items()}
+        e2e_line["backend"] = {k: {"mpkts": round(v["mpkts"], 1), "dev_frac": v.get("device_roofline_frac")}
+                               for k, v in be.items()}
         if e2e.get("consumer"):
             e2e_line["consumer"] = e2e["consumer"]
     return {

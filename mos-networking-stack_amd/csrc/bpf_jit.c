@@ -251,7 +251,7 @@ static void gen_ind(struct sbuf *s, uint32_t k, uint32_t size, int msh, const st
 		gen_ld(s, k + 20, size, g);
 		sb_printf(s, " : hk_ld_le32(rs, o + kk))");
 	} else if (!msh && g->lds) {
-		sb_printf(s, "hk_ind_le32(bw, kk, rs, o)");
+		sb_printf(s, "hk_ind_le32<HL>(bw, kk, rs, o)");
 	} else {
 		sb_printf(s, "hk_ld_le32(rs, o + kk)");
 	}
@@ -462,7 +462,7 @@ static int gen_pred(struct sbuf *s, const mosrx_bpf_insn *f, uint32_t len, const
 				gen_ld(s, k + 20, size, g);
 				sb_printf(s, "; if (__any(c && X != 20u)) v = X == 20u ? v : hk_ld_le32(rs, o + kk); ");
 			} else if (g->fused && !(tgt[i] & TG_XMSH) && g->lds) {
-				sb_printf(s, "v = hk_ind_le32(bw, c ? kk : 2u, rs, o); ");
+				sb_printf(s, "v = hk_ind_le32<HL>(bw, c ? kk : 2u, rs, o); ");
 			} else if (g->fused) {
 				sb_printf(s, "v = hk_ld_le32(rs, o + kk); ");   /* a buffer load: out-of-range offsets read 0 */
 			} else {   /* lanes off the path read the stage at offset 0, not at their X + k */
@@ -725,19 +725,23 @@ static const char k_hook_pre[] =
 	"  const u32 hi = __builtin_amdgcn_raw_buffer_load_b32(rs, a4 + 4u, 0, 0);\n"
 	"  return __builtin_amdgcn_alignbyte(hi, lo, a & 3u);\n"
 	"}\n"
-	"/* frame bytes [kk, kk+4) at a run-time offset: the hook's LDS copy of the window (column bw[256 j]), memory past it */\n"
+	"/* frame bytes [kk, kk+4) at a run-time offset: the hook's LDS copy of the window (dword j of the lane at\n"
+	"   bw[HL j], HL header lanes per workgroup), memory past it */\n"
+	"template <u32 HL>\n"
 	"static __device__ __attribute__((always_inline)) inline u32 hk_ind_le32(const u32 *bw, u32 kk,\n"
 	"    __amdgpu_buffer_rsrc_t rs, u32 o) {\n"
 	"  if (kk >= 2u && kk + 8u <= MOSRX_BPF_WEND) {\n"
 	"    const u32 a = kk - 2u;\n"
-	"    return __builtin_amdgcn_alignbyte(bw[256u * ((a >> 2) + 1u)], bw[256u * (a >> 2)], a & 3u);\n"
+	"    return __builtin_amdgcn_alignbyte(bw[HL * ((a >> 2) + 1u)], bw[HL * (a >> 2)], a & 3u);\n"
 	"  }\n"
 	"  return hk_ld_le32(rs, o + kk);\n"
 	"}\n"
 	"/* frame bytes [k, k+4), k constant in [2, 86]: the realigned window registers */\n"
 	"#define RW32(k) (((k) - 2u) % 4u == 0u ? w[((k) - 2u) / 4u] \\\n"
 	"                 : __builtin_amdgcn_alignbyte(w[((k) - 2u) / 4u + 1u], w[((k) - 2u) / 4u], ((k) - 2u) % 4u))\n"
-	"/* w: the header wave's realigned window, frame bytes [4j + 2, 4j + 6) in w[j], valid up to MOSRX_BPF_WEND */\n"
+	"/* w: the header wave's realigned window, frame bytes [4j + 2, 4j + 6) in w[j], valid up to MOSRX_BPF_WEND;\n"
+	"   HL: the workgroup's header lanes (the SMALL tile 256, the stream tile's one header wave 64) */\n"
+	"template <u32 HL>\n"
 	"static __device__ __attribute__((always_inline)) inline u32 mosrx_bpf_hook(const u32 *w, u32 o, u32 cap,\n"
 	"    bool live, __amdgpu_buffer_rsrc_t rs) {\n"
 	"  u32 lip = 0;\n"
@@ -800,8 +804,9 @@ static uint32_t hook_wend(const mosrx_bpf_insn *insns, const mosrx_bparams *t, i
 			if (c == (LD | W | ABS) || c == (LD | H | ABS) || c == (LD | B | ABS) || c == (LDX | MSH | B))
 				end = f[i].k >= 2 ? (uint64_t)f[i].k + 8 : 0;
 			else if (c == (LD | W | IND) || c == (LD | H | IND) || c == (LD | B | IND))
-				/* X = 4 * ihl: ihl 5; any other X: a payload offset past IPv4 + TCP headers without options */
-				end = (uint64_t)f[i].k + ((tg[i] & TG_XMSH) ? 20 : 40) + 8;
+				/* X = 4 * ihl: ihl 5; any other X: a payload offset past IPv4 + a TCP header with
+				 * timestamps (20 + 32: 42 % of the IMIX trace's segments, most of a real trace's) */
+				end = (uint64_t)f[i].k + ((tg[i] & TG_XMSH) ? 20 : 52) + 8;
 			if (end > need && end <= MOSRX_WINDOW_END_FULL)
 				need = end;
 		}
@@ -821,10 +826,10 @@ int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams 
 	g.wend = hook_wend(insns, t, &g.lds);
 	sb_printf(&s, "/* generated by bpf_jit.c */\n#define MOSRX_BPF_WEND %u\n%s", g.wend, k_hook_pre);
 	if (g.lds)   /* the window, column per lane (conflict-free): loads at X + k index it */
-		sb_printf(&s, "  __shared__ u32 s_bw[(MOSRX_BPF_WEND - 2u) / 4u * 256u];\n"
-		              "  u32 *const bw = s_bw + (threadIdx.x & 255u);\n"
+		sb_printf(&s, "  __shared__ u32 s_bw[(MOSRX_BPF_WEND - 2u) / 4u * HL];\n"
+		              "  u32 *const bw = s_bw + threadIdx.x % HL;\n"
 		              "#pragma unroll\n"
-		              "  for (u32 j = 0; j < (MOSRX_BPF_WEND - 2u) / 4u; j++) bw[256u * j] = w[j];\n");
+		              "  for (u32 j = 0; j < (MOSRX_BPF_WEND - 2u) / 4u; j++) bw[HL * j] = w[j];\n");
 	for (j = 0; j < t->nprog; j++)
 		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u, &g))) {
 			free(s.p);

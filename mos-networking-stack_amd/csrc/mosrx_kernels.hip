@@ -300,7 +300,7 @@ __device__ __forceinline__ hdr_t hdr_parse(hdr_win_t win, uint32_t o, uint32_t c
 	// the set first, on the registers the parse is about to read: no second
 	// realignment, and the raw window is dead from here on
 	if constexpr ((VAR & VAR_BPF) != 0)
-		h.bmatch = mosrx_bpf_hook(w, o, cap, active, rs);
+		h.bmatch = mosrx_bpf_hook<WEND == MOSRX_WINDOW_END_SMALL ? SMALL_THREADS : 64u>(w, o, cap, active, rs);
 #endif
 
 	// frame byte f sits in byte (f-2)&3 of w[(f-2)>>2]

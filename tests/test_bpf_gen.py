@@ -70,8 +70,8 @@ static unsigned buf_ld(const unsigned char *rs, unsigned a) { unsigned v; memcpy
 static struct { unsigned x; } threadIdx;
 static unsigned be16hi(unsigned w) { return ((w >> 8) & 0xFF00u) | (w >> 24); }
 HOOK
-void eval(const unsigned char *buf, unsigned nbytes, const unsigned *off, const unsigned short *len, unsigned n,
-          unsigned *out)
+extern "C" void eval(const unsigned char *buf, unsigned nbytes, const unsigned *off, const unsigned short *len,
+                     unsigned n, unsigned *out)
 {
   for (unsigned p = 0; p < n; p++) {
     const unsigned o = off[p] < nbytes ? off[p] : nbytes, l = len[p];
@@ -79,7 +79,7 @@ void eval(const unsigned char *buf, unsigned nbytes, const unsigned *off, const 
     unsigned w[23];
     threadIdx.x = p & 255u;
     for (unsigned j = 0; j < 23; j++) w[j] = buf_ld(buf, o + 2u + 4u * j);
-    out[p] = mosrx_bpf_hook(w, o, cap, true, buf);
+    out[p] = mosrx_bpf_hook<256u>(w, o, cap, true, buf);
   }
 }
 """
@@ -91,14 +91,15 @@ def build_hook(tmp_path, ps, pred):
         src = mosrx.bpf_jit_hook_source(ps)
     finally:
         del os.environ["MOSRX_BPF_PRED"]
-    return compile_c(tmp_path, f"hook{pred}", HOOK_HARNESS.replace("HOOK", src))
+    return compile_c(tmp_path, f"hook{pred}", HOOK_HARNESS.replace("HOOK", src), cxx=True)   # (a template)
 
 
-def compile_c(tmp_path, name, text):
-    c = tmp_path / f"{name}.c"
+def compile_c(tmp_path, name, text, cxx=False):
+    c = tmp_path / (f"{name}.cc" if cxx else f"{name}.c")
     c.write_text(text)
     so = tmp_path / f"{name}.so"
-    r = subprocess.run(["gcc", "-O1", "-shared", "-fPIC", "-w", "-o", str(so), str(c)], capture_output=True, text=True)
+    r = subprocess.run(["g++" if cxx else "gcc", "-O1", "-shared", "-fPIC", "-w", "-o", str(so), str(c)],
+                       capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     return C.CDLL(str(so))
 

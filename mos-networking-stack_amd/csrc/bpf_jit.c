@@ -853,7 +853,9 @@ static int compile_code_h(const char *src, int nh, const char *const *htexts, co
                           char **code, size_t *size, char *log, size_t logsz)
 {
 	hiprtcProgram prog;
-	const char *opts[] = {"--offload-arch=gfx950", "-O3"};
+	/* the library's kernarg preloading (Makefile KFLAGS): the kernels' leading
+	 * scalar arguments arrive in SGPRs at dispatch */
+	const char *opts[] = {"--offload-arch=gfx950", "-O3", "-mllvm", "-amdgpu-kernarg-preload-count=7"};
 	size_t sz = 0;
 	int rc = 0;
 	*code = NULL;
@@ -863,7 +865,7 @@ static int compile_code_h(const char *src, int nh, const char *const *htexts, co
 		pthread_mutex_unlock(&g_rtc_lock);
 		return -EIO;
 	}
-	if (hiprtcCompileProgram(prog, 2, opts) != HIPRTC_SUCCESS) {
+	if (hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts) != HIPRTC_SUCCESS) {
 		size_t ls = 0;
 		if (log && logsz && hiprtcGetProgramLogSize(prog, &ls) == HIPRTC_SUCCESS && ls) {
 			char *l = malloc(ls + 1);

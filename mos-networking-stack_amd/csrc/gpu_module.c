@@ -565,14 +565,20 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
 		s->n = src->fill(src, s->frames, cap, s->off, s->len, g_cfg.batch, mf, &s->bytes);
 		fpos = s->bytes;
 	} else {
-		while (i < g_cfg.batch && src && fpos + mf + 16 <= cap) {
-			int l = src->next(src, s->frames + fpos, mf);
+		while (i < g_cfg.batch && src && fpos + mf + 32 <= cap) {
+			/* received into the aligned slot; a frame that packs moves back (mosrx__frame_at) */
+			const uint64_t al = mosrx__frame_at(fpos, MOSRX_PACK_MAX + 1);
+			int l = src->next(src, s->frames + al, mf);
 			if (l <= 0)
 				break;
+			if (mosrx__frame_at(fpos, (uint32_t)l) != al)
+				memmove(s->frames + fpos, s->frames + al, (size_t)l);
+			else
+				fpos = al;
 			s->off[i] = (uint32_t)fpos;
 			s->len[i] = (uint16_t)l;
 			i++;
-			fpos = ((fpos + (uint64_t)l - 2 + 15) & ~15ull) + 2;   /* next frame at 16 B + 2 */
+			fpos += (uint64_t)l;
 		}
 		s->n = i;
 		s->bytes = fpos;

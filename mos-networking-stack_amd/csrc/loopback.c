@@ -77,11 +77,19 @@ static uint32_t mem_fill(struct mosrx_source *s_, uint8_t *dst, uint64_t cap, ui
 	uint32_t k = 0;
 	if (s->max_len > max_frame) {   /* frames to truncate: the per-frame path */
 		int l;
-		while (k < max_n && pos + max_frame + 16 <= cap && (l = mem_next(s_, dst + pos, max_frame)) > 0) {
+		while (k < max_n && pos + max_frame + 32 <= cap) {
+			/* the frame's own length places it: read it into the aligned slot, move it back if it packs */
+			const uint64_t al = mosrx__frame_at(pos, MOSRX_PACK_MAX + 1);
+			if ((l = mem_next(s_, dst + al, max_frame)) <= 0)
+				break;
+			if (mosrx__frame_at(pos, (uint32_t)l) != al)
+				memmove(dst + pos, dst + al, (size_t)l);
+			else
+				pos = al;
 			off[k] = (uint32_t)pos;
 			len[k] = (uint16_t)l;
 			k++;
-			pos = ((pos + (uint64_t)l - 2 + 15) & ~15ull) + 2;
+			pos += (uint64_t)l;
 		}
 		*end = pos;
 		return k;
@@ -95,9 +103,14 @@ static uint32_t mem_fill(struct mosrx_source *s_, uint8_t *dst, uint64_t cap, ui
 				break;
 			s->i = 0;
 		}
-		/* the run [a, b) of source frames that fits the count and the space left */
+		/* the run [a, b) of source frames that fits the count and the space left,
+		 * copied whole at the source's alignment mod 16 (its frames keep their
+		 * places in the layout) */
 		a = s->i;
 		base = s->off[a];
+		pos += (base - pos) & 15u;
+		if (pos + 32 > cap)
+			break;
 		room = cap - pos;
 		b = a;
 		while (b < s->n && k + (b - a) < max_n && (uint64_t)(s->off[b] - base) + max_frame + 16 <= room)
@@ -109,7 +122,7 @@ static uint32_t mem_fill(struct mosrx_source *s_, uint8_t *dst, uint64_t cap, ui
 			off[k] = (uint32_t)(pos + (s->off[j] - base));
 			len[k] = s->len[j];
 		}
-		pos = ((pos + (s->off[b - 1] - base) + s->len[b - 1] - 2 + 15) & ~15ull) + 2;
+		pos += (uint64_t)(s->off[b - 1] - base) + s->len[b - 1];
 		s->i = b;
 	}
 	*end = pos;
@@ -133,7 +146,7 @@ static uint32_t mem_borrow(struct mosrx_source *s_, uint32_t max_n, uint32_t max
 	}
 	a = s->i;
 	b = s->n - a > max_n ? a + max_n : s->n;
-	base = s->off[a] - 2;
+	base = (s->off[a] - 2) & ~15u;   /* the run handed out from a 16-byte boundary */
 	for (k = 0; a + k < b; k++) {
 		off[k] = s->off[a + k] - base;
 		len[k] = s->len[a + k] < max_frame ? s->len[a + k] : (uint16_t)max_frame;
@@ -184,12 +197,13 @@ mosrx_source *mosrx_source_mem(const uint8_t *frames, const uint32_t *off, const
 	}
 	pos = 2;
 	for (i = 0; i < n; i++) {
+		pos = mosrx__frame_at(pos, len[i]);
 		memcpy(s->frames + pos, frames + off[i], len[i]);
 		s->off[i] = (uint32_t)pos;
 		s->len[i] = len[i];
 		if (len[i] > s->max_len)
 			s->max_len = len[i];
-		pos = ((pos + len[i] - 2 + 15) & ~15ull) + 2;
+		pos += len[i];
 	}
 	s->n = n;
 	s->loops = loops;
@@ -292,7 +306,7 @@ static int pcap_next_frame(struct mosrx_source *s_, uint8_t *dst, uint32_t cap)
 	return (int)take;
 }
 
-/* A batch into the stage, frames at 16-byte boundaries + 2 (the backend's layout). */
+/* A batch into the stage, in the backend's layout (mosrx__frame_at). */
 static uint32_t pcap_fill(struct mosrx_source *s_, uint8_t *dst, uint64_t cap, uint32_t *off, uint16_t *len,
                           uint32_t max_n, uint32_t max_frame, uint64_t *end)
 {
@@ -305,12 +319,13 @@ static uint32_t pcap_fill(struct mosrx_source *s_, uint8_t *dst, uint64_t cap, u
 		if (!rec)
 			break;
 		take = incl < max_frame ? incl : max_frame;
+		pos = mosrx__frame_at(pos, take);
 		memcpy(dst + pos, rec, take);
 		s->pos += 16 + (size_t)incl;
 		off[k] = (uint32_t)pos;
 		len[k] = (uint16_t)take;
 		k++;
-		pos = ((pos + (uint64_t)take - 2 + 15) & ~15ull) + 2;
+		pos += take;
 	}
 	*end = pos;
 	return k;

@@ -139,6 +139,14 @@ int           mosrx_source_afpacket_info(mosrx_source *s, mosrx_afpacket_info *i
 mosrx_source *mosrx_source_tpacket_v3(void *ring, uint32_t nblocks, uint32_t block_size);
 /* Pull the next frame into dst (at most cap bytes); returns its caplen, 0 when none. */
 int           mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap);
+/* Receive up to max_n frames (at most max_frame bytes each) into dst[0, cap)
+ * in gpu_module_func's staging layout: the first frame at byte 2, a frame of
+ * up to 128 bytes right after the previous one, a longer one at the next
+ * 16-byte boundary + 2; off[]/len[] written, *end = the bytes used.  What
+ * the backend does for every batch it copies (the batch form of the source,
+ * or mosrx_source_next per frame).  Returns the count or -EINVAL. */
+int           mosrx_source_fill(mosrx_source *s, uint8_t *dst, uint64_t cap, uint32_t *off, uint16_t *len,
+                                uint32_t max_n, uint32_t max_frame, uint64_t *end);
 /* Zero-copy runs (what gpu_module_func lends to the GPU copy): up to max_n
  * frames that sit in the source's own memory, as one run from *frames in
  * buffer order -- off[]/len[] relative to it, len clamped to max_frame --

@@ -561,27 +561,14 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
 			s->bytes = 2;
 		}
 		fpos = 0;
-	} else if (src && src->fill) {
-		s->n = src->fill(src, s->frames, cap, s->off, s->len, g_cfg.batch, mf, &s->bytes);
+	} else if (src) {                 /* the source's batch form, or frame by frame (mosrx_source_fill) */
+		const int k = mosrx_source_fill(src, s->frames, cap, s->off, s->len, g_cfg.batch, mf, &s->bytes);
+		s->n = k > 0 ? (uint32_t)k : 0;
+		if (k <= 0)
+			s->bytes = 2;
 		fpos = s->bytes;
 	} else {
-		while (i < g_cfg.batch && src && fpos + mf + 32 <= cap) {
-			/* received into the aligned slot; a frame that packs moves back (mosrx__frame_at) */
-			const uint64_t al = mosrx__frame_at(fpos, MOSRX_PACK_MAX + 1);
-			int l = src->next(src, s->frames + al, mf);
-			if (l <= 0)
-				break;
-			if (mosrx__frame_at(fpos, (uint32_t)l) != al)
-				memmove(s->frames + fpos, s->frames + al, (size_t)l);
-			else
-				fpos = al;
-			s->off[i] = (uint32_t)fpos;
-			s->len[i] = (uint16_t)l;
-			i++;
-			fpos += (uint64_t)l;
-		}
-		s->n = i;
-		s->bytes = fpos;
+		s->bytes = 2;
 	}
 	for (i = 0; i < s->n; i++)        /* the batch's real largest frame picks the kernel shape */
 		m = s->len[i] > m ? s->len[i] : m;

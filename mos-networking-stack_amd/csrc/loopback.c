@@ -777,6 +777,36 @@ int mosrx_source_give_back(mosrx_source *s)
 	return 0;
 }
 
+int mosrx_source_fill(mosrx_source *s, uint8_t *dst, uint64_t cap, uint32_t *off, uint16_t *len, uint32_t max_n,
+                      uint32_t max_frame, uint64_t *end)
+{
+	uint64_t pos = 2;
+	uint32_t k = 0;
+	if (!s || !dst || !off || !len || !end || max_frame == 0 || max_frame > 65535)
+		return -EINVAL;
+	if (s->fill)
+		return (int)s->fill(s, dst, cap, off, len, max_n, max_frame, end);
+	if (!s->next)
+		return -EINVAL;
+	while (k < max_n && pos + max_frame + 32 <= cap) {
+		/* received into the aligned slot; a frame that packs moves back (mosrx__frame_at) */
+		const uint64_t al = mosrx__frame_at(pos, MOSRX_PACK_MAX + 1);
+		const int l = s->next(s, dst + al, max_frame);
+		if (l <= 0)
+			break;
+		if (mosrx__frame_at(pos, (uint32_t)l) != al)
+			memmove(dst + pos, dst + al, (size_t)l);
+		else
+			pos = al;
+		off[k] = (uint32_t)pos;
+		len[k] = (uint16_t)l;
+		k++;
+		pos += (uint64_t)l;
+	}
+	*end = pos;
+	return (int)k;
+}
+
 int mosrx_source_next(mosrx_source *s, uint8_t *dst, uint32_t cap)
 {
 	if (!s || !dst || !s->next)

@@ -225,6 +225,7 @@ def lib():
             "mosrx_source_afpacket": (P, [C.c_char_p]),
             "mosrx_source_close": (None, [P]),
             "mosrx_source_next": (I, [P, P, U32]),
+            "mosrx_source_fill": (I, [P, P, U64, P, P, U32, U32, C.POINTER(U64)]),
             "mosrx_source_borrow": (I, [P, U32, U32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), P, P]),
             "mosrx_source_give_back": (I, [P]),
             "mosrx_source_mem_set_mode": (I, [P, I]),

@@ -4,7 +4,7 @@ programs (`ret #1`: the fused tile's fixed cost, masks stored), and fused with
 the bench's 8 mOS filters; dispatch-stamped medians.  Records and masks are
 checked against the oracle first.
 
-    python3 scripts/probe_fused_cost.py [S64|IMIX] [set indices, comma separated: 0 plain, 1 8 x ret, 2 the 8 filters, 3+j 8 x filter j]
+    python3 scripts/probe_fused_cost.py [S64|IMIX] [set indices, comma separated: 0 plain, 1 8 x ret, 2 the 8 filters, 3+j 8 x filter j, 11 / 12 one trivial program]
 
 PROBE_SHORT=1: no prewarm and a handful of launches (for rocprofv3 --pmc passes).
 """
@@ -26,6 +26,8 @@ trivial = [(np.array([(0x06, 0, 0, 1)], mosrx.BPF_INSN), m % 2) for m in range(8
 sets = {"plain": None, "fused, 8 x ret #1": trivial, "fused, 8 mOS filters": bench.bpf_bench_programs()}
 for j, (p, m) in enumerate(bench.bpf_bench_programs()):   # one filter's cost: 8 copies of it
     sets[f"fused, 8 x filter {j}"] = [(p, m)] * 8
+sets["fused, 1 x ret #1 (frame length)"] = trivial[:1]    # 11: the fixed cost of the fused tile
+sets["fused, 1 x ret #1 (datagram length)"] = trivial[1:2]  # 12
 if len(sys.argv) > 2:
     sets = dict([list(sets.items())[int(a)] for a in sys.argv[2].split(",")])
 short = os.environ.get("PROBE_SHORT") == "1"

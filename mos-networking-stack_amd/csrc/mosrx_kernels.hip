@@ -1024,7 +1024,10 @@ __device__ __forceinline__ void stream_frames(__amdgpu_buffer_rsrc_t rs, uint32_
 // DBG (probe builds only, the library uses 0): 1 no parse/records, 2 no header
 // window loads, 4 streamer loads only, 16 no unsorted-tile path, 32 header wave
 // at raised issue priority, 128 per-tile timeline stamps into kp.bmatch
-// (scripts/probe_timeline.hip: 16 words per tile, 100 MHz real-time clock).
+// (scripts/probe_timeline.hip: 16 words per tile, 100 MHz real-time clock),
+// 131072 the fused set's masks computed but (almost) never stored, 262144 a
+// constant mask stored without a set, 524288 the masks stored through the
+// cache instead of non-temporally (scripts/probe_fused_fixed.hip).
 #define TILE_STAMP(i)                                                                             \
 	do {                                                                                          \
 		if constexpr ((DBG & 128) != 0) {                                                         \
@@ -1142,10 +1145,18 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 				}
 #ifdef MOSRX_RTC_BPF
 				if constexpr ((VAR & VAR_BPF) != 0) {
-					if (active)
-						out_store(kp.bmatch, p, h.bmatch);
+					if (active && ((DBG & 131072) == 0 || h.bmatch == 0x5A5A5A5Au)) {
+						if constexpr ((DBG & 524288) != 0)
+							kp.bmatch[p] = h.bmatch;   // probe: a cached store
+						else
+							out_store(kp.bmatch, p, h.bmatch);
+					}
 				}
 #endif
+				if constexpr ((DBG & 262144) != 0) {
+					if (active)
+						out_store(kp.bmatch, p, 0xFFu);
+				}
 				const hdr_pend_t q =
 				    hdr_pend(h, kp.flags, sorted && cand ? chunk_overshoot(ov, (hi_l - 1u) & ~15u, hi_l) : 0u);
 				TILE_STAMP(3);

@@ -6,6 +6,8 @@
 // (scripts/probe_fused/mosrx_bpf_hook.h):
 //   plain       classify_tile_stream<3, 0>          (the library's IMIX variant)
 //   fused       classify_tile_stream<3, VAR_BPF>    (hook + 4-byte mask per frame)
+//   fused, masks not stored (DBG 131072); plain + a constant mask stored (DBG 262144);
+//   fused with the masks stored through the cache (DBG 524288)
 // one 256K IMIX batch per launch and a ring of 8 batches per launch (the
 // batch-queue kernel), dispatch-stamped medians.  If hipcc's fused form costs
 // what the hipRTC module does, the cost is the tile's; if not, the module path.
@@ -36,6 +38,21 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(8))) void k_
 	classify_tile_stream<S, VAR_BPF>(kp, blockIdx.x);
 }
 
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(8))) void k_fused_nostore(mosrx_kparams kp)
+{
+	classify_tile_stream<S, VAR_BPF, 131072>(kp, blockIdx.x);
+}
+
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(8))) void k_fused_cached(mosrx_kparams kp)
+{
+	classify_tile_stream<S, VAR_BPF, 524288>(kp, blockIdx.x);
+}
+
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(8))) void k_plain_store(mosrx_kparams kp)
+{
+	classify_tile_stream<S, 0, 262144>(kp, blockIdx.x);
+}
+
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(8)))
 void kq_plain(const mosrx_qdesc *desc, uint32_t tpb, uint32_t nb, mosrx_qparams qp)
 {
@@ -63,8 +80,11 @@ static int stamped(int f, const std::vector<mosrx_kparams> &kps, const std::vect
 		switch (f) {
 		case 0: hipExtLaunchKernelGGL(k_plain, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kp); break;
 		case 1: hipExtLaunchKernelGGL(k_fused, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kp); break;
+		case 4: hipExtLaunchKernelGGL(k_fused_nostore, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kp); break;
+		case 6: hipExtLaunchKernelGGL(k_fused_cached, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kp); break;
+		case 5: hipExtLaunchKernelGGL(k_plain_store, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kp); break;
 		case 2: hipExtLaunchKernelGGL(kq_plain, dim3(rtiles), dim3(WG), 0, 0, e0[i], e1[i], 0, d, tpb, rb, qp); break;
-		default: hipExtLaunchKernelGGL(kq_fused, dim3(rtiles), dim3(WG), 0, 0, e0[i], e1[i], 0, d, tpb, rb, qp); break;
+		case 3: hipExtLaunchKernelGGL(kq_fused, dim3(rtiles), dim3(WG), 0, 0, e0[i], e1[i], 0, d, tpb, rb, qp); break;
 		}
 	}
 	CHK(hipDeviceSynchronize());
@@ -156,14 +176,15 @@ int main(int argc, char **argv)
 	const double bytes = (double)t.caplen_sum + 22.0 * n;
 	printf("IMIX %u frames per batch, %u tiles; %.2f MB algorithmic per batch; masks zero for %u frames\n", n, tiles,
 	       bytes / 1e6, zero);
-	static const char *names[4] = {"single, plain", "single, fused (trivial)", "ring of 8, plain",
-	                               "ring of 8, fused (trivial)"};
+	static const char *names[7] = {"single, plain", "single, fused (trivial)", "ring of 8, plain",
+	                               "ring of 8, fused (trivial)", "single, fused, masks not stored",
+	                               "single, plain + constant masks", "single, fused, cached mask stores"};
 	for (int rep = 0; rep < 3; rep++)
-		for (int f = 0; f < 4; f++) {
+		for (int f = 0; f < 7; f++) {
 			double med;
 			if (stamped(f, kps, rings, tiles, tiles * rb, tiles, rb, qp, 128, &med))
 				return 1;
-			const double by = bytes * (f >= 2 ? rb : 1);
+			const double by = bytes * (f == 2 || f == 3 ? rb : 1);
 			printf("rep %d %-28s stamped median %8.2f us (%.3f of 8 TB/s)\n", rep, names[f], med,
 			       by / (med * 1e-6) / 8e12);
 		}

@@ -153,3 +153,24 @@ def test_generated_random_programs(tmp_path, pred, seed, fused):
         exp = O.bpf_eval(ps, z["frames"], z["off"], z["len"])
         bad = np.nonzero(got != exp)[0]
         assert not len(bad), (i, bad[:5], hex(int(got[bad[0]] ^ exp[bad[0]])))
+
+
+def test_hook_window_and_lds_copy():
+    """The fused hook's window (MOSRX_BPF_WEND) and LDS copy follow the set
+    (bpf_jit.c hook_wend / x_provenance): header filters whose indexed loads
+    take X = 4 * ihl read registers of the stream tile's 62-byte window and
+    copy nothing to LDS; a payload-offset load (X computed from the TCP data
+    offset, mOS's HTTP-GET filter) sizes the window for IPv4 + a timestamped
+    TCP header (78) and reads the hook's LDS copy of it."""
+    import bench
+    progs = bench.bpf_bench_programs()
+    names = [e for e, _ in bench.BPF_BENCH]
+    get = names.index("tcp[((tcp[12:1] & 0xf0) >> 2):4] = 0x47455420")
+    header = [p for j, p in enumerate(progs) if j != get]
+    src = mosrx.bpf_jit_hook_source(header)
+    assert "#define MOSRX_BPF_WEND 62" in src and "s_bw" not in src and "hk_ind_le32<HL>(bw" not in src
+    assert "X == 20u ? RW32(" in src                       # the ihl = 5 speculation
+    src = mosrx.bpf_jit_hook_source([progs[get]])
+    assert "#define MOSRX_BPF_WEND 78" in src and "__shared__ u32 s_bw" in src and "hk_ind_le32<HL>(bw" in src
+    # the same filter's X = 4 * ihl load (tcp[12:1]) still takes the register speculation
+    assert "X == 20u ? RW32(46u)" in src

@@ -248,6 +248,7 @@ void mosrx_close(mosrx_ctx *c)
 		if (c->slot[i].h_qdesc) hipHostFree(c->slot[i].h_qdesc);
 		if (c->slot[i].d_cnt) hipFree(c->slot[i].d_cnt);
 		if (c->slot[i].h_cnt) hipHostFree(c->slot[i].h_cnt);
+		if (c->slot[i].h_txc) hipHostFree(c->slot[i].h_txc);
 		slot_free(&c->slot[i]);
 	}
 	mosrx__bpf_jit_free(c);   /* (joins the compile thread; launches drained above) */
@@ -365,6 +366,25 @@ int mosrx_tx_csum_dev(mosrx_ctx *c, const mosrx_batch *b, int flags, void *strea
 	                    stream ? (hipStream_t)stream : c->stream);
 }
 
+/* The host side of the TX pass: each frame's checks into the caller's frames,
+ * the bytes the in-place rewrite would have stored (little-endian u16). */
+static void tx_patch(uint8_t *frames, const uint32_t *off, uint32_t n, const mosrx_tx_check *r)
+{
+	uint32_t i;
+	for (i = 0; i < n; i++) {
+		uint8_t *f = frames + off[i];
+		if (r[i].what & 1u) {
+			f[24] = (uint8_t)r[i].ip_check;
+			f[25] = (uint8_t)(r[i].ip_check >> 8);
+		}
+		if (r[i].what & 2u) {
+			uint8_t *t = f + 30u + 4u * r[i].ihl;
+			t[0] = (uint8_t)r[i].tcp_check;
+			t[1] = (uint8_t)(r[i].tcp_check >> 8);
+		}
+	}
+}
+
 int mosrx_tx_csum_host(mosrx_ctx *c, const mosrx_batch *b, int flags)
 {
 	struct slot *s;
@@ -381,14 +401,38 @@ int mosrx_tx_csum_host(mosrx_ctx *c, const mosrx_batch *b, int flags)
 	HIPCHK(hipSetDevice(c->device));
 	if ((rc = mosrx__slot_reserve(c, s, b->frames_bytes, b->n)))
 		return rc;
+	if (getenv("MOSRX_TX_HOST_INPLACE")) {   /* diagnostic: round 3's pass, the frames rewritten and copied back */
+		HIPCHK(hipMemcpyAsync(s->d_frames, b->frames, b->frames_bytes, hipMemcpyHostToDevice, s->stream));
+		HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
+		HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
+		if ((rc = launch_flags(c, b, s->d_frames, s->d_off, s->d_len, NULL, NULL, NULL, NULL, tx_kflags(flags),
+		                       s->stream)))
+			return rc;
+		HIPCHK(hipMemcpyAsync((void *)b->frames, s->d_frames, b->frames_bytes, hipMemcpyDeviceToHost, s->stream));
+		HIPCHK(hipStreamSynchronize(s->stream));
+		return 0;
+	}
+	if (s->h_txc_n < b->n) {          /* the check records come back into pinned memory */
+		if (s->h_txc)
+			hipHostFree(s->h_txc);
+		s->h_txc = NULL;
+		s->h_txc_n = 0;
+		if (hipHostMalloc((void **)&s->h_txc, (size_t)s->cap_n * sizeof(mosrx_tx_check), hipHostMallocDefault) !=
+		    hipSuccess)
+			return -ENOMEM;
+		s->h_txc_n = s->cap_n;
+	}
 	HIPCHK(hipMemcpyAsync(s->d_frames, b->frames, b->frames_bytes, hipMemcpyHostToDevice, s->stream));
 	HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
 	HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
-	if ((rc = launch_flags(c, b, s->d_frames, s->d_off, s->d_len, NULL, NULL, NULL, NULL, tx_kflags(flags),
+	/* the kernel writes 8-byte check records (into the records' buffer, 16 B per frame), not the frames */
+	if ((rc = launch_flags(c, b, s->d_frames, s->d_off, s->d_len, s->d_res, NULL, NULL, NULL, tx_kflags(flags),
 	                       s->stream)))
 		return rc;
-	HIPCHK(hipMemcpyAsync((void *)b->frames, s->d_frames, b->frames_bytes, hipMemcpyDeviceToHost, s->stream));
+	HIPCHK(hipMemcpyAsync(s->h_txc, s->d_res, (size_t)b->n * sizeof(mosrx_tx_check), hipMemcpyDeviceToHost,
+	                      s->stream));
 	HIPCHK(hipStreamSynchronize(s->stream));
+	tx_patch((uint8_t *)b->frames, b->off, b->n, s->h_txc);
 	return 0;
 }
 

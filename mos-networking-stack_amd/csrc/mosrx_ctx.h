@@ -47,6 +47,8 @@ struct slot {
 	uint32_t *h_cnt;   /* MOSRX_R_COUNT, pinned: a D2H copy into pageable memory blocks the host */
 	hipEvent_t kev0, kev1;     /* around the kernel of the last submit (when the context times) */
 	mosrx_qdesc *h_qdesc;      /* MOSRX_MAX_GROUP, pinned: a group's batch table */
+	mosrx_tx_check *h_txc;     /* pinned: the TX pass's check records (mosrx_tx_csum_host), h_txc_n of them */
+	uint32_t h_txc_n;
 	mosrx_qdesc *d_qdesc;
 	int timed;
 	int busy;

@@ -508,21 +508,19 @@ __device__ __forceinline__ void store_tcpinfo(mosrx_tcpinfo *ti, uint32_t p, con
 // The TCP value is the full-segment sum with the old check word taken out in
 // one's-complement arithmetic: TCPCalcChecksum depends only on the sum mod
 // 0xFFFF (the sum is > 0: the pseudo header holds 0x0600).
+// With kp.out set the frames stay untouched: each frame's checks go out as an
+// 8-byte record (mosrx_tx_check: the two check words, which of them apply,
+// ihl) and the host writes them into its own copy of the frames -- what
+// crosses PCIe back is 8 bytes per frame instead of the frame.
 __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffer_rsrc_t rs, const hdr_t &h,
-                                         uint32_t tail_sum)
+                                         uint32_t tail_sum, uint32_t p, bool active)
 {
 	// an even frame start puts both check words on 2-byte boundaries: one short
 	// store each (1.5-3 % faster than byte pairs; tails read with the default
 	// cache policy so the stores hit L2 lines measured 20 % slower)
 	const bool even = (h.o & 1u) == 0u;
-	if (h.tx_ip && (kp.flags & MOSRX_KF_TX_IP)) {
-		if (even) {
-			__builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipc_tx, rs, h.o + 24u, 0, 0);
-		} else {
-			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)h.ipc_tx, rs, h.o + 24u, 0, 0);
-			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)(h.ipc_tx >> 8), rs, h.o + 25u, 0, 0);
-		}
-	}
+	const bool ip = h.tx_ip && (kp.flags & MOSRX_KF_TX_IP);
+	uint32_t c = 0;
 	if (h.need_tcp) {
 		const uint32_t seglen = (h.ip_len - h.ihl * 4u) & 0xFFFFu;
 		uint32_t s = h.wsum + (h.saddr & 0xFFFFu) + (h.saddr >> 16) + (h.daddr & 0xFFFFu) + (h.daddr >> 16) +
@@ -540,7 +538,26 @@ __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffe
 		const uint32_t tcw_in = seglen >= 18u ? h.tcw : seglen == 17u ? (h.tcw & 0xFFu) : 0u;
 		uint32_t v = (s & 0xFFFFu) + (0xFFFFu - tcw_in);
 		v = (v & 0xFFFFu) + (v >> 16);
-		const uint32_t c = (~v) & 0xFFFFu;
+		c = (~v) & 0xFFFFu;
+	}
+	if (kp.out) {
+		if (active) {
+			u32x2 r;
+			r.x = (h.ipc_tx & 0xFFFFu) | (c << 16);
+			r.y = (ip ? 1u : 0u) | (h.need_tcp ? 2u : 0u) | (h.ihl << 8);
+			out_store(reinterpret_cast<u32x2 *>(kp.out), p, r);
+		}
+		return;
+	}
+	if (ip) {
+		if (even) {
+			__builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipc_tx, rs, h.o + 24u, 0, 0);
+		} else {
+			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)h.ipc_tx, rs, h.o + 24u, 0, 0);
+			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)(h.ipc_tx >> 8), rs, h.o + 25u, 0, 0);
+		}
+	}
+	if (h.need_tcp) {
 		const uint32_t at = h.o + 30u + 4u * h.ihl;
 		if (even) {
 			__builtin_amdgcn_raw_buffer_store_b16((uint16_t)c, rs, at, 0, 0);
@@ -695,7 +712,7 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 			tail = x;
 	}
 	if constexpr (IS_TX(VAR)) {
-		tx_store(kp, rs, h, tail);
+		tx_store(kp, rs, h, tail, p, active);
 	} else if constexpr ((DBG & 4) != 0) {   // probe: records kept live, (almost) never stored
 		const u32x4 r = hdr_finish(h, tail, kp.flags);
 		if (active && (r.x ^ r.y ^ r.z ^ r.w) == 0x9E3779B9u)
@@ -761,7 +778,7 @@ __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffe
 			tail -= s;
 	}
 	if constexpr (IS_TX(VAR)) {
-		tx_store(kp, rs, h, tail);
+		tx_store(kp, rs, h, tail, p, active);
 	} else if (active) {
 		store_record<VAR>(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (kp.fhash)

@@ -107,3 +107,25 @@ def test_tx_full_size_traces(gpu_ctx, kind, n):
     gpu_ctx.classify_dev(db)
     assert np.all(db.results()["reason"] == mosrx.R["TCP_OK"])
     db.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_tx_host_records_full_size(gpu_ctx, shift):
+    """mosrx_tx_csum_host brings back 8-byte check records and writes them into
+    the caller's frames on the host (csrc/mosrx_api.c tx_patch): the frames
+    equal the oracle's rewrite and the device's in-place one, at every frame
+    alignment (odd starts store the check words byte by byte on the GPU)."""
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 65_536)
+    buf = np.zeros(len(t.frames) + 8, np.uint8)
+    buf[shift:shift + len(t.frames)] = t.frames
+    off = (t.off + shift).astype(np.uint32)
+    exp = O.tx_csum(buf, off, t.len, IP | TCP)
+    got = gpu_ctx.tx_csum_host(buf, off, t.len, IP | TCP)
+    np.testing.assert_array_equal(got, exp)
+    for flags in (IP, TCP):
+        np.testing.assert_array_equal(gpu_ctx.tx_csum_host(buf, off, t.len, flags), O.tx_csum(buf, off, t.len, flags))
+    db = gpu_ctx.upload(buf, off, t.len)
+    gpu_ctx.tx_csum_dev(db, IP | TCP)
+    np.testing.assert_array_equal(db.frames(len(buf)), exp)
+    db.free()

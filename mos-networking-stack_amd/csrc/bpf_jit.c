@@ -18,6 +18,15 @@
  * Compiled sets are cached per context by content hash, so re-installing a set
  * costs a lookup.  When hipRTC is unavailable or fails the set runs on the
  * interpreter (mosrx_bpf_engine() reports which engine is installed).
+ *
+ * The same generator writes the fused form (mosrx__bpf_jit_hook_source): the
+ * set as a device function the classify tiles' header wave calls on its
+ * realigned window.  There, constant-offset loads read the window's registers;
+ * an indexed load whose X can only be 4 * ihl (x_provenance) speculates ihl = 5
+ * and reads registers too; any other indexed load reads a copy of the window
+ * the hook writes to LDS.  MOSRX_BPF_PRED=1 emits the programs if-converted
+ * (gen_pred) instead of branchy; tests/test_bpf_gen.py runs both forms of both
+ * outputs on the CPU against mOS's results.
  */
 #include <errno.h>
 #include <pthread.h>

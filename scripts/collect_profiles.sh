@@ -1,4 +1,4 @@
-# Copy the judged evidence of a scripts/gpu_r2_final.sh run from gpurun_out/ (scratch,
+# Copy the judged evidence of a scripts/runs/gpu_r2_final.sh run from gpurun_out/ (scratch,
 # merged back by gpurun) into profiles/ (tracked).  Run here, after the GPU call.
 #   kernel-trace summaries : profiles/<round>_kt_<W>_kernel_stats.csv + the bench line of that run
 #   PMC passes             : profiles/<round>_pmc_{fetch,write}_<W>.csv + profiles/pmc_traffic.json

@@ -1,6 +1,6 @@
 # round-2 final evidence on the current tree.  PART=1: GPU suite + smoke, the
 # driver-style and default bench; PART=2: PMC traffic passes and kernel-trace
-# summaries (scripts/gpu_r2_profiles.sh), then the two-rank rehearsal
+# summaries (scripts/runs/gpu_r2_profiles.sh), then the two-rank rehearsal
 set -o pipefail
 mkdir -p gpurun_out
 if [ "${PART:-1}" = 1 ]; then
@@ -10,7 +10,7 @@ if [ "${PART:-1}" = 1 ]; then
   tail -1 gpurun_out/smoke.log; [ $rc -ne 0 ] && exit $rc
   bash scripts/gpu_bench.sh || exit $?
 else
-  bash scripts/gpu_r2_profiles.sh > gpurun_out/profiles_run.log 2>&1; rc=$?
+  bash scripts/runs/gpu_r2_profiles.sh > gpurun_out/profiles_run.log 2>&1; rc=$?
   tail -30 gpurun_out/profiles_run.log; [ $rc -ne 0 ] && exit $rc
-  bash scripts/gpu_dist_rehearsal.sh
+  bash scripts/runs/gpu_dist_rehearsal.sh
 fi

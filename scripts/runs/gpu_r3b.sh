@@ -6,4 +6,4 @@ timeout -k 10 420 python -u -m pytest -x -v --timeout 120 --timeout-method threa
     tests/test_mos_consumer.py tests/test_backend_gpu.py > gpurun_out/r3b/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/r3b/pytest.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-bash scripts/gpu_r3_profiles.sh
+bash scripts/runs/gpu_r3_profiles.sh

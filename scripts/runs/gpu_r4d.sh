@@ -8,5 +8,5 @@ timeout -k 10 400 python -u -m pytest -v --maxfail=5 --timeout 120 --timeout-met
     tests/test_bpf.py tests/test_bpf_groups.py > $out/pytest_bpf.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -2 $out/pytest_bpf.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-bash scripts/gpu_r4c.sh || exit $?
-bash scripts/gpu_probe_persist2.sh
+bash scripts/runs/gpu_r4c.sh || exit $?
+bash scripts/runs/gpu_probe_persist2.sh

@@ -103,12 +103,15 @@ static const char k_preamble[] =
 	"  const u32 hi = __builtin_amdgcn_raw_buffer_load_b32(rs, a4 + 4u, 0, 0);\n"
 	"  return __builtin_amdgcn_alignbyte(hi, lo, a & 3u);\n"
 	"}\n"
+	"/* frame bytes [k, k+4): the LDS stage (sets with loads at an X not 4 * ihl), else memory */\n"
 	"static __device__ __attribute__((always_inline)) inline u32 fr_le32(const u32 *win, u32 sh, __amdgpu_buffer_rsrc_t rs, u32 o,\n"
 	"                                              u32 k, u32 size) {\n"
+	"#if STAGE_LDS\n"
 	"  if (k + size <= STAGE_B) {\n"
 	"    const u32 a = sh + k;\n"
 	"    return __builtin_amdgcn_alignbyte(win[(a >> 2) + 1u], win[a >> 2], a & 3u);\n"
 	"  }\n"
+	"#endif\n"
 	"  return ld_le32(rs, o + k);\n"
 	"}\n"
 	"#define STAGE_W (4u * STAGE_V - 1u)\n"
@@ -118,7 +121,9 @@ static const char k_preamble[] =
 	"static __device__ __attribute__((always_inline)) inline u32 be16(u32 v) { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); }\n"
 	"extern \"C\" __global__ __launch_bounds__(256) void mosrx_bpf_jit(const u8 *frames, const u32 *offs,\n"
 	"    const u16 *lens, u32 *match_out, u32 nbytes, u32 n) {\n"
+	"#if STAGE_LDS\n"
 	"  __shared__ u32 s_win[STAGE_LD * 256];\n"
+	"#endif\n"
 	"  const u32 t = threadIdx.x;\n"
 	"  const u32 p = blockIdx.x * 256u + t;\n"
 	"  const bool live = p < n;\n"
@@ -130,7 +135,11 @@ static const char k_preamble[] =
 	"    const u32 l = lens[p];\n"
 	"    cap = (o >= nbytes) ? 0u : (l < nbytes - o ? l : nbytes - o);\n"
 	"  }\n"
+	"#if STAGE_LDS\n"
 	"  u32 *win = s_win + STAGE_LD * t;\n"
+	"#else\n"
+	"  const u32 *win = nullptr;\n"
+	"#endif\n"
 	"  const u32 sh = o & 3u;\n"
 	"  u32 w[STAGE_W];   /* frame bytes [4i, 4i + 4) in w[i]: constant-offset loads read registers */\n"
 	"  {\n"
@@ -142,7 +151,9 @@ static const char k_preamble[] =
 	"#pragma unroll\n"
 	"    for (u32 m = 0; m < STAGE_V; m++) {\n"
 	"      r[4 * m + 0] = v[m].x; r[4 * m + 1] = v[m].y; r[4 * m + 2] = v[m].z; r[4 * m + 3] = v[m].w;\n"
+	"#if STAGE_LDS\n"
 	"      win[4 * m + 0] = v[m].x; win[4 * m + 1] = v[m].y; win[4 * m + 2] = v[m].z; win[4 * m + 3] = v[m].w;\n"
+	"#endif\n"
 	"    }\n"
 	"#pragma unroll\n"
 	"    for (u32 i = 0; i < STAGE_W; i++) w[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sh);\n"
@@ -251,8 +262,11 @@ static void gen_ld(struct sbuf *s, uint32_t k, uint32_t size, const struct genop
  * the 64 B ring 19 us per such program. */
 static void gen_ind(struct sbuf *s, uint32_t k, uint32_t size, int msh, const struct genopt *g)
 {
-	if (!g->fused) {
-		sb_printf(s, "fr_le32(win, sh, rs, o, kk, %uu)", size);
+	if (!g->fused) {   /* the same speculation from the realigned staged registers */
+		if (msh && (uint64_t)k + 20 + 8 <= 4ull * g->stage_w)
+			sb_printf(s, "(X == 20u ? W32(%uu) : fr_le32(win, sh, rs, o, kk, %uu))", k + 20, size);
+		else
+			sb_printf(s, "fr_le32(win, sh, rs, o, kk, %uu)", size);
 		return;
 	}
 	if (msh && (uint64_t)k + 20 + 8 <= g->wend) {
@@ -474,6 +488,9 @@ static int gen_pred(struct sbuf *s, const mosrx_bpf_insn *f, uint32_t len, const
 				sb_printf(s, "v = hk_ind_le32<HL>(bw, c ? kk : 2u, rs, o); ");
 			} else if (g->fused) {
 				sb_printf(s, "v = hk_ld_le32(rs, o + kk); ");   /* a buffer load: out-of-range offsets read 0 */
+			} else if ((tgt[i] & TG_XMSH) && (uint64_t)k + 20 + 8 <= 4ull * g->stage_w) {
+				sb_printf(s, "v = W32(%uu); if (__any(c && X != 20u)) v = X == 20u ? v : fr_le32(win, sh, rs, o, kk, %uu); ",
+				          k + 20, size);
 			} else {   /* lanes off the path read the stage at offset 0, not at their X + k */
 				sb_printf(s, "v = fr_le32(win, sh, rs, o, c ? kk : 0u, %uu); ", size);
 			}
@@ -673,24 +690,37 @@ static uint64_t set_hash(const mosrx_bpf_insn *insns, const mosrx_bparams *t)
 }
 
 /* 16-byte pieces of each frame to stage in LDS: enough for every constant
- * offset the set loads, and 96 bytes (Ethernet + IP + TCP headers with
- * options) when a program loads at X + k; loads past the stage read memory. */
+ * offset the set loads, and for loads at X + k the offset X most frames give:
+ * 4 * ihl with ihl 5 where only `ldxb 4*([k]&0xf)` defines X (x_provenance),
+ * else IPv4 + a TCP header with timestamps (52); loads past the stage read
+ * memory.  A window read costs the HBM sectors it touches (the IMIX launch
+ * moved 2x its algorithmic bytes staging 96 bytes per frame), so it is no
+ * longer than the set needs. */
 static uint32_t stage_pieces(const mosrx_bpf_insn *insns, const mosrx_bparams *t)
 {
 	uint64_t need = 18;   /* the datagram-length probe reads frame bytes 12..17 */
 	uint32_t j, i;
-	for (j = 0; j < t->nprog; j++)
+	for (j = 0; j < t->nprog; j++) {
+		const mosrx_bpf_insn *f = &insns[t->prog_off[j]];
+		uint8_t *tg = calloc((size_t)t->prog_len[j] + 1, 1);
+		if (!tg)
+			return 9;
+		x_provenance(f, t->prog_len[j], tg);
 		for (i = 0; i < t->prog_len[j]; i++) {
-			const mosrx_bpf_insn *f = &insns[t->prog_off[j] + i];
-			const uint16_t c = f->code;
+			const uint16_t c = f[i].code;
+			const uint64_t size = (c & 0x18) == W ? 4 : (c & 0x18) == H ? 2 : 1;
 			uint64_t end = 0;
-			if (c == (LD | W | ABS)) end = (uint64_t)f->k + 4;
-			else if (c == (LD | H | ABS)) end = (uint64_t)f->k + 2;
-			else if (c == (LD | B | ABS) || c == (LDX | MSH | B)) end = (uint64_t)f->k + 1;
-			else if (c == (LD | W | IND) || c == (LD | H | IND) || c == (LD | B | IND)) end = 96;
+			if (c == (LD | W | ABS) || c == (LD | H | ABS) || c == (LD | B | ABS) || c == (LDX | MSH | B))
+				end = (uint64_t)f[i].k + size;
+			else if (c == (LD | W | IND) || c == (LD | H | IND) || c == (LD | B | IND))
+				end = (uint64_t)f[i].k + size + ((tg[i] & TG_XMSH) ? 20 : 52);
 			if (end > need)
 				need = end;
 		}
+		free(tg);
+	}
+	if (getenv("MOSRX_BPF_STAGE96") && need < 96)   /* diagnostic: round 3's 96 bytes for any indexed load */
+		need = 96;
 	/* frame bytes [0, 16 V - 3) are staged whatever the start alignment */
 	need = (need + 3 + 15) / 16;
 	return need > 9 ? 9 : (uint32_t)need;
@@ -702,9 +732,15 @@ int mosrx__bpf_jit_source(const mosrx_bpf_insn *insns, const mosrx_bparams *t, c
 	const uint32_t v = stage_pieces(insns, t);
 	const struct genopt g = {0, 4 * v - 1, 0, pred_mode(), 0};
 	uint32_t j;
-	int rc;
+	int rc, lds = 0;
 	*out = NULL;
-	sb_printf(&s, "#define STAGE_V %uu\n#define STAGE_LD %uu\n#define STAGE_B %uu\n", v, 4 * v + 1, 16 * v - 3);
+	for (j = 0; j < t->nprog && !lds; j++) {
+		uint8_t *tg = calloc((size_t)t->prog_len[j] + 1, 1);
+		lds = !tg || x_provenance(insns + t->prog_off[j], t->prog_len[j], tg);
+		free(tg);
+	}
+	sb_printf(&s, "#define STAGE_V %uu\n#define STAGE_LD %uu\n#define STAGE_B %uu\n#define STAGE_LDS %d\n", v, 4 * v + 1,
+	          16 * v - 3, lds);
 	sb_printf(&s, "%s", k_preamble);
 	for (j = 0; j < t->nprog; j++)
 		if ((rc = gen_program(&s, j, insns + t->prog_off[j], t->prog_len[j], (t->ip_mode >> j) & 1u, &g))) {

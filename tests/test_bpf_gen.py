@@ -174,3 +174,20 @@ def test_hook_window_and_lds_copy():
     assert "#define MOSRX_BPF_WEND 78" in src and "__shared__ u32 s_bw" in src and "hk_ind_le32<HL>(bw" in src
     # the same filter's X = 4 * ihl load (tcp[12:1]) still takes the register speculation
     assert "X == 20u ? RW32(46u)" in src
+
+
+def test_standalone_stage_follows_the_set():
+    """The standalone kernel stages what the set reads (stage_pieces): header
+    filters keep their bytes in registers only (no LDS stage; X = 4 * ihl loads
+    speculate ihl = 5), a payload-offset load adds the LDS stage of the frame's
+    first 80 bytes."""
+    import bench
+    progs = bench.bpf_bench_programs()
+    names = [e for e, _ in bench.BPF_BENCH]
+    get = names.index("tcp[((tcp[12:1] & 0xf0) >> 2):4] = 0x47455420")
+    header = [p for j, p in enumerate(progs) if j != get]
+    src = mosrx.bpf_jit_source(header)
+    assert "#define STAGE_LDS 0" in src and "#define STAGE_V 4u" in src   # tcp[13] at X + 27: bytes [0, 61)
+    assert "X == 20u ? W32(" in src
+    src = mosrx.bpf_jit_source(progs)
+    assert "#define STAGE_LDS 1" in src and "#define STAGE_V 5u" in src

@@ -401,7 +401,10 @@ int mosrx_tx_csum_host(mosrx_ctx *c, const mosrx_batch *b, int flags)
 	HIPCHK(hipSetDevice(c->device));
 	if ((rc = mosrx__slot_reserve(c, s, b->frames_bytes, b->n)))
 		return rc;
-	if (getenv("MOSRX_TX_HOST_INPLACE")) {   /* diagnostic: round 3's pass, the frames rewritten and copied back */
+	static int inplace = -1;                 /* diagnostic: round 3's pass, the frames rewritten and copied back */
+	if (inplace < 0)
+		inplace = getenv("MOSRX_TX_HOST_INPLACE") != NULL;
+	if (inplace) {
 		HIPCHK(hipMemcpyAsync(s->d_frames, b->frames, b->frames_bytes, hipMemcpyHostToDevice, s->stream));
 		HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
 		HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));

@@ -893,6 +893,70 @@ int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams 
  * its own compile thread, and the compiles are rare (a filter set change). */
 static pthread_mutex_t g_rtc_lock = PTHREAD_MUTEX_INITIALIZER;
 
+/* Code objects already built in this process, by source text: every mTCP
+ * thread's context compiles the same set when mOS installs its filters, and
+ * after the first one the others only load it (hipRTC through comgr's disk
+ * cache still takes ~50 ms a time, serialised by g_rtc_lock). */
+#define RTC_CACHE 8
+static struct rtc_cached {
+	char *src, *hook;   /* the program text and its last header (the generated hook), exact keys */
+	int nh;
+	char *code;
+	size_t size;
+	uint64_t used;
+} g_rtc_cache[RTC_CACHE];
+static uint64_t g_rtc_tick;
+
+static int rtc_cache_get(const char *src, int nh, const char *hook, char **code, size_t *size)
+{
+	int i;
+	for (i = 0; i < RTC_CACHE; i++) {
+		struct rtc_cached *e = &g_rtc_cache[i];
+		if (e->code && e->nh == nh && !strcmp(e->src, src) && !strcmp(e->hook, hook)) {
+			if (!(*code = malloc(e->size)))
+				return 0;
+			memcpy(*code, e->code, e->size);
+			*size = e->size;
+			e->used = ++g_rtc_tick;
+			return 1;
+		}
+	}
+	return 0;
+}
+
+static void rtc_cache_put(const char *src, int nh, const char *hook, const char *code, size_t size)
+{
+	struct rtc_cached *e = NULL;
+	char *s2, *h2, *c2;
+	int i;
+	for (i = 0; i < RTC_CACHE && !e; i++)   /* an empty slot, else the least recently used */
+		if (!g_rtc_cache[i].code)
+			e = &g_rtc_cache[i];
+	if (!e)
+		for (e = &g_rtc_cache[0], i = 1; i < RTC_CACHE; i++)
+			if (g_rtc_cache[i].used < e->used)
+				e = &g_rtc_cache[i];
+	s2 = strdup(src);
+	h2 = strdup(hook);
+	c2 = malloc(size);
+	if (!s2 || !h2 || !c2) {
+		free(s2);
+		free(h2);
+		free(c2);
+		return;
+	}
+	memcpy(c2, code, size);
+	free(e->src);
+	free(e->hook);
+	free(e->code);
+	e->src = s2;
+	e->hook = h2;
+	e->nh = nh;
+	e->code = c2;
+	e->size = size;
+	e->used = ++g_rtc_tick;
+}
+
 /* hipRTC: source -> gfx950 code object (malloc'd into *code). */
 static int compile_code_h(const char *src, int nh, const char *const *htexts, const char *const *hnames,
                           char **code, size_t *size, char *log, size_t logsz)
@@ -903,8 +967,13 @@ static int compile_code_h(const char *src, int nh, const char *const *htexts, co
 	const char *opts[] = {"--offload-arch=gfx950", "-O3", "-mllvm", "-amdgpu-kernarg-preload-count=7"};
 	size_t sz = 0;
 	int rc = 0;
+	const char *hook = nh ? htexts[nh - 1] : "";
 	*code = NULL;
 	pthread_mutex_lock(&g_rtc_lock);
+	if (rtc_cache_get(src, nh, hook, code, size)) {
+		pthread_mutex_unlock(&g_rtc_lock);
+		return 0;
+	}
 	if (hiprtcCreateProgram(&prog, src, "mosrx_bpf_jit.hip", nh, (const char **)htexts, (const char **)hnames) !=
 	    HIPRTC_SUCCESS) {
 		pthread_mutex_unlock(&g_rtc_lock);
@@ -929,6 +998,8 @@ static int compile_code_h(const char *src, int nh, const char *const *htexts, co
 	else if (hiprtcGetCode(prog, *code) != HIPRTC_SUCCESS)
 		rc = -EIO;
 	hiprtcDestroyProgram(&prog);
+	if (!rc)
+		rtc_cache_put(src, nh, hook, *code, sz);
 	pthread_mutex_unlock(&g_rtc_lock);
 	if (!rc && getenv("MOSRX_BPF_DUMP")) {   /* diagnostics: the code object, for llvm-readelf --notes */
 		char path[512];

@@ -191,3 +191,17 @@ def test_standalone_stage_follows_the_set():
     assert "X == 20u ? W32(" in src
     src = mosrx.bpf_jit_source(progs)
     assert "#define STAGE_LDS 1" in src and "#define STAGE_V 5u" in src
+
+
+def test_compiled_sets_shared_in_process():
+    """A set compiled once in the process is not compiled again (bpf_jit.c
+    rtc_cache_*): every mTCP thread's context installs the same filters, and
+    after the first only loads the code object."""
+    import time
+    import bench
+    ps = bench.bpf_bench_programs()[2:5]
+    rc, size, log = mosrx.bpf_jit_compile_fused(ps)
+    assert rc == 0 and size > 0, log
+    t0 = time.perf_counter()
+    rc2, size2, _ = mosrx.bpf_jit_compile_fused(ps)
+    assert (rc2, size2) == (0, size) and time.perf_counter() - t0 < 0.02

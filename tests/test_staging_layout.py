@@ -112,3 +112,24 @@ def test_packed_64b_batch_bytes():
         assert len(o) == 1000 and end == 2 + 60 * 1000
     finally:
         mosrx.lib().mosrx_source_close(src)
+
+
+def test_mem_source_runs_across_replay_loops():
+    """A batch longer than the replay buffer takes several runs of it: each run
+    is copied whole at the source's alignment mod 16, so its long frames stay
+    at 16 B + 2; between runs at most 15 bytes of gap."""
+    fr, buf, off, ln = frames_of(SIZES)
+    src = mosrx.mem_source(buf, off, ln, loops=4, mode=mosrx.SRC_FILL)
+    try:
+        dst, o, n, end = fill(src, 3 * len(SIZES), 2048)
+        assert len(o) == 3 * len(SIZES)
+        want = fr * 3
+        for i, (a, m) in enumerate(zip(o.tolist(), n.tolist())):
+            assert bytes(dst[a:a + m]) == bytes(want[i][:m]), i
+            if m > 128:
+                assert a % 16 == 2, (i, a)
+            if i:
+                prev_end = int(o[i - 1]) + int(n[i - 1])
+                assert 0 <= a - prev_end < 16, (i, a, prev_end)
+    finally:
+        mosrx.lib().mosrx_source_close(src)

@@ -1044,7 +1044,8 @@ __device__ __forceinline__ void stream_frames(__amdgpu_buffer_rsrc_t rs, uint32_
 // (scripts/probe_timeline.hip: 16 words per tile, 100 MHz real-time clock),
 // 131072 the fused set's masks computed but (almost) never stored, 262144 a
 // constant mask stored without a set, 524288 the masks stored through the
-// cache instead of non-temporally (scripts/probe_fused_fixed.hip).
+// cache instead of non-temporally (scripts/probe_fused_fixed.hip), 1048576 the
+// 78-byte (5-chunk) window (scripts/probe_guided.hip).
 #define TILE_STAMP(i)                                                                             \
 	do {                                                                                          \
 		if constexpr ((DBG & 128) != 0) {                                                         \
@@ -1061,7 +1062,8 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 {
 	constexpr int AUX = TAIL_AUX(VAR);
 	// DBG 2048: the full 96-byte window (the round-1 form, 4 % slower)
-	constexpr int WEND = (DBG & 2048) ? MOSRX_WINDOW_END_FULL : MOSRX_WINDOW_END_STREAM;
+	constexpr int WEND = (DBG & 2048) ? MOSRX_WINDOW_END_FULL : (DBG & 1048576) ? MOSRX_WINDOW_END_SMALL
+	                                                                             : MOSRX_WINDOW_END_STREAM;
 	constexpr int NLOAD = (VAR & VAR_BPF) ? BPF_NLOAD(WEND) : WIN_NLOAD(WEND);
 	// DBG 16384 / 32768 / 65536: RSS form 1 / 2 / 3 of hdr_parse (probe builds)
 	constexpr int RSS = (DBG & 16384) ? 1 : (DBG & 32768) ? 2 : (DBG & 65536) ? 3 : 0;

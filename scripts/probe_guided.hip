@@ -24,6 +24,12 @@ __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(8))) void k_
 	classify_tile_stream<S, 0>(kp, blockIdx.x);
 }
 
+// the library's tile with the 78-byte window (5 chunks: a 64-byte frame needs no streamer)
+__global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(8))) void k_w78(mosrx_kparams kp)
+{
+	classify_tile_stream<S, 0, 1048576>(kp, blockIdx.x);
+}
+
 __global__ __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(8))) void k_guided(mosrx_kparams kp, uint32_t b1)
 {
 	const uint32_t b = blockIdx.x;
@@ -67,6 +73,14 @@ int main(int argc, char **argv)
 	hipLaunchKernelGGL(k_plain, dim3(tiles), dim3(WG), 0, 0, kps[0]);
 	CHK(hipDeviceSynchronize());
 	CHK(hipMemcpy(a.data(), kps[0].out, n * 16, hipMemcpyDeviceToHost));
+	CHK(hipMemset(kps[0].out, 0xEE, n * 16));
+	hipLaunchKernelGGL(k_w78, dim3(tiles), dim3(WG), 0, 0, kps[0]);
+	CHK(hipDeviceSynchronize());
+	CHK(hipMemcpy(b.data(), kps[0].out, n * 16, hipMemcpyDeviceToHost));
+	if (memcmp(a.data(), b.data(), (size_t)n * 16)) {
+		printf("78-byte window: RECORDS DIFFER\n");
+		return 2;
+	}
 	const double bytes = (double)t.caplen_sum + 22.0 * n;
 	// b1 = tiles * q / 8 blocks of 64 frames, the rest in 32-frame tiles
 	const int qs[] = {8, 7, 6, 4, 0};
@@ -89,7 +103,20 @@ int main(int argc, char **argv)
 		CHK(hipEventCreate(&e1[i]));
 	}
 	for (int rep = 0; rep < 3; rep++)
-		for (int qi = -1; qi < 5; qi++) {
+		for (int qi = -2; qi < 5; qi++) {
+			if (qi == -2) {
+				for (int i = 0; i < iters; i++)
+					hipExtLaunchKernelGGL(k_w78, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kps[i % nb]);
+				CHK(hipDeviceSynchronize());
+				std::vector<float> d(iters);
+				for (int i = 0; i < iters; i++)
+					CHK(hipEventElapsedTime(&d[i], e0[i], e1[i]));
+				std::sort(d.begin(), d.end());
+				const double med = d[iters / 2] * 1e-3;
+				printf("rep %d 78-byte window                 %7.2f us (%.3f of 8 TB/s)\n", rep, med * 1e6,
+				       bytes / med / 8e12);
+				continue;
+			}
 			const int q = qi < 0 ? 8 : qs[qi];
 			const uint32_t b1 = tiles * q / 8, nblk = b1 + (n - 64u * b1 + 31u) / 32u;
 			for (int i = 0; i < iters; i++) {

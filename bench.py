@@ -30,6 +30,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import struct
@@ -657,16 +658,28 @@ def measure_fw64_boundary(tr: mosrx.Trace, loops: int = 50):
 def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
     """End-to-end host->HBM->host rate (pinned staging, 2 slots); recorded in DESIGN.md."""
     ctx.set_params(mosrx.default_params())
-    # one pinned staging block per slot, frames | off | len (as the gpu_module
-    # backend stages a batch): the library moves it over PCIe in one copy
-    fb = tr.frames_bytes
+    # one pinned staging block per slot, frames | off | len, the frames in the
+    # gpu_module backend's staging layout (mosrx_source_fill: frames of up to
+    # 128 bytes back to back): the library moves it over PCIe in one copy
+    src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=1, mode=mosrx.SRC_FILL)
+    mf = max(int(tr.max_len), 64)
+    cap = tr.frames_bytes + 2 * mf + 4096      # the fill keeps a largest frame's room past its last frame
+    staged = np.zeros(cap, np.uint8)
+    soff = np.zeros(tr.n, np.uint32)
+    slen = np.zeros(tr.n, np.uint16)
+    end = C.c_uint64(0)
+    got = mosrx.lib().mosrx_source_fill(src, staged.ctypes.data, cap, soff.ctypes.data, slen.ctypes.data, tr.n,
+                                         mf, C.byref(end))
+    mosrx.lib().mosrx_source_close(src)
+    assert got == tr.n, got
+    fb = int(end.value)
     fa = (fb + 15) & ~15
     bufs, outs, batches = [], [], []
     for _ in range(2):
         pb, ab = ctx.host_alloc(fa + tr.n * 6)
-        ab[:fb] = tr.frames[:fb]
-        ab[fa:fa + tr.n * 4].view(np.uint32)[:] = tr.off
-        ab[fa + tr.n * 4:].view(np.uint16)[:] = tr.len
+        ab[:fb] = staged[:fb]
+        ab[fa:fa + tr.n * 4].view(np.uint32)[:] = soff
+        ab[fa + tr.n * 4:].view(np.uint16)[:] = slen
         pr, _ = ctx.host_alloc(tr.n * 16)
         bufs += [pb, pr]
         outs.append(pr)
@@ -678,7 +691,8 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
     ab = algo_bytes(tr)
     return {"gbps": ab * iters / (ms * 1e-3) / 1e9, "mpkts": tr.n * iters / (ms * 1e-3) / 1e6,
             "ms_per_batch": ms / iters,
-            "method": "pinned hipHostMalloc staging (one block: frames | off | len), one H2D copy, kernel, D2H records; 2 streams"}
+            "method": "pinned hipHostMalloc staging (one block: frames | off | len, the backend's layout: "
+                      "mosrx_source_fill), one H2D copy, kernel, D2H records; 2 streams"}
 
 
 def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1, bpf=None):

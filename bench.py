@@ -71,6 +71,8 @@ WORKLOADS = {
     "M1500_fh": (mosrx.TRACE_M1500, 65_536, 0, "config #3 classify + flow-table hash (HashFlow of FindStream's tuple)"),
     "M1500_ti": (mosrx.TRACE_M1500, 65_536, 0, "config #3 classify + pkt_info TCP fields (FillPacketContextTCPInfo)"),
     "M1500_tx": (mosrx.TRACE_M1500, 65_536, 0, "config #3 TX checksum rewrite (MOS_UPDATE_IP|TCP_CHKSUM), in place"),
+    "M1500_txc": (mosrx.TRACE_M1500, 65_536, 0, "config #3 TX checksums as 8-byte records, frames untouched "
+                  "(mosrx_tx_csum_dev_checks)"),
     "IMIX_bpf": (mosrx.TRACE_IMIX, 262_144, 0, "config #4 batched BPF, 8 mOS filter programs (sfbpf_compile output)"),
     "IMIX_cls_bpf": (mosrx.TRACE_IMIX, 262_144, 0, "config #4 classify + the 8 BPF programs fused in one pass"),
     # the fused pass over a ring (the batch queue: gpu_module_func's groups with filters installed)
@@ -80,8 +82,9 @@ WORKLOADS = {
                                                        "launch over 256 batches"),
 }
 DEFAULT_WORKLOADS = ("M1500,S64,S64_hdr,S64_hdr16,S64_hdr_packed,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,"
-                     "M1500_tx,IMIX_bpf,IMIX_cls_bpf,IMIX_cls_bpf_ring,S64_cls_bpf_ring")
+                     "M1500_tx,M1500_txc,IMIX_bpf,IMIX_cls_bpf,IMIX_cls_bpf_ring,S64_cls_bpf_ring")
 OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_ti": mosrx.OP_CLASSIFY_TI, "M1500_tx": mosrx.OP_TX_CSUM,
+       "M1500_txc": mosrx.OP_TX_CHECKS,
        "IMIX_bpf": mosrx.OP_BPF, "IMIX_cls_bpf": mosrx.OP_CLASSIFY_BPF}
 # filter expressions whose compiled programs (tests/golden/bpf.npz, mOS's own compiler) the BPF row runs
 BPF_BENCH = [("tcp", 0), ("tcp port 80", 0), ("tcp[tcpflags] & tcp-syn != 0", 1), ("net 192.168.0.0/16 and tcp", 1),
@@ -145,6 +148,8 @@ def algo_bytes(tr: mosrx.Trace, key: str = "") -> int:
     bytes per frame (the line a filter reads; deeper loads are extra)."""
     if key.endswith("_tx"):
         return tr.caplen_sum + tr.n * (DESC_BYTES + 4)
+    if key.endswith("_txc"):       # the 8-byte check record per frame
+        return tr.caplen_sum + tr.n * (DESC_BYTES + 8)
     if "_cls_bpf" in key:          # the classify bytes + the 4-byte match mask
         return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES + 4)
     if key in ("S64_hdr", "S64_hdr_packed"):   # 8-byte compact records
@@ -251,7 +256,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
     ab = algo_bytes(tr, key)
     if key in OPS:
         op = OPS[key]
-        arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op == mosrx.OP_TX_CSUM else 0
+        arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op in (mosrx.OP_TX_CSUM, mosrx.OP_TX_CHECKS) else 0
         if op in (mosrx.OP_BPF, mosrx.OP_CLASSIFY_BPF):
             ctx.bpf_set(bpf_bench_programs())
         step_fn = lambda k, ns: ctx.time_op(op, dbs, k, ns, arg, kernels=False)[0]   # noqa: E731
@@ -476,7 +481,7 @@ def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
     while True:
         if key.endswith("_fh") or key.endswith("_ti"):
             O.classify_ex(tr.frames, tr.off, tr.len, O.params())
-        elif key.endswith("_tx"):
+        elif key.endswith("_tx") or key.endswith("_txc"):
             O.tx_csum(tr.frames, tr.off, tr.len, mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM)
         elif "_cls_bpf" in key:
             O.classify(tr.frames, tr.off, tr.len, O.params())
@@ -488,7 +493,8 @@ def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
         if el >= min_s:
             break
     fn = ("mo_classify + mo_bpf_eval" if "_cls_bpf" in key else
-          {"_fh": "mo_classify_ex", "_ti": "mo_classify_ex", "_tx": "mo_tx_csum", "bpf": "mo_bpf_eval"}[key[-3:]])
+          {"_fh": "mo_classify_ex", "_ti": "mo_classify_ex", "_tx": "mo_tx_csum", "txc": "mo_tx_csum",
+           "bpf": "mo_bpf_eval"}[key[-3:]])
     return {"value": round(reps * ab / el / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "mpkts": round(reps * tr.n / el / 1e6, 3),
             "sample": f"{reps} passes over one {tr.n}-frame batch ({el:.1f} s), oracle {fn}, 1 thread"}

@@ -329,7 +329,8 @@ int  mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb,
  * (TX_CSUM, `arg` = its flags); aux[i]: flow hashes (CLASSIFY_FH), match masks
  * (CLASSIFY_BPF). */
 enum { MOSRX_OP_CLASSIFY = 0, MOSRX_OP_CLASSIFY_FH = 1, MOSRX_OP_BPF = 2, MOSRX_OP_TX_CSUM = 3,
-       MOSRX_OP_CLASSIFY_BPF = 4, MOSRX_OP_CLASSIFY_TI = 5 /* aux[i]: mosrx_tcpinfo side arrays */ };
+       MOSRX_OP_CLASSIFY_BPF = 4, MOSRX_OP_CLASSIFY_TI = 5 /* aux[i]: mosrx_tcpinfo side arrays */,
+       MOSRX_OP_TX_CHECKS = 6 /* out[i]: mosrx_tx_check records, `arg` the flags */ };
 int  mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t nb, void *const *out,
                    void *const *aux, uint32_t iters, uint32_t nstreams, float *total_ms, float *avg_kernel_ms);
 /* The kernel's own duration, averaged over `iters` back-to-back launches on
@@ -462,7 +463,23 @@ int  mosrx_bpf_host(mosrx_ctx *c, const mosrx_batch *b, uint32_t *h_match);
 #define MOSRX_TX_IP_CSUM  (1 << 4)   /* MOS_UPDATE_IP_CHKSUM */
 #define MOSRX_TX_TCP_CSUM (1 << 5)   /* MOS_UPDATE_TCP_CHKSUM */
 int  mosrx_tx_csum_dev(mosrx_ctx *c, const mosrx_batch *b, int flags, void *stream);
-/* End-to-end from host memory: frames go to the GPU and come back rewritten (blocking). */
+/* The same checks without touching the frames: one 8-byte record per frame
+ * into d_checks (8-byte aligned, b->n of them).  `what` bit 0: ip_check is the
+ * frame's new iph->check (little-endian u16 at frame byte 24), bit 1:
+ * tcp_check its new tcph->check (at frame byte 14 + 4 * ihl + 16); frames the
+ * rewrite would leave untouched have what = 0.  For a consumer that writes
+ * the words itself (mosrx_tx_csum_host does, on the host). */
+typedef struct mosrx_tx_check {
+	uint16_t ip_check;
+	uint16_t tcp_check;
+	uint8_t  what;
+	uint8_t  ihl;
+	uint16_t pad;
+} mosrx_tx_check;
+int  mosrx_tx_csum_dev_checks(mosrx_ctx *c, const mosrx_batch *b, int flags, mosrx_tx_check *d_checks,
+                              void *stream);
+/* End-to-end from host memory (blocking): the frames cross PCIe once, the
+ * check records come back and are written into b->frames. */
 int  mosrx_tx_csum_host(mosrx_ctx *c, const mosrx_batch *b, int flags);
 
 /* ---- RSS helpers (host-side table build; the hash itself runs on the GPU) -- */

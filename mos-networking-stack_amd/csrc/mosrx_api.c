@@ -366,6 +366,24 @@ int mosrx_tx_csum_dev(mosrx_ctx *c, const mosrx_batch *b, int flags, void *strea
 	                    stream ? (hipStream_t)stream : c->stream);
 }
 
+int mosrx_tx_csum_dev_checks(mosrx_ctx *c, const mosrx_batch *b, int flags, mosrx_tx_check *d_checks, void *stream)
+{
+	int rc;
+	if (!c || (rc = mosrx__check_batch(b, 1)))
+		return c ? rc : -EINVAL;
+	if ((flags & ~(MOSRX_TX_IP_CSUM | MOSRX_TX_TCP_CSUM)) || !d_checks || ((uintptr_t)d_checks & 7))
+		return -EINVAL;
+	if (b->n == 0)
+		return 0;
+	if (!flags) {   /* no check requested: every record says `what` = 0 */
+		HIPCHK(hipMemsetAsync(d_checks, 0, (size_t)b->n * sizeof(*d_checks),
+		                      stream ? (hipStream_t)stream : c->stream));
+		return 0;
+	}
+	return launch_flags(c, b, b->frames, b->off, b->len, (mosrx_result *)d_checks, NULL, NULL, NULL,
+	                    tx_kflags(flags), stream ? (hipStream_t)stream : c->stream);
+}
+
 /* The host side of the TX pass: each frame's checks into the caller's frames,
  * the bytes the in-place rewrite would have stored (little-endian u16). */
 static void tx_patch(uint8_t *frames, const uint32_t *off, uint32_t n, const mosrx_tx_check *r)
@@ -1276,6 +1294,7 @@ static int run_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, void *out
 	case MOSRX_OP_TX_CSUM: return mosrx_tx_csum_dev(c, b, arg, s);
 	case MOSRX_OP_CLASSIFY_BPF: return mosrx_classify_bpf_dev(c, b, (mosrx_result *)out, (uint32_t *)aux, s);
 	case MOSRX_OP_CLASSIFY_TI: return mosrx_classify_dev_ex(c, b, (mosrx_result *)out, NULL, (mosrx_tcpinfo *)aux, s);
+	case MOSRX_OP_TX_CHECKS: return mosrx_tx_csum_dev_checks(c, b, arg, (mosrx_tx_check *)out, s);
 	default: return -EINVAL;
 	}
 }
@@ -1362,7 +1381,7 @@ int mosrx_time_op(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, uint32_t 
 {
 	int rc;
 	if (!c || !b || nb == 0 || iters == 0 || nstreams == 0 || nstreams > MOSRX_MAX_STREAMS ||
-	    op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_CLASSIFY_TI || (op != MOSRX_OP_TX_CSUM && !out) ||
+	    op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_TX_CHECKS || (op != MOSRX_OP_TX_CSUM && !out) ||
 	    ((op == MOSRX_OP_CLASSIFY_FH || op == MOSRX_OP_CLASSIFY_BPF || op == MOSRX_OP_CLASSIFY_TI) && !aux))
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
@@ -1428,7 +1447,7 @@ int mosrx_time_op_dispatch(mosrx_ctx *c, int op, int arg, const mosrx_batch *b, 
                            void *const *aux, uint32_t iters, float *avg_ms)
 {
 	struct op_run r = {op, arg, b, nb, out, aux};
-	if (!c || !b || nb == 0 || iters == 0 || !avg_ms || op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_CLASSIFY_TI ||
+	if (!c || !b || nb == 0 || iters == 0 || !avg_ms || op < MOSRX_OP_CLASSIFY || op > MOSRX_OP_TX_CHECKS ||
 	    (op != MOSRX_OP_TX_CSUM && !out) ||
 	    ((op == MOSRX_OP_CLASSIFY_FH || op == MOSRX_OP_CLASSIFY_BPF || op == MOSRX_OP_CLASSIFY_TI) && !aux))
 		return -EINVAL;

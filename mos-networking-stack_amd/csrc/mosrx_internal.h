@@ -80,18 +80,7 @@ enum { MOSRX_KIND_SMALL = 0, MOSRX_KIND_S13 = 1, MOSRX_KIND_COUNT = 2 };
 #define MOSRX_WINDOW_END_STREAM 62
 #define MOSRX_WINDOW_END_FULL   94
 
-/* A frame's TX checks as the TX rewrite writes them when kp.out is set (the
- * host's pass, mosrx_tx_csum_host): the frame itself stays as it was.  `what`
- * bit 0: ip_check applies (iph->check at frame byte 24), bit 1: tcp_check
- * (tcph->check at frame byte 14 + 4 * ihl + 16); both little-endian u16 as
- * the in-place rewrite stores them. */
-typedef struct mosrx_tx_check {
-	uint16_t ip_check;
-	uint16_t tcp_check;
-	uint8_t  what;
-	uint8_t  ihl;
-	uint16_t pad;
-} mosrx_tx_check;
+/* (mosrx_tx_check, include/mosrx.h: the TX rewrite's records when kp.out is set) */
 
 /* Batch-queue descriptor (device resident), 64 bytes. */
 typedef struct mosrx_qdesc {

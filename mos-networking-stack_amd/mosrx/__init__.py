@@ -80,7 +80,10 @@ class Batch(C.Structure):
 BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])   # mosrx_bpf_insn
 BPF_LEN_FRAME, BPF_LEN_IP = 0, 1
 TX_IP_CSUM, TX_TCP_CSUM = 1 << 4, 1 << 5   # MOS_UPDATE_IP_CHKSUM / MOS_UPDATE_TCP_CHKSUM
-OP_CLASSIFY, OP_CLASSIFY_FH, OP_BPF, OP_TX_CSUM, OP_CLASSIFY_BPF, OP_CLASSIFY_TI = 0, 1, 2, 3, 4, 5
+OP_CLASSIFY, OP_CLASSIFY_FH, OP_BPF, OP_TX_CSUM, OP_CLASSIFY_BPF, OP_CLASSIFY_TI, OP_TX_CHECKS = 0, 1, 2, 3, 4, 5, 6
+# include/mosrx.h mosrx_tx_check: the TX checks of a frame, the frame untouched
+TX_CHECK_DTYPE = np.dtype([("ip_check", "<u2"), ("tcp_check", "<u2"), ("what", "u1"), ("ihl", "u1"),
+                           ("pad", "<u2")])
 BPF_MAX_PROGS = 32
 
 
@@ -202,6 +205,7 @@ def lib():
             "mosrx_rss_tables": (I, [C.c_char_p, U32, C.POINTER(U32)]),
             "mosrx_tx_csum_dev": (I, [P, C.POINTER(Batch), I, P]),
             "mosrx_tx_csum_host": (I, [P, C.POINTER(Batch), I]),
+            "mosrx_tx_csum_dev_checks": (I, [P, C.POINTER(Batch), I, P, P]),
             "mosrx_bpf_check": (I, [P, U32]),
             "mosrx_bpf_set": (I, [P, C.POINTER(BpfProg), U32]),
             "mosrx_bpf_dev": (I, [P, C.POINTER(Batch), P, P]),
@@ -556,6 +560,17 @@ class Context:
                   off.ctypes.data, ln.ctypes.data, len(off), 0)
         _chk(lib().mosrx_tx_csum_host(self.handle, C.byref(b), flags), "mosrx_tx_csum_host")
         return out
+
+    def tx_csum_dev_checks(self, db: "DevBatch", flags=TX_IP_CSUM | TX_TCP_CSUM) -> np.ndarray:
+        """mosrx_tx_csum_dev_checks into the batch's record buffer: one
+        TX_CHECK_DTYPE record per frame, the frames left as they are."""
+        b = db.batch()
+        _chk(lib().mosrx_tx_csum_dev_checks(self.handle, C.byref(b), flags, db.d_out.ptr, None),
+             "mosrx_tx_csum_dev_checks")
+        _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
+        raw = np.empty(max(db.n, 1) * 8, np.uint8)
+        db.d_out.download(raw)
+        return raw.view(TX_CHECK_DTYPE)[:db.n].copy()
 
     def tx_csum_dev(self, db: "DevBatch", flags=TX_IP_CSUM | TX_TCP_CSUM, sync: bool = True) -> None:
         b = db.batch()

@@ -39,7 +39,7 @@ else:
     op = bench.OPS.get(key, mosrx.OP_CLASSIFY)
     if op in (mosrx.OP_BPF, mosrx.OP_CLASSIFY_BPF):
         ctx.bpf_set(bench.bpf_bench_programs())
-    arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op == mosrx.OP_TX_CSUM else 0
+    arg = mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM if op in (mosrx.OP_TX_CSUM, mosrx.OP_TX_CHECKS) else 0
     _, avg = ctx.time_op(op, dbs, iters, 1, arg, total=False)
 print(f"{key}: {iters} isolated launches, avg {avg * 1e3:.2f} us (HIP events), "
       f"algo bytes/launch {ab}", flush=True)

@@ -129,3 +129,42 @@ def test_tx_host_records_full_size(gpu_ctx, shift):
     gpu_ctx.tx_csum_dev(db, IP | TCP)
     np.testing.assert_array_equal(db.frames(len(buf)), exp)
     db.free()
+
+
+def apply_checks(buf, off, checks):
+    """The host side of mosrx_tx_check records: the words into a copy of the frames."""
+    out = np.array(buf, np.uint8, copy=True)
+    for o, r in zip(off.tolist(), checks):
+        if r["what"] & 1:
+            out[o + 24] = r["ip_check"] & 0xFF
+            out[o + 25] = r["ip_check"] >> 8
+        if r["what"] & 2:
+            at = o + 30 + 4 * int(r["ihl"])
+            out[at] = r["tcp_check"] & 0xFF
+            out[at + 1] = r["tcp_check"] >> 8
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fix", FIXTURES)
+@pytest.mark.parametrize("flags", FLAGS)
+def test_tx_dev_checks_golden(gpu_ctx, fix, flags):
+    """mosrx_tx_csum_dev_checks: the frames stay as they were, and the records
+    written into them give mOS's rewrite (the reference's own fixtures)."""
+    z = np.load(os.path.join(GOLDEN, f"{fix}.npz"))
+    db = gpu_ctx.upload(z["frames"], z["off"], z["len"])
+    checks = gpu_ctx.tx_csum_dev_checks(db, flags)
+    np.testing.assert_array_equal(db.frames(len(z["frames"])), z["frames"])
+    np.testing.assert_array_equal(apply_checks(z["frames"], z["off"], checks), expected(z, flags))
+    db.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n", [(mosrx.TRACE_M1500, 65_536), (mosrx.TRACE_IMIX, 262_144)])
+def test_tx_dev_checks_full_size(gpu_ctx, kind, n):
+    t = mosrx.Trace(kind, n)
+    db = gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len)
+    checks = gpu_ctx.tx_csum_dev_checks(db)
+    np.testing.assert_array_equal(apply_checks(t.frames, t.off, checks), O.tx_csum(t.frames, t.off, t.len, IP | TCP))
+    assert not gpu_ctx.tx_csum_dev_checks(db, 0)["what"].any()
+    db.free()

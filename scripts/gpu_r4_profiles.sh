@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-.}"
 rm -f gpurun_out/prof4/pmc_traffic.json
 for W in ${PMC_W:-M1500 IMIX S64 S64_hdr S64_hdr_packed S64_cls_bpf_ring IMIX_cls_bpf_ring M1500_1 IMIX_1 S64_1}; do
-  case $W in *_1) K=mosrx_classify_kernel ;; *_cls_bpf_ring) K=mosrx_classify_bpf_queue ;; *) K=mosrx_classify_queue_kernel ;; esac
+  case $W in *_1|*_tx|*_txc|*_fh|*_ti) K=mosrx_classify_kernel ;; *_cls_bpf_ring) K=mosrx_classify_bpf_queue ;; *) K=mosrx_classify_queue_kernel ;; esac
   N=40; case $W in S64*|S64_hdr*) N=12 ;; M1500|IMIX|IMIX_cls_bpf_ring) N=16 ;; esac
   case $W in *_1) N=40 ;; esac
   timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof4/pmcf_$W -o pmc --output-format csv -- python3 scripts/pmc_run.py $W $N > gpurun_out/prof4/pmcf_$W.log 2>&1; rc=$?

@@ -168,3 +168,66 @@ def test_tx_dev_checks_full_size(gpu_ctx, kind, n):
     np.testing.assert_array_equal(apply_checks(t.frames, t.off, checks), O.tx_csum(t.frames, t.off, t.len, IP | TCP))
     assert not gpu_ctx.tx_csum_dev_checks(db, 0)["what"].any()
     db.free()
+
+
+def fuzz_frames(seed, n=8192):
+    """Header-mutated frames at every alignment: IPv4 mostly, ihl mostly 5 but any
+    nibble, tot_len equal to / around / far from the capture, TCP mostly with any
+    doff, captures cut anywhere (inside Ethernet, IP, TCP, options)."""
+    rng = np.random.default_rng(seed)
+    cls = rng.integers(0, 10, n)
+    lens = np.where(cls == 0, rng.integers(0, 34, n),
+                    np.where(cls < 4, rng.integers(34, 80, n), rng.integers(60, 1515, n))).astype(np.uint16)
+    gaps = rng.integers(0, 8, n)
+    off = (np.cumsum(np.concatenate([[0], lens[:-1].astype(np.int64) + gaps[:-1]])) + 1).astype(np.uint32)
+    buf = rng.integers(0, 256, int(off[-1]) + int(lens[-1]) + 64, dtype=np.uint8)
+    for i in range(n):
+        o, m = int(off[i]), int(lens[i])
+        if m >= 14 and rng.random() < 0.85:
+            buf[o + 12], buf[o + 13] = 0x08, 0x00
+        if m >= 15:
+            ihl = 5 if rng.random() < 0.7 else int(rng.integers(0, 16))
+            buf[o + 14] = (0x40 if rng.random() < 0.9 else int(rng.integers(0, 16)) << 4) | ihl
+            if m >= 18:
+                r = rng.random()
+                tl = m - 14 if r < 0.6 else (m - 14 + int(rng.integers(-24, 25)) if r < 0.85
+                                              else int(rng.integers(0, 65536)))
+                tl &= 0xFFFF
+                buf[o + 16], buf[o + 17] = tl >> 8, tl & 0xFF
+            if m >= 24 and rng.random() < 0.8:
+                buf[o + 23] = 6
+            d = o + 14 + 4 * ihl + 12
+            if d < o + m and rng.random() < 0.8:
+                buf[d] = (5 if rng.random() < 0.6 else int(rng.integers(0, 16))) << 4
+    return buf, off, lens
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_tx_fuzz_headers(gpu_ctx, seed):
+    """Mutated headers through all three TX forms (in place on the device, host
+    records, device records applied on the host), each equal to the oracle's
+    rewrite for every flag combination; the frames are never touched by the
+    records form."""
+    buf, off, lens = fuzz_frames(seed)
+    db = gpu_ctx.upload(buf, off, lens)
+    for flags in FLAGS:
+        exp = O.tx_csum(buf, off, lens, flags)
+        assert (exp != buf).any()
+        np.testing.assert_array_equal(gpu_ctx.tx_csum_host(buf, off, lens, flags), exp)
+        checks = gpu_ctx.tx_csum_dev_checks(db, flags)
+        np.testing.assert_array_equal(db.frames(len(buf)), buf)
+        np.testing.assert_array_equal(apply_checks(buf, off, checks), exp)
+    gpu_ctx.tx_csum_dev(db, IP | TCP)
+    np.testing.assert_array_equal(db.frames(len(buf)), O.tx_csum(buf, off, lens, IP | TCP))
+    db.free()
+
+
+def test_tx_fuzz_frames_cover_edges():
+    """The fuzz input holds the cases the rewrite must tell apart (oracle only)."""
+    buf, off, lens = fuzz_frames(1)
+    after = O.tx_csum(buf, off, lens, IP | TCP)
+    changed = np.array([(after[o:o + m] != buf[o:o + m]).any() for o, m in zip(off.tolist(), lens.tolist())])
+    ihl = np.array([buf[o + 14] & 0xF if m > 14 else 0 for o, m in zip(off.tolist(), lens.tolist())])
+    assert 0.2 < changed.mean() < 0.95
+    assert (lens < 34).any() and (ihl < 5).any() and (ihl > 5).any() and (off % 2 == 1).any()

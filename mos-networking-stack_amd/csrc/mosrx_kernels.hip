@@ -1045,7 +1045,10 @@ __device__ __forceinline__ void stream_frames(__amdgpu_buffer_rsrc_t rs, uint32_
 // 131072 the fused set's masks computed but (almost) never stored, 262144 a
 // constant mask stored without a set, 524288 the masks stored through the
 // cache instead of non-temporally (scripts/probe_fused_fixed.hip), 1048576 the
-// 78-byte (5-chunk) window (scripts/probe_guided.hip).
+// 78-byte (5-chunk) window (scripts/probe_guided.hip), 2097152 streamer 0
+// reads the descriptors of tile + 2048 (the tile that takes this slot's place
+// in a 4096-tile launch, same XCD) into L2, 4194304 also the first line of
+// each of that tile's frames (scripts/probe_prefetch.hip).
 #define TILE_STAMP(i)                                                                             \
 	do {                                                                                          \
 		if constexpr ((DBG & 128) != 0) {                                                         \
@@ -1204,6 +1207,14 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 		uint32_t *row = s_part[sidx];
 		if (sidx == 0)
 			TILE_STAMP(6);
+		uint32_t pf_o = 0, pf_l = 0;
+		if constexpr ((DBG & (2097152 | 4194304)) != 0) {
+			const uint32_t qn = first + 2048u * T + lane;
+			if (sidx == 0 && qn < kp.n) {
+				pf_o = kp.off[qn];
+				pf_l = kp.len[qn];
+			}
+		}
 		row[lane] = 0;
 		const uint64_t cmask = __ballot(hi_l > lo_l);
 		if (sorted && cmask) {
@@ -1222,6 +1233,13 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 		} else if (!sorted) {
 			if constexpr (!(DBG & 16))
 				stream_frames<S, AUX>(rs, lo_l, hi_l, sidx, lane, row);
+		}
+		if constexpr ((DBG & (2097152 | 4194304)) != 0) {
+			if constexpr ((DBG & 4194304) != 0) {
+				if (sidx == 0 && pf_l)
+					pf_l += load16<0>(rs, pf_o & ~15u, nbytes).x;
+			}
+			asm volatile("" ::"v"(pf_o), "v"(pf_l));
 		}
 		TILE_STAMP(7 + sidx);
 		__syncthreads();   // B

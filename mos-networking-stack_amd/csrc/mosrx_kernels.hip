@@ -512,6 +512,7 @@ __device__ __forceinline__ void store_tcpinfo(mosrx_tcpinfo *ti, uint32_t p, con
 // 8-byte record (mosrx_tx_check: the two check words, which of them apply,
 // ihl) and the host writes them into its own copy of the frames -- what
 // crosses PCIe back is 8 bytes per frame instead of the frame.
+template <int SAUX = 0, bool DENSE = false>
 __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffer_rsrc_t rs, const hdr_t &h,
                                          uint32_t tail_sum, uint32_t p, bool active)
 {
@@ -549,21 +550,26 @@ __device__ __forceinline__ void tx_store(const mosrx_kparams &kp, __amdgpu_buffe
 		}
 		return;
 	}
+	if constexpr (DENSE) {   // probe: the same two words, into a dense array instead of the frames
+		if (active)
+			reinterpret_cast<uint32_t *>(kp.fhash)[p] = (ip ? (h.ipc_tx & 0xFFFFu) : 0u) | (h.need_tcp ? c << 16 : 0u);
+		return;
+	}
 	if (ip) {
 		if (even) {
-			__builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipc_tx, rs, h.o + 24u, 0, 0);
+			__builtin_amdgcn_raw_buffer_store_b16((uint16_t)h.ipc_tx, rs, h.o + 24u, 0, SAUX);
 		} else {
-			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)h.ipc_tx, rs, h.o + 24u, 0, 0);
-			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)(h.ipc_tx >> 8), rs, h.o + 25u, 0, 0);
+			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)h.ipc_tx, rs, h.o + 24u, 0, SAUX);
+			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)(h.ipc_tx >> 8), rs, h.o + 25u, 0, SAUX);
 		}
 	}
 	if (h.need_tcp) {
 		const uint32_t at = h.o + 30u + 4u * h.ihl;
 		if (even) {
-			__builtin_amdgcn_raw_buffer_store_b16((uint16_t)c, rs, at, 0, 0);
+			__builtin_amdgcn_raw_buffer_store_b16((uint16_t)c, rs, at, 0, SAUX);
 		} else {
-			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, rs, at, 0, 0);
-			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), rs, at + 1u, 0, 0);
+			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, rs, at, 0, SAUX);
+			__builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), rs, at + 1u, 0, SAUX);
 		}
 	}
 }
@@ -761,7 +767,7 @@ __device__ __forceinline__ uint32_t range_sum(__amdgpu_buffer_rsrc_t rs, uint32_
 // capture end (Ethernet padding of a long capture) were summed too: subtract
 // them (exact integer sums, so the difference is the true tail sum).  Rare: a
 // wave-wide pass per such frame.  Then the record (or the TX rewrite).
-template <int VAR>
+template <int VAR, int DBG = 0>
 __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffer_rsrc_t rs, uint32_t nbytes,
                                          const hdr_t &h, uint32_t lo_l, uint32_t hi_l, uint32_t tail, uint32_t p,
                                          bool active, uint32_t lane, uint32_t *s_cnt)
@@ -778,7 +784,7 @@ __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffe
 			tail -= s;
 	}
 	if constexpr (IS_TX(VAR)) {
-		tx_store(kp, rs, h, tail, p, active);
+		tx_store<(DBG & 8388608) ? 2 : 0, (DBG & 16777216) != 0>(kp, rs, h, tail, p, active);
 	} else if (active) {
 		store_record<VAR>(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (kp.fhash)
@@ -1048,7 +1054,9 @@ __device__ __forceinline__ void stream_frames(__amdgpu_buffer_rsrc_t rs, uint32_
 // 78-byte (5-chunk) window (scripts/probe_guided.hip), 2097152 streamer 0
 // reads the descriptors of tile + 2048 (the tile that takes this slot's place
 // in a 4096-tile launch, same XCD) into L2, 4194304 also the first line of
-// each of that tile's frames (scripts/probe_prefetch.hip).
+// each of that tile's frames (scripts/probe_prefetch.hip), 8388608 the TX
+// check words stored non-temporally, 16777216 stored as one u32 per frame into
+// a dense array (kp.fhash) instead of the frames (scripts/probe_tx_store.hip).
 #define TILE_STAMP(i)                                                                             \
 	do {                                                                                          \
 		if constexpr ((DBG & 128) != 0) {                                                         \
@@ -1156,7 +1164,7 @@ __device__ __forceinline__ void classify_span_stream(const mosrx_kparams &kp, ui
 					if (sorted)
 						tail -= chunk_overshoot(ov, (hi_l - 1u) & ~15u, hi_l);
 				}
-				hdr_emit<VAR>(kp, rs, nbytes, h, lo_l, hi_l, tail, p, active, lane, s_cnt);
+				hdr_emit<VAR, DBG>(kp, rs, nbytes, h, lo_l, hi_l, tail, p, active, lane, s_cnt);
 			} else {
 				// the outputs that do not need the tail sum go out before the barrier
 				if (active && kp.fhash)

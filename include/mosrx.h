@@ -468,7 +468,10 @@ int  mosrx_tx_csum_dev(mosrx_ctx *c, const mosrx_batch *b, int flags, void *stre
  * frame's new iph->check (little-endian u16 at frame byte 24), bit 1:
  * tcp_check its new tcph->check (at frame byte 14 + 4 * ihl + 16); frames the
  * rewrite would leave untouched have what = 0.  For a consumer that writes
- * the words itself (mosrx_tx_csum_host does, on the host). */
+ * the words itself (mosrx_tx_csum_host does, on the host).  Same checks as
+ * mtcp_setlastpkt's MOS_UPDATE_IP_CHKSUM / MOS_UPDATE_TCP_CHKSUM
+ * (core/src/mos_api.c:1177-1193) and the S/W paths of ip_out.c:169-174,
+ * tcp_out.c:207-218. */
 typedef struct mosrx_tx_check {
 	uint16_t ip_check;
 	uint16_t tcp_check;

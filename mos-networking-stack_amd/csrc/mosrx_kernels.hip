@@ -784,7 +784,7 @@ __device__ __forceinline__ void hdr_emit(const mosrx_kparams &kp, __amdgpu_buffe
 			tail -= s;
 	}
 	if constexpr (IS_TX(VAR)) {
-		tx_store<(DBG & 8388608) ? 2 : 0, (DBG & 16777216) != 0>(kp, rs, h, tail, p, active);
+		tx_store<(DBG & 8388608) ? 2 : (DBG & 33554432) ? 17 : 0, (DBG & 16777216) != 0>(kp, rs, h, tail, p, active);
 	} else if (active) {
 		store_record<VAR>(kp, p, hdr_finish(h, tail, kp.flags), s_cnt);
 		if (kp.fhash)
@@ -1056,7 +1056,8 @@ __device__ __forceinline__ void stream_frames(__amdgpu_buffer_rsrc_t rs, uint32_
 // in a 4096-tile launch, same XCD) into L2, 4194304 also the first line of
 // each of that tile's frames (scripts/probe_prefetch.hip), 8388608 the TX
 // check words stored non-temporally, 16777216 stored as one u32 per frame into
-// a dense array (kp.fhash) instead of the frames (scripts/probe_tx_store.hip).
+// a dense array (kp.fhash) instead of the frames, 33554432 stored write-through
+// at system scope (sc0 | sc1) (scripts/probe_tx_store.hip).
 #define TILE_STAMP(i)                                                                             \
 	do {                                                                                          \
 		if constexpr ((DBG & 128) != 0) {                                                         \

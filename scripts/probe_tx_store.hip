@@ -6,7 +6,9 @@
 // 2-byte check-word stores per frame as the library issues them and with them
 // non-temporal (DBG 8388608), with the same two words written as one u32 per
 // frame into a dense array instead (DBG 16777216: the frames' scattered
-// partial lines out of the picture), and timed against the records form, over 24
+// partial lines out of the picture), with them written through at system
+// scope (DBG 33554432: no dirty lines left for the end-of-kernel writeback),
+// and timed against the records form, over 24
 // resident 64K-frame batches, dispatch-stamped, interleaved, 3 rounds.  Frames
 // are restored between rounds (every form rewrites the same words).
 //
@@ -47,6 +49,7 @@ static int stamped(int f, const std::vector<mosrx_kparams> &kps, uint32_t tiles,
 		case 0: case 2: hipExtLaunchKernelGGL(k_tx<0>, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kp); break;
 		case 1: hipExtLaunchKernelGGL(k_tx<8388608>, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kp); break;
 		case 3: hipExtLaunchKernelGGL(k_tx<16777216>, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kp); break;
+		case 4: hipExtLaunchKernelGGL(k_tx<33554432>, dim3(tiles), dim3(WG), 0, 0, e0[i], e1[i], 0, kp); break;
 		}
 	}
 	CHK(hipDeviceSynchronize());
@@ -108,13 +111,21 @@ int main(int argc, char **argv)
 		printf("non-temporal stores give other frames\n");
 		return 2;
 	}
+	CHK(hipMemcpy(fr[0], t.frames, t.frames_bytes, hipMemcpyHostToDevice));
+	hipLaunchKernelGGL(k_tx<33554432>, dim3(tiles), dim3(WG), 0, 0, kp);
+	CHK(hipDeviceSynchronize());
+	CHK(hipMemcpy(b.data(), fr[0], t.frames_bytes, hipMemcpyDeviceToHost));
+	if (memcmp(a.data(), b.data(), t.frames_bytes)) {
+		printf("write-through stores give other frames\n");
+		return 2;
+	}
 	const double bytes = (double)t.caplen_sum + 10.0 * n;
-	printf("M1500 %u frames, %u tiles, %.2f MB algorithmic (in place); both in-place forms give the same frames\n", n,
+	printf("M1500 %u frames, %u tiles, %.2f MB algorithmic (in place); the three in-place forms give the same frames\n", n,
 	       tiles, bytes / 1e6);
-	static const char *names[4] = {"in place (library)", "in place, non-temporal stores", "8-byte records",
-	                               "4-byte words, dense array"};
+	static const char *names[5] = {"in place (library)", "in place, non-temporal stores", "8-byte records",
+	                               "4-byte words, dense array", "in place, write-through stores"};
 	for (int rep = 0; rep < 3; rep++)
-		for (int f = 0; f < 4; f++) {
+		for (int f = 0; f < 5; f++) {
 			for (int i = 0; i < nb; i++)
 				CHK(hipMemcpy(fr[i], t.frames, t.frames_bytes, hipMemcpyHostToDevice));
 			double med;

@@ -49,7 +49,7 @@ typedef unsigned long size_t;
 extern "C" {
 #endif
 
-#define MOSRX_ABI_VERSION 2
+#define MOSRX_ABI_VERSION 3
 
 /* ---- per-frame result record (16 bytes) -------------------- */
 
@@ -155,7 +155,19 @@ typedef struct mosrx_batch {
 	const uint16_t *len;          /* n capture lengths (pcap caplen / get_rptr *len, core.c:903-905) */
 	uint32_t        n;            /* frames in the batch */
 	uint32_t        max_len;      /* max(len[]) if known, else 0 (selects the kernel variant) */
+	/* Layout hint (ABI 3).  MOSRX_BATCH_UNIFORM: the producer packed the frames
+	 * at a fixed stride, frame i at off0 + i * stride (an rx ring of fixed-size
+	 * buffers, a stage of equal-size frames).  The kernel then issues each
+	 * frame's header loads from that address together with its descriptor
+	 * loads instead of behind them; off[] still decides: a frame whose off[i]
+	 * differs is re-read from off[i], so a wrong hint costs time, never a
+	 * result.  Used when off0 and stride fit 16 bits; 0 = no hint. */
+	uint32_t        layout;       /* MOSRX_BATCH_* */
+	uint32_t        off0;
+	uint32_t        stride;
+	uint32_t        reserved;     /* 0 */
 } mosrx_batch;
+enum { MOSRX_BATCH_UNIFORM = 1 };
 
 typedef struct mosrx_ctx mosrx_ctx;
 
@@ -264,6 +276,12 @@ int  mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch 
 int  mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
                                          mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo,
                                          uint32_t *const *h_fhash);
+/* The same with 8-byte records (mosrx_result8) into h_out8[i] and, when
+ * h_fhash is not NULL, the flow hashes (no pkt_info fields): the group's records are written and copied back at half the bytes
+ * (gpu_module_func's cfg.compact, the records an rx loop consumes when it
+ * takes pkt_info's lengths from the header, tcp.c:258-270). */
+int  mosrx_classify_host_group_submit_c8(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                         mosrx_result8 *const *h_out8, uint32_t *const *h_fhash);
 /* The same for a context with a BPF set installed: the records, the flow
  * hashes (h_fhash, NULL: none) and the set's match masks into h_match[i] from
  * ONE launch of the fused classify + BPF queue kernel (the set's compiled

@@ -84,11 +84,14 @@ typedef struct {
 #define MOSRX_PKT_SET_BPF    0x16   /* argp: const mosrx_bpf_set_arg * -- the monitor filters to evaluate in
                                      * the classify pass from now on (nprog 0: none); batches not yet
                                      * handed out are classified again with them */
+#define MOSRX_PKT_RX_RESULTS8 0x18  /* argp: const mosrx_result8 ** (whole batch): the records of a batch
+                                     * classified in compact form (cfg.compact); RX_RESULTS is -1 for it */
 typedef struct mosrx_rx_state {
 	uint32_t num_msp, num_esp;   /* the stack state of the batch's verdicts */
 	uint32_t gen;                /* the netdev's parameter / filter generation they were made with */
 	uint32_t bpf_nprog;          /* programs in its match masks (0: no masks) */
 	uint32_t n;                  /* frames in the batch */
+	uint32_t rec_bytes;          /* its records: 16 (mosrx_result, RX_RESULTS) or 8 (mosrx_result8, RX_RESULTS8) */
 } mosrx_rx_state;
 typedef struct mosrx_bpf_set_arg {
 	const mosrx_bpf_prog *progs;
@@ -208,6 +211,15 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * computes them (ip_out.c:169-174, tcp_out.c:207-218) */
 	int32_t       numa;                             /* 1 (default): core c drives a GPU on c's NUMA node
 	                                                 * (mosrx_numa_pick); 0: gpu_base + c % ngpu */
+	int32_t       compact;                          /* 1: 8-byte records (mosrx_result8: rss, reason, queue,
+	                                                 * verdict, tcp_flags; dev_ioctl(MOSRX_PKT_RX_RESULTS8)),
+	                                                 * written and copied back at half the bytes; the consumer
+	                                                 * takes pkt_info's lengths from the header as
+	                                                 * FillPacketContextTCPInfo does (tcp.c:258-270).  Batches
+	                                                 * classified with BPF filters keep 16-byte records (the
+	                                                 * batch's mosrx_rx_state.rec_bytes says which).  Not with
+	                                                 * tcpinfo.  Default 0 standalone, 1 in an mOS build left
+	                                                 * unconfigured (its consumer, mos_rx.c, reads both). */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
 #define MOSRX_GROUP_AUTO_BYTES  (256ull << 20)   /* per pipeline slot; 64 B frames: ~120 batches of 32K
@@ -275,7 +287,9 @@ typedef struct mosrx_rx_stats {
 } mosrx_rx_stats;
 
 /* Per-frame consumer: the part of ProcessPacket after the checks (flow lookup,
- * callbacks).  Gets the frame and its precomputed record; may be NULL. */
+ * callbacks).  Gets the frame and its precomputed record; may be NULL.  For a
+ * compact batch the record carries the mosrx_result8 fields (rss, reason,
+ * queue, verdict, tcp_flags) and zero elsewhere. */
 typedef void (*mosrx_pkt_fn)(void *arg, int ifidx, int index, const uint8_t *pkt, uint16_t len,
                              const mosrx_result *res);
 

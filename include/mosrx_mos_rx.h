@@ -66,6 +66,7 @@ typedef struct mosrx_mos_rx_stats {
 	uint64_t max_filter_sync_ns;/* longest filter install (the rx loop's stall: set + reclassify) */
 	uint64_t gpu_errors;        /* batches (or their rest) left without records: the backend failed */
 	uint64_t gpu_dropped;       /* frames of those batches, dropped and counted in rx_errors */
+	uint64_t batches_c8;        /* batch record sets read in the 8-byte form (cfg.compact) */
 } mosrx_mos_rx_stats;
 
 /* Counters of the mTCP thread running core `cpu` (mtcp->ctx->cpu). */

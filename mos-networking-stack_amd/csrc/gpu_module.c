@@ -68,6 +68,7 @@ struct stage {
 	uint32_t *match;          /* pinned, BPF match masks (a filter set installed) */
 	uint32_t *fh;             /* pinned, flow-table hashes (cfg.flowhash) */
 	uint32_t n, max_len;
+	uint32_t stride;          /* frame i at off[0] + i * stride (a fixed-size packing), else 0: the layout hint */
 	uint64_t bytes;
 	int borrowed;             /* frames lent by the source: give them back when the group is recycled */
 	/* what its records were made under: mOS's socket counts, the netdev's
@@ -75,7 +76,9 @@ struct stage {
 	 * which side arrays the launch filled (pkt_info fields are not made in a
 	 * BPF pass) */
 	uint32_t msp, esp, gen, nprog, has_fh, has_ti;
+	int compact;              /* its records are mosrx_result8 (cfg.compact, no filters): res8 */
 };
+#define RES8(s) ((mosrx_result8 *)(s)->res)   /* a compact stage's records, in its 16-byte slots' place */
 
 struct group {
 	uint8_t *blk;             /* pinned block the group's stages are packed into */
@@ -145,7 +148,8 @@ int mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg)
 {
 	if (!cfg || cfg->num_ifs == 0 || cfg->num_ifs > MOSRX_MAX_DEVICES || cfg->batch == 0 ||
 	    cfg->max_frame < 64 || cfg->max_frame > 65535 || cfg->group > MOSRX_MAX_GROUP ||
-	    cfg->bpf_nprog > MOSRX_BPF_MAX_PROGS || cfg->params.num_local > MOSRX_MAX_LOCAL)
+	    cfg->bpf_nprog > MOSRX_BPF_MAX_PROGS || cfg->params.num_local > MOSRX_MAX_LOCAL ||
+	    (cfg->compact && cfg->tcpinfo))
 		return -EINVAL;
 	pthread_mutex_lock(&g_lock);
 	g_cfg = *cfg;
@@ -286,6 +290,7 @@ static void gpu_configure_from_mos(void)
 		exit(EXIT_FAILURE);
 	}
 	cfg.num_ifs = (uint32_t)nd->num;
+	cfg.compact = 1;   /* mOS's consumer (mos_rx.c) reads 8-byte records */
 	for (i = 0; i < nd->num; i++) {
 		strncpy(cfg.if_names[i], nd->ent[i]->dev_name, sizeof(cfg.if_names[i]) - 1);
 		cfg.src[i] = mosrx_source_afpacket(cfg.if_names[i]);
@@ -570,8 +575,15 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
 	} else {
 		s->bytes = 2;
 	}
-	for (i = 0; i < s->n; i++)        /* the batch's real largest frame picks the kernel shape */
+	/* the batch's real largest frame picks the kernel shape; equal frames packed
+	 * at one stride (the fill's back-to-back small frames, a ring of fixed-size
+	 * buffers) are handed over with that layout as a hint (mosrx_batch.layout) */
+	s->stride = s->n > 1 && s->off[1] > s->off[0] ? s->off[1] - s->off[0] : 0;
+	for (i = 0; i < s->n; i++) {
 		m = s->len[i] > m ? s->len[i] : m;
+		if (s->off[i] != s->off[0] + i * s->stride)
+			s->stride = 0;
+	}
 	s->max_len = m;
 	*pos = at + fpos;
 }
@@ -641,6 +653,10 @@ static void stage_batch(const struct stage *s, mosrx_batch *b)
 	b->len = s->len;
 	b->n = s->n;
 	b->max_len = s->max_len;
+	b->layout = s->stride ? MOSRX_BATCH_UNIFORM : 0;
+	b->off0 = s->n ? s->off[0] : 0;
+	b->stride = s->stride;
+	b->reserved = 0;
 }
 
 /* Classify stages [first, nst) of group k on pipeline slot k, under mOS's
@@ -652,6 +668,7 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 	struct group *g = &is->g[k];
 	mosrx_batch b[MOSRX_MAX_GROUP];
 	mosrx_result *out[MOSRX_MAX_GROUP];
+	mosrx_result8 *out8[MOSRX_MAX_GROUP];
 	mosrx_tcpinfo *ti[MOSRX_MAX_GROUP];
 	uint32_t *fh[MOSRX_MAX_GROUP], *mt[MOSRX_MAX_GROUP];
 	uint32_t i, nb = g->nst - first;
@@ -661,6 +678,7 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 		struct stage *s = &g->st[i];
 		stage_batch(s, &b[i - first]);
 		out[i - first] = s->res;
+		out8[i - first] = RES8(s);
 		ti[i - first] = s->ti;
 		fh[i - first] = s->fh;
 		mt[i - first] = s->match;
@@ -670,7 +688,10 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 		s->nprog = is->nprog;
 		s->has_fh = s->fh != NULL;
 		s->has_ti = s->ti != NULL && !is->nprog;
+		s->compact = g_cfg.compact && !is->nprog;
 	}
+	if (g_cfg.compact && !is->nprog)   /* 8-byte records (filters keep 16-byte ones: the fused kernels) */
+		return mosrx_classify_host_group_submit_c8(is->mc, k, b, nb, out8, g_cfg.flowhash ? fh : NULL);
 	if (is->nprog)
 		return mosrx_classify_host_group_submit_bpf(is->mc, k, b, nb, out, g_cfg.flowhash ? fh : NULL, mt);
 	if (nb == 1 && !g_cfg.flowhash)
@@ -819,7 +840,7 @@ static void tx_csum_fill(struct gpu_priv *pv, struct if_state *is)
 	uint32_t *off = is->tx_poff, i, n, fl;
 	uint16_t *len = is->tx_plen;
 	for (fl = 1; fl <= (TXF_IP | TXF_TCP); fl++) {
-		mosrx_batch b;
+		mosrx_batch b = {0};
 		uint32_t m = 0;
 		uint64_t end = 0;
 		int rc;
@@ -964,13 +985,18 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
 		RssInfo *ri = argp;
 		if (!s || ri->pktidx < 0 || (uint32_t)ri->pktidx >= s->n)
 			return -1;
-		ri->hash_value = s->res[ri->pktidx].rss;
+		ri->hash_value = s->compact ? RES8(s)[ri->pktidx].rss : s->res[ri->pktidx].rss;
 		return 0;
 	}
 	case MOSRX_PKT_RX_RESULTS:
-		if (!s)
+		if (!s || s->compact)
 			return -1;
 		*(const mosrx_result **)argp = s->res;
+		return 0;
+	case MOSRX_PKT_RX_RESULTS8:
+		if (!s || !s->compact)
+			return -1;
+		*(const mosrx_result8 **)argp = RES8(s);
 		return 0;
 	case MOSRX_PKT_RX_MATCH:
 		if (!s || !s->match || !s->nprog)
@@ -1008,6 +1034,7 @@ static int32_t gpu_dev_ioctl(struct mtcp_thread_context *ctx, int nif, int cmd, 
 		st->gen = s->gen;
 		st->bpf_nprog = s->nprog;
 		st->n = s->n;
+		st->rec_bytes = s->compact ? 8u : 16u;
 		return 0;
 	}
 	case MOSRX_PKT_RX_RECLASSIFY: {

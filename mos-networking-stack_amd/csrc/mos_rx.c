@@ -21,10 +21,12 @@
  *   tcp.c:418-427       pkt_info TCP fields (record + header); every raw
  *                       monitor: MOS_ON_PKT_IN
  *   tcp.c:429-444       too short -> -1; bad TCP checksum -> forward, -1
- *   tcp.c:445-514       the stream step (restated below with mOS's exported
- *                       functions: FindStream / CreateStream / DetectStreamType
- *                       / CreateServerStream / HandleSockStream /
- *                       HandleMonitorStream are static in tcp.c)
+ *   tcp.c:445-514       the stream step: FindStream on the GPU's bucket, then
+ *                       mOS's CreateStream / HandleSockStream /
+ *                       HandleMonitorStream when tcp.c exports them (the
+ *                       upstream patch, INTEGRATION.md §2b, -DMOSRX_MOS_TCP_EXPORTS);
+ *                       otherwise -- they are static in tcp.c -- restated below
+ *                       with mOS's exported functions
  *   eth_in.c:80-84      NETSTAT rx_errors for a negative return
  *
  * TRUNCATED frames (headers claiming bytes past the capture; the reference
@@ -66,6 +68,10 @@
 #define MAX_CORES 64
 #define NO_BIT    (-1)
 
+/* tcp.c:258-270, defined with external linkage (`inline` under -fgnu89-inline)
+ * but declared in no header */
+void FillPacketContextTCPInfo(struct pkt_ctx *pctx, struct tcphdr *tcph);
+
 /* A filter program mOS holds for a monitor, and where its result comes from.
  * Keyed by its instructions, not by where mOS keeps them: a monitor that
  * closes frees its compiled filter (FreeMonListener, socket.c:33-36) and the
@@ -85,7 +91,8 @@ struct filt {
 struct rx_view {
 	struct mtcp_manager *mtcp;
 	int ifidx;
-	const mosrx_result *res;
+	const mosrx_result *res;     /* the batch's records: 16-byte ones, */
+	const mosrx_result8 *res8;   /* or a compact batch's 8-byte ones (cfg.compact) */
 	const uint32_t *match;       /* NULL: no masks for this batch */
 	const uint32_t *fhash;       /* NULL: no flow-table hashes for this batch */
 	mosrx_rx_state state;
@@ -139,20 +146,39 @@ static void view_fetch(struct rx_view *v, struct mtcp_manager *mtcp, int ifidx)
 	v->mtcp = mtcp;
 	v->ifidx = ifidx;
 	v->res = NULL;
+	v->res8 = NULL;
 	v->match = NULL;
 	v->fhash = NULL;
 	v->dead_from = -1;
-	if (!iom->dev_ioctl || iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_RESULTS, (void *)&v->res) || !v->res ||
-	    iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_STATE, &v->state)) {
+	if (!iom->dev_ioctl || iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_STATE, &v->state) ||
+	    (v->state.rec_bytes == 8
+	         ? iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_RESULTS8, (void *)&v->res8) || !v->res8
+	         : iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_RESULTS, (void *)&v->res) || !v->res)) {
 		v->res = NULL;
+		v->res8 = NULL;
 		v->state.n = 0x7FFFFFFF;   /* whatever get_rptr hands out goes the dropped way */
 		view_lost(v, mtcp, 0, "no GPU records for the batch (is gpu_module_func mOS's I/O module?)");
 		return;
 	}
+	if (v->res8)
+		stats_of(mtcp)->batches_c8++;
 	if (v->state.bpf_nprog && iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_MATCH, (void *)&v->match))
 		v->match = NULL;
 	if (iom->dev_ioctl(mtcp->ctx, ifidx, MOSRX_PKT_RX_FHASH, (void *)&v->fhash))
 		v->fhash = NULL;
+}
+
+/* What the consumer reads of a record, in either form: the reason code and
+ * the TCP flags byte.  pkt_info's lengths come from the header itself
+ * (FillPacketContextTCPInfo, tcp.c:258-270), as mOS takes them. */
+static inline uint8_t rec_reason(const struct rx_view *v, int i)
+{
+	return v->res8 ? v->res8[i].reason : v->res[i].reason;
+}
+
+static inline uint8_t rec_flags(const struct rx_view *v, int i)
+{
+	return v->res8 ? v->res8[i].tcp_flags : v->res[i].tcp_flags;
 }
 
 /* FindStream (tcp.c:181-191) -> HTSearch (fhash.c:184-214) with the bucket the
@@ -315,9 +341,9 @@ static void filters_check(struct rx_view *v, struct mtcp_manager *mtcp, int ifid
 static int filter_eval(struct rx_view *v, int index, const struct sfbpf_program *fc, int mode, uint8_t *p, int l)
 {
 	struct filt *f = filt_find(v, fc, mode);
-	/* bound since the last install (a full table keeps the rest on the CPU
-	 * rather than installing again for every frame) */
-	if (!f && v->nfilt < sizeof(v->filt) / sizeof(v->filt[0])) {
+	/* bound since the last install (a full table or instruction arena keeps
+	 * the rest on the CPU rather than installing again for every frame) */
+	if (!f && v->nfilt < sizeof(v->filt) / sizeof(v->filt[0]) && v->narena + fc->bf_len <= FILT_INSNS) {
 		filters_sync(v, v->mtcp, v->ifidx, index);
 		f = filt_find(v, fc, mode);
 	}
@@ -328,6 +354,21 @@ static int filter_eval(struct rx_view *v, int index, const struct sfbpf_program 
 
 /* ---- the stream step, tcp.c:445-514 ---------------------------------------- */
 
+#ifdef MOSRX_MOS_TCP_EXPORTS
+/* mOS's own stream functions, given external linkage by the upstream patch of
+ * INTEGRATION.md §2b (tcp.c:25, :195, :275, :377: `static` dropped; gnu89
+ * `inline` then emits an external definition): CreateStream (with
+ * DetectStreamType inside it, so a SYN filter is evaluated by mOS on the CPU,
+ * once per connection), HandleSockStream, HandleMonitorStream.  The consumer
+ * keeps only FindStream's lookup on the GPU's bucket and the orphan path's
+ * filters from the GPU masks. */
+struct tcp_stream *CreateStream(mtcp_manager_t mtcp, struct pkt_ctx *pctx, unsigned int *hash);
+void HandleSockStream(mtcp_manager_t mtcp, struct tcp_stream *cur_stream, struct pkt_ctx *pctx);
+void HandleMonitorStream(mtcp_manager_t mtcp, struct tcp_stream *sendside_stream,
+                         struct tcp_stream *recvside_stream, struct pkt_ctx *pctx);
+#else
+/* Without the patch those functions are static in tcp.c: restated here with
+ * mOS's exported functions, the SYN filter from the GPU's mask. */
 /* DetectStreamType, tcp.c:25-85: which sockets want a stream for this SYN. */
 static uint32_t detect_stream_type(struct rx_view *v, int index, mtcp_manager_t mtcp, struct pkt_ctx *pctx,
                                    uint32_t ip, uint16_t port)
@@ -390,7 +431,7 @@ static tcp_stream *server_stream(mtcp_manager_t mtcp, int type, struct pkt_ctx *
 static tcp_stream *create_stream(struct rx_view *v, int index, mtcp_manager_t mtcp, struct pkt_ctx *pctx,
                                  unsigned int *hash)
 {
-	const uint8_t flags = v->res[index].tcp_flags;
+	const uint8_t flags = rec_flags(v, index);
 	uint32_t type;
 	if (!((flags & TCP_FLAG_SYN) && !(flags & TCP_FLAG_ACK)))
 		return NULL;
@@ -428,6 +469,8 @@ static void monitor_stream(mtcp_manager_t mtcp, tcp_stream *snd, struct pkt_ctx 
 	}
 }
 
+#endif
+
 /* tcp.c:445-514 for a segment that passed the checks. */
 static int stream_step(struct rx_view *v, int index, mtcp_manager_t mtcp, struct pkt_ctx *pctx)
 {
@@ -448,7 +491,11 @@ static int stream_step(struct rx_view *v, int index, mtcp_manager_t mtcp, struct
 	if (!cur) {
 		if (mtcp->listener == NULL && mtcp->num_msp == 0)
 			return TRUE;                  /* a client-only end host: nothing to do (tcp.c:454-458) */
+#ifdef MOSRX_MOS_TCP_EXPORTS
+		cur = CreateStream(mtcp, pctx, &hash);
+#else
 		cur = create_stream(v, index, mtcp, pctx, &hash);
+#endif
 		if (!cur)
 			events = MOS_ON_ORPHAN;
 	}
@@ -456,12 +503,19 @@ static int stream_step(struct rx_view *v, int index, mtcp_manager_t mtcp, struct
 		cur->cb_events = events;
 		if (cur->rcvvar && cur->rcvvar->rcvbuf)
 			pctx->p.offset = (uint64_t)seq2loff(cur->rcvvar->rcvbuf, pctx->p.seq, cur->rcvvar->irs + 1);
+#ifdef MOSRX_MOS_TCP_EXPORTS
+		if (IS_STREAM_TYPE(cur, MOS_SOCK_STREAM))
+			HandleSockStream(mtcp, cur, pctx);
+		else if (HAS_STREAM_TYPE(cur, MOS_SOCK_MONITOR_STREAM_ACTIVE))
+			HandleMonitorStream(mtcp, cur, cur->pair_stream, pctx);
+#else
 		if (IS_STREAM_TYPE(cur, MOS_SOCK_STREAM)) {
 			UpdateRecvTCPContext(mtcp, cur, pctx);    /* HandleSockStream, tcp.c:275-281 */
 			DoActionEndTCPPacket(mtcp, cur, pctx);
 		} else if (HAS_STREAM_TYPE(cur, MOS_SOCK_MONITOR_STREAM_ACTIVE)) {
 			monitor_stream(mtcp, cur, pctx);
 		}
+#endif
 		return TRUE;
 	}
 	/* an orphan: MOS_ON_ORPHAN for every monitor whose orphan filter takes it */
@@ -473,7 +527,7 @@ static int stream_step(struct rx_view *v, int index, mtcp_manager_t mtcp, struct
 			HandleCallback(mtcp, MOS_NULL, walk->socket, MOS_SIDE_BOTH, pctx, events);
 	}
 	if (mtcp->listener) {
-		if (!(v->res[index].tcp_flags & TCP_FLAG_RST))   /* RFC 793: a RST is never answered */
+		if (!(rec_flags(v, index) & TCP_FLAG_RST))   /* RFC 793: a RST is never answered */
 			SendTCPPacketStandalone(mtcp, iph->daddr, tcph->dest, iph->saddr, tcph->source, 0,
 			                        pctx->p.seq + pctx->p.payloadlen + 1, 0, TCP_FLAG_RST | TCP_FLAG_ACK,
 			                        NULL, 0, pctx->p.cur_ts, 0, 0, -1);
@@ -495,13 +549,13 @@ static void release(mtcp_manager_t mtcp, struct pkt_ctx *pctx)
  * (tcp.c:408-514), from the record. */
 static int ipv4(struct rx_view *v, int index, mtcp_manager_t mtcp, struct pkt_ctx *pctx)
 {
-	const mosrx_result *r = &v->res[index];
+	uint8_t reason = rec_reason(v, index);
 	struct iphdr *iph = (struct iphdr *)((uint8_t *)pctx->p.ethh + sizeof(struct ethhdr));
 	struct mon_listener *walk;
 
-	if (r->reason == MOSRX_R_IP_SHORT)
+	if (reason == MOSRX_R_IP_SHORT)
 		return ERROR;
-	if (r->reason == MOSRX_R_IP_BADVER) {
+	if (reason == MOSRX_R_IP_BADVER) {
 		release(mtcp, pctx);
 		return FALSE;
 	}
@@ -522,40 +576,35 @@ static int ipv4(struct rx_view *v, int index, mtcp_manager_t mtcp, struct pkt_ct
 		release(mtcp, pctx);
 		return ERROR;
 	}
-	r = &v->res[index];                          /* (a filter install reclassifies the batch too) */
+	reason = rec_reason(v, index);               /* (a filter install reclassifies the batch too) */
 	if (mtcp->num_msp == 0 && mtcp->num_esp == 0) {
 		if (pctx->forward)
 			ForwardIPPacket(mtcp, pctx);
 		return TRUE;
 	}
-	if (r->reason == MOSRX_R_IP_BADCSUM)
+	if (reason == MOSRX_R_IP_BADCSUM)
 		return ERROR;
-	if (r->reason == MOSRX_R_ICMP_LOCAL && ProcessICMPPacket(mtcp, pctx))
+	if (reason == MOSRX_R_ICMP_LOCAL && ProcessICMPPacket(mtcp, pctx))
 		return TRUE;
-	if (r->reason == MOSRX_R_NOT_TCP || r->reason == MOSRX_R_ICMP_LOCAL) {
+	if (reason == MOSRX_R_NOT_TCP || reason == MOSRX_R_ICMP_LOCAL) {
 		if (!mtcp->num_msp || !pctx->forward)
 			release(mtcp, pctx);
 		else
 			ForwardIPPacket(mtcp, pctx);
 		return FALSE;
 	}
-	/* TCP: FillPacketContextTCPInfo (tcp.c:258-270) from the record */
-	{
-		struct tcphdr *tcph = (struct tcphdr *)((uint8_t *)iph + (r->ihl_doff >> 4) * 4);
-		pctx->p.tcph = tcph;
-		pctx->p.payload = (uint8_t *)pctx->p.ethh + r->payload_off;
-		pctx->p.payloadlen = r->payloadlen;
-		pctx->p.seq = ntohl(tcph->seq);
-		pctx->p.ack_seq = ntohl(tcph->ack_seq);
-		pctx->p.window = ntohs(tcph->window);
-		pctx->p.offset = 0;
-	}
+	/* TCP: mOS's own FillPacketContextTCPInfo (tcp.c:258-270; an external
+	 * definition under -fgnu89-inline) on the header as ProcessInTCPPacket
+	 * finds it (tcp.c:417): pkt_info's payload, payloadlen (u16, before the
+	 * length check), seq, ack_seq, window.  The record's verdict says these
+	 * bytes lie inside the capture (TRUNCATED frames never get here) */
+	FillPacketContextTCPInfo(pctx, (struct tcphdr *)((uint8_t *)iph + (iph->ihl << 2)));
 	TAILQ_FOREACH(walk, &mtcp->monitors, link)   /* tcp.c:424-427 */
 		if (walk->socket->socktype == MOS_SOCK_MONITOR_RAW)
 			HandleCallback(mtcp, MOS_NULL, walk->socket, MOS_SIDE_BOTH, pctx, MOS_ON_PKT_IN);
-	if (r->reason == MOSRX_R_TCP_SHORT)
+	if (reason == MOSRX_R_TCP_SHORT)
 		return ERROR;
-	if (r->reason == MOSRX_R_TCP_BADCSUM) {
+	if (reason == MOSRX_R_TCP_BADCSUM) {
 		if (pctx->forward && mtcp->num_msp)
 			ForwardIPPacket(mtcp, pctx);
 		return ERROR;
@@ -568,10 +617,10 @@ int mosrx_mos_process_packet(struct mtcp_manager *mtcp, const int ifidx, const i
 {
 	struct rx_view *v = &t_view;
 	struct pkt_ctx pctx;
-	const mosrx_result *r;
+	uint8_t reason;
 	int ret;
 
-	if (index == 0 || v->mtcp != mtcp || v->ifidx != ifidx || (!v->res && v->dead_from < 0)) {
+	if (index == 0 || v->mtcp != mtcp || v->ifidx != ifidx || (!v->res && !v->res8 && v->dead_from < 0)) {
 		view_fetch(v, mtcp, ifidx);
 		if (index == 0 && v->dead_from < 0)
 			filters_check(v, mtcp, ifidx);
@@ -584,7 +633,8 @@ int mosrx_mos_process_packet(struct mtcp_manager *mtcp, const int ifidx, const i
 	mtcp->nstat.rx_packets[ifidx]++;
 	mtcp->nstat.rx_bytes[ifidx] += len + ETHER_OVR;
 #endif
-	if (v->dead_from >= 0 && index >= v->dead_from) {   /* no records: dropped, as a NIC would */
+	/* no records (a negative index has none either): dropped, as a NIC would */
+	if (v->dead_from >= 0 && (index < 0 || index >= v->dead_from)) {
 		stats_of(mtcp)->gpu_dropped++;
 		if (mtcp->iom->release_pkt)
 			mtcp->iom->release_pkt(mtcp->ctx, ifidx, pkt_data, len);
@@ -593,7 +643,7 @@ int mosrx_mos_process_packet(struct mtcp_manager *mtcp, const int ifidx, const i
 #endif
 		return ERROR;
 	}
-	r = &v->res[index];
+	reason = rec_reason(v, index);
 	memset(&pctx, 0, sizeof(pctx));              /* FillInPacketEthContext, eth_in.c:12-25 */
 	pctx.p.cur_ts = cur_ts;
 	pctx.p.in_ifidx = ifidx;
@@ -603,9 +653,9 @@ int mosrx_mos_process_packet(struct mtcp_manager *mtcp, const int ifidx, const i
 	pctx.batch_index = index;
 	pctx.forward = g_config.mos->forward;
 
-	if (r->reason == MOSRX_R_ARP || r->reason == MOSRX_R_NON_IPV4) {
+	if (reason == MOSRX_R_ARP || reason == MOSRX_R_NON_IPV4) {
 		if (!mtcp->num_msp || !pctx.forward) {
-			if (r->reason == MOSRX_R_ARP) {
+			if (reason == MOSRX_R_ARP) {
 				ProcessARPPacket(mtcp, cur_ts, ifidx, pkt_data, len);
 				return TRUE;
 			}
@@ -617,7 +667,7 @@ int mosrx_mos_process_packet(struct mtcp_manager *mtcp, const int ifidx, const i
 			ForwardEthernetFrame(mtcp, &pctx);
 			return TRUE;
 		}
-	} else if (r->reason == MOSRX_R_TRUNCATED) {
+	} else if (reason == MOSRX_R_TRUNCATED) {
 		if (mtcp->iom->release_pkt)
 			mtcp->iom->release_pkt(mtcp->ctx, ifidx, pkt_data, len);
 		ret = ERROR;

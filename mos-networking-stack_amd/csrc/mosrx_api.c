@@ -338,6 +338,7 @@ static int launch_flags(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frame
 	kp.frames_bytes = (uint32_t)b->frames_bytes;
 	kp.n = b->n;
 	kp.flags = kflags;
+	kp.uni = mosrx_uni_pack(b);
 	return mosrx_launch_classify(&kp, tile_for(c, b), mosrx__tail_variant(c, b->frames_bytes, b->n), (void *)s);
 }
 
@@ -522,6 +523,7 @@ static int cls_bpf_launch(mosrx_ctx *c, const mosrx_batch *db, mosrx_result *out
 	kp.frames_bytes = (uint32_t)db->frames_bytes;
 	kp.n = db->n;
 	kp.flags = c->kflags;
+	kp.uni = 0;   /* the fused kernels take no layout hint */
 	return mosrx__bpf_fused_launch(c, &kp, kind == MOSRX_KIND_SMALL, s);
 }
 
@@ -859,17 +861,20 @@ int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *
  * the fused classify + BPF queue kernel, or the classify queue + the set's
  * kernel per batch while the set has no compiled form). */
 static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb, mosrx_result *const *h_out,
-                        mosrx_tcpinfo *const *h_tcpinfo, uint32_t *const *h_fhash, uint32_t *const *h_match)
+                        mosrx_tcpinfo *const *h_tcpinfo, uint32_t *const *h_fhash, uint32_t *const *h_match,
+                        int compact)
 {
+	/* compact: h_out[i] are mosrx_result8 arrays (8-byte records, VAR_C8); flow hashes, no pkt_info */
+	const size_t rsz = compact ? sizeof(mosrx_result8) : sizeof(mosrx_result);
 	struct region r[3 * MOSRX_MAX_GROUP];
 	uint32_t i, nr = 0, tiles = 0, maxl = 0, ntot = 0, tile;
 	uint64_t dev_bytes = 0, pre = 0;
 	mosrx_qparams qp;
 	struct slot *s;
 	int rc, unknown = 0, kind, tpb_ok = 1;
-	int fused = 0;
+	int fused = 0, uni = 0;
 	if (!c || slot < 0 || slot >= NSLOT || !b || !h_out || nb == 0 || nb > MOSRX_MAX_GROUP ||
-	    (h_match && h_tcpinfo))
+	    (h_match && h_tcpinfo) || (compact && (h_match || h_tcpinfo)))
 		return -EINVAL;
 	s = &c->slot[slot];
 	if (s->busy)
@@ -914,7 +919,7 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 		mosrx_qdesc *d = &s->h_qdesc[i];
 		memset(d, 0, sizeof(*d));
 		d->tile_base = tiles;
-		d->out = s->d_res + pre;
+		d->out = (mosrx_result *)((uint8_t *)s->d_res + pre * rsz);
 		if (fused)
 			d->bmatch = s->d_match + pre;
 		else
@@ -926,6 +931,8 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 			d->len = (const uint16_t *)r[nr + 2].dev;
 			d->frames_bytes = (uint32_t)b[i].frames_bytes;
 			d->n = b[i].n;
+			d->uni = mosrx_uni_pack(&b[i]);   /* the copy keeps the layout: offsets are relative to frames */
+			uni |= d->uni != 0;
 			nr += 3;
 		}
 		tiles += (b[i].n + tile - 1) / tile;
@@ -941,7 +948,8 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 	qp.nb = nb;
 	qp.flags = c->kflags;
 	qp.tpb = tpb_ok ? tiles / nb : 0;
-	qp.tinfo = h_tcpinfo ? 1u : 0u;
+	qp.tinfo = h_tcpinfo ? 1u : compact ? 2u : 0u;
+	qp.uni = (uint32_t)uni;
 	if (c->timing)
 		HIPCHK(hipEventRecord(s->kev0, s->stream));
 	if (fused) {
@@ -963,14 +971,14 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 	for (i = 0, pre = 0; i < nb;) {
 		uint32_t j = i + 1;
 		uint64_t n = b[i].n;
-		while (j < nb && h_out[j] == h_out[j - 1] + b[j - 1].n &&
+		while (j < nb && (uint8_t *)h_out[j] == (uint8_t *)h_out[j - 1] + b[j - 1].n * rsz &&
 		       (!h_tcpinfo || h_tcpinfo[j] == h_tcpinfo[j - 1] + b[j - 1].n) &&
 		       (!h_fhash || h_fhash[j] == h_fhash[j - 1] + b[j - 1].n) &&
 		       (!h_match || h_match[j] == h_match[j - 1] + b[j - 1].n))
 			n += b[j++].n;
 		if (n) {
-			HIPCHK(hipMemcpyAsync(h_out[i], s->d_res + pre, (size_t)n * sizeof(mosrx_result),
-			                      hipMemcpyDeviceToHost, s->stream));
+			HIPCHK(hipMemcpyAsync(h_out[i], (uint8_t *)s->d_res + pre * rsz, (size_t)n * rsz, hipMemcpyDeviceToHost,
+			                      s->stream));
 			if (h_tcpinfo)
 				HIPCHK(hipMemcpyAsync(h_tcpinfo[i], s->d_ti + pre, (size_t)n * sizeof(mosrx_tcpinfo),
 				                      hipMemcpyDeviceToHost, s->stream));
@@ -993,7 +1001,13 @@ int mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_batc
                                         mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo,
                                         uint32_t *const *h_fhash)
 {
-	return group_submit(c, slot, b, nb, h_out, h_tcpinfo, h_fhash, NULL);
+	return group_submit(c, slot, b, nb, h_out, h_tcpinfo, h_fhash, NULL, 0);
+}
+
+int mosrx_classify_host_group_submit_c8(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                        mosrx_result8 *const *h_out8, uint32_t *const *h_fhash)
+{
+	return group_submit(c, slot, b, nb, (mosrx_result *const *)h_out8, NULL, h_fhash, NULL, 1);
 }
 
 int mosrx_classify_host_group_submit_bpf(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
@@ -1002,7 +1016,7 @@ int mosrx_classify_host_group_submit_bpf(mosrx_ctx *c, int slot, const mosrx_bat
 {
 	if (!h_match)
 		return -EINVAL;
-	return group_submit(c, slot, b, nb, h_out, NULL, h_fhash, h_match);
+	return group_submit(c, slot, b, nb, h_out, NULL, h_fhash, h_match, 0);
 }
 
 int mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out,
@@ -1550,6 +1564,7 @@ struct mosrx_queue {
 	int tile;
 	uint64_t bytes, n;   /* frame bytes and frames of all batches (tail policy) */
 	int compact;         /* 8-byte records */
+	int uni;             /* some batch carries a layout hint */
 	int match;           /* the descriptors' bmatch: the installed BPF set's masks */
 	uint32_t **d_match;  /* per batch (the non-fused form) */
 };
@@ -1603,6 +1618,8 @@ int mosrx_queue_create_ex(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, void 
 		}
 		h[i].frames_bytes = (uint32_t)b[i].frames_bytes;
 		h[i].n = b[i].n;
+		h[i].uni = mosrx_uni_pack(&b[i]);
+		qq->uni |= h[i].uni != 0;
 		h[i].tile_base = tiles;
 		tiles += (b[i].n + (uint32_t)tile - 1) / (uint32_t)tile;
 	}
@@ -1654,6 +1671,7 @@ int mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream)
 	qp.flags = c->kflags;
 	qp.tpb = q->tpb;
 	qp.tinfo = q->compact ? 2u : 0u;
+	qp.uni = (uint32_t)q->uni;
 	if (!q->match)
 		return mosrx_launch_queue(&qp, q->total_tiles, q->tile, variant, s);
 	mosrx__bpf_poll(c);

@@ -47,7 +47,20 @@ typedef struct mosrx_kparams {
 	uint32_t        frames_bytes;
 	uint32_t        n;
 	uint32_t        flags;      /* MOSRX_KF_* */
+	uint32_t        uni;        /* layout hint (mosrx_uni_pack): frame i expected at (uni >> 16) + i * (uni & 0xFFFF);
+	                             * 0 = none.  Read by the SMALL tile's VAR_UNI kernels only */
 } mosrx_kparams;
+
+/* The uniform-layout hint of a batch (MOSRX_BATCH_UNIFORM, include/mosrx.h) in
+ * the 32 bits a kernel argument / queue descriptor carries: 0 when the batch
+ * has none or its first offset or stride does not fit 16 bits (the kernels
+ * then wait for the descriptors, as without a hint). */
+static inline uint32_t mosrx_uni_pack(const mosrx_batch *b)
+{
+	if (!(b->layout & MOSRX_BATCH_UNIFORM) || b->stride == 0 || b->stride > 0xFFFFu || b->off0 > 0xFFFFu)
+		return 0;
+	return (b->off0 << 16) | b->stride;
+}
 
 /* Reason counters: workgroup b adds to shard b % MOSRX_CNT_SHARDS, one 64-byte line each */
 #define MOSRX_CNT_SHARDS 256
@@ -96,7 +109,7 @@ typedef struct mosrx_qdesc {
 	uint32_t        frames_bytes;
 	uint32_t        n;
 	uint32_t        tile_base;   /* first workgroup of this batch in the launch */
-	uint32_t        pad;
+	uint32_t        uni;         /* the batch's layout hint (mosrx_uni_pack), 0 = none */
 } mosrx_qdesc;
 
 typedef struct mosrx_qparams {
@@ -108,6 +121,7 @@ typedef struct mosrx_qparams {
 	uint32_t           tpb;      /* tiles per batch when every batch has the same tile count, else 0 */
 	uint32_t           tinfo;    /* 1: the descriptors carry pkt_info TCP field buffers (VAR_TI);
 	                              * 2: the records are the 8-byte compact form (VAR_C8) */
+	uint32_t           uni;      /* 1: some descriptor carries a layout hint (the SMALL tile's VAR_UNI forms) */
 } mosrx_qparams;
 
 /* Batched BPF launch: the program table rides in the kernel arguments, the

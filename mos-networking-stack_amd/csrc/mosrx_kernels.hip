@@ -85,6 +85,10 @@ __device__ __forceinline__ u32x4 load16(__amdgpu_buffer_rsrc_t r, uint32_t c, ui
 #define VAR_C8 128
 #define IS_C8(v) (((v) & VAR_C8) != 0)
 static_assert(sizeof(mosrx_result8) == 8, "compact record size");
+// Variant bit 8: the batch's uniform-layout hint (kp.uni) is used by the SMALL
+// tile: window loads at the hinted address leave with the descriptor loads.
+#define VAR_UNI 256
+#define IS_UNI(v) (((v) & VAR_UNI) != 0)
 
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 __device__ __forceinline__ uint32_t be16hi(uint32_t w) { return ((w >> 8) & 0xFF00u) | (w >> 24); } // bytes 2,3
@@ -653,6 +657,27 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	const uint32_t nbytes = kp.frames_bytes;
 	uint32_t pv[FPL], ov[FPL], capv[FPL];
 	bool actv[FPL];
+	hdr_win_t winv[FPL];
+	const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
+	u32x4 ta, tb;   // the lane's share of the LDS tables
+	// VAR_UNI: frame p is expected at (uni >> 16) + p * (uni & 0xFFFF) (the
+	// batch's layout hint): its window and the tables are requested first, the
+	// descriptors behind them, so all of the tile's loads are in flight before
+	// its first wait -- one HBM round trip instead of two.  off[p] still
+	// decides: a lane whose offset differs reloads its window (below).
+	// uni == 0 (a queue batch without a hint): the hinted loads are off and
+	// every lane reloads, i.e. waits for its descriptor as without VAR_UNI.
+	const bool hinted = IS_UNI(VAR) && kp.uni != 0u;
+	if constexpr (IS_UNI(VAR) && (DBG & 2) == 0) {
+#pragma unroll
+		for (uint32_t i = 0; i < FPL; i++) {
+			const uint32_t p = tile * TILE + 256u * i + t;
+			hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, (kp.uni >> 16) + p * (kp.uni & 0xFFFFu), p < kp.n && hinted,
+			                              winv[i]);
+		}
+		ta = tg[lane];
+		tb = tg[lane + 64];
+	}
 #pragma unroll
 	for (uint32_t i = 0; i < FPL; i++) {
 		pv[i] = tile * TILE + 256u * i + t;
@@ -667,23 +692,34 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 		ov[i] = actv[i] ? o : 0u;
 		capv[i] = actv[i] ? eff_caplen(o, l, nbytes) : 0u;
 	}
-	hdr_win_t winv[FPL];
+	if constexpr (IS_UNI(VAR) && (DBG & 2) == 0) {
 #pragma unroll
-	for (uint32_t i = 0; i < FPL; i++) {
-		if constexpr (DBG & 2) {
+		for (uint32_t i = 0; i < FPL; i++) {
+			const bool miss = actv[i] && (!hinted || ov[i] != (kp.uni >> 16) + pv[i] * (kp.uni & 0xFFFFu));
+			if (__ballot(miss)) {                 // the hint was wrong for some lane (or absent): reload
+				hdr_win_t w2;
+				hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, ov[i], miss, w2);
 #pragma unroll
-			for (int j = 0; j < WIN_RAW; j++)
-				winv[i].raw[j] = ov[i] + j;
-		} else {
-			hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, ov[i], actv[i], winv[i]);
+				for (int j = 0; j < WIN_RAW; j++)
+					winv[i].raw[j] = miss ? w2.raw[j] : winv[i].raw[j];
+			}
 		}
+	} else {
+#pragma unroll
+		for (uint32_t i = 0; i < FPL; i++) {
+			if constexpr (DBG & 2) {
+#pragma unroll
+				for (int j = 0; j < WIN_RAW; j++)
+					winv[i].raw[j] = ov[i] + j;
+			} else {
+				hdr_load<WIN_AUX(VAR), NLOAD>(rs, nbytes, ov[i], actv[i], winv[i]);
+			}
+		}
+		ta = tg[lane];
+		tb = tg[lane + 64];
 	}
-	{
-		const u32x4 *tg = reinterpret_cast<const u32x4 *>(kp.tables);
-		const u32x4 a = tg[lane], b = tg[lane + 64];
-		reinterpret_cast<u32x4 *>(s_tab)[lane] = a;
-		reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = b;
-	}
+	reinterpret_cast<u32x4 *>(s_tab)[lane] = ta;
+	reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = tb;
 	if (kp.counters) {                        // uniform: the whole workgroup takes this barrier or none
 		if (t <= MOSRX_R_COUNT)
 			s_cnt[t] = 0;
@@ -1281,7 +1317,7 @@ __device__ __forceinline__ void classify_tile(const mosrx_kparams &kp, uint32_t 
 template <int KIND, int VAR>
 __global__ __launch_bounds__(WG_THREADS(KIND)) __attribute__((amdgpu_waves_per_eu(MIN_WAVES(KIND))))
 void mosrx_classify_kernel(const uint32_t *off, const uint16_t *len, const uint8_t *frames, const uint32_t *tables,
-                           uint32_t frames_bytes, uint32_t n, uint32_t flags, mosrx_kparams kp)
+                           uint32_t frames_bytes, uint32_t n, uint32_t flags, uint32_t uni, mosrx_kparams kp)
 {
 	kp.off = off;
 	kp.len = len;
@@ -1290,6 +1326,7 @@ void mosrx_classify_kernel(const uint32_t *off, const uint16_t *len, const uint8
 	kp.frames_bytes = frames_bytes;
 	kp.n = n;
 	kp.flags = flags;
+	kp.uni = uni;
 	classify_tile<KIND, VAR>(kp, blockIdx.x);
 }
 
@@ -1328,6 +1365,7 @@ __device__ __forceinline__ void queue_tile(const mosrx_qdesc *desc, uint32_t tpb
 	kp.frames_bytes = d->frames_bytes;
 	kp.n = d->n;
 	kp.flags = qp.flags;
+	kp.uni = d->uni;
 	classify_tile<KIND, VAR>(kp, b - d->tile_base);
 }
 
@@ -1430,7 +1468,7 @@ static void launch_v(const mosrx_kparams *kp, hipStream_t s)
 {
 	constexpr uint32_t tile = MOSRX_KIND_FRAMES(KIND);
 	launch_one(mosrx_classify_kernel<KIND, VAR>, (kp->n + tile - 1) / tile, WG_THREADS(KIND), s, kp->off, kp->len,
-	           kp->frames, kp->tables, kp->frames_bytes, kp->n, kp->flags, *kp);
+	           kp->frames, kp->tables, kp->frames_bytes, kp->n, kp->flags, kp->uni, *kp);
 }
 
 // Compiled variants: 0 = default cache policy, 2 = non-temporal tail stream
@@ -1443,14 +1481,16 @@ extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles,
 	if (kind < 0 || kind >= MOSRX_KIND_COUNT)
 		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-#define QROW(k)                                                                                         \
-	{launch_queue_v<k, 0>, launch_queue_v<k, 2>, launch_queue_v<k, 2 | VAR_TI>, launch_queue_v<k, VAR_C8>, \
-	 launch_queue_v<k, 2 | VAR_C8>}
-	static void (*const tab[MOSRX_KIND_COUNT][5])(const mosrx_qparams *, uint32_t, hipStream_t) = {
-		QROW(MOSRX_KIND_SMALL), QROW(MOSRX_KIND_S13)};
+	// [hinted][kind][form]: the SMALL tile's hinted forms (VAR_UNI) when some
+	// batch of the queue carries a layout hint (qp->uni); the stream tile has none
+#define QROW(k, u)                                                                                                 \
+	{launch_queue_v<k, 0 | (u)>, launch_queue_v<k, 2 | (u)>, launch_queue_v<k, 2 | VAR_TI>,                        \
+	 launch_queue_v<k, VAR_C8 | (u)>, launch_queue_v<k, 2 | VAR_C8 | (u)>}
+	static void (*const tab[2][MOSRX_KIND_COUNT][5])(const mosrx_qparams *, uint32_t, hipStream_t) = {
+		{QROW(MOSRX_KIND_SMALL, 0), QROW(MOSRX_KIND_S13, 0)}, {QROW(MOSRX_KIND_SMALL, VAR_UNI), QROW(MOSRX_KIND_S13, 0)}};
 #undef QROW
 	const int tv = (variant >> 1) & 1;
-	tab[kind][qp->tinfo == 1 ? 2 : qp->tinfo == 2 ? 3 + tv : tv](qp, total_tiles, s);
+	tab[qp->uni ? 1 : 0][kind][qp->tinfo == 1 ? 2 : qp->tinfo == 2 ? 3 + tv : tv](qp, total_tiles, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -1461,11 +1501,12 @@ extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int vari
 	if (kind < 0 || kind >= MOSRX_KIND_COUNT)
 		return -EINVAL;
 	const hipStream_t s = (hipStream_t)stream;
-#define KROW(k)                                                                                    \
-	{launch_v<k, 0>, launch_v<k, 2>, launch_v<k, 2 | VAR_TX>, launch_v<k, 2 | VAR_TI>, launch_v<k, VAR_C8>, \
-	 launch_v<k, 2 | VAR_C8>}
-	static void (*const tab[MOSRX_KIND_COUNT][6])(const mosrx_kparams *, hipStream_t) = {
-		KROW(MOSRX_KIND_SMALL), KROW(MOSRX_KIND_S13)};
+	// [hinted][kind][form], as in mosrx_launch_queue (kp->uni != 0: the SMALL tile's VAR_UNI forms)
+#define KROW(k, u)                                                                                         \
+	{launch_v<k, 0 | (u)>, launch_v<k, 2 | (u)>, launch_v<k, 2 | VAR_TX>, launch_v<k, 2 | VAR_TI>,          \
+	 launch_v<k, VAR_C8 | (u)>, launch_v<k, 2 | VAR_C8 | (u)>}
+	static void (*const tab[2][MOSRX_KIND_COUNT][6])(const mosrx_kparams *, hipStream_t) = {
+		{KROW(MOSRX_KIND_SMALL, 0), KROW(MOSRX_KIND_S13, 0)}, {KROW(MOSRX_KIND_SMALL, VAR_UNI), KROW(MOSRX_KIND_S13, 0)}};
 #undef KROW
 	const int tv = (variant >> 1) & 1;
 	// MOSRX_KF_COMPACT is the host's request for 8-byte records; the kernel's flags never carry it
@@ -1473,7 +1514,7 @@ extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int vari
 	            : (kp->flags & MOSRX_KF_COMPACT) ? 4 + tv : tv;
 	mosrx_kparams k = *kp;
 	k.flags &= ~(uint32_t)MOSRX_KF_COMPACT;
-	tab[kind][v](&k, s);
+	tab[k.uni ? 1 : 0][kind][v](&k, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 #endif   // __HIPCC_RTC__

@@ -45,6 +45,8 @@ int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx,
 		st->rounds++;
 		for (rx_inf = 0; rx_inf < nif; rx_inf++) {
 			const mosrx_result *res = NULL;
+			const mosrx_result8 *res8 = NULL;
+			mosrx_result one;
 			int32_t recv_cnt = iom->recv_pkts(ctx, rx_inf);
 			int32_t i;
 			if (recv_cnt < 0) {        /* RunMainLoop's for loop just skips it (core.c:899-902) */
@@ -55,14 +57,25 @@ int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx,
 				continue;
 			any = 1;
 			st->batches++;
-			if (!iom->dev_ioctl || iom->dev_ioctl(ctx, rx_inf, MOSRX_PKT_RX_RESULTS, &res) || !res)
-				return -ENOTSUP;   /* the backend must be a classifying one */
+			/* the backend must be a classifying one: 16-byte records, or a compact batch's 8-byte ones */
+			if (!iom->dev_ioctl ||
+			    ((iom->dev_ioctl(ctx, rx_inf, MOSRX_PKT_RX_RESULTS, &res) || !res) &&
+			     (iom->dev_ioctl(ctx, rx_inf, MOSRX_PKT_RX_RESULTS8, &res8) || !res8)))
+				return -ENOTSUP;
+			memset(&one, 0, sizeof(one));
 			for (i = 0; i < recv_cnt; i++) {
 				uint16_t len = 0;
 				const uint8_t *pkt = iom->get_rptr(ctx, rx_inf, i, &len);
-				const mosrx_result *r = &res[i];
+				const mosrx_result *r = res ? &res[i] : &one;
 				if (!pkt)
 					return -EIO;
+				if (!res) {           /* the compact record's fields, zero elsewhere */
+					one.rss = res8[i].rss;
+					one.reason = res8[i].reason;
+					one.queue = res8[i].queue;
+					one.verdict = res8[i].verdict;
+					one.tcp_flags = res8[i].tcp_flags;
+				}
 				st->rx_packets++;
 				st->rx_bytes += (uint64_t)len + ETHER_OVR;
 				if (r->verdict < 0)

@@ -74,7 +74,30 @@ def ip_raw(a: str) -> int:
 
 class Batch(C.Structure):
     _fields_ = [("frames", C.c_void_p), ("frames_bytes", C.c_uint64), ("off", C.c_void_p),
-                ("len", C.c_void_p), ("n", C.c_uint32), ("max_len", C.c_uint32)]
+                ("len", C.c_void_p), ("n", C.c_uint32), ("max_len", C.c_uint32),
+                ("layout", C.c_uint32), ("off0", C.c_uint32), ("stride", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+BATCH_UNIFORM = 1   # mosrx_batch.layout: frame i expected at off0 + i * stride (a hint; off[] decides)
+
+
+def uniform_layout(off: np.ndarray):
+    """(off0, stride) when off[i] == off[0] + i * stride for every i (a fixed-stride
+    packing, as a ring of equal-size frames has), else None."""
+    off = np.asarray(off)
+    if len(off) < 2:
+        return None
+    st = int(off[1]) - int(off[0])
+    if st <= 0 or not (np.diff(off.astype(np.int64)) == st).all():
+        return None
+    return int(off[0]), st
+
+
+def with_hint(b: Batch, hint) -> Batch:
+    """b with the layout hint (off0, stride) set (None: no hint)."""
+    if hint is not None:
+        b.layout, b.off0, b.stride = BATCH_UNIFORM, int(hint[0]), int(hint[1])
+    return b
 
 
 BPF_INSN = np.dtype([("code", "<u2"), ("jt", "u1"), ("jf", "u1"), ("k", "<u4")])   # mosrx_bpf_insn
@@ -110,7 +133,7 @@ class ModuleCfg(C.Structure):
                 ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32),
                 ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32),
                 ("group_bytes", C.c_uint64), ("flowhash", C.c_int32), ("tx_csum", C.c_int32),
-                ("numa", C.c_int32)]
+                ("numa", C.c_int32), ("compact", C.c_int32)]
 
 
 class ModuleStats(C.Structure):
@@ -418,11 +441,15 @@ class DevBatch:
     """A batch resident in HBM: frames + off + len, and its result buffer."""
 
     def __init__(self, ctx: "Context", frames: np.ndarray, off: np.ndarray, ln: np.ndarray,
-                 frames_bytes: int | None = None, max_len: int | None = None):
+                 frames_bytes: int | None = None, max_len: int | None = None, hint="auto"):
         frames = np.ascontiguousarray(frames, np.uint8)
         off = np.ascontiguousarray(off, np.uint32)
         ln = np.ascontiguousarray(ln, np.uint16)
         self.n = len(off)
+        # the layout hint the batch is handed over with: "auto" = its own fixed
+        # stride if it has one (the producer knows how it packed the frames),
+        # None = none, or an explicit (off0, stride) -- tests give wrong ones
+        self.hint = uniform_layout(off) if isinstance(hint, str) else hint
         self.frames_bytes = int(frames_bytes if frames_bytes is not None else len(frames))
         self.d_frames = DevBuffer(ctx, max(len(frames), 16))
         self.d_frames.upload(frames)
@@ -439,8 +466,8 @@ class DevBatch:
         self.caplen_sum = int(ln.astype(np.uint64).sum())
 
     def batch(self) -> Batch:
-        return Batch(self.d_frames.ptr, self.frames_bytes, self.d_off.ptr, self.d_len.ptr, self.n,
-                     self.max_len)
+        return with_hint(Batch(self.d_frames.ptr, self.frames_bytes, self.d_off.ptr, self.d_len.ptr, self.n,
+                               self.max_len), self.hint)
 
     def results(self) -> np.ndarray:
         out = np.zeros(self.n, RESULT_DTYPE)
@@ -660,8 +687,8 @@ class Context:
         return np.array(c[:], np.uint64)
 
     # ---- device resident ----
-    def upload(self, frames, off, ln, frames_bytes=None, max_len=None) -> DevBatch:
-        return DevBatch(self, frames, off, ln, frames_bytes, max_len)
+    def upload(self, frames, off, ln, frames_bytes=None, max_len=None, hint="auto") -> DevBatch:
+        return DevBatch(self, frames, off, ln, frames_bytes, max_len, hint)
 
     def classify_dev(self, db: DevBatch, sync: bool = True, flow_hash: bool = False, tcpinfo: bool = False) -> None:
         b = db.batch()
@@ -897,6 +924,7 @@ PKT_TX_IP_CSUM, PKT_TX_TCP_CSUM = 0x01, 0x02
 PKT_RX_RSS, DRV_NAME, PKT_RX_RESULTS, PKT_RX_MATCH = 0x03, 0x08, 0x10, 0x11
 PKT_RX_TCPINFO, PKT_SET_PARAMS = 0x12, 0x13
 PKT_RX_STATE, PKT_RX_RECLASSIFY, PKT_SET_BPF, PKT_RX_FHASH = 0x14, 0x15, 0x16, 0x17
+PKT_RX_RESULTS8 = 0x18
 
 
 class IoModuleFunc(C.Structure):
@@ -921,7 +949,7 @@ class GpuBackend:
     def __init__(self, sources: list[int], params: Params | None = None, batch: int = 32768,
                  max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
                  ngpu: int = 1, bpf=None, group: int = 1, tcpinfo: bool = False, tx_batch: int = 64,
-                 timing: bool = False, flowhash: bool = False, tx_csum: bool = False):
+                 timing: bool = False, flowhash: bool = False, tx_csum: bool = False, compact: bool = False):
         cfg = ModuleCfg()
         lib().mosrx_gpu_module_cfg_default(C.byref(cfg))
         cfg.num_ifs = len(sources)
@@ -932,6 +960,7 @@ class GpuBackend:
         cfg.gpu_base, cfg.ngpu = gpu_base, ngpu
         cfg.group, cfg.tcpinfo, cfg.tx_batch, cfg.flowhash = group, int(tcpinfo), tx_batch, int(flowhash)
         cfg.tx_csum = int(tx_csum)
+        cfg.compact = int(compact)          # 8-byte records (results8); 16-byte ones with filters
         if params is not None:
             cfg.params = params
         self.params = Params.from_buffer_copy(cfg.params)
@@ -970,6 +999,13 @@ class GpuBackend:
         if self._ioctl(self.ctx, ifidx, PKT_RX_RESULTS, C.byref(p)):
             raise MosrxError(5, "dev_ioctl(MOSRX_PKT_RX_RESULTS)")
         return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), (n * 16,)).view(RESULT_DTYPE).copy()
+
+    def results8(self, ifidx: int, n: int) -> np.ndarray:
+        """The exposed batch's 8-byte records (a compact backend's batch without filters)."""
+        p = C.c_void_p()
+        if self._ioctl(self.ctx, ifidx, PKT_RX_RESULTS8, C.byref(p)):
+            raise MosrxError(5, "dev_ioctl(MOSRX_PKT_RX_RESULTS8)")
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), (n * 8,)).view(RESULT8_DTYPE).copy()
 
     def matches(self, ifidx: int, n: int) -> np.ndarray:
         """dev_ioctl(MOSRX_PKT_RX_MATCH): the batch's BPF match masks."""

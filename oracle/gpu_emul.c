@@ -142,6 +142,33 @@ int __wrap_mosrx_classify_host_group_submit_ex(mosrx_ctx *mc, int slot, const mo
 	return 0;
 }
 
+/* 8-byte records (gpu_module_func cfg.compact): the oracle's 16-byte record projected
+ * onto mosrx_result8's fields, and the flow hashes when asked for */
+int __wrap_mosrx_classify_host_group_submit_c8(mosrx_ctx *mc, int slot, const mosrx_batch *b, uint32_t nb,
+                                               mosrx_result8 *const *out8, uint32_t *const *fh)
+{
+	struct emul_ctx *c = (struct emul_ctx *)mc;
+	uint32_t i, k;
+	int rc = 0;
+	(void)slot;
+	for (i = 0; i < nb && !rc; i++) {
+		mosrx_result *r = malloc((size_t)(b[i].n ? b[i].n : 1) * sizeof(*r));
+		if (!r)
+			return -ENOMEM;
+		rc = mo_classify_ex(&c->p, b[i].frames, b[i].frames_bytes, b[i].off, b[i].len, b[i].n, r,
+		                    fh ? fh[i] : NULL, NULL);
+		for (k = 0; !rc && k < b[i].n; k++) {
+			out8[i][k].rss = r[k].rss;
+			out8[i][k].reason = r[k].reason;
+			out8[i][k].queue = r[k].queue;
+			out8[i][k].verdict = r[k].verdict;
+			out8[i][k].tcp_flags = r[k].tcp_flags;
+		}
+		free(r);
+	}
+	return rc;
+}
+
 int __wrap_mosrx_classify_bpf_host_submit(mosrx_ctx *mc, int slot, const mosrx_batch *b, mosrx_result *out,
                                           uint32_t *match)
 {

@@ -442,6 +442,8 @@ int main(int argc, char **argv)
 	cfg.flowhash = getenv("MOSAPP_FLOWHASH") ? atoi(getenv("MOSAPP_FLOWHASH")) : 1;   /* FindStream's bucket too */
 	/* mOS's TX checksums on the GPU (dev_ioctl PKT_TX_*_CSUM, as with DPDK's offload) */
 	cfg.tx_csum = getenv("MOSAPP_TX_CSUM") ? atoi(getenv("MOSAPP_TX_CSUM")) : 0;
+	/* 8-byte records (what an unconfigured mOS build of the module uses), or 16-byte ones */
+	cfg.compact = getenv("MOSAPP_COMPACT") ? atoi(getenv("MOSAPP_COMPACT")) : 1;
 	cfg.params.num_queues = nq;
 	cfg.params.queue_mode = qmode;
 	cfg.params.num_msp = 0;                       /* followed from mOS's manager (mos_state) */
@@ -534,7 +536,7 @@ int main(int argc, char **argv)
 		       "\"consumer_frames\": %lu, \"stream_step\": %lu, \"gpu_flow_hash\": %lu, \"reclassified\": %lu, "
 		       "\"filter_installs\": %lu, \"max_filter_sync_ns\": %lu, \"gpu_errors\": %lu, \"gpu_dropped\": %lu, "
 		       "\"filters_gpu\": %lu, \"filters_cpu\": %lu, \"tx_packets\": %lu, \"tx_csum_offloaded\": %lu, "
-		       "\"tx_errors\": %lu, \"arp_sent\": %lu, \"reopen_same_addr\": %d}\n",
+		       "\"tx_errors\": %lu, \"arp_sent\": %lu, \"reopen_same_addr\": %d, \"batches_c8\": %lu}\n",
 		       argv[1], (unsigned long)g_total, (unsigned long)g_rx_frames,
 		       g_rx_frames ? g_rx_ns / (double)g_rx_frames : 0.0,
 		       g_rx_frames ? (g_rx_ns - g_tx_ns) / (double)g_rx_frames : 0.0, (unsigned long)cs.frames,
@@ -543,7 +545,7 @@ int main(int argc, char **argv)
 		       (unsigned long)cs.gpu_dropped,
 		       (unsigned long)cs.filters_gpu, (unsigned long)cs.filters_cpu, (unsigned long)g_tx_stats.tx_packets,
 		       (unsigned long)g_tx_stats.tx_csum_offloaded, (unsigned long)g_tx_stats.tx_errors, g_arp_sent,
-		       g_reopen_same_addr);
+		       g_reopen_same_addr, (unsigned long)cs.batches_c8);
 	}
 	mosrx_source_close(src);
 	return 0;

@@ -34,7 +34,7 @@ def test_every_declared_symbol_is_exported():
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
     assert hasattr(lib, "gpu_module_func")
-    assert mosrx.lib().mosrx_abi_version() == 2
+    assert mosrx.lib().mosrx_abi_version() == 3
 
 
 def test_no_oracle_in_product_library():
@@ -48,7 +48,8 @@ def test_no_oracle_in_product_library():
 def test_struct_layouts():
     assert C.sizeof(mosrx.Params) == 148          # + num_local, local_ip[16] (ABI 2)
     assert C.sizeof(mosrx.Params) == C.sizeof(O.Params)
-    assert C.sizeof(mosrx.Batch) == 40
+    assert C.sizeof(mosrx.Batch) == 56          # + layout, off0, stride, reserved (ABI 3)
+    assert mosrx.Batch.layout.offset == 40 and mosrx.Batch.stride.offset == 48
     assert mosrx.RESULT_DTYPE.itemsize == 16
     assert mosrx.TCPINFO_DTYPE.itemsize == 12
 
@@ -206,7 +207,7 @@ def test_module_struct_layouts_match_the_header(tmp_path):
     subprocess.run(["gcc", "-I" + os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
     got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
     assert got == [C.sizeof(mosrx.ModuleCfg), mosrx.ModuleCfg.group_bytes.offset, C.sizeof(mosrx.ModuleStats),
-                   mosrx.ModuleStats.device.offset, 20, 16]
+                   mosrx.ModuleStats.device.offset, 24, 16]
 
 
 @pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "mos_rx_mos.o")),

@@ -35,6 +35,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.path.join(ROOT, "oracle", "_ref")
 APP = os.path.join(REF, "mos_app")
 APP_EMUL = os.path.join(REF, "mos_app_emul")
+# the builds and record forms every scenario runs in: the consumer restating
+# tcp.c's static stream functions, with 8-byte records (the module's default in
+# an mOS build) and with 16-byte ones; and the consumer calling mOS's own
+# functions under the upstream patch of INTEGRATION.md §2b (mos_app_x)
+FORMS = {"c8": ("", {}), "rec16": ("", {"MOSAPP_COMPACT": "0"}), "tcp_exports": ("_x", {})}
 
 CONF = """mos {{
 	forward = {forward}
@@ -174,8 +179,11 @@ def run_app(exe, mode, tmp, name, sc, frames, extra_env=None):
                 callbacks=(d / "callbacks.txt").read_text(), tx=pcap_frames(d / "tx.pcap"), stats=stats)
 
 
-def compare_modes(exe, tmp, name):
-    sc = SCENARIOS[name]
+def compare_modes(exe, tmp, name, form="c8"):
+    suffix, form_env = FORMS[form]
+    exe += suffix
+    sc = dict(SCENARIOS[name])
+    sc["env"] = dict(sc["env"], **form_env)
     if "fixture" in sc:
         frames = fixture_frames(sc["fixture"])
     else:
@@ -207,24 +215,54 @@ def _have(exe):
     return os.access(exe, os.X_OK)
 
 
-@pytest.mark.skipif(not _have(APP_EMUL), reason="needs oracle/_ref/mos_app_emul (make -C oracle ref)")
+@pytest.mark.skipif(not _have(APP_EMUL) or not _have(APP_EMUL + "_x"),
+                    reason="needs oracle/_ref/mos_app_emul{,_x} (make -C oracle ref)")
+@pytest.mark.parametrize("form", sorted(FORMS))
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
-def test_consumer_matches_processpacket_emulated(tmp_path, name):
-    pp, gpu = compare_modes(APP_EMUL, tmp_path, name)
-    _check_scenario(name, pp, gpu)
+def test_consumer_matches_processpacket_emulated(tmp_path, name, form):
+    pp, gpu = compare_modes(APP_EMUL, tmp_path, name, form)
+    _check_scenario(name, pp, gpu, form)
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not _have(APP), reason="needs oracle/_ref/mos_app (built by make -C oracle ref)")
+@pytest.mark.skipif(not _have(APP) or not _have(APP + "_x"),
+                    reason="needs oracle/_ref/mos_app{,_x} (built by make -C oracle ref)")
+@pytest.mark.parametrize("form", sorted(FORMS))
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
-def test_consumer_matches_processpacket_on_gpu(tmp_path, name):
-    pp, gpu = compare_modes(APP, tmp_path, name)
-    _check_scenario(name, pp, gpu)
+def test_consumer_matches_processpacket_on_gpu(tmp_path, name, form):
+    pp, gpu = compare_modes(APP, tmp_path, name, form)
+    _check_scenario(name, pp, gpu, form)
 
 
-def _check_scenario(name, pp, gpu):
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "mos_rx_mos_x.o")),
+                    reason="needs oracle/_ref (make -C oracle ref)")
+def test_patched_build_calls_mos_own_stream_functions():
+    """Under the upstream patch the consumer compiles none of its tcp.c
+    restatement and calls mOS's CreateStream / HandleSockStream /
+    HandleMonitorStream, which the patched tcp.c object defines."""
+    def syms(obj, *flags):
+        out = subprocess.run(["nm", *flags, os.path.join(REF, obj)], capture_output=True, text=True,
+                             check=True).stdout
+        return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    # (the restated functions are static and inlined: what they call tells them apart --
+    # CreateServerStream's ParseTCPOptions, CreateStream's CreateClientTCPStream,
+    # HandleMonitorStream's UpdateMonitor)
+    restated = {"ParseTCPOptions", "CreateClientTCPStream", "UpdateMonitor"}
+    assert restated <= syms("mos_rx_mos.o", "-u") and not (restated & syms("mos_rx_mos_x.o", "-u"))
+    want = {"CreateStream", "HandleSockStream", "HandleMonitorStream"}
+    assert want <= syms("mos_rx_mos_x.o", "-u") and not (want & syms("mos_rx_mos.o", "-u"))
+    assert want | {"DetectStreamType"} <= syms("tcp_x.o", "-g", "--defined-only")
+
+
+def _check_scenario(name, pp, gpu, form="c8"):
     """What each scenario must have exercised (so a scenario cannot pass vacuously)."""
     st, cb = gpu["stats"], pp["callbacks"]
+    # the record form the consumer read: 8-byte records for every batch classified
+    # without filters in the compact forms, none in the 16-byte one
+    if form == "rec16":
+        assert st["batches_c8"] == 0
+    elif not any(k in SCENARIOS[name]["env"] for k in ("MOSAPP_RAW", "MOSAPP_SYN", "MOSAPP_ORPHAN")):
+        assert st["batches_c8"] > 0
     nstat = pp["state"].splitlines()[-1].split()
     assert int(nstat[6]) > 0                                   # rx_errors: bad checksums etc. were seen
     if name in ("monitor_fwd", "filters", "two_monitors_raw", "listener", "late_filter", "batch_1_per_launch",

@@ -57,6 +57,9 @@ WORKLOADS = {
     "S64_hdr": (mosrx.TRACE_S64, 32_768, 256, "config #2 header parse + IP cksum + RSS only (skip_tcp_csum), "
                                               "8-byte records (mosrx_result8)"),
     "S64_hdr16": (mosrx.TRACE_S64, 32_768, 256, "config #2 header-only as S64_hdr, 16-byte records"),
+    # the full verdict (TCP checksum included) with the 8-byte records the drop-in path
+    # hands mOS (gpu_module_func cfg.compact)
+    "S64_c8": (mosrx.TRACE_S64, 32_768, 256, "config #2 full verdict, 8-byte records (mosrx_result8)"),
     # the same frames packed back to back (60-byte stride, every frame at a different
     # alignment) instead of at 16-byte boundary + 2: the inter-frame pad is the 64 B
     # rows' only traffic beyond the algorithmic bytes (diagnostic row)
@@ -81,7 +84,7 @@ WORKLOADS = {
     "S64_cls_bpf_ring": (mosrx.TRACE_S64, 32_768, 256, "config #2 classify + 8 BPF programs fused, one batch-queue "
                                                        "launch over 256 batches"),
 }
-DEFAULT_WORKLOADS = ("M1500,S64,S64_hdr,S64_hdr16,S64_hdr_packed,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,"
+DEFAULT_WORKLOADS = ("M1500,S64,S64_c8,S64_hdr,S64_hdr16,S64_hdr_packed,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,"
                      "M1500_tx,M1500_txc,IMIX_bpf,IMIX_cls_bpf,IMIX_cls_bpf_ring,S64_cls_bpf_ring")
 OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_ti": mosrx.OP_CLASSIFY_TI, "M1500_tx": mosrx.OP_TX_CSUM,
        "M1500_txc": mosrx.OP_TX_CHECKS,
@@ -90,8 +93,13 @@ OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_ti": mosrx.OP_CLASSIFY_TI, "M150
 BPF_BENCH = [("tcp", 0), ("tcp port 80", 0), ("tcp[tcpflags] & tcp-syn != 0", 1), ("net 192.168.0.0/16 and tcp", 1),
              ("host 10.0.0.1 and port 80", 0), ("ip[8] < 64", 1), ("tcp[((tcp[12:1] & 0xf0) >> 2):4] = 0x47455420", 1),
              ("portrange 1000-2000", 0)]
+# rows whose records are the 8-byte mosrx_result8 (the drop-in path's compact form)
+COMPACT = ("S64_hdr", "S64_hdr_packed", "S64_c8", "c8")
 PREWARM_S = 0.3
 STREAMS = 2      # rx batches in flight per GPU for the one-launch-per-batch rows
+# the layout hint the resident batches are handed over with (mosrx_batch.layout): "auto" =
+# their own fixed stride when they have one (the 64 B traces), None = none (A/B runs)
+HINT = "auto"
 DISTINCT = 8     # distinct batch contents generated per rank (the rest are resident copies of them)
 
 
@@ -103,7 +111,8 @@ def dist_env():
 
 
 class Dist:
-    """Barrier + max-reduce over ranks (gloo, CPU); nothing on the data path."""
+    """Barrier, max and gather over ranks (gloo, CPU): the timed regions' bounds and
+    the reduction of the per-rank figures; nothing on the data path."""
 
     def __init__(self, ws: int, rank: int):
         self.ws, self.rank, self.pg = ws, rank, None
@@ -125,9 +134,46 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather(self, x: list[float]) -> list[list[float]]:
+        """Every rank's vector x (same length on all ranks), in rank order."""
+        if self.ws == 1:
+            return [list(x)]
+        import torch
+        t = torch.zeros(self.ws, len(x), dtype=torch.float64)
+        t[self.rank] = torch.tensor(x, dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t.tolist()
+
+    def leg(self, fn):
+        """Run one end-to-end leg on every rank between barriers (each rank on its
+        own GPU and host thread, all at once) and reduce it: fn() returns a dict
+        with this rank's `frames` and `bytes`; the wall time is the host clock
+        around fn.  Returns (this rank's dict, the job's aggregate)."""
+        self.barrier()
+        t0 = time.perf_counter()
+        r = fn()
+        wall = time.perf_counter() - t0
+        self.barrier()
+        rows = self.gather([float(r["frames"]), float(r["bytes"]), wall])
+        return r, aggregate(rows)
+
     def close(self):
         if self.ws > 1:
             self.dist.destroy_process_group()
+
+
+def aggregate(rows: list[list[float]]) -> dict:
+    """The job's rate from per-rank (frames, bytes, wall seconds) of legs run at the
+    same time on every rank: everything all ranks moved over the longest rank's
+    wall time (the job ends with its last rank), and each rank's own rate."""
+    frames = sum(r[0] for r in rows)
+    nbytes = sum(r[1] for r in rows)
+    wall = max(r[2] for r in rows)
+    per = [r[0] / r[2] / 1e6 if r[2] > 0 else 0.0 for r in rows]
+    return {"ranks": len(rows), "frames": int(frames), "seconds": round(wall, 4),
+            "mpkts": round(frames / wall / 1e6, 2) if wall > 0 else None,
+            "gbps": round(nbytes / wall / 1e9, 2) if wall > 0 else None,
+            "per_rank_mpkts": {"min": round(min(per), 2), "max": round(max(per), 2)}}
 
 
 def job_seed(kind: int, b: int) -> int:
@@ -152,7 +198,7 @@ def algo_bytes(tr: mosrx.Trace, key: str = "") -> int:
         return tr.caplen_sum + tr.n * (DESC_BYTES + 8)
     if "_cls_bpf" in key:          # the classify bytes + the 4-byte match mask
         return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES + 4)
-    if key in ("S64_hdr", "S64_hdr_packed"):   # 8-byte compact records
+    if key in COMPACT:                         # 8-byte compact records
         return tr.caplen_sum + tr.n * (DESC_BYTES + 8)
     if key.endswith("_bpf"):
         return tr.n * (DESC_BYTES + 4) + int(np.minimum(tr.len, 64).astype(np.int64).sum())
@@ -235,7 +281,7 @@ def resident_batches(ctx, key, world, rank, nres):
     trs = [mosrx.Trace(kind, batch, seed=job_seed(kind, b)) for b in mine]
     if key.endswith("_packed"):
         trs = [pack_uniform(t) for t in trs]
-    dbs = [ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len)
+    dbs = [ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len, hint=HINT)
            for t in (trs[i % len(trs)] for i in range(nres))]
     return dbs, trs, mine
 
@@ -285,7 +331,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         # disjoint resident copies cycle so the working set stays past the L3
         if "_cls_bpf" in key:
             ctx.bpf_set(bpf_bench_programs())   # (compiled before the queues run)
-        compact = key in ("S64_hdr", "S64_hdr_packed")
+        compact = key in COMPACT
         qs = [ctx.queue_ex(dbs[i:i + ring], match="_cls_bpf" in key, compact=compact)
               for i in range(0, len(dbs), ring)]
         prewarm(lambda: qs[0].time(8, qs[1:], kernels=False))
@@ -337,6 +383,8 @@ def measure(ctx, dist, key, steps, warmup, rank):
     for d in dbs:
         d.free()
     n = dist.ws
+    # each rank's own device rate over its timed steps (HIP events on its kernel stream)
+    per_rank = [r[0] for r in dist.gather([ab_step * steps / (dev_ms * 1e-3) / 1e9 if dev_ms > 0 else 0.0])]
     out = {
         "workload": label,
         "batch": batch,
@@ -355,6 +403,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         "kernel_ms": kern_ms,
         "kernel_ms_back_to_back": kern_b2b,
         "kernel_ms_isolated": kern_iso,
+        "per_rank_device_gbps": {"min": round(min(per_rank), 1), "max": round(max(per_rank), 1)},
     }
     achieved = ab_step / (kern_ms * 1e-3) / 1e9
     pmc = load_pmc(key)
@@ -379,13 +428,15 @@ def measure(ctx, dist, key, steps, warmup, rank):
     return out, tr
 
 
-def cpu_threads():
-    """Threads for the all-cores CPU leg: the process's CPU affinity, capped by the
-    box's CPU share when the environment states it (OMP_NUM_THREADS / MOSRX_CPU_THREADS:
-    16 per GPU on the pool's boxes, whose nproc shows the whole machine)."""
+def cpu_share():
+    """Threads one GPU's share of the host may use: the process's CPU affinity,
+    capped by the share the environment states (MOSRX_CPU_THREADS /
+    OMP_NUM_THREADS: 16 per GPU on the pool's boxes, whose nproc shows the whole
+    machine).  Returns (threads, affinity size, the stated cap or None)."""
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     cap = os.environ.get("MOSRX_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
-    return max(1, min(aff, int(cap))) if cap else aff, aff
+    cap = int(cap) if cap else None
+    return (max(1, min(aff, cap)) if cap else aff), aff, cap
 
 
 def host_model():
@@ -396,10 +447,15 @@ def host_model():
         return ""
 
 
-def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, all_cores: bool = True):
-    """The oracle (bit-exact C restatement, oracle/mosrx_oracle.c) on this host's cores.
-
-    Reported baseline only; never the measured product path."""
+def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, shares: bool = True, ws: int = 1,
+                 host_cpus=None):
+    """The oracle (bit-exact C restatement, oracle/mosrx_oracle.c) on this host's cores:
+    one core (`value`), one GPU's share of the host (`per_gpu_share`: the threads a
+    rank may use, e.g. 16 of 256 CPUs on the pool's 1-GPU boxes), and for a job of
+    `ws` GPUs the whole job's share (`job_share`: ws x that, over the CPUs the
+    process had before its NUMA binding, `host_cpus`) -- the host-core figure the
+    ws-GPU line stands next to.  One pthread per core over disjoint trace slices,
+    as mOS shards per core.  Reported baseline only; never the measured product path."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O
     p = O.params(skip_tcp_csum=1 if key.startswith("S64_hdr") else 0)
@@ -417,6 +473,13 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, all_cores: bool 
             if el >= min_s:
                 return reps, el
 
+    def leg(nt, what):
+        rn, en = run(nt)
+        return {"value": round(rn * ab / en / 1e9, 3), "unit": "GB/s", "cores": nt, "kind": "port",
+                "mpkts": round(rn * tr.n / en / 1e6, 3),
+                "sample": f"{rn} passes over one {tr.n}-frame batch, {nt} pthreads over disjoint slices "
+                          f"({en:.1f} s); {what}; host nproc {os.cpu_count()}"}
+
     r1, e1 = run(1)
     gb1 = r1 * ab / e1 / 1e9
     out = {
@@ -425,14 +488,23 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, all_cores: bool 
         "sample": f"{r1} passes over one {tr.n}-frame batch of this workload ({e1:.1f} s), "
                   f"oracle/mosrx_oracle.c mo_classify, 1 thread; host '{host_model()}', nproc {os.cpu_count()}",
     }
-    if all_cores:
-        nt, aff = cpu_threads()
-        rn, en = run(nt)
-        gbn = rn * ab / en / 1e9
-        out["all_cores"] = {"value": round(gbn, 3), "unit": "GB/s", "cores": nt, "affinity": aff,
-                            "mpkts": round(rn * tr.n / en / 1e6, 3),
-                            "sample": f"{rn} passes, {nt} pthreads over disjoint slices ({en:.1f} s); "
-                                      f"process affinity {aff} CPUs"}
+    if not shares:
+        return out
+    nt, aff, cap = cpu_share()
+    out["per_gpu_share"] = leg(nt, f"one GPU's share of the host: {nt} of {os.cpu_count()} CPUs "
+                                   f"(affinity {aff}, stated share {cap})")
+    out["per_gpu_share"]["host_cpus"] = os.cpu_count()
+    if ws > 1 and host_cpus:
+        # the job's share: ws GPUs' worth of threads over the CPUs the job's process had
+        # before its NUMA binding (rank 0 alone runs this, after every GPU leg)
+        nj = max(1, min(len(host_cpus), (cap or len(host_cpus)) * ws))
+        mine = os.sched_getaffinity(0)
+        try:
+            os.sched_setaffinity(0, host_cpus)
+            out["job_share"] = leg(nj, f"the {ws}-GPU job's share of the host: {nj} of {os.cpu_count()} CPUs")
+        finally:
+            os.sched_setaffinity(0, mine)
+        out["job_share"]["host_cpus"] = os.cpu_count()
     return out
 
 
@@ -610,7 +682,7 @@ def measure_fw64(ctx, seconds: float):
     out = {"workload": "config #1: simple_firewall state, 1 core, 10k x 64B (60 B caplen), one flow",
            "batch": tr.n, "algo_bytes_per_batch": algo_bytes(tr)}
     ref = cpu_reference(tr, "FW64", seconds)
-    port = cpu_baseline(tr, "FW64", min_s=seconds, all_cores=False)
+    port = cpu_baseline(tr, "FW64", min_s=seconds, shares=False)
     if ref:
         port["reference"] = ref
     # mOS's ProcessPacket itself in the firewall's state, forward = 1: every
@@ -689,19 +761,22 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
         pr, _ = ctx.host_alloc(tr.n * 16)
         bufs += [pb, pr]
         outs.append(pr)
-        batches.append(mosrx.Batch(pb, fb, pb + fa, pb + fa + tr.n * 4, tr.n, tr.max_len))
+        # the staged 64 B frames sit at one stride (back to back): handed over with that hint
+        batches.append(mosrx.with_hint(mosrx.Batch(pb, fb, pb + fa, pb + fa + tr.n * 4, tr.n, tr.max_len),
+                                       mosrx.uniform_layout(soff) if HINT else None))
     ctx.time_host(batches, outs, 8)             # warm: both slots, pinned pages mapped
     ms = ctx.time_host(batches, outs, iters)
     for p in bufs:
         ctx.host_free(p)
     ab = algo_bytes(tr)
     return {"gbps": ab * iters / (ms * 1e-3) / 1e9, "mpkts": tr.n * iters / (ms * 1e-3) / 1e6,
-            "ms_per_batch": ms / iters,
+            "ms_per_batch": ms / iters, "frames": tr.n * iters, "bytes": ab * iters,
             "method": "pinned hipHostMalloc staging (one block: frames | off | len, the backend's layout: "
                       "mosrx_source_fill), one H2D copy, kernel, D2H records; 2 streams"}
 
 
-def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1, bpf=None):
+def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1, bpf=None,
+                    compact: bool = True):
     """The drop-in boundary's own rate: mosrx_rx_loop (RunMainLoop's rx section,
     core.c:897-909) over gpu_module_func (io_module.h:63-78) fed by an in-memory
     source replaying the trace — per group of batches: source -> pinned
@@ -722,7 +797,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     loops = max(1, frames_target // tr.n)
     src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
     be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
-                          group=group, timing=True, bpf=bpf)
+                          group=group, timing=True, bpf=bpf, compact=compact)
     try:
         be.run_loop(max_pkts=2 * ctx_batch * max(group, 128 if key == "S64" else 4))    # warm-up: staging sized, module loaded
         st0 = be.stats()
@@ -738,16 +813,21 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     kms = st1.kernel_ms - st0.kernel_ms
     batches = st1.rx_batches - st0.rx_batches
     dev_us = 1e3 * kms / max(batches, 1)
-    ab = (algo_bytes(tr, "_cls_bpf" if bpf else "")) * (ctx_batch / tr.n)
-    return {"mpkts": n / dt / 1e6, "gbps": nb * algo_bytes(tr, "_cls_bpf" if bpf else "") / dt / 1e9, "frames": n,
+    # records: 16 bytes with filters (the fused kernels), 8 in compact mode, else 16
+    akey = "_cls_bpf" if bpf else "c8" if compact else ""
+    ab = algo_bytes(tr, akey) * (ctx_batch / tr.n)
+    return {"mpkts": n / dt / 1e6, "gbps": nb * algo_bytes(tr, akey) / dt / 1e9, "frames": n,
+            "bytes": int(nb * algo_bytes(tr, akey)),
             "seconds": round(dt, 3), "filters": len(bpf) if bpf else 0,
+            "records": 16 if (bpf or not compact) else 8,
             "distinct_frames": tr.n,
             "group": group if group else "auto", "batches_per_launch": round(batches / max(launches, 1), 2),
             "kernel_launches": int(launches), "batches": int(batches),
             "device_us_per_batch": round(dev_us, 3),
             "device_roofline_frac": round(ab / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if dev_us > 0 else None,
             "method": f"mosrx_rx_loop over gpu_module_func (pipelined, "
-                      f"{group if group else 'auto (MOSRX_GROUP_AUTO)'} batch(es) per launch"
+                      f"{group if group else 'auto (MOSRX_GROUP_AUTO)'} batch(es) per launch, "
+                      f"{'8-byte records (cfg.compact)' if compact and not bpf else '16-byte records'}"
                       f"{', ' + str(len(bpf)) + ' monitor filters installed: the fused classify + BPF queue kernel' if bpf else ''}), "
                       f"in-memory source replaying {tr.n} distinct frames; every batch crosses PCIe; device "
                       f"time = HIP events around each kernel (its frames were just copied in)"}
@@ -822,7 +902,7 @@ def measure_backend_threads(key: str, nthreads: int, group: int, frames_per_thre
 
 
 def main():
-    global STREAMS
+    global STREAMS, HINT
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -830,12 +910,16 @@ def main():
     ap.add_argument("--workloads", default=DEFAULT_WORKLOADS)
     ap.add_argument("--streams", type=int, default=STREAMS,
                     help="batches in flight for the one-launch-per-batch rows (1 = strictly serial launches)")
+    ap.add_argument("--no-hint", action="store_true",
+                    help="hand the resident batches over without their layout hint (A/B of MOSRX_BATCH_UNIFORM)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline legs")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (PCIe) and backend legs")
     ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
                     help="where the full record (every row and leg) is written")
     args = ap.parse_args()
     STREAMS = args.streams
+    if args.no_hint:
+        HINT = None
 
     ws, rank, local = dist_env()
     if ws != args.gpus:
@@ -847,6 +931,7 @@ def main():
     # each rank on its GPU's NUMA node before its first GPU call (mOS binds
     # every mTCP thread to its core's node, cpu.c:56-87): the host side of the batches it
     # stages and waits for stays node-local
+    host_cpus = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
     numa = mosrx.bind_to_gpu_node(device)
     ctx = mosrx.Context(device)
     keys = [k for k in args.workloads.split(",") if k]
@@ -860,28 +945,37 @@ def main():
                   file=sys.stderr, flush=True)
     e2e = None
     if not args.no_e2e and any(k in traces for k in ("M1500", "S64", "IMIX")):
-        e2e = {k: measure_e2e(ctx, traces[k], {"M1500": 60, "S64": 800}[k]) for k in ("M1500", "S64") if k in traces}
-        # the gpu_module_func backend itself (host thread = this rank)
-        # the module's default configuration (cfg.group auto: batches per launch sized to what is ready)
+        # every leg runs on every rank at once, between barriers (Dist.leg), each rank
+        # on its own GPU and host thread; e2e[...] is this rank's figure (rank 0's in
+        # the record), e2e["aggregate"][...] the job's: all ranks' frames over the
+        # longest rank's wall time
+        e2e, agg = {}, {}
+        for k, iters in (("M1500", 60), ("S64", 800)):
+            if k in traces:
+                e2e[k], agg[k] = dist.leg(lambda: measure_e2e(ctx, traces[k], iters))
+        # the gpu_module_func backend itself (host thread = this rank), the module's
+        # configuration inside mOS: auto groups, 8-byte records (cfg.compact)
         # (frames through each leg: enough that the timed part holds several launches after the
         # warm-up's pipelined group -- an IMIX auto group is 3 batches of 100 MB)
         target = {"S64": 32_000_000, "M1500": 2_000_000, "IMIX": 12_000_000}
-        e2e["backend"] = {k: measure_backend(traces[k], k, target[k], device, group=0)
-                          for k in ("M1500", "S64", "IMIX") if k in traces}
-        # one launch per batch, and explicit rings (cfg.group)
-        if "S64" in traces:
-            e2e["backend"]["S64_group1"] = measure_backend(traces["S64"], "S64", 16_000_000, device, group=1)
-            e2e["backend"]["S64_group128"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=128)
-            # 8 monitor filters installed (mtcp_bind_monitor_filter): auto groups through the fused
-            # classify + BPF queue kernel, as without filters
-            e2e["backend"]["S64_bpf"] = measure_backend(traces["S64"], "S64", 32_000_000, device, group=0,
-                                                        bpf=bpf_bench_programs())
-        if "IMIX" in traces:
-            e2e["backend"]["IMIX_bpf"] = measure_backend(traces["IMIX"], "IMIX", 12_000_000, device, group=0,
-                                                         bpf=bpf_bench_programs())
-        if "M1500" in traces:
-            e2e["backend"]["M1500_group1"] = measure_backend(traces["M1500"], "M1500", 2_000_000, device, group=1)
-            e2e["backend"]["M1500_group8"] = measure_backend(traces["M1500"], "M1500", 4_000_000, device, group=8)
+        be, be_agg = {}, {}
+        legs = [(k, dict(frames_target=target[k], group=0)) for k in ("M1500", "S64", "IMIX")]
+        legs += [("S64_rec16", dict(frames_target=32_000_000, group=0, compact=False)),   # 16-byte records
+                 ("S64_group1", dict(frames_target=16_000_000, group=1)),      # one launch per batch
+                 ("S64_group128", dict(frames_target=32_000_000, group=128)),
+                 # 8 monitor filters installed (mtcp_bind_monitor_filter): auto groups through the
+                 # fused classify + BPF queue kernel (16-byte records), as without filters
+                 ("S64_bpf", dict(frames_target=32_000_000, group=0, bpf=bpf_bench_programs())),
+                 ("IMIX_bpf", dict(frames_target=12_000_000, group=0, bpf=bpf_bench_programs())),
+                 ("M1500_group1", dict(frames_target=2_000_000, group=1)),
+                 ("M1500_group8", dict(frames_target=4_000_000, group=8))]
+        for name, kw in legs:
+            k = name.split("_")[0]
+            if k in traces:
+                be[name], be_agg[name] = dist.leg(lambda: measure_backend(traces[k], k, cpu=device, **kw))
+        e2e["backend"] = be
+        agg["backend"] = be_agg
+        e2e["aggregate"] = agg
         # one mTCP thread per core, each with its own context / source / rx loop
         # (one GPU's host side: single-rank runs only)
         if ws == 1:
@@ -891,10 +985,13 @@ def main():
             if "M1500" in traces:
                 mt["M1500"] = [measure_backend_threads("M1500", t, 1, 2_000_000, device) for t in (1, 2, 4)]
             e2e["backend_threads"] = mt
+    # the last barrier of the GPU legs: from here rank 0 alone runs the host-core
+    # baselines, with no other rank's timed region in flight, and the others wait
+    dist.barrier()
     cpu = None
-    if rank == 0 and ws == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         head = "M1500" if "M1500" in traces else keys[0]
-        cpu = cpu_baseline(traces[head], head, min_s=10.0)
+        cpu = cpu_baseline(traces[head], head, min_s=10.0, ws=ws, host_cpus=host_cpus)
         ref = cpu_reference(traces[head], head, 10.0)
         if ref:
             cpu["reference"] = ref
@@ -916,7 +1013,7 @@ def main():
             cpu["mos_rx_loop_FW64_bare"] = rx
         for k in keys:
             if k != head:
-                results[k]["cpu_baseline"] = cpu_baseline(traces[k], k, min_s=2.0)
+                results[k]["cpu_baseline"] = cpu_baseline(traces[k], k, min_s=2.0, shares=False)
                 if k in ("S64", "IMIX"):
                     ref = cpu_reference(traces[k], k, 2.0)
                     if ref:
@@ -930,6 +1027,7 @@ def main():
         read_ceiling = {"launch_128MiB": round(ctx.probe_read_bw(128 << 20, 12, 96), 1),
                         "launch_768MiB": round(ctx.probe_read_bw(768 << 20, 3, 48), 1)}
     ctx.close()
+    dist.barrier()   # the other ranks wait here while rank 0 runs the host legs
     dist.close()
     if rank != 0:
         return
@@ -999,9 +1097,10 @@ def headline_line(detail, h, head, results, e2e):
     cpu_line = None
     if cpu:
         cpu_line = _compact_cpu(cpu)
-        for leg in ("all_cores", "reference", "reference_processpacket"):
+        for leg in ("per_gpu_share", "job_share", "reference", "reference_processpacket"):
             if cpu.get(leg):
-                cpu_line[leg] = {k: cpu[leg][k] for k in ("value", "unit", "cores", "kind", "mpkts") if k in cpu[leg]}
+                cpu_line[leg] = {k: cpu[leg][k] for k in ("value", "unit", "cores", "host_cpus", "kind", "mpkts")
+                                 if k in cpu[leg]}
         for leg in ("mos_rx_loop_M1500", "mos_rx_loop_FW64", "mos_rx_loop_FW64_bare"):
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("processpacket_ns_per_frame", "gpu_records_ns_per_frame",
@@ -1019,6 +1118,8 @@ def headline_line(detail, h, head, results, e2e):
             continue
         sec[k] = {"mpkts": round(r["mpkts"], 1), "launch_us": r["roofline"]["launch_us"],
                   "frac": r["roofline"]["frac"]}   # (GB/s: the detail record)
+        if detail["n_gpus"] > 1:
+            sec[k]["per_rank_device_gbps"] = r["per_rank_device_gbps"]
     e2e_line = None
     if e2e:
         e2e_line = {k: {"gbps": round(v["gbps"], 1), "mpkts": round(v["mpkts"], 1)}
@@ -1026,6 +1127,13 @@ def headline_line(detail, h, head, results, e2e):
         be = e2e.get("backend") or {}
         e2e_line["backend"] = {k: {"mpkts": round(v["mpkts"], 1), "dev_frac": v.get("device_roofline_frac")}
                                for k, v in be.items()}
+        # the job's end-to-end rates: every rank's legs at once, all frames over the longest wall
+        ag = e2e.get("aggregate") or {}
+        e2e_line["aggregate"] = {k: {kk: v[kk] for kk in ("ranks", "mpkts", "gbps", "per_rank_mpkts")}
+                                 for k, v in ag.items() if k in ("M1500", "S64")}
+        e2e_line["aggregate"]["backend"] = {k: {kk: v[kk] for kk in ("mpkts", "per_rank_mpkts")}
+                                            for k, v in (ag.get("backend") or {}).items()
+                                            if k in ("M1500", "S64", "IMIX")}
         if e2e.get("consumer"):
             e2e_line["consumer"] = e2e["consumer"]
     return {
@@ -1047,6 +1155,7 @@ def headline_line(detail, h, head, results, e2e):
                    "parallelism": detail["config"]["parallelism"]},
         "roofline": {k: rf[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_us",
                                          "launch_timing")},
+        "per_rank_device_gbps": h["per_rank_device_gbps"],
         "read_ceiling_gbps": detail["read_ceiling_gbps"],
         "frac_of_read_ceiling": detail["frac_of_read_ceiling"],
         "cpu_baseline": cpu_line,

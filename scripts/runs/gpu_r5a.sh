@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r5a
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest tests/test_layout_hint.py tests/test_parity_gpu.py -m gpu -x -q \
+timeout -k 10 700 python -u -m pytest tests/test_layout_hint.py tests/test_parity_gpu.py tests/test_mos_consumer.py -m gpu -x -q \
   --timeout 120 --timeout-method thread > gpurun_out/r5a/pytest.log 2>&1; rc=$?
 tail -3 gpurun_out/r5a/pytest.log; [ $rc -ne 0 ] && exit $rc
 for W in S64_1 S64 S64_hdr; do

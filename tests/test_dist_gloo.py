@@ -85,3 +85,51 @@ def test_shard_plan():
     assert allb == list(range(37))
     with pytest.raises(ValueError):
         mosrx.shard_plan(4, 2, 2)
+
+
+def _leg_worker(rank, world, port, out_dir):
+    """Each rank runs one end-to-end leg between barriers (bench.Dist.leg): rank r
+    moves (r + 1) * 1000 frames of 100 bytes in about 0.2 * (r + 1) s."""
+    import json
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import bench
+    d = bench.Dist(world, rank)
+
+    def fn():
+        time.sleep(0.2 * (rank + 1))
+        return {"frames": (rank + 1) * 1000, "bytes": (rank + 1) * 100_000}
+    mine, agg = d.leg(fn)
+    spread = d.gather([float(rank + 1), 10.0 * rank])
+    with open(os.path.join(out_dir, f"leg{rank}.json"), "w") as fh:
+        json.dump({"mine": mine, "agg": agg, "spread": spread}, fh)
+    d.close()
+
+
+def test_bench_leg_aggregate_over_ranks(tmp_path):
+    """The N>1 end-to-end figure: every rank's frames and bytes summed over the
+    longest rank's wall time (the job ends with its last rank), and each rank's
+    own rate as min / max; every rank computes the same aggregate."""
+    import json
+    world = 2
+    mp.start_processes(_leg_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    outs = [json.load(open(tmp_path / f"leg{r}.json")) for r in range(world)]
+    agg = outs[0]["agg"]
+    assert outs[1]["agg"] == agg
+    assert agg["ranks"] == 2 and agg["frames"] == 3000
+    wall = agg["seconds"]
+    assert 0.4 <= wall < 1.5                                   # the slower rank's ~0.4 s (between barriers)
+    assert abs(agg["mpkts"] - 3000 / wall / 1e6) < 1e-2
+    assert abs(agg["gbps"] - 300_000 / wall / 1e9) < 1e-2
+    assert agg["per_rank_mpkts"]["min"] <= agg["per_rank_mpkts"]["max"]
+    assert outs[0]["spread"] == [[1.0, 0.0], [2.0, 10.0]]       # gather: rank order, every rank
+
+
+def test_aggregate_rows():
+    import bench
+    a = bench.aggregate([[1e6, 1e9, 0.5], [3e6, 2e9, 1.0]])
+    assert a["frames"] == 4_000_000 and a["seconds"] == 1.0
+    assert a["mpkts"] == 4.0 and a["gbps"] == 3.0
+    assert a["per_rank_mpkts"] == {"min": 2.0, "max": 3.0}

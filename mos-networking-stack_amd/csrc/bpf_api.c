@@ -198,25 +198,54 @@ const char *mosrx_bpf_jit_log(const mosrx_ctx *c)
 	return c ? c->bpf_jit_log : "";
 }
 
+void mosrx__note_stream(mosrx_ctx *c, hipStream_t s)
+{
+	uint32_t k;
+	if (s && s == c->stream)
+		return;
+	for (k = 0; k < NSLOT; k++)
+		if (s && s == c->slot[k].stream)
+			return;
+	for (k = 0; k < c->nxs; k++)
+		if (s && s == c->xs[k])
+			return;
+	c->foreign_streams = 1;   /* a caller's stream (or the null stream): only a device sync covers it */
+}
+
+int mosrx__drain(mosrx_ctx *c)
+{
+	uint32_t k;
+	HIPCHK(hipSetDevice(c->device));
+	if (c->foreign_streams) {
+		HIPCHK(hipDeviceSynchronize());
+		c->foreign_streams = 0;
+		return 0;
+	}
+	HIPCHK(hipStreamSynchronize(c->stream));
+	for (k = 0; k < NSLOT; k++)
+		HIPCHK(hipStreamSynchronize(c->slot[k].stream));
+	for (k = 0; k < c->nxs; k++)
+		HIPCHK(hipStreamSynchronize(c->xs[k]));
+	return 0;
+}
+
 /* The interpreter reads the installed instructions from device memory while
- * earlier launches may still be in flight on the context's streams (a group
- * classified behind the rx loop), so each set goes to the next buffer of a
- * pool: a buffer is written again only after the context's streams drained,
- * and only if a launch may have read it since its last write.  The compiled
- * kernels carry their programs in their code. */
+ * earlier launches may still be in flight (a group classified behind the rx
+ * loop on the context's streams, or a caller's mosrx_bpf_dev /
+ * mosrx_queue_run on its own stream), so each set goes to the next buffer of a
+ * pool: a buffer is written again only after those launches drained
+ * (mosrx__drain), and only if a launch may have read it since its last
+ * write.  The compiled kernels carry their programs in their code. */
 static int stage_insns(mosrx_ctx *c, const mosrx_bpf_insn *staged, uint32_t total)
 {
 	const uint32_t i = c->bpf_pool_next;
+	int rc;
 	if (!c->d_bpf_pool[i] &&
 	    hipMalloc((void **)&c->d_bpf_pool[i], MOSRX_BPF_MAX_INSNS * sizeof(mosrx_bpf_insn)) != hipSuccess)
 		return -ENOMEM;
 	if (c->bpf_pool_used[i]) {
-		uint32_t k;
-		HIPCHK(hipStreamSynchronize(c->stream));
-		for (k = 0; k < NSLOT; k++)
-			HIPCHK(hipStreamSynchronize(c->slot[k].stream));
-		for (k = 0; k < c->nxs; k++)
-			HIPCHK(hipStreamSynchronize(c->xs[k]));
+		if ((rc = mosrx__drain(c)))
+			return rc;
 		memset(c->bpf_pool_used, 0, sizeof(c->bpf_pool_used));
 	}
 	if (total)
@@ -282,6 +311,7 @@ int mosrx__bpf_launch_dev(mosrx_ctx *c, const uint8_t *frames, uint64_t frames_b
 	if (!n)
 		return 0;
 	mosrx__bpf_poll(c);
+	mosrx__note_stream(c, s);
 	bp.frames = frames;
 	bp.off = off;
 	bp.len = len;

@@ -1160,6 +1160,8 @@ static void *worker_main(void *arg)
 	mosrx_bpf_insn *insns = malloc(MOSRX_BPF_MAX_INSNS * sizeof(*insns));
 	hipSetDevice(w->device);
 	pthread_mutex_lock(&w->mu);
+	if (!insns)
+		w->stop = 1;   /* no buffer to compile from: the thread is gone, its sets stay on the interpreter */
 	for (;;) {
 		struct mosrx_jit_entry e;
 		mosrx_bparams t;
@@ -1222,16 +1224,6 @@ static struct mosrx_bpf_worker *worker_get(mosrx_ctx *c)
 	return w;
 }
 
-static void sync_own_streams(mosrx_ctx *c)
-{
-	uint32_t i;
-	hipSetDevice(c->device);
-	hipStreamSynchronize(c->stream);
-	for (i = 0; i < NSLOT; i++)
-		hipStreamSynchronize(c->slot[i].stream);
-	for (i = 0; i < c->nxs; i++)
-		hipStreamSynchronize(c->xs[i]);
-}
 
 static void install(mosrx_ctx *c, const struct mosrx_jit_entry *e)
 {
@@ -1243,8 +1235,8 @@ static void install(mosrx_ctx *c, const struct mosrx_jit_entry *e)
 }
 
 /* Into the cache, evicting the oldest entry that is not the installed set's
- * (its kernels may be in use; launches still in flight on the context's
- * streams are drained before a module goes). */
+ * (its kernels may be in use; launches still in flight -- on the context's
+ * streams or a caller's -- are drained before a module goes, mosrx__drain). */
 static void cache_put(mosrx_ctx *c, const struct mosrx_jit_entry *e)
 {
 	uint32_t i;
@@ -1260,7 +1252,7 @@ static void cache_put(mosrx_ctx *c, const struct mosrx_jit_entry *e)
 			v++;
 		if (v == c->njit)
 			v = 0;
-		sync_own_streams(c);
+		mosrx__drain(c);
 		entry_unload(&c->jit[v]);
 		memmove(&c->jit[v], &c->jit[v + 1], sizeof(c->jit[0]) * (MOSRX_BPF_JIT_CACHE - 1 - v));
 		c->njit--;
@@ -1340,6 +1332,10 @@ int mosrx__bpf_jit_request(mosrx_ctx *c, const mosrx_bpf_insn *insns)
 	for (j = 0; j < t->nprog; j++)
 		total += t->prog_len[j];
 	pthread_mutex_lock(&w->mu);
+	if (w->stop) {                                  /* the thread is gone: the interpreter keeps the set */
+		pthread_mutex_unlock(&w->mu);
+		return -EAGAIN;
+	}
 	if (!(w->busy && w->busy_key == c->bpf_key)) {   /* (being compiled already: wait for that one) */
 		w->want_t = *t;
 		w->want_key = c->bpf_key;
@@ -1407,6 +1403,7 @@ int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hi
 	void *args[] = {&k};
 	if (!f)
 		return -EINVAL;
+	mosrx__note_stream(c, s);
 	return module_launch(f, (kp->n + tile - 1) / tile, threads, s, args);
 }
 
@@ -1425,6 +1422,7 @@ int mosrx__bpf_fused_queue_launch(mosrx_ctx *c, const mosrx_qparams *qp, uint32_
 		return -EINVAL;
 	if (!total_tiles)
 		return 0;
+	mosrx__note_stream(c, s);
 	return module_launch(f, total_tiles, threads, s, args);
 }
 

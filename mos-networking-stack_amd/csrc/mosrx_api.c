@@ -234,6 +234,8 @@ void mosrx_close(mosrx_ctx *c)
 	if (!c)
 		return;
 	hipSetDevice(c->device);
+	if (c->foreign_streams)   /* a caller's stream may still run the set's kernels: they go below */
+		hipDeviceSynchronize();
 	if (c->stream)
 		hipStreamSynchronize(c->stream);
 	for (i = 0; i < NSLOT; i++) {

@@ -637,12 +637,12 @@ class Context:
         """The installed set has a fused classify + BPF kernel."""
         return lib().mosrx_bpf_fused(self.handle) == 1
 
-    def classify_bpf_dev(self, db: "DevBatch", sync: bool = True) -> None:
+    def classify_bpf_dev(self, db: "DevBatch", sync: bool = True, stream: int | None = None) -> None:
         """Records into db.d_out and match masks into db.d_match in one pass."""
         if db.d_match is None:
             db.d_match = DevBuffer(self, max(db.n * 4, 4))
         b = db.batch()
-        _chk(lib().mosrx_classify_bpf_dev(self.handle, C.byref(b), db.d_out.ptr, db.d_match.ptr, None),
+        _chk(lib().mosrx_classify_bpf_dev(self.handle, C.byref(b), db.d_out.ptr, db.d_match.ptr, stream),
              "mosrx_classify_bpf_dev")
         if sync:
             _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
@@ -673,11 +673,12 @@ class Context:
         _chk(lib().mosrx_bpf_host(self.handle, C.byref(b), out.ctypes.data), "mosrx_bpf_host")
         return out
 
-    def bpf_dev(self, db: "DevBatch", sync: bool = True) -> None:
+    def bpf_dev(self, db: "DevBatch", sync: bool = True, stream: int | None = None) -> None:
+        """Match masks into db.d_match; `stream`: a caller's hipStream_t (None: the context's)."""
         if db.d_match is None:
             db.d_match = DevBuffer(self, max(db.n * 4, 4))
         b = db.batch()
-        _chk(lib().mosrx_bpf_dev(self.handle, C.byref(b), db.d_match.ptr, None), "mosrx_bpf_dev")
+        _chk(lib().mosrx_bpf_dev(self.handle, C.byref(b), db.d_match.ptr, stream), "mosrx_bpf_dev")
         if sync:
             _chk(lib().mosrx_sync(self.handle), "mosrx_sync")
 

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r5b
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_backend_gpu.py tests/test_layout_hint.py -m gpu -x -q \
+timeout -k 10 400 python -u -m pytest tests/test_backend_gpu.py tests/test_layout_hint.py tests/test_bpf_streams.py -m gpu -x -q \
   --timeout 120 --timeout-method thread > gpurun_out/r5b/pytest.log 2>&1; rc=$?
 tail -2 gpurun_out/r5b/pytest.log; [ $rc -ne 0 ] && exit $rc
 for r in 1 2; do

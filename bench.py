@@ -145,16 +145,14 @@ class Dist:
         return t.tolist()
 
     def leg(self, fn):
-        """Run one end-to-end leg on every rank between barriers (each rank on its
-        own GPU and host thread, all at once) and reduce it: fn() returns a dict
-        with this rank's `frames` and `bytes`; the wall time is the host clock
-        around fn.  Returns (this rank's dict, the job's aggregate)."""
-        self.barrier()
-        t0 = time.perf_counter()
-        r = fn()
-        wall = time.perf_counter() - t0
-        self.barrier()
-        rows = self.gather([float(r["frames"]), float(r["bytes"]), wall])
+        """Run one end-to-end leg on every rank at once (each rank on its own GPU
+        and host thread) and reduce it.  fn(sync) sets its leg up, calls sync()
+        right before and right after its timed region -- a barrier, so every
+        rank's timed region starts together -- and returns this rank's `frames`,
+        `bytes` and `seconds` (the timed region).  Returns (this rank's dict, the
+        job's aggregate)."""
+        r = fn(self.barrier)
+        rows = self.gather([float(r["frames"]), float(r["bytes"]), float(r["seconds"])])
         return r, aggregate(rows)
 
     def close(self):
@@ -733,8 +731,9 @@ def measure_fw64_boundary(tr: mosrx.Trace, loops: int = 50):
                       f"mosrx_rx_loop + mosrx_forward_frame -> source TX (pcap dump), one host thread"}
 
 
-def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
-    """End-to-end host->HBM->host rate (pinned staging, 2 slots); recorded in DESIGN.md."""
+def measure_e2e(ctx, tr: mosrx.Trace, iters: int, sync=lambda: None):
+    """End-to-end host->HBM->host rate (pinned staging, 2 slots); recorded in DESIGN.md.
+    sync() brackets the timed region (the ranks' barrier in a multi-GPU job)."""
     ctx.set_params(mosrx.default_params())
     # one pinned staging block per slot, frames | off | len, the frames in the
     # gpu_module backend's staging layout (mosrx_source_fill: frames of up to
@@ -765,18 +764,22 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int):
         batches.append(mosrx.with_hint(mosrx.Batch(pb, fb, pb + fa, pb + fa + tr.n * 4, tr.n, tr.max_len),
                                        mosrx.uniform_layout(soff) if HINT else None))
     ctx.time_host(batches, outs, 8)             # warm: both slots, pinned pages mapped
+    sync()
+    t0 = time.perf_counter()
     ms = ctx.time_host(batches, outs, iters)
+    wall = time.perf_counter() - t0
+    sync()
     for p in bufs:
         ctx.host_free(p)
     ab = algo_bytes(tr)
     return {"gbps": ab * iters / (ms * 1e-3) / 1e9, "mpkts": tr.n * iters / (ms * 1e-3) / 1e6,
-            "ms_per_batch": ms / iters, "frames": tr.n * iters, "bytes": ab * iters,
+            "ms_per_batch": ms / iters, "frames": tr.n * iters, "bytes": ab * iters, "seconds": wall,
             "method": "pinned hipHostMalloc staging (one block: frames | off | len, the backend's layout: "
                       "mosrx_source_fill), one H2D copy, kernel, D2H records; 2 streams"}
 
 
 def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1, bpf=None,
-                    compact: bool = True):
+                    compact: bool = True, sync=lambda: None):
     """The drop-in boundary's own rate: mosrx_rx_loop (RunMainLoop's rx section,
     core.c:897-909) over gpu_module_func (io_module.h:63-78) fed by an in-memory
     source replaying the trace — per group of batches: source -> pinned
@@ -801,9 +804,11 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     try:
         be.run_loop(max_pkts=2 * ctx_batch * max(group, 128 if key == "S64" else 4))    # warm-up: staging sized, module loaded
         st0 = be.stats()
+        sync()
         t0 = time.perf_counter()
         st = be.run_loop()
         dt = time.perf_counter() - t0
+        sync()
         st1 = be.stats()
     finally:
         be.close()
@@ -818,7 +823,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     ab = algo_bytes(tr, akey) * (ctx_batch / tr.n)
     return {"mpkts": n / dt / 1e6, "gbps": nb * algo_bytes(tr, akey) / dt / 1e9, "frames": n,
             "bytes": int(nb * algo_bytes(tr, akey)),
-            "seconds": round(dt, 3), "filters": len(bpf) if bpf else 0,
+            "seconds": dt, "filters": len(bpf) if bpf else 0,
             "records": 16 if (bpf or not compact) else 8,
             "distinct_frames": tr.n,
             "group": group if group else "auto", "batches_per_launch": round(batches / max(launches, 1), 2),
@@ -952,7 +957,7 @@ def main():
         e2e, agg = {}, {}
         for k, iters in (("M1500", 60), ("S64", 800)):
             if k in traces:
-                e2e[k], agg[k] = dist.leg(lambda: measure_e2e(ctx, traces[k], iters))
+                e2e[k], agg[k] = dist.leg(lambda sync: measure_e2e(ctx, traces[k], iters, sync))
         # the gpu_module_func backend itself (host thread = this rank), the module's
         # configuration inside mOS: auto groups, 8-byte records (cfg.compact)
         # (frames through each leg: enough that the timed part holds several launches after the
@@ -972,7 +977,8 @@ def main():
         for name, kw in legs:
             k = name.split("_")[0]
             if k in traces:
-                be[name], be_agg[name] = dist.leg(lambda: measure_backend(traces[k], k, cpu=device, **kw))
+                be[name], be_agg[name] = dist.leg(lambda sync: measure_backend(traces[k], k, cpu=device, sync=sync,
+                                                                               **kw))
         e2e["backend"] = be
         agg["backend"] = be_agg
         e2e["aggregate"] = agg
@@ -1126,7 +1132,7 @@ def headline_line(detail, h, head, results, e2e):
                     for k, v in e2e.items() if k in ("M1500", "S64")}
         be = e2e.get("backend") or {}
         e2e_line["backend"] = {k: {"mpkts": round(v["mpkts"], 1), "dev_frac": v.get("device_roofline_frac")}
-                               for k, v in be.items()}
+                               for k, v in be.items() if k not in ("S64_group128", "M1500_group8")}
         # the job's end-to-end rates: every rank's legs at once, all frames over the longest wall
         ag = e2e.get("aggregate") or {}
         e2e_line["aggregate"] = {k: {kk: v[kk] for kk in ("ranks", "mpkts", "gbps", "per_rank_mpkts")}

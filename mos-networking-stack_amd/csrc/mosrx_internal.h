@@ -51,6 +51,14 @@ typedef struct mosrx_kparams {
 	                             * 0 = none.  Read by the SMALL tile's VAR_UNI kernels only */
 } mosrx_kparams;
 
+/* Launches of at most this many workgroups take the SMALL tile's hinted forms
+ * (VAR_UNI): one round of resident workgroups, latency-bound, where the
+ * descriptor -> window round trip is the launch's critical path (config #2's
+ * single 32K batch: 128 workgroups).  Larger launches keep the plain forms:
+ * with every slot busy the round trip is hidden, and the hinted form measured
+ * 1-2.5 % slower on the 64 B rings (profiles/r05/hint_ab). */
+#define MOSRX_UNI_MAX_TILES 2048u
+
 /* The uniform-layout hint of a batch (MOSRX_BATCH_UNIFORM, include/mosrx.h) in
  * the 32 bits a kernel argument / queue descriptor carries: 0 when the batch
  * has none or its first offset or stride does not fit 16 bits (the kernels

@@ -1490,7 +1490,8 @@ extern "C" int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles,
 		{QROW(MOSRX_KIND_SMALL, 0), QROW(MOSRX_KIND_S13, 0)}, {QROW(MOSRX_KIND_SMALL, VAR_UNI), QROW(MOSRX_KIND_S13, 0)}};
 #undef QROW
 	const int tv = (variant >> 1) & 1;
-	tab[qp->uni ? 1 : 0][kind][qp->tinfo == 1 ? 2 : qp->tinfo == 2 ? 3 + tv : tv](qp, total_tiles, s);
+	const int hinted = qp->uni && total_tiles <= MOSRX_UNI_MAX_TILES;
+	tab[hinted][kind][qp->tinfo == 1 ? 2 : qp->tinfo == 2 ? 3 + tv : tv](qp, total_tiles, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -1514,7 +1515,8 @@ extern "C" int mosrx_launch_classify(const mosrx_kparams *kp, int kind, int vari
 	            : (kp->flags & MOSRX_KF_COMPACT) ? 4 + tv : tv;
 	mosrx_kparams k = *kp;
 	k.flags &= ~(uint32_t)MOSRX_KF_COMPACT;
-	tab[k.uni ? 1 : 0][kind][v](&k, s);
+	const uint32_t tiles = (k.n + MOSRX_KIND_FRAMES(kind) - 1) / MOSRX_KIND_FRAMES(kind);
+	tab[k.uni && tiles <= MOSRX_UNI_MAX_TILES ? 1 : 0][kind][v](&k, s);
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 #endif   // __HIPCC_RTC__

@@ -88,8 +88,8 @@ def test_shard_plan():
 
 
 def _leg_worker(rank, world, port, out_dir):
-    """Each rank runs one end-to-end leg between barriers (bench.Dist.leg): rank r
-    moves (r + 1) * 1000 frames of 100 bytes in about 0.2 * (r + 1) s."""
+    """Each rank runs one end-to-end leg (bench.Dist.leg), its timed region between
+    barriers: rank r moves (r + 1) * 1000 frames of 100 bytes in about 0.2 * (r + 1) s."""
     import json
     import time
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -97,9 +97,14 @@ def _leg_worker(rank, world, port, out_dir):
     import bench
     d = bench.Dist(world, rank)
 
-    def fn():
+    def fn(sync):
+        time.sleep(0.3 * (1 - rank))          # set-up of different lengths: the timed regions still start together
+        sync()
+        t0 = time.perf_counter()
         time.sleep(0.2 * (rank + 1))
-        return {"frames": (rank + 1) * 1000, "bytes": (rank + 1) * 100_000}
+        dt = time.perf_counter() - t0
+        sync()
+        return {"frames": (rank + 1) * 1000, "bytes": (rank + 1) * 100_000, "seconds": dt}
     mine, agg = d.leg(fn)
     spread = d.gather([float(rank + 1), 10.0 * rank])
     with open(os.path.join(out_dir, f"leg{rank}.json"), "w") as fh:
@@ -120,7 +125,7 @@ def test_bench_leg_aggregate_over_ranks(tmp_path):
     assert outs[1]["agg"] == agg
     assert agg["ranks"] == 2 and agg["frames"] == 3000
     wall = agg["seconds"]
-    assert 0.4 <= wall < 1.5                                   # the slower rank's ~0.4 s (between barriers)
+    assert 0.4 <= wall < 0.7                                   # the slower rank's ~0.4 s timed region
     assert abs(agg["mpkts"] - 3000 / wall / 1e6) < 1e-2
     assert abs(agg["gbps"] - 300_000 / wall / 1e9) < 1e-2
     assert agg["per_rank_mpkts"]["min"] <= agg["per_rank_mpkts"]["max"]

@@ -785,7 +785,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     source replaying the trace — per group of batches: source -> pinned
     staging, H2D, ONE classify launch, D2H records, then the per-frame get_rptr
     + NETSTAT walk on the host, with the next group in flight while this one is
-    consumed.  The kernels are timed with HIP events (device time per batch);
+    consumed.  The kernels are timed by their dispatch-stamped durations (per batch);
     the host loop's rate is reported beside it.  Never the bench value."""
     ctx_batch = {"S64": 32_768, "M1500": 65_536, "IMIX": 262_144}[key]
     if group != 1:
@@ -835,7 +835,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
                       f"{'8-byte records (cfg.compact)' if compact and not bpf else '16-byte records'}"
                       f"{', ' + str(len(bpf)) + ' monitor filters installed: the fused classify + BPF queue kernel' if bpf else ''}), "
                       f"in-memory source replaying {tr.n} distinct frames; every batch crosses PCIe; device "
-                      f"time = HIP events around each kernel (its frames were just copied in)"}
+                      f"time = each kernel launch's dispatch-stamped duration (its frames were just copied in)"}
 
 
 def measure_backend_threads(key: str, nthreads: int, group: int, frames_per_thread: int, device: int):
@@ -1091,7 +1091,7 @@ def _compact_cpu(c):
     if not c:
         return None
     out = {k: c[k] for k in ("value", "unit", "cores", "kind", "mpkts") if k in c}
-    out["sample"] = c.get("sample", "")[:160]
+    out["sample"] = c.get("sample", "")[:120]
     return out
 
 
@@ -1110,7 +1110,7 @@ def headline_line(detail, h, head, results, e2e):
         for leg in ("mos_rx_loop_M1500", "mos_rx_loop_FW64", "mos_rx_loop_FW64_bare"):
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("processpacket_ns_per_frame", "gpu_records_ns_per_frame",
-                                                          "saved_ns_per_frame", "spread_ns")}
+                                                          "saved_ns_per_frame")}
     sec = {}
     for k, r in results.items():
         if k == head:
@@ -1122,10 +1122,8 @@ def headline_line(detail, h, head, results, e2e):
                       "cpu_ref_processpacket_mpkts": (cb.get("reference_processpacket") or {}).get("mpkts"),
                       "boundary_mpkts": round(r["e2e_boundary"]["mpkts"], 2)}
             continue
-        sec[k] = {"mpkts": round(r["mpkts"], 1), "launch_us": r["roofline"]["launch_us"],
-                  "frac": r["roofline"]["frac"]}   # (GB/s: the detail record)
-        if detail["n_gpus"] > 1:
-            sec[k]["per_rank_device_gbps"] = r["per_rank_device_gbps"]
+        # [Mpkt/s, launch us, roofline frac]; GB/s and the per-rank spread: the detail record
+        sec[k] = [round(r["mpkts"], 1), round(r["roofline"]["launch_us"], 2), round(r["roofline"]["frac"], 3)]
     e2e_line = None
     if e2e:
         e2e_line = {k: {"gbps": round(v["gbps"], 1), "mpkts": round(v["mpkts"], 1)}
@@ -1134,12 +1132,15 @@ def headline_line(detail, h, head, results, e2e):
         e2e_line["backend"] = {k: {"mpkts": round(v["mpkts"], 1), "dev_frac": v.get("device_roofline_frac")}
                                for k, v in be.items() if k not in ("S64_group128", "M1500_group8")}
         # the job's end-to-end rates: every rank's legs at once, all frames over the longest wall
-        ag = e2e.get("aggregate") or {}
-        e2e_line["aggregate"] = {k: {kk: v[kk] for kk in ("ranks", "mpkts", "gbps", "per_rank_mpkts")}
-                                 for k, v in ag.items() if k in ("M1500", "S64")}
-        e2e_line["aggregate"]["backend"] = {k: {kk: v[kk] for kk in ("mpkts", "per_rank_mpkts")}
-                                            for k, v in (ag.get("backend") or {}).items()
-                                            if k in ("M1500", "S64", "IMIX")}
+        # (at N = 1 the same as the rank's own)
+        ag = e2e.get("aggregate") if detail["n_gpus"] > 1 else None
+        ag = ag or {}
+        if ag:
+            e2e_line["aggregate"] = {k: {kk: v[kk] for kk in ("ranks", "mpkts", "gbps", "per_rank_mpkts")}
+                                     for k, v in ag.items() if k in ("M1500", "S64")}
+            e2e_line["aggregate"]["backend"] = {k: {kk: v[kk] for kk in ("mpkts", "per_rank_mpkts")}
+                                                for k, v in (ag.get("backend") or {}).items()
+                                                if k in ("M1500", "S64", "IMIX")}
         if e2e.get("consumer"):
             e2e_line["consumer"] = e2e["consumer"]
     return {
@@ -1165,6 +1166,7 @@ def headline_line(detail, h, head, results, e2e):
         "read_ceiling_gbps": detail["read_ceiling_gbps"],
         "frac_of_read_ceiling": detail["frac_of_read_ceiling"],
         "cpu_baseline": cpu_line,
+        "secondary_fields": "Mpkt/s, launch us, roofline frac",
         "secondary": sec,
         "e2e": e2e_line,
         "detail": "full record: stderr line '[bench-detail]' and --detail file",

@@ -292,9 +292,11 @@ int  mosrx_classify_host_group_submit_bpf(mosrx_ctx *c, int slot, const mosrx_ba
                                           mosrx_result *const *h_out, uint32_t *const *h_fhash,
                                           uint32_t *const *h_match);
 
-/* Kernel timing on the end-to-end path: with timing on, every submit records
- * HIP events around its kernel on the slot's stream, and after the wait
- * mosrx_last_kernel_ms gives that kernel's device time (-ENODATA if the last
+/* Kernel timing on the end-to-end path: with timing on, every submit's kernel
+ * launch carries a start / stop event pair its dispatch stamps (the kernel's
+ * own duration, as rocprofv3 reports it; events recorded around the two
+ * launches of a classify + BPF pair without the fused kernel), and after the
+ * wait mosrx_last_kernel_ms gives that device time (-ENODATA if the last
  * waited submit was not timed). */
 int  mosrx_set_timing(mosrx_ctx *c, int on);
 int  mosrx_last_kernel_ms(mosrx_ctx *c, float *ms);

@@ -68,6 +68,7 @@ struct stage {
 	uint32_t *match;          /* pinned, BPF match masks (a filter set installed) */
 	uint32_t *fh;             /* pinned, flow-table hashes (cfg.flowhash) */
 	uint32_t n, max_len;
+	uint32_t rec0;            /* its first record's index in the group's record arrays */
 	uint32_t stride;          /* frame i at off[0] + i * stride (a fixed-size packing), else 0: the layout hint */
 	uint64_t bytes;
 	int borrowed;             /* frames lent by the source: give them back when the group is recycled */
@@ -76,9 +77,11 @@ struct stage {
 	 * which side arrays the launch filled (pkt_info fields are not made in a
 	 * BPF pass) */
 	uint32_t msp, esp, gen, nprog, has_fh, has_ti;
-	int compact;              /* its records are mosrx_result8 (cfg.compact, no filters): res8 */
+	int compact;              /* its records are mosrx_result8 (cfg.compact, no filters): RES8 */
 };
-#define RES8(s) ((mosrx_result8 *)(s)->res)   /* a compact stage's records, in its 16-byte slots' place */
+/* A compact stage's records.  Set at submit (stage_records): a group's compact
+ * records are packed back to back in 8-byte slots, so they come back in one copy. */
+#define RES8(s) ((mosrx_result8 *)(s)->res)
 
 struct group {
 	uint8_t *blk;             /* pinned block the group's stages are packed into */
@@ -609,6 +612,7 @@ static void group_fill(struct if_state *is, struct group *g)
 		if (pos + need > g->blk_bytes || recs + g_cfg.batch > g->rec_cap)
 			break;
 		stage_fill(g, s, is->src, &pos);
+		s->rec0 = (uint32_t)recs;
 		s->res = g->res + recs;
 		s->ti = g->ti ? g->ti + recs : NULL;
 		s->match = g->match ? g->match + recs : NULL;
@@ -674,9 +678,12 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 	uint32_t i, nb = g->nst - first;
 	if (follow_mos_state(pv, is))
 		return -1;
+	const int compact = g_cfg.compact && !is->nprog;   /* filters keep 16-byte records (the fused kernels) */
 	for (i = first; i < g->nst; i++) {
 		struct stage *s = &g->st[i];
 		stage_batch(s, &b[i - first]);
+		/* the records' slots in the group's array: 8 or 16 bytes each, back to back */
+		s->res = compact ? (mosrx_result *)((mosrx_result8 *)g->res + s->rec0) : g->res + s->rec0;
 		out[i - first] = s->res;
 		out8[i - first] = RES8(s);
 		ti[i - first] = s->ti;
@@ -688,9 +695,9 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 		s->nprog = is->nprog;
 		s->has_fh = s->fh != NULL;
 		s->has_ti = s->ti != NULL && !is->nprog;
-		s->compact = g_cfg.compact && !is->nprog;
+		s->compact = compact;
 	}
-	if (g_cfg.compact && !is->nprog)   /* 8-byte records (filters keep 16-byte ones: the fused kernels) */
+	if (compact)
 		return mosrx_classify_host_group_submit_c8(is->mc, k, b, nb, out8, g_cfg.flowhash ? fh : NULL);
 	if (is->nprog)
 		return mosrx_classify_host_group_submit_bpf(is->mc, k, b, nb, out, g_cfg.flowhash ? fh : NULL, mt);
@@ -966,7 +973,7 @@ static int32_t set_bpf(struct gpu_priv *pv, struct if_state *is, const mosrx_bpf
 		if (!g->match && mosrx_host_alloc(is->mc, g->rec_cap * 4, (void **)&g->match))
 			return -1;
 		for (i = 0; i < g->nst; i++)
-			g->st[i].match = g->match + (g->st[i].res - g->res);
+			g->st[i].match = g->match + g->st[i].rec0;
 	}
 	is->nprog = a->nprog;
 	is->gen++;

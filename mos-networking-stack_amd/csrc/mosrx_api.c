@@ -647,8 +647,14 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 		HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
 	}
 	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_CNT_WORDS * 4, s->stream));
-	if (c->timing)
-		HIPCHK(hipEventRecord(s->kev0, s->stream));
+	if (c->timing) {
+		/* one launch: its dispatch stamps its own duration (no queueing gap before it);
+		 * the classify + BPF pair: events around both */
+		if (!h_match)
+			mosrx__stamp_next(s->kev0, s->kev1);
+		else
+			HIPCHK(hipEventRecord(s->kev0, s->stream));
+	}
 	if (h_match) {
 		mosrx_batch db = *b;
 		db.frames = dframes;
@@ -659,9 +665,10 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 		rc = launch(c, b, dframes, doff, dlen, s->d_res, s->d_cnt, h_fhash ? s->d_fh : NULL,
 		            h_ti ? s->d_ti : NULL, s->stream);
 	}
+	mosrx__stamp_next(NULL, NULL);
 	if (rc)
 		return rc;
-	if (c->timing)
+	if (c->timing && h_match)
 		HIPCHK(hipEventRecord(s->kev1, s->stream));
 	s->timed = c->timing;
 	HIPCHK(hipMemcpyAsync(h_out, s->d_res, (size_t)b->n * sizeof(mosrx_result), hipMemcpyDeviceToHost,
@@ -952,8 +959,15 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 	qp.tpb = tpb_ok ? tiles / nb : 0;
 	qp.tinfo = h_tcpinfo ? 1u : compact ? 2u : 0u;
 	qp.uni = (uint32_t)uni;
-	if (c->timing)
-		HIPCHK(hipEventRecord(s->kev0, s->stream));
+	if (c->timing) {
+		/* one launch (the queue kernel, fused or not): its dispatch stamps the
+		 * kernel's own duration -- events recorded around it would also count the
+		 * wait behind the other slot's kernel; the per-batch BPF fallback: events */
+		if (!h_match || fused)
+			mosrx__stamp_next(s->kev0, s->kev1);
+		else
+			HIPCHK(hipEventRecord(s->kev0, s->stream));
+	}
 	if (fused) {
 		if ((rc = mosrx__bpf_fused_queue_launch(c, &qp, tiles, kind == MOSRX_KIND_SMALL,
 		                                        mosrx__tail_variant(c, dev_bytes, ntot), s->stream)))
@@ -966,7 +980,8 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 			                                s->h_qdesc[i].len, b[i].n, s->d_match + pre, s->stream)))
 				return rc;
 	}
-	if (c->timing)
+	mosrx__stamp_next(NULL, NULL);   /* (a stamp pair no launch took is not left for the next one) */
+	if (c->timing && h_match && !fused)
 		HIPCHK(hipEventRecord(s->kev1, s->stream));
 	s->timed = c->timing;
 	/* results: one copy when the host buffers follow each other, else per batch */

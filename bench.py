@@ -779,7 +779,7 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int, sync=lambda: None):
 
 
 def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1, bpf=None,
-                    compact: bool = True, sync=lambda: None):
+                    compact: bool = True, sync=lambda: None, group_bytes: int = 0):
     """The drop-in boundary's own rate: mosrx_rx_loop (RunMainLoop's rx section,
     core.c:897-909) over gpu_module_func (io_module.h:63-78) fed by an in-memory
     source replaying the trace — per group of batches: source -> pinned
@@ -792,17 +792,17 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
         # a group's batches must be distinct frames: replaying one batch would let
         # the group's copy carry it once and the kernel re-read it from cache
         # (group 0 = the module's default, auto: as many batches per launch as are
-        # ready, up to MOSRX_GROUP_AUTO_BYTES of frames -- ~120 of 64 B, 2 of 1500 B; more
+        # ready, up to MOSRX_GROUP_AUTO_BYTES of frames -- ~240 of 64 B, 5 of 1500 B; more
         # distinct batches than a launch takes, so no launch holds the same frames twice)
-        nb = group or {"S64": 160, "M1500": 6, "IMIX": 6}[key]
+        nb = group or {"S64": 320, "M1500": 10, "IMIX": 12}[key]
         tr = mosrx.Trace({"S64": mosrx.TRACE_S64, "M1500": mosrx.TRACE_M1500,
                           "IMIX": mosrx.TRACE_IMIX}[key], ctx_batch * nb)
     loops = max(1, frames_target // tr.n)
     src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
     be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
-                          group=group, timing=True, bpf=bpf, compact=compact)
+                          group=group, timing=True, bpf=bpf, compact=compact, group_bytes=group_bytes)
     try:
-        be.run_loop(max_pkts=2 * ctx_batch * max(group, 128 if key == "S64" else 4))    # warm-up: staging sized, module loaded
+        be.run_loop(max_pkts=2 * ctx_batch * max(group, 256 if key == "S64" else 6))    # warm-up: staging sized, module loaded
         st0 = be.stats()
         sync()
         t0 = time.perf_counter()
@@ -962,16 +962,18 @@ def main():
         # configuration inside mOS: auto groups, 8-byte records (cfg.compact)
         # (frames through each leg: enough that the timed part holds several launches after the
         # warm-up's pipelined group -- an IMIX auto group is 3 batches of 100 MB)
-        target = {"S64": 32_000_000, "M1500": 2_000_000, "IMIX": 12_000_000}
+        target = {"S64": 64_000_000, "M1500": 3_000_000, "IMIX": 20_000_000}
         be, be_agg = {}, {}
         legs = [(k, dict(frames_target=target[k], group=0)) for k in ("M1500", "S64", "IMIX")]
-        legs += [("S64_rec16", dict(frames_target=32_000_000, group=0, compact=False)),   # 16-byte records
+        legs += [("S64_rec16", dict(frames_target=64_000_000, group=0, compact=False)),   # 16-byte records
                  ("S64_group1", dict(frames_target=16_000_000, group=1)),      # one launch per batch
+                 # auto groups of half the default bytes (256 MiB of frames per launch, round 4's default)
+                 ("S64_auto256", dict(frames_target=32_000_000, group=0, group_bytes=256 << 20)),
                  ("S64_group128", dict(frames_target=32_000_000, group=128)),
                  # 8 monitor filters installed (mtcp_bind_monitor_filter): auto groups through the
                  # fused classify + BPF queue kernel (16-byte records), as without filters
-                 ("S64_bpf", dict(frames_target=32_000_000, group=0, bpf=bpf_bench_programs())),
-                 ("IMIX_bpf", dict(frames_target=12_000_000, group=0, bpf=bpf_bench_programs())),
+                 ("S64_bpf", dict(frames_target=64_000_000, group=0, bpf=bpf_bench_programs())),
+                 ("IMIX_bpf", dict(frames_target=20_000_000, group=0, bpf=bpf_bench_programs())),
                  ("M1500_group1", dict(frames_target=2_000_000, group=1)),
                  ("M1500_group8", dict(frames_target=4_000_000, group=8))]
         for name, kw in legs:
@@ -1130,7 +1132,7 @@ def headline_line(detail, h, head, results, e2e):
                     for k, v in e2e.items() if k in ("M1500", "S64")}
         be = e2e.get("backend") or {}
         e2e_line["backend"] = {k: {"mpkts": round(v["mpkts"], 1), "dev_frac": v.get("device_roofline_frac")}
-                               for k, v in be.items() if k not in ("S64_group128", "M1500_group8")}
+                               for k, v in be.items() if k not in ("S64_group128", "M1500_group8", "S64_auto256")}
         # the job's end-to-end rates: every rank's legs at once, all frames over the longest wall
         # (at N = 1 the same as the rank's own)
         ag = e2e.get("aggregate") if detail["n_gpus"] > 1 else None

@@ -222,8 +222,11 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * unconfigured (its consumer, mos_rx.c, reads both). */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
-#define MOSRX_GROUP_AUTO_BYTES  (256ull << 20)   /* per pipeline slot; 64 B frames: ~120 batches of 32K
-                                                   * per launch, 1500 B: 2 of 64K */
+#define MOSRX_GROUP_AUTO_BYTES  (512ull << 20)   /* per pipeline slot; 64 B frames: ~240 batches of 32K
+                                                   * per launch, 1500 B: 5 of 64K.  Round 5: 256 MiB groups
+                                                   * of 64 B frames ran 0.43 us per batch on the device, 512
+                                                   * MiB ones 0.40 (the launch's ramp and drain spread
+                                                   * over twice the batches; profiles/r05/backend_groups) */
 
 void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg);
 int  mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg);

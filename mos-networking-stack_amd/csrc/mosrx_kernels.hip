@@ -640,7 +640,8 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 	// the fused BPF hook reads the window up to MOSRX_BPF_WEND
 	constexpr int NLOAD = (VAR & VAR_BPF) ? BPF_NLOAD(WEND) : WIN_NLOAD(WEND);
 	constexpr int RSS = (DBG & 16384) ? 1 : 0;   // probe builds: no Toeplitz (hdr_parse RSS form 1)
-	// DBG 2 skips the window loads, DBG 4 the record stores (probe builds only).  Tried and slower:
+	// DBG 2 skips the window loads, DBG 4 the record stores, DBG 256 fills the LDS
+	// tables once per workgroup behind a barrier (probe builds only).  Tried and slower:
 	// windows staged through LDS from contiguous wave loads (64 B config 192 vs
 	// 125 us per 8M frames).
 	__shared__ __attribute__((aligned(16))) uint32_t s_tab[MOSRX_TAB_WORDS];
@@ -718,8 +719,16 @@ __device__ __forceinline__ void classify_tile_small(const mosrx_kparams &kp, uin
 		ta = tg[lane];
 		tb = tg[lane + 64];
 	}
-	reinterpret_cast<u32x4 *>(s_tab)[lane] = ta;
-	reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = tb;
+	if constexpr ((DBG & 256) != 0 && TILE >= 256u) {
+		// probe builds: the workgroup fills the tables once (8 bytes per lane) and
+		// waits at a barrier, instead of each wave filling all of them itself
+		(void)ta; (void)tb;
+		reinterpret_cast<u32x2 *>(s_tab)[t] = reinterpret_cast<const u32x2 *>(kp.tables)[t];
+		__syncthreads();
+	} else {
+		reinterpret_cast<u32x4 *>(s_tab)[lane] = ta;
+		reinterpret_cast<u32x4 *>(s_tab)[lane + 64] = tb;
+	}
 	if (kp.counters) {                        // uniform: the whole workgroup takes this barrier or none
 		if (t <= MOSRX_R_COUNT)
 			s_cnt[t] = 0;

@@ -62,6 +62,19 @@ int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx,
 			    ((iom->dev_ioctl(ctx, rx_inf, MOSRX_PKT_RX_RESULTS, &res) || !res) &&
 			     (iom->dev_ioctl(ctx, rx_inf, MOSRX_PKT_RX_RESULTS8, &res8) || !res8)))
 				return -ENOTSUP;
+			if (!res && !fn) {          /* 8-byte records, nothing to hand them to: the census only */
+				for (i = 0; i < recv_cnt; i++) {
+					uint16_t len = 0;
+					if (!iom->get_rptr(ctx, rx_inf, i, &len))
+						return -EIO;
+					st->rx_packets++;
+					st->rx_bytes += (uint64_t)len + ETHER_OVR;
+					st->rx_errors += res8[i].verdict < 0;
+					if (res8[i].reason < MOSRX_R_COUNT)
+						st->by_reason[res8[i].reason]++;
+				}
+				continue;
+			}
 			memset(&one, 0, sizeof(one));
 			for (i = 0; i < recv_cnt; i++) {
 				uint16_t len = 0;

@@ -950,7 +950,8 @@ class GpuBackend:
     def __init__(self, sources: list[int], params: Params | None = None, batch: int = 32768,
                  max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
                  ngpu: int = 1, bpf=None, group: int = 1, tcpinfo: bool = False, tx_batch: int = 64,
-                 timing: bool = False, flowhash: bool = False, tx_csum: bool = False, compact: bool = False):
+                 timing: bool = False, flowhash: bool = False, tx_csum: bool = False, compact: bool = False,
+                 group_bytes: int = 0):
         cfg = ModuleCfg()
         lib().mosrx_gpu_module_cfg_default(C.byref(cfg))
         cfg.num_ifs = len(sources)
@@ -962,6 +963,7 @@ class GpuBackend:
         cfg.group, cfg.tcpinfo, cfg.tx_batch, cfg.flowhash = group, int(tcpinfo), tx_batch, int(flowhash)
         cfg.tx_csum = int(tx_csum)
         cfg.compact = int(compact)          # 8-byte records (results8); 16-byte ones with filters
+        cfg.group_bytes = group_bytes       # auto groups' frame bytes per launch (0: MOSRX_GROUP_AUTO_BYTES)
         if params is not None:
             cfg.params = params
         self.params = Params.from_buffer_copy(cfg.params)

@@ -444,6 +444,8 @@ int main(int argc, char **argv)
 	cfg.tx_csum = getenv("MOSAPP_TX_CSUM") ? atoi(getenv("MOSAPP_TX_CSUM")) : 0;
 	/* 8-byte records (what an unconfigured mOS build of the module uses), or 16-byte ones */
 	cfg.compact = getenv("MOSAPP_COMPACT") ? atoi(getenv("MOSAPP_COMPACT")) : 1;
+	/* the harness's traces are small: 64 MiB auto groups (pinned twice) instead of the default */
+	cfg.group_bytes = getenv("MOSAPP_GROUP_BYTES") ? strtoull(getenv("MOSAPP_GROUP_BYTES"), NULL, 10) : 64ull << 20;
 	cfg.params.num_queues = nq;
 	cfg.params.queue_mode = qmode;
 	cfg.params.num_msp = 0;                       /* followed from mOS's manager (mos_state) */

@@ -194,8 +194,8 @@ def algo_bytes(tr: mosrx.Trace, key: str = "") -> int:
         return tr.caplen_sum + tr.n * (DESC_BYTES + 4)
     if key.endswith("_txc"):       # the 8-byte check record per frame
         return tr.caplen_sum + tr.n * (DESC_BYTES + 8)
-    if "_cls_bpf" in key:          # the classify bytes + the 4-byte match mask
-        return tr.caplen_sum + tr.n * (DESC_BYTES + RESULT_BYTES + 4)
+    if "_cls_bpf" in key:          # the classify bytes + the 4-byte match mask (8-byte records: _c8)
+        return tr.caplen_sum + tr.n * (DESC_BYTES + (8 if key.endswith("_c8") else RESULT_BYTES) + 4)
     if key in COMPACT:                         # 8-byte compact records
         return tr.caplen_sum + tr.n * (DESC_BYTES + 8)
     if key.endswith("_bpf"):
@@ -818,13 +818,13 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     kms = st1.kernel_ms - st0.kernel_ms
     batches = st1.rx_batches - st0.rx_batches
     dev_us = 1e3 * kms / max(batches, 1)
-    # records: 16 bytes with filters (the fused kernels), 8 in compact mode, else 16
-    akey = "_cls_bpf" if bpf else "c8" if compact else ""
+    # records: 8 bytes in compact mode (the module's configuration inside mOS), filters or not
+    akey = ("_cls_bpf" if bpf else "") + ("_c8" if compact else "") if bpf else "c8" if compact else ""
     ab = algo_bytes(tr, akey) * (ctx_batch / tr.n)
     return {"mpkts": n / dt / 1e6, "gbps": nb * algo_bytes(tr, akey) / dt / 1e9, "frames": n,
             "bytes": int(nb * algo_bytes(tr, akey)),
             "seconds": dt, "filters": len(bpf) if bpf else 0,
-            "records": 16 if (bpf or not compact) else 8,
+            "records": 8 if compact else 16,
             "distinct_frames": tr.n,
             "group": group if group else "auto", "batches_per_launch": round(batches / max(launches, 1), 2),
             "kernel_launches": int(launches), "batches": int(batches),
@@ -832,7 +832,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
             "device_roofline_frac": round(ab / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if dev_us > 0 else None,
             "method": f"mosrx_rx_loop over gpu_module_func (pipelined, "
                       f"{group if group else 'auto (MOSRX_GROUP_AUTO)'} batch(es) per launch, "
-                      f"{'8-byte records (cfg.compact)' if compact and not bpf else '16-byte records'}"
+                      f"{'8-byte records (cfg.compact)' if compact else '16-byte records'}"
                       f"{', ' + str(len(bpf)) + ' monitor filters installed: the fused classify + BPF queue kernel' if bpf else ''}), "
                       f"in-memory source replaying {tr.n} distinct frames; every batch crosses PCIe; device "
                       f"time = each kernel launch's dispatch-stamped duration (its frames were just copied in)"}

@@ -225,7 +225,7 @@ void mosrx_queue_destroy(mosrx_ctx *c, mosrx_queue *q);
  * installed when the queue runs -- one launch of the fused classify + BPF
  * queue kernel when the set has its compiled form, else the classify launch
  * followed by the set's kernel per batch (same results).  Compact records go
- * with neither side array (-EINVAL). */
+ * with both side arrays (the fused kernels have 8-byte forms). */
 enum { MOSRX_QUEUE_COMPACT = 1 };
 int  mosrx_queue_create_ex(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, void *const *d_out,
                            uint32_t *const *d_fhash, uint32_t *const *d_match, int flags, mosrx_queue **q);
@@ -282,6 +282,13 @@ int  mosrx_classify_host_group_submit_ex(mosrx_ctx *c, int slot, const mosrx_bat
  * takes pkt_info's lengths from the header, tcp.c:258-270). */
 int  mosrx_classify_host_group_submit_c8(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
                                          mosrx_result8 *const *h_out8, uint32_t *const *h_fhash);
+/* The same with a BPF set installed: 8-byte records, the flow hashes (NULL:
+ * none) and the set's match masks, from one launch of the fused kernel's
+ * 8-byte form (or the classify launch + the set per batch while the set has
+ * no compiled form). */
+int  mosrx_classify_host_group_submit_bpf_c8(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                             mosrx_result8 *const *h_out8, uint32_t *const *h_fhash,
+                                             uint32_t *const *h_match);
 /* The same for a context with a BPF set installed: the records, the flow
  * hashes (h_fhash, NULL: none) and the set's match masks into h_match[i] from
  * ONE launch of the fused classify + BPF queue kernel (the set's compiled

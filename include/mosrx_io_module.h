@@ -215,11 +215,11 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * verdict, tcp_flags; dev_ioctl(MOSRX_PKT_RX_RESULTS8)),
 	                                                 * written and copied back at half the bytes; the consumer
 	                                                 * takes pkt_info's lengths from the header as
-	                                                 * FillPacketContextTCPInfo does (tcp.c:258-270).  Batches
-	                                                 * classified with BPF filters keep 16-byte records (the
-	                                                 * batch's mosrx_rx_state.rec_bytes says which).  Not with
-	                                                 * tcpinfo.  Default 0 standalone, 1 in an mOS build left
-	                                                 * unconfigured (its consumer, mos_rx.c, reads both). */
+	                                                 * FillPacketContextTCPInfo does (tcp.c:258-270); with BPF
+	                                                 * filters too (the fused kernels' 8-byte forms).  A batch's
+	                                                 * mosrx_rx_state.rec_bytes says which form it has.  Not
+	                                                 * with tcpinfo.  Default 0 standalone, 1 in an mOS build
+	                                                 * left unconfigured (its consumer, mos_rx.c, reads both). */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
 #define MOSRX_GROUP_AUTO_BYTES  (512ull << 20)   /* per pipeline slot; 64 B frames: ~240 batches of 32K

@@ -819,11 +819,22 @@ static const char k_fused_main[] =
 	"{ queue_tile<MOSRX_KIND_S13, VAR_BPF>(desc, tpb, nb, qp); }\n"
 	"extern \"C\" __global__ WGM void mosrx_classify_bpf_queue_small(const mosrx_qdesc *desc, uint32_t tpb, uint32_t nb,\n"
 	"    mosrx_qparams qp)\n"
-	"{ queue_tile<MOSRX_KIND_SMALL, 2 | VAR_BPF>(desc, tpb, nb, qp); }\n";
+	"{ queue_tile<MOSRX_KIND_SMALL, 2 | VAR_BPF>(desc, tpb, nb, qp); }\n"
+	/* the same three queue forms with 8-byte records (gpu_module_func cfg.compact with filters) */
+	"extern \"C\" __global__ WGS void mosrx_classify_bpf_queue_stream_c8(const mosrx_qdesc *desc, uint32_t tpb,\n"
+	"    uint32_t nb, mosrx_qparams qp)\n"
+	"{ queue_tile<MOSRX_KIND_S13, 2 | VAR_BPF | VAR_C8>(desc, tpb, nb, qp); }\n"
+	"extern \"C\" __global__ WGS void mosrx_classify_bpf_queue_stream_rt_c8(const mosrx_qdesc *desc, uint32_t tpb,\n"
+	"    uint32_t nb, mosrx_qparams qp)\n"
+	"{ queue_tile<MOSRX_KIND_S13, VAR_BPF | VAR_C8>(desc, tpb, nb, qp); }\n"
+	"extern \"C\" __global__ WGM void mosrx_classify_bpf_queue_small_c8(const mosrx_qdesc *desc, uint32_t tpb,\n"
+	"    uint32_t nb, mosrx_qparams qp)\n"
+	"{ queue_tile<MOSRX_KIND_SMALL, 2 | VAR_BPF | VAR_C8>(desc, tpb, nb, qp); }\n";
 
 static const char *const k_fused_names[MOSRX_BPF_NFUSED] = {
 	"mosrx_classify_bpf_stream", "mosrx_classify_bpf_stream_rt", "mosrx_classify_bpf_small",
-	"mosrx_classify_bpf_queue_stream", "mosrx_classify_bpf_queue_stream_rt", "mosrx_classify_bpf_queue_small"};
+	"mosrx_classify_bpf_queue_stream", "mosrx_classify_bpf_queue_stream_rt", "mosrx_classify_bpf_queue_small",
+	"mosrx_classify_bpf_queue_stream_c8", "mosrx_classify_bpf_queue_stream_rt_c8", "mosrx_classify_bpf_queue_small_c8"};
 
 /* The header window a fused set needs: every constant-offset load at frame
  * bytes [k, k + 8) with k >= 2 -- and every indexed load at its speculated
@@ -1411,8 +1422,9 @@ int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hi
 int mosrx__bpf_fused_queue_launch(mosrx_ctx *c, const mosrx_qparams *qp, uint32_t total_tiles, int small,
                                   int variant, hipStream_t s)
 {
-	hipFunction_t f = small ? c->bpf_fu[FU_QM] : !(variant & 2) && c->bpf_fu[FU_QSR] ? c->bpf_fu[FU_QSR]
-	                                                                                : c->bpf_fu[FU_QS];
+	const int c8 = qp->tinfo == 2 ? FU_QS8 - FU_QS : 0;   /* 8-byte records: the _c8 forms */
+	hipFunction_t f = small ? c->bpf_fu[FU_QM + c8]
+	                        : !(variant & 2) && c->bpf_fu[FU_QSR + c8] ? c->bpf_fu[FU_QSR + c8] : c->bpf_fu[FU_QS + c8];
 	const unsigned threads = small ? 256u : 64u * (1u + MOSRX_STREAMERS);
 	const mosrx_qdesc *desc = qp->desc;
 	uint32_t tpb = qp->tpb, nb = qp->nb;

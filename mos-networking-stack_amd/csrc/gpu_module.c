@@ -77,7 +77,7 @@ struct stage {
 	 * which side arrays the launch filled (pkt_info fields are not made in a
 	 * BPF pass) */
 	uint32_t msp, esp, gen, nprog, has_fh, has_ti;
-	int compact;              /* its records are mosrx_result8 (cfg.compact, no filters): RES8 */
+	int compact;              /* its records are mosrx_result8 (cfg.compact): RES8 */
 };
 /* A compact stage's records.  Set at submit (stage_records): a group's compact
  * records are packed back to back in 8-byte slots, so they come back in one copy. */
@@ -678,7 +678,7 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 	uint32_t i, nb = g->nst - first;
 	if (follow_mos_state(pv, is))
 		return -1;
-	const int compact = g_cfg.compact && !is->nprog;   /* filters keep 16-byte records (the fused kernels) */
+	const int compact = g_cfg.compact;
 	for (i = first; i < g->nst; i++) {
 		struct stage *s = &g->st[i];
 		stage_batch(s, &b[i - first]);
@@ -697,6 +697,8 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 		s->has_ti = s->ti != NULL && !is->nprog;
 		s->compact = compact;
 	}
+	if (compact && is->nprog)   /* 8-byte records + the set's masks: the fused kernel's 8-byte form */
+		return mosrx_classify_host_group_submit_bpf_c8(is->mc, k, b, nb, out8, g_cfg.flowhash ? fh : NULL, mt);
 	if (compact)
 		return mosrx_classify_host_group_submit_c8(is->mc, k, b, nb, out8, g_cfg.flowhash ? fh : NULL);
 	if (is->nprog)

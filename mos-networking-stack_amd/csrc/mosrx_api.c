@@ -873,7 +873,7 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
                         mosrx_tcpinfo *const *h_tcpinfo, uint32_t *const *h_fhash, uint32_t *const *h_match,
                         int compact)
 {
-	/* compact: h_out[i] are mosrx_result8 arrays (8-byte records, VAR_C8); flow hashes, no pkt_info */
+	/* compact: h_out[i] are mosrx_result8 arrays (8-byte records, VAR_C8); flow hashes and masks, no pkt_info */
 	const size_t rsz = compact ? sizeof(mosrx_result8) : sizeof(mosrx_result);
 	struct region r[3 * MOSRX_MAX_GROUP];
 	uint32_t i, nr = 0, tiles = 0, maxl = 0, ntot = 0, tile;
@@ -883,7 +883,7 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 	int rc, unknown = 0, kind, tpb_ok = 1;
 	int fused = 0, uni = 0;
 	if (!c || slot < 0 || slot >= NSLOT || !b || !h_out || nb == 0 || nb > MOSRX_MAX_GROUP ||
-	    (h_match && h_tcpinfo) || (compact && (h_match || h_tcpinfo)))
+	    (h_match && h_tcpinfo) || (compact && h_tcpinfo))
 		return -EINVAL;
 	s = &c->slot[slot];
 	if (s->busy)
@@ -922,7 +922,8 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 	tile = MOSRX_KIND_FRAMES(kind);
 	if (h_match) {
 		mosrx__bpf_poll(c);   /* the set's compiled kernels, once its compile is in */
-		fused = c->bpf_fu[FU_QS] && c->bpf_fu[FU_QM] && (kind == MOSRX_KIND_SMALL || kind == MOSRX_KIND_S13);
+		fused = (compact ? c->bpf_fu[FU_QS8] && c->bpf_fu[FU_QM8] : c->bpf_fu[FU_QS] && c->bpf_fu[FU_QM]) &&
+		        (kind == MOSRX_KIND_SMALL || kind == MOSRX_KIND_S13);
 	}
 	for (i = 0, nr = 0; i < nb; i++) {
 		mosrx_qdesc *d = &s->h_qdesc[i];
@@ -1025,6 +1026,15 @@ int mosrx_classify_host_group_submit_c8(mosrx_ctx *c, int slot, const mosrx_batc
                                         mosrx_result8 *const *h_out8, uint32_t *const *h_fhash)
 {
 	return group_submit(c, slot, b, nb, (mosrx_result *const *)h_out8, NULL, h_fhash, NULL, 1);
+}
+
+int mosrx_classify_host_group_submit_bpf_c8(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
+                                            mosrx_result8 *const *h_out8, uint32_t *const *h_fhash,
+                                            uint32_t *const *h_match)
+{
+	if (!h_match)
+		return -EINVAL;
+	return group_submit(c, slot, b, nb, (mosrx_result *const *)h_out8, NULL, h_fhash, h_match, 1);
 }
 
 int mosrx_classify_host_group_submit_bpf(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
@@ -1595,7 +1605,7 @@ int mosrx_queue_create_ex(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, void 
 	uint64_t bytes = 0, frames = 0;
 	const int compact = (flags & MOSRX_QUEUE_COMPACT) != 0;
 	int rc, unknown = 0, kind;
-	if (!c || !b || !d_out || !q || nb == 0 || (flags & ~MOSRX_QUEUE_COMPACT) || (compact && (d_fhash || d_match)))
+	if (!c || !b || !d_out || !q || nb == 0 || (flags & ~MOSRX_QUEUE_COMPACT))
 		return -EINVAL;
 	*q = NULL;
 	for (i = 0; i < nb; i++) {
@@ -1692,7 +1702,7 @@ int mosrx_queue_run(mosrx_ctx *c, const mosrx_queue *q, void *stream)
 	if (!q->match)
 		return mosrx_launch_queue(&qp, q->total_tiles, q->tile, variant, s);
 	mosrx__bpf_poll(c);
-	if (c->bpf_fu[FU_QS] && c->bpf_fu[FU_QM])
+	if (q->compact ? c->bpf_fu[FU_QS8] && c->bpf_fu[FU_QM8] : c->bpf_fu[FU_QS] && c->bpf_fu[FU_QM])
 		return mosrx__bpf_fused_queue_launch(c, &qp, q->total_tiles, q->tile == MOSRX_KIND_SMALL, variant, s);
 	if ((rc = mosrx_launch_queue(&qp, q->total_tiles, q->tile, variant, s)))
 		return rc;

@@ -17,9 +17,9 @@
 
 /* The fused classify + BPF kernels of a compiled set (bpf_jit.c k_fused_main):
  * one batch as the stream tile (non-temporal / cached tails) or the SMALL tile,
- * and the same three over a batch queue. */
-#define MOSRX_BPF_NFUSED 6
-enum { FU_S = 0, FU_SR = 1, FU_M = 2, FU_QS = 3, FU_QSR = 4, FU_QM = 5 };
+ * the same three over a batch queue, and those three with 8-byte records. */
+#define MOSRX_BPF_NFUSED 9
+enum { FU_S = 0, FU_SR = 1, FU_M = 2, FU_QS = 3, FU_QSR = 4, FU_QM = 5, FU_QS8 = 6, FU_QSR8 = 7, FU_QM8 = 8 };
 struct mosrx_jit_entry {
 	uint64_t key;                          /* set_hash of the set */
 	hipModule_t mod, fmod;

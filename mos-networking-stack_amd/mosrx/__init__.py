@@ -288,6 +288,9 @@ def lib():
                                           C.POINTER(P)]),
             "mosrx_classify_host_group_submit_bpf": (I, [P, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P),
                                                          C.POINTER(P)]),
+            "mosrx_classify_host_group_submit_c8": (I, [P, I, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
+            "mosrx_classify_host_group_submit_bpf_c8": (I, [P, I, C.POINTER(Batch), U32, C.POINTER(P),
+                                                            C.POINTER(P), C.POINTER(P)]),
             "mosrx_host_register": (I, [P, P, C.c_size_t, I]),
             "mosrx_host_unregister": (I, [P, P]),
             "mosrx_pci_numa_node": (I, [C.c_char_p]),
@@ -729,6 +732,22 @@ class Context:
         m = (C.c_void_p * n)(*match)
         _chk(lib().mosrx_classify_host_group_submit_bpf(self.handle, slot, bs, n, o, f, m),
              "mosrx_classify_host_group_submit_bpf")
+
+    def group_submit_c8(self, slot: int, batches: list, outs8: list, fhash: list | None = None,
+                        match: list | None = None) -> None:
+        """mosrx_classify_host_group_submit_c8 (match None) or _bpf_c8: 8-byte records
+        into outs8 (host pointers), flow hashes and the installed set's masks."""
+        n = len(batches)
+        bs = (Batch * n)(*batches)
+        o = (C.c_void_p * n)(*outs8)
+        f = (C.c_void_p * n)(*fhash) if fhash is not None else None
+        if match is None:
+            _chk(lib().mosrx_classify_host_group_submit_c8(self.handle, slot, bs, n, o, f),
+                 "mosrx_classify_host_group_submit_c8")
+        else:
+            m = (C.c_void_p * n)(*match)
+            _chk(lib().mosrx_classify_host_group_submit_bpf_c8(self.handle, slot, bs, n, o, f, m),
+                 "mosrx_classify_host_group_submit_bpf_c8")
 
     def group_wait(self, slot: int) -> None:
         _chk(lib().mosrx_classify_host_wait(self.handle, slot), "mosrx_classify_host_wait")

@@ -169,6 +169,18 @@ int __wrap_mosrx_classify_host_group_submit_c8(mosrx_ctx *mc, int slot, const mo
 	return rc;
 }
 
+int __wrap_mosrx_classify_host_group_submit_bpf_c8(mosrx_ctx *mc, int slot, const mosrx_batch *b, uint32_t nb,
+                                                   mosrx_result8 *const *out8, uint32_t *const *fh,
+                                                   uint32_t *const *match)
+{
+	struct emul_ctx *c = (struct emul_ctx *)mc;
+	uint32_t i;
+	int rc = __wrap_mosrx_classify_host_group_submit_c8(mc, slot, b, nb, out8, fh);
+	for (i = 0; i < nb && !rc; i++)
+		rc = mo_bpf_eval(c->progs, c->nprog, b[i].frames, b[i].frames_bytes, b[i].off, b[i].len, b[i].n, match[i]);
+	return rc;
+}
+
 int __wrap_mosrx_classify_bpf_host_submit(mosrx_ctx *mc, int slot, const mosrx_batch *b, mosrx_result *out,
                                           uint32_t *match)
 {

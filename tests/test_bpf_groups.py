@@ -277,3 +277,86 @@ def test_compact_records_golden(gpu_ctx):
         db.free()
         assert np.array_equal(got.view(np.uint8), project8(O.classify(frames, off, ln, op)).view(np.uint8))
     gpu_ctx.set_params(mosrx.default_params())
+
+
+@pytest.mark.parametrize("kind,n,nb", [(mosrx.TRACE_IMIX, 40_000, 5), (mosrx.TRACE_S64, 65_536, 8)])
+@pytest.mark.parametrize("mode", ["fused", "interp", "nofilter"])
+def test_group_submit_c8(gpu_ctx, kind, n, nb, mode):
+    """mosrx_classify_host_group_submit_c8 / _bpf_c8: a group's 8-byte records, flow
+    hashes and (with a set) masks from one launch (the fused kernel's 8-byte form)
+    or the classify launch + the interpreter per batch, equal to the oracle."""
+    z, progs = load()
+    ps = program_sets(z, progs)[0][0][:8]
+    t = mosrx.Trace(kind, n, nflows=2000, seed=5)
+    gpu_ctx.set_params(mosrx.default_params())
+    gpu_ctx.bpf_set_engine(mosrx.BPF_ENGINE_INTERP if mode == "interp" else mosrx.BPF_ENGINE_JIT)
+    try:
+        if mode != "nofilter":
+            _set(gpu_ctx, ps)
+            assert gpu_ctx.bpf_fused() == (mode == "fused"), gpu_ctx.bpf_jit_log()
+        batches, parts, base = _host_group(gpu_ctx, t, nb)
+        recs = [np.zeros(b.n, mosrx.RESULT8_DTYPE) for b in batches]
+        fhs = [np.zeros(b.n, np.uint32) for b in batches]
+        mts = [np.full(b.n, 0xDEADBEEF, np.uint32) for b in batches]
+        gpu_ctx.group_submit_c8(0, batches, [r.ctypes.data for r in recs], [f.ctypes.data for f in fhs],
+                                None if mode == "nofilter" else [m.ctypes.data for m in mts])
+        gpu_ctx.group_wait(0)
+        for i, (fr, o, ln, fb) in enumerate(parts):
+            orec, ofh = O.classify_fh(fr[:fb], o, ln, O.params())
+            assert np.array_equal(recs[i].view(np.uint8), project8(orec).view(np.uint8)), f"batch {i}"
+            np.testing.assert_array_equal(fhs[i], ofh)
+            if mode != "nofilter":
+                np.testing.assert_array_equal(mts[i], O.bpf_eval(ps, fr[:fb], o, ln))
+        gpu_ctx.host_free(base)
+    finally:
+        gpu_ctx.bpf_set_async([])
+        gpu_ctx.bpf_set_engine(mosrx.BPF_ENGINE_JIT)
+
+
+def test_queue_compact_with_masks_and_hashes(gpu_ctx):
+    """A resident queue with 8-byte records, flow hashes and masks (ABI 3 lifts
+    the compact queue's side-array restriction)."""
+    z, progs = load()
+    gpu_ctx.set_params(mosrx.default_params())
+    trs = [mosrx.Trace(mosrx.TRACE_IMIX, 30_000, nflows=1500, seed=s) for s in (1, 2)]
+    dbs = [gpu_ctx.upload(t.frames, t.off, t.len, frames_bytes=t.frames_bytes, max_len=t.max_len) for t in trs]
+    q = gpu_ctx.queue_ex(dbs, flow_hash=True, match=True, compact=True)
+    try:
+        ps = program_sets(z, progs)[0][0][:8]
+        _set(gpu_ctx, ps)
+        q.run()
+        for t, d in zip(trs, dbs):
+            orec, ofh = O.classify_fh(t.frames[:t.frames_bytes], t.off, t.len, O.params())
+            assert np.array_equal(d.results8().view(np.uint8), project8(orec).view(np.uint8))
+            np.testing.assert_array_equal(d.flow_hashes(), ofh)
+            np.testing.assert_array_equal(d.matches(), O.bpf_eval(ps, t.frames[:t.frames_bytes], t.off, t.len))
+    finally:
+        q.destroy()
+        gpu_ctx.bpf_set_async([])
+        for d in dbs:
+            d.free()
+
+
+@pytest.mark.parametrize("group", [0, 3])
+def test_backend_compact_with_filters(group):
+    """gpu_module_func with cfg.compact and monitor filters: 8-byte records, masks
+    and flow hashes per batch through dev_ioctl, equal to the oracle."""
+    z, progs = load()
+    ps = program_sets(z, progs)[0][0][:8]
+    t = mosrx.Trace(mosrx.TRACE_IMIX, 24_000, nflows=800, seed=3)
+    ora, ofh = O.classify_fh(t.frames, t.off, t.len, O.params())
+    om = O.bpf_eval(ps, t.frames[:t.frames_bytes], t.off, t.len)
+    src = mosrx.mem_source(t.frames, t.off, t.len, loops=1)
+    be = mosrx.GpuBackend([src], batch=2000, pipeline=True, cpu=8, bpf=ps, group=group, flowhash=True,
+                          compact=True)
+    try:
+        seen = 0
+        while (n := be.recv_pkts(0)) > 0:
+            got = be.results8(0, n)
+            assert np.array_equal(got.view(np.uint8), project8(ora[seen:seen + n]).view(np.uint8)), f"@{seen}"
+            np.testing.assert_array_equal(be.matches(0, n), om[seen:seen + n])
+            np.testing.assert_array_equal(be.fhashes(0, n), ofh[seen:seen + n])
+            seen += n
+        assert seen == t.n
+    finally:
+        be.close()

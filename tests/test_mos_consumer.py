@@ -257,12 +257,9 @@ def test_patched_build_calls_mos_own_stream_functions():
 def _check_scenario(name, pp, gpu, form="c8"):
     """What each scenario must have exercised (so a scenario cannot pass vacuously)."""
     st, cb = gpu["stats"], pp["callbacks"]
-    # the record form the consumer read: 8-byte records for every batch classified
-    # without filters in the compact forms, none in the 16-byte one
-    if form == "rec16":
-        assert st["batches_c8"] == 0
-    elif not any(k in SCENARIOS[name]["env"] for k in ("MOSAPP_RAW", "MOSAPP_SYN", "MOSAPP_ORPHAN")):
-        assert st["batches_c8"] > 0
+    # the record form the consumer read: 8-byte records in the compact forms (with
+    # filters too: the fused kernels' 8-byte forms), none in the 16-byte one
+    assert (st["batches_c8"] == 0) if form == "rec16" else (st["batches_c8"] > 0)
     nstat = pp["state"].splitlines()[-1].split()
     assert int(nstat[6]) > 0                                   # rx_errors: bad checksums etc. were seen
     if name in ("monitor_fwd", "filters", "two_monitors_raw", "listener", "late_filter", "batch_1_per_launch",

@@ -30,7 +30,7 @@ ab = bench.algo_bytes(tr, key) * (ring or 1)
 if ring:   # the queues bench.measure builds for the row
     if "_cls_bpf" in key:
         ctx.bpf_set(bench.bpf_bench_programs())
-    qs = [ctx.queue_ex(dbs[i:i + ring], match="_cls_bpf" in key, compact=key in ("S64_hdr", "S64_hdr_packed"))
+    qs = [ctx.queue_ex(dbs[i:i + ring], match="_cls_bpf" in key, compact=key in bench.COMPACT)
           for i in range(0, len(dbs), ring)]
     _, avg = qs[0].time(iters, qs[1:])
     for q in qs:

@@ -65,6 +65,10 @@ WORKLOADS = {
     # rows' only traffic beyond the algorithmic bytes (diagnostic row)
     "S64_hdr_packed": (mosrx.TRACE_S64, 32_768, 256, "config #2 header-only, 8-byte records, frames packed back to "
                                                      "back (60 B stride)"),
+    # the full verdict with 8-byte records on the layout the drop-in backend stages small
+    # frames in (back to back, mosrx_source_fill)
+    "S64_c8_packed": (mosrx.TRACE_S64, 32_768, 256, "config #2 full verdict, 8-byte records, frames packed back "
+                                                    "to back as the backend stages them (60 B stride)"),
     "IMIX": (mosrx.TRACE_IMIX, 262_144, 8, "IMIX 60/590/1514 7:4:1, 1M flows, batch=256K (BASELINE config #4)"),
     # one kernel launch per batch, two batches in flight (two rx queues)
     "M1500_1": (mosrx.TRACE_M1500, 65_536, 0, "config #3, one launch per 64K batch"),
@@ -84,7 +88,7 @@ WORKLOADS = {
     "S64_cls_bpf_ring": (mosrx.TRACE_S64, 32_768, 256, "config #2 classify + 8 BPF programs fused, one batch-queue "
                                                        "launch over 256 batches"),
 }
-DEFAULT_WORKLOADS = ("M1500,S64,S64_c8,S64_hdr,S64_hdr16,S64_hdr_packed,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,"
+DEFAULT_WORKLOADS = ("M1500,S64,S64_c8,S64_c8_packed,S64_hdr,S64_hdr16,S64_hdr_packed,IMIX,M1500_1,S64_1,IMIX_1,M1500_fh,M1500_ti,"
                      "M1500_tx,M1500_txc,IMIX_bpf,IMIX_cls_bpf,IMIX_cls_bpf_ring,S64_cls_bpf_ring")
 OPS = {"M1500_fh": mosrx.OP_CLASSIFY_FH, "M1500_ti": mosrx.OP_CLASSIFY_TI, "M1500_tx": mosrx.OP_TX_CSUM,
        "M1500_txc": mosrx.OP_TX_CHECKS,
@@ -94,7 +98,7 @@ BPF_BENCH = [("tcp", 0), ("tcp port 80", 0), ("tcp[tcpflags] & tcp-syn != 0", 1)
              ("host 10.0.0.1 and port 80", 0), ("ip[8] < 64", 1), ("tcp[((tcp[12:1] & 0xf0) >> 2):4] = 0x47455420", 1),
              ("portrange 1000-2000", 0)]
 # rows whose records are the 8-byte mosrx_result8 (the drop-in path's compact form)
-COMPACT = ("S64_hdr", "S64_hdr_packed", "S64_c8", "c8")
+COMPACT = ("S64_hdr", "S64_hdr_packed", "S64_c8", "S64_c8_packed", "c8")
 PREWARM_S = 0.3
 STREAMS = 2      # rx batches in flight per GPU for the one-launch-per-batch rows
 # the layout hint the resident batches are handed over with (mosrx_batch.layout): "auto" =
@@ -250,6 +254,14 @@ def kernel_duration(stamped, back_to_back: float):
     return back_to_back, "HIP events around back-to-back launches, median of 5"
 
 
+def stamp_floor(ctx, db, iters, timing):
+    """ms the dispatch stamp reads for an empty kernel with db's classify grid
+    (median of 5), when the row's own figure is dispatch-stamped; else None."""
+    if not timing.startswith("dispatch-stamped"):
+        return None
+    return median_of(lambda: ctx.probe_stamp_floor(db, iters))
+
+
 def pack_uniform(t: mosrx.Trace) -> mosrx.Trace:
     """Trace t with its frames packed back to back (all frames one length, as in the
     64 B traces): frame i at 2 + i * len instead of at a 16-byte boundary + 2."""
@@ -321,6 +333,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         kern_b2b = median_of(lambda: step_fn(kk, 1) / kk)
         kern_ms, timing = kernel_duration(lambda: ctx.time_op_dispatch(op, dbs, kk, arg), kern_b2b)
         kern_iso = None
+        floor_ms = stamp_floor(ctx, dbs[0], kk, timing)
         frames_per_step, ab_step = batch, ab
         method = f"one launch per batch, batch i on stream i % {STREAMS}"
     elif ring:
@@ -346,6 +359,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         kk = max(16, 4 * len(qs))
         kern_b2b = median_of(lambda: qs[0].time(kk, qs[1:], kernels=False)[0] / kk)
         kern_ms, timing = kernel_duration(lambda: qs[0].time_dispatch(kk, qs[1:]), kern_b2b)
+        floor_ms = None
         _, kern_iso = qs[0].time(min(kk, 32), qs[1:])
         for q in qs:
             q.destroy()
@@ -376,6 +390,7 @@ def measure(ctx, dist, key, steps, warmup, rank):
         kern_b2b = median_of(lambda: ctx.time_dev_streams(dbs, kk, 1) / kk)
         kern_ms, timing = kernel_duration(lambda: ctx.time_op_dispatch(mosrx.OP_CLASSIFY, dbs, kk), kern_b2b)
         kern_iso = ctx.time_dev_kernels(dbs, kk)
+        floor_ms = stamp_floor(ctx, dbs[0], kk, timing)
         frames_per_step, ab_step = batch, ab
         method = f"one launch per batch, batch i on stream i % {STREAMS}"
     for d in dbs:
@@ -421,6 +436,11 @@ def measure(ctx, dist, key, steps, warmup, rank):
         "launch_us_back_to_back": round(kern_b2b * 1e3, 3),
         "timed_region_device_us_per_step": round(1e3 * dev_ms / steps, 3),
     }
+    if floor_ms is not None:
+        # the stamp's own reading for an empty kernel of this launch's grid: a short
+        # launch's stamped figure is stated against it (rocprofv3's trace in profiles/)
+        out["roofline"]["stamp_floor_us"] = round(floor_ms * 1e3, 3)
+        out["roofline"]["launch_us_over_empty"] = round((kern_ms - floor_ms) * 1e3, 3)
     if pmc:
         out["roofline"]["traffic_source"] = pmc.get("source")
     return out, tr
@@ -1126,6 +1146,8 @@ def headline_line(detail, h, head, results, e2e):
             continue
         # [Mpkt/s, launch us, roofline frac]; GB/s and the per-rank spread: the detail record
         sec[k] = [round(r["mpkts"], 1), round(r["roofline"]["launch_us"], 2), round(r["roofline"]["frac"], 3)]
+        if "stamp_floor_us" in r["roofline"]:
+            sec[k].append(round(r["roofline"]["stamp_floor_us"], 2))
     e2e_line = None
     if e2e:
         e2e_line = {k: {"gbps": round(v["gbps"], 1), "mpkts": round(v["mpkts"], 1)}
@@ -1168,7 +1190,8 @@ def headline_line(detail, h, head, results, e2e):
         "read_ceiling_gbps": detail["read_ceiling_gbps"],
         "frac_of_read_ceiling": detail["frac_of_read_ceiling"],
         "cpu_baseline": cpu_line,
-        "secondary_fields": "Mpkt/s, launch us, roofline frac",
+        "secondary_fields": "Mpkt/s, launch us, roofline frac[, one-launch rows: the stamp's reading for an "
+                            "empty kernel of the same grid, us]",
         "secondary": sec,
         "e2e": e2e_line,
         "detail": "full record: stderr line '[bench-detail]' and --detail file",

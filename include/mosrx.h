@@ -372,6 +372,12 @@ int  mosrx_time_queue_dispatch(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq,
  * cycling over `nbuf` buffers of `bytes` each (sized past the 256 MiB Infinity
  * Cache), in GB/s.  The roofline figure next to the 8 TB/s spec peak. */
 int  mosrx_probe_read_bw(mosrx_ctx *c, uint64_t bytes, uint32_t nbuf, uint32_t iters, float *gbps);
+/* The stamp's own floor: the average dispatch-stamped duration (as
+ * mosrx_time_op_dispatch measures it) of an empty kernel with the grid a
+ * classify launch of `b` would have.  A short launch's stamped figure is
+ * stated against it (the stamp reads ~4 us for a kernel that does nothing,
+ * rocprofv3's trace 1.5-2.9 us).  Diagnostic; no mOS counterpart. */
+int  mosrx_probe_stamp_floor(mosrx_ctx *c, const mosrx_batch *b, uint32_t iters, float *avg_ms);
 /* hipDeviceSynchronize on the context's device. */
 int  mosrx_device_sync(mosrx_ctx *c);
 /* Same, end-to-end from host buffers through pinned staging, double-buffered. */

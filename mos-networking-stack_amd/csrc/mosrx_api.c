@@ -1515,6 +1515,26 @@ int mosrx_time_queue_dispatch(mosrx_ctx *c, mosrx_queue *const *q, uint32_t nq, 
 	return time_stamped(c, iters, queue_once, &r, avg_ms);
 }
 
+struct empty_run { int kind; uint32_t tiles; };
+
+static int empty_once(mosrx_ctx *c, uint32_t i, void *a)
+{
+	const struct empty_run *r = a;
+	(void)i;
+	return mosrx_launch_empty(r->kind, r->tiles, c->stream);
+}
+
+int mosrx_probe_stamp_floor(mosrx_ctx *c, const mosrx_batch *b, uint32_t iters, float *avg_ms)
+{
+	struct empty_run r;
+	if (!c || !b || b->n == 0 || iters == 0 || !avg_ms)
+		return -EINVAL;
+	r.kind = tile_for(c, b);
+	r.tiles = (uint32_t)((b->n + MOSRX_KIND_FRAMES(r.kind) - 1) / MOSRX_KIND_FRAMES(r.kind));
+	HIPCHK(hipSetDevice(c->device));
+	return time_stamped(c, iters, empty_once, &r, avg_ms);
+}
+
 int mosrx_time_dev_kernels(mosrx_ctx *c, const mosrx_batch *b, uint32_t nb, mosrx_result *const *d_out,
                            uint32_t iters, float *avg_ms)
 {

@@ -152,6 +152,7 @@ int mosrx_launch_bpf(const mosrx_bparams *bp, void *stream);
 
 int mosrx_launch_queue(const mosrx_qparams *qp, uint32_t total_tiles, int tile, int variant, void *stream);
 int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sink, void *stream);
+int mosrx_launch_empty(int kind, uint32_t tiles, void *stream);
 
 /* Launch one classify kernel; returns 0 or -EINVAL / -EIO.  `stream` is a hipStream_t. */
 int mosrx_launch_classify(const mosrx_kparams *kp, int tile, int variant, void *stream);

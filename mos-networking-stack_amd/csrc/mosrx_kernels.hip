@@ -1427,6 +1427,13 @@ extern "C" int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sin
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// An empty kernel of a classify launch's grid: its dispatch-stamped duration is
+// what the stamp itself reads for a launch that does nothing (mosrx_probe_stamp_floor;
+// the short rows' bench figures are stated against it).  Diagnostic only.
+__global__ void mosrx_empty_kernel(uint32_t) {}
+#endif
+
+#ifndef __HIPCC_RTC__
 // Dispatch-stamped timing (mosrx_time_op_dispatch / mosrx_time_queue_dispatch):
 // the next classify or queue launch of this thread carries a start / stop
 // event pair that the runtime stamps at the dispatch's own begin and end
@@ -1463,6 +1470,14 @@ static void launch_one(void (*k)(P...), uint32_t grid, uint32_t block, hipStream
 	} else {
 		hipLaunchKernelGGL(k, dim3(grid), dim3(block), 0, s, a...);
 	}
+}
+
+extern "C" int mosrx_launch_empty(int kind, uint32_t tiles, void *stream)
+{
+	if (kind < 0 || kind >= MOSRX_KIND_COUNT || tiles == 0)
+		return -EINVAL;
+	launch_one(mosrx_empty_kernel, tiles, WG_THREADS(kind), (hipStream_t)stream, tiles);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 template <int KIND, int VAR>

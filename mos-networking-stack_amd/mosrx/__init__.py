@@ -220,6 +220,7 @@ def lib():
                                            C.POINTER(C.c_float)]),
             "mosrx_time_queue_dispatch": (I, [P, C.POINTER(P), U32, U32, C.POINTER(C.c_float)]),
             "mosrx_probe_read_bw": (I, [P, U64, U32, U32, C.POINTER(C.c_float)]),
+            "mosrx_probe_stamp_floor": (I, [P, C.POINTER(Batch), U32, C.POINTER(C.c_float)]),
             "mosrx_queue_create": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), C.POINTER(P)]),
             "mosrx_queue_run": (I, [P, P, P]),
             "mosrx_queue_destroy": (None, [P, P]),
@@ -834,6 +835,14 @@ class Context:
         g = C.c_float()
         _chk(lib().mosrx_probe_read_bw(self.handle, nbytes, nbuf, iters, C.byref(g)), "mosrx_probe_read_bw")
         return float(g.value)
+
+    def probe_stamp_floor(self, db: DevBatch, iters: int = 500) -> float:
+        """mosrx_probe_stamp_floor: the dispatch-stamped duration (ms) of an empty
+        kernel with the grid a classify launch of `db` has."""
+        ms = C.c_float()
+        b = db.batch()
+        _chk(lib().mosrx_probe_stamp_floor(self.handle, C.byref(b), iters, C.byref(ms)), "mosrx_probe_stamp_floor")
+        return float(ms.value)
 
     def device_sync(self):
         _chk(lib().mosrx_device_sync(self.handle), "mosrx_device_sync")

@@ -361,6 +361,10 @@ def test_dispatch_stamped_kernel_timing(gpu_ctx):
     assert 0 < stamped <= b2b * 1.02, (stamped, b2b)
     for t, d in zip(trs, dbs):
         assert_records_equal(d.results(), O.classify(t.frames, t.off, t.len, O.params()), "stamped")
+    # the stamp's reading for an empty kernel of the same grid (the bench's short-row floor):
+    # positive, and no longer than the classify launch it is stated against
+    floor = gpu_ctx.probe_stamp_floor(dbs[0], 64)
+    assert 0 < floor <= stamped * 1.05, (floor, stamped)
     gpu_ctx.time_op(mosrx.OP_CLASSIFY_FH, dbs, 2, kernels=False)                # side buffers allocated
     assert gpu_ctx.time_op_dispatch(mosrx.OP_CLASSIFY_FH, dbs, 16) > 0
     progs = [(np.array([(0x28, 0, 0, 12), (0x15, 0, 1, 0x800), (0x06, 0, 0, 1), (0x06, 0, 0, 0)],

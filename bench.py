@@ -457,6 +457,25 @@ def cpu_share():
     return (max(1, min(aff, cap)) if cap else aff), aff, cap
 
 
+def cpu_quota():
+    """CPUs' worth of time the process's cgroup may use (cpu.max / cfs quota), or
+    None when unlimited: a thread count above it measures the quota, not the cores."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            per = int(fh.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def host_model():
     try:
         with open("/proc/cpuinfo") as fh:
@@ -512,10 +531,14 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, shares: bool = T
     out["per_gpu_share"] = leg(nt, f"one GPU's share of the host: {nt} of {os.cpu_count()} CPUs "
                                    f"(affinity {aff}, stated share {cap})")
     out["per_gpu_share"]["host_cpus"] = os.cpu_count()
+    out["per_gpu_share"]["cpu_quota"] = cpu_quota()
     if ws > 1 and host_cpus:
         # the job's share: ws GPUs' worth of threads over the CPUs the job's process had
         # before its NUMA binding (rank 0 alone runs this, after every GPU leg)
         nj = max(1, min(len(host_cpus), (cap or len(host_cpus)) * ws))
+        quota = cpu_quota()
+        if quota:                  # (a one-GPU box rehearsing N ranks has one GPU's quota)
+            nj = max(1, min(nj, int(quota)))
         mine = os.sched_getaffinity(0)
         try:
             os.sched_setaffinity(0, host_cpus)
@@ -523,6 +546,7 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, shares: bool = T
         finally:
             os.sched_setaffinity(0, mine)
         out["job_share"]["host_cpus"] = os.cpu_count()
+        out["job_share"]["cpu_quota"] = quota
     return out
 
 
@@ -817,12 +841,15 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
         nb = group or {"S64": 320, "M1500": 10, "IMIX": 12}[key]
         tr = mosrx.Trace({"S64": mosrx.TRACE_S64, "M1500": mosrx.TRACE_M1500,
                           "IMIX": mosrx.TRACE_IMIX}[key], ctx_batch * nb)
-    loops = max(1, frames_target // tr.n)
+    # warm-up (staging sized, module loaded): two launches' worth of frames, on top of
+    # the timed part's frames_target
+    warm = 2 * ctx_batch * (group or (256 if key == "S64" else 6))
+    loops = max(1, -(-(frames_target + warm) // tr.n))
     src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
     be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
                           group=group, timing=True, bpf=bpf, compact=compact, group_bytes=group_bytes)
     try:
-        be.run_loop(max_pkts=2 * ctx_batch * max(group, 256 if key == "S64" else 6))    # warm-up: staging sized, module loaded
+        be.run_loop(max_pkts=warm)
         st0 = be.stats()
         sync()
         t0 = time.perf_counter()
@@ -1127,8 +1154,8 @@ def headline_line(detail, h, head, results, e2e):
         cpu_line = _compact_cpu(cpu)
         for leg in ("per_gpu_share", "job_share", "reference", "reference_processpacket"):
             if cpu.get(leg):
-                cpu_line[leg] = {k: cpu[leg][k] for k in ("value", "unit", "cores", "host_cpus", "kind", "mpkts")
-                                 if k in cpu[leg]}
+                cpu_line[leg] = {k: cpu[leg][k] for k in ("value", "unit", "cores", "host_cpus", "cpu_quota", "kind",
+                                                          "mpkts") if k in cpu[leg]}
         for leg in ("mos_rx_loop_M1500", "mos_rx_loop_FW64", "mos_rx_loop_FW64_bare"):
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("processpacket_ns_per_frame", "gpu_records_ns_per_frame",

@@ -242,6 +242,22 @@ def test_consumer_matches_processpacket_on_gpu(tmp_path, name, form):
     _check_scenario(name, pp, gpu, form)
 
 
+ASAN_APP = os.path.join(REF, "asan", "mos_app_emul")
+
+
+@pytest.mark.skipif(not _have(ASAN_APP), reason="needs oracle/_ref/asan/mos_app_emul (make -C oracle asan)")
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_consumer_under_sanitizers(tmp_path, monkeypatch, name):
+    """Host code only: the backend (gpu_module.c), the consumer (mos_rx.c) and the
+    frame sources (loopback.c) built with AddressSanitizer + UBSan into the
+    emulated program; every scenario gives the suite's results and the
+    sanitizers report nothing (a report ends the run with a non-zero status)."""
+    monkeypatch.setenv("ASAN_OPTIONS", "detect_leaks=0:verify_asan_link_order=0:halt_on_error=1")
+    monkeypatch.setenv("UBSAN_OPTIONS", "print_stacktrace=1:halt_on_error=1")
+    pp, gpu = compare_modes(ASAN_APP, tmp_path, name, "c8")
+    _check_scenario(name, pp, gpu, "c8")
+
+
 @pytest.mark.skipif(not os.path.exists(os.path.join(REF, "mos_rx_mos_x.o")),
                     reason="needs oracle/_ref (make -C oracle ref)")
 def test_patched_build_calls_mos_own_stream_functions():

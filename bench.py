@@ -324,8 +324,8 @@ def measure(ctx, dist, key, steps, warmup, rank):
         t0 = time.perf_counter()
         dev_ms = step_fn(steps, STREAMS)
         ctx.device_sync()
+        wall = time.perf_counter() - t0     # this rank's region; the max over ranks below
         dist.barrier()
-        wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         kk = 500
         # the kernel's own duration (each launch stamped by its dispatch, as
@@ -353,8 +353,8 @@ def measure(ctx, dist, key, steps, warmup, rank):
         t0 = time.perf_counter()
         dev_ms, _ = qs[0].time(steps, qs[1:], kernels=False)
         ctx.device_sync()
+        wall = time.perf_counter() - t0     # this rank's region; the max over ranks below
         dist.barrier()
-        wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         kk = max(16, 4 * len(qs))
         kern_b2b = median_of(lambda: qs[0].time(kk, qs[1:], kernels=False)[0] / kk)
@@ -378,8 +378,8 @@ def measure(ctx, dist, key, steps, warmup, rank):
         # batches overlap launch and drain); HIP events on the kernel streams
         dev_ms = ctx.time_dev_streams(dbs, steps, STREAMS)
         ctx.device_sync()
+        wall = time.perf_counter() - t0     # this rank's region; the max over ranks below
         dist.barrier()
-        wall = time.perf_counter() - t0
         wall_max = dist.max(wall)
         # roofline: the kernel's own duration over 500 back-to-back launches on
         # ONE stream, each launch stamped by its dispatch (hipExtLaunchKernel: the

@@ -1,6 +1,6 @@
 """Soak of the mOS verdict consumer (diagnostic, not a test).
 
-    python3 scripts/soak_consumer.py [seconds=300] [seed=1] [emul|gpu]
+    python3 scripts/soak_consumer.py [seconds=300] [seed=1] [emul|gpu|asan]
 
 Random setups of tests/test_mos_consumer.py's harness (oracle/_ref/mos_app:
 mOS itself, mtcp_init + RunMainLoop over gpu_module_func) until the time is
@@ -12,7 +12,8 @@ by the GPU (cfg.tx_csum, clock frozen), the flow lookup on the GPU hash or on
 mOS's.  Each setup runs mOS twice -- ProcessPacket, then the consumer on the
 GPU records -- and every per-frame return, NETSTAT, callback, the flow table
 and every frame sent must agree.  "emul" (default) runs the CPU stand-in for
-the GPU (oracle/_ref/mos_app_emul), "gpu" the real kernels.  A mismatch
+the GPU (oracle/_ref/mos_app_emul), "gpu" the real kernels, "asan" the
+stand-in with the host code under AddressSanitizer + UBSan.  A mismatch
 prints the setup and exits 1.
 """
 import os
@@ -78,7 +79,11 @@ def describe(pp, gpu):
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 300.0
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-    exe = T.APP if len(sys.argv) > 3 and sys.argv[3] == "gpu" else T.APP_EMUL
+    mode = sys.argv[3] if len(sys.argv) > 3 else "emul"
+    exe = {"gpu": T.APP, "asan": T.ASAN_APP}.get(mode, T.APP_EMUL)
+    if mode == "asan":      # the host-side sanitizer build (make -C oracle asan)
+        os.environ["ASAN_OPTIONS"] = "detect_leaks=0:verify_asan_link_order=0:halt_on_error=1"
+        os.environ["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
     rnd = random.Random(seed)
     fixtures = {fix: T.fixture_frames(fix) for fix in ("edge", "rand_small", "rand_mid")}
     t0 = last = time.time()

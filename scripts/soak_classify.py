@@ -11,7 +11,10 @@ stack state (monitor / end-host sockets, forward, 1-16 queues and both queue
 maps, skip_tcp_csum, random or MSDN RSS keys, netdev addresses) and a random
 kernel shape (library choice, or SMALL / stream tile forced with either tail
 cache policy).  Records, flow hashes and pkt_info fields through the host and
-the device paths, and the TX rewrite, must equal the oracle's.  A mismatch
+the device paths, and the TX rewrite, must equal the oracle's.  Some batches
+are small frames at a fixed stride handed over with a layout hint (right,
+right but for moved lanes, wrong, unpackable), in 16- and 8-byte records; the
+queue mode mixes them in and runs some queues with 8-byte records.  A mismatch
 prints the seed and exits 1.
 """
 import os
@@ -108,6 +111,57 @@ def rand_batch(rng):
     return buf, off, ln, packed
 
 
+def uniform_batch(rng):
+    """(buf, off, len, hint) of a batch of small frames (the SMALL tile's) at a fixed
+    stride, some lanes moved elsewhere, with a hint that is right, right for the
+    unmoved lanes, wholly wrong, or unpackable."""
+    n = rng.choice([1, 2, 255, 256, 257, rng.randint(1, 40_000)])
+    ln_ = rng.choice([14, 34, 54, 58, 60, 64, 74, 78])
+    stride = rng.choice([ln_, ln_ + 2, 64, 80, 128, 2048]) if ln_ <= 64 else rng.choice([ln_, 80, 128, 2048])
+    stride = max(stride, ln_)
+    off0 = rng.choice([0, 2, 18, rng.randint(0, 200)])
+    moved = rng.sample(range(n), k=min(n, rng.choice([0, 0, 1, 5, 300])))
+    buf = np.zeros(off0 + stride * n + 128 * (len(moved) + 1), np.uint8)
+    off = (off0 + stride * np.arange(n, dtype=np.int64)).astype(np.uint32)
+    lens = np.full(n, ln_, np.uint16)
+    for i in range(n):
+        f = rand_frame(rng)[:ln_]
+        f = f + bytes(ln_ - len(f))
+        buf[off[i]:off[i] + ln_] = np.frombuffer(f, np.uint8)
+    at = off0 + stride * n + 2
+    for i in moved:                          # moved: the hinted address now holds other bytes
+        buf[at:at + ln_] = buf[off[i]:off[i] + ln_]
+        buf[off[i]:off[i] + ln_] = rng.getrandbits(8)
+        off[i] = at
+        at += 128
+    for i in rng.sample(range(n), k=min(n, rng.randint(0, 3))):
+        lens[i] = rng.randint(0, ln_)       # captures cut short
+    hint = rng.choice([(off0, stride), (off0, stride), (rng.randint(0, 300), rng.randint(1, 300)),
+                       (off0, 0x10000), "auto", None])
+    return buf, off, lens, hint
+
+
+def hint_check(ctx, rng, p):
+    """A fixed-stride batch handed over with a layout hint (mosrx_batch.layout):
+    16- and 8-byte records through the single launch equal the oracle's."""
+    buf, off, ln, hint = uniform_batch(rng)
+    ctx.set_params(p)
+    want = O.classify(buf, off, ln, oparams(p))
+    db = ctx.upload(buf, off, ln, frames_bytes=len(buf), hint=hint)
+    try:
+        ctx.classify_dev(db)
+        if db.results().tobytes() != want.tobytes():
+            raise AssertionError(f"hinted batch ({hint}, {len(off)} frames) differs")
+        ctx.classify_dev_compact(db)
+        r8 = db.results8()
+        for f in ("rss", "reason", "queue", "verdict", "tcp_flags"):
+            if not np.array_equal(r8[f], want[f]):
+                raise AssertionError(f"hinted batch ({hint}): compact {f} differs")
+    finally:
+        db.free()
+    return len(off)
+
+
 def queue_soak(ctx, rnd, budget):
     """`queue` mode: random batch queues (mosrx_queue_*: one launch over 1-40
     resident batches of different sizes, layouts and frame mixes) against the
@@ -121,14 +175,23 @@ def queue_soak(ctx, rnd, budget):
         variant = rng.choice(ALL_VARIANTS)
         ctx.set_variant(variant)
         ctx.set_params(p)
-        batches = [rand_batch(rng) for _ in range(rng.choice([1, 2, 3, 8, rng.randint(1, 40)]))]
-        dbs = [ctx.upload(b, o, l, frames_bytes=len(b)) for b, o, l, _ in batches]
-        q = ctx.queue(dbs)
+        batches = [rand_batch(rng) if rng.random() < 0.7 else uniform_batch(rng)
+                   for _ in range(rng.choice([1, 2, 3, 8, rng.randint(1, 40)]))]
+        dbs = [ctx.upload(b, o, l, frames_bytes=len(b), hint=x if not isinstance(x, bool) else None)
+               for b, o, l, x in batches]
+        compact = rng.random() < 0.3                 # 8-byte records (the drop-in path's form)
+        q = ctx.queue_ex(dbs, compact=compact)
         q.run()
         for k, ((b, o, l, _), db) in enumerate(zip(batches, dbs)):
             want = O.classify(b, o, l, oparams(p))
-            if db.results().tobytes() != want.tobytes():
-                print(f"FAIL queue seed {s} variant {variant}: batch {k} of {len(dbs)} differs", flush=True)
+            if compact:
+                r8 = db.results8()
+                ok = all(np.array_equal(r8[f], want[f]) for f in ("rss", "reason", "queue", "verdict", "tcp_flags"))
+            else:
+                ok = db.results().tobytes() == want.tobytes()
+            if not ok:
+                print(f"FAIL queue seed {s} variant {variant}: batch {k} of {len(dbs)} differs "
+                      f"(compact {compact})", flush=True)
                 sys.exit(1)
             frames += len(o)
         q.destroy()
@@ -174,6 +237,8 @@ def main():
         try:
             ctx.set_variant(variant)
             run_both(ctx, buf, off, ln, p, side=True)
+            if rng.random() < 0.3:          # a fixed-stride batch of small frames with a layout hint
+                frames += hint_check(ctx, rng, p)
             # the TX rewrite of frames that overlap depends on the order they are written in
             if rng.random() < 0.3 and packed:
                 fl = rng.choice([mosrx.TX_IP_CSUM, mosrx.TX_TCP_CSUM, mosrx.TX_IP_CSUM | mosrx.TX_TCP_CSUM])

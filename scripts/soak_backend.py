@@ -4,8 +4,9 @@
 
 Random scenarios until the time is up, each a fresh backend over an in-memory
 source: trace kind and size, frames per batch, batches per launch (auto or
-1..8), pipelining, how the source hands frames over (lent / runs / frame by
-frame), replays, pkt_info and flow-hash side arrays, and stack-state changes
+1..8; auto groups of random byte budgets), pipelining, how the source hands
+frames over (lent / runs / frame by frame), replays, 16- or 8-byte records
+(cfg.compact), pkt_info and flow-hash side arrays, and stack-state changes
 (num_msp / num_esp / forward through dev_ioctl(MOSRX_PKT_SET_PARAMS)) at
 random points between recv_pkts calls.  Every batch handed out must equal the
 oracle's records (and side arrays) for its frames under the state in effect
@@ -44,15 +45,19 @@ def scenario(rnd):
                 group=rnd.choice([0, 0, 1, 2, 3, 8]), pipeline=rnd.random() < 0.7,
                 mode=rnd.choice([mosrx.SRC_BEST, mosrx.SRC_FILL, mosrx.SRC_PER_FRAME]),
                 loops=rnd.choice([1, 1, 2, 3]), tcpinfo=rnd.random() < 0.3, flowhash=rnd.random() < 0.3,
-                toggle=rnd.choice([0.0, 0.0, 0.1, 0.5]), fwd=rnd.randint(0, 1))
+                toggle=rnd.choice([0.0, 0.0, 0.1, 0.5]), fwd=rnd.randint(0, 1),
+                compact=rnd.random() < 0.4,
+                group_bytes=rnd.choice([0, 0, 1 << 16, 1 << 20, 16 << 20]))
 
 
 def run(sc, rnd):
     t = mosrx.Trace(sc["kind"], sc["n"], nflows=sc["nflows"], seed=sc["seed"])
     p = mosrx.default_params(forward=sc["fwd"])
     src = mosrx.mem_source(t.frames, t.off, t.len, loops=sc["loops"], mode=sc["mode"])
+    compact = sc["compact"] and not sc["tcpinfo"]     # (the module refuses compact records with pkt_info)
     be = mosrx.GpuBackend([src], params=p, batch=sc["batch"], pipeline=sc["pipeline"], cpu=rnd.randint(0, 7),
-                          group=sc["group"], tcpinfo=sc["tcpinfo"], flowhash=sc["flowhash"])
+                          group=sc["group"], tcpinfo=sc["tcpinfo"], flowhash=sc["flowhash"], compact=compact,
+                          group_bytes=sc["group_bytes"])
     cache = {}
 
     def ora(state):
@@ -77,8 +82,15 @@ def run(sc, rnd):
                 break
             idx = (seen + np.arange(n)) % t.n
             rec, fh, ti = ora(state)
-            got = be.results(0, n)
-            if got.tobytes() != rec[idx].tobytes():
+            if compact:
+                got8 = be.results8(0, n)
+                for f in ("rss", "reason", "queue", "verdict", "tcp_flags"):
+                    if not np.array_equal(got8[f], rec[idx][f]):
+                        return f"8-byte records' {f} differ at batch {batches} (frames {seen}..), state {state}"
+                got = None
+            else:
+                got = be.results(0, n)
+            if got is not None and got.tobytes() != rec[idx].tobytes():
                 i = int(np.nonzero(np.any(got.view(np.uint8).reshape(-1, 16) !=
                                           rec[idx].view(np.uint8).reshape(-1, 16), axis=1))[0][0])
                 return f"records differ at batch {batches} (frames {seen}..), first {i}: {got[i]} vs {rec[idx][i]}, state {state}"

@@ -539,14 +539,22 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, shares: bool = T
         quota = cpu_quota()
         if quota:                  # (a one-GPU box rehearsing N ranks has one GPU's quota)
             nj = max(1, min(nj, int(quota)))
+        # the whole host: every CPU the process had, as far as the
+        # cgroup quota lets threads run at once; only when that is more than the job's share
+        nh = max(1, min(len(host_cpus), int(quota) if quota else len(host_cpus)))
         mine = os.sched_getaffinity(0)
         try:
             os.sched_setaffinity(0, host_cpus)
             out["job_share"] = leg(nj, f"the {ws}-GPU job's share of the host: {nj} of {os.cpu_count()} CPUs")
+            if nh > nj:
+                out["whole_host"] = leg(nh, f"every CPU the job may run on: {nh} of {os.cpu_count()} CPUs")
         finally:
             os.sched_setaffinity(0, mine)
         out["job_share"]["host_cpus"] = os.cpu_count()
         out["job_share"]["cpu_quota"] = quota
+        if "whole_host" in out:
+            out["whole_host"]["host_cpus"] = os.cpu_count()
+            out["whole_host"]["cpu_quota"] = quota
     return out
 
 
@@ -1152,7 +1160,7 @@ def headline_line(detail, h, head, results, e2e):
     cpu_line = None
     if cpu:
         cpu_line = _compact_cpu(cpu)
-        for leg in ("per_gpu_share", "job_share", "reference", "reference_processpacket"):
+        for leg in ("per_gpu_share", "job_share", "whole_host", "reference", "reference_processpacket"):
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("value", "unit", "cores", "host_cpus", "cpu_quota", "kind",
                                                           "mpkts") if k in cpu[leg]}

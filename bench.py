@@ -558,7 +558,8 @@ def cpu_baseline(tr: mosrx.Trace, key: str, min_s: float = 3.0, shares: bool = T
     return out
 
 
-def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: bool = False, forward: int = 0):
+def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: bool = False, forward: int = 0,
+                  threads: int = 1):
     """mOS's own compiled functions on one host core, when the reference build
     travelled with the tree; else None.  A reported baseline, never the
     measured path.  Default: `mosref --time` = ref_frame, i.e. the header
@@ -568,7 +569,9 @@ def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: boo
     the rx loop calls it (checks + checksums + FindStream on an empty flow
     table; no RSS, which the NIC computes in mOS).  forward: mos.conf `forward`
     under which ProcessPacket runs (1: its ForwardIPPacket / ForwardEthernetFrame
-    calls are recorded by the harness, not transmitted)."""
+    calls are recorded by the harness, not transmitted).  threads > 1 (`--time`
+    only): one pthread per disjoint slice of the trace, as mOS shards its frames
+    over one mTCP thread per core (core.c:1369-1466)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "mosref")
     if not os.access(exe, os.X_OK):
         return None
@@ -579,8 +582,10 @@ def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: boo
         path = os.path.join(td, "trace.mrxt")
         pktlib.write_ref_trace(path, tr.frames[:tr.frames_bytes], tr.off, tr.len, forward=forward)
         try:
-            out = subprocess.run([exe, "--time-pp" if process_packet else "--time", path, str(seconds)],
-                                 capture_output=True, text=True, timeout=seconds + 60)
+            cmd = [exe, "--time-pp" if process_packet else "--time", path, str(seconds)]
+            if threads > 1 and not process_packet:
+                cmd.append(str(threads))
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds + 60)
             r = json.loads(out.stdout.strip().splitlines()[-1])
         except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
             return None
@@ -590,9 +595,12 @@ def cpu_reference(tr: mosrx.Trace, key: str, seconds: float, process_packet: boo
             if process_packet else
             "ip_fast_csum + TCPCalcChecksum + GetRSSHash + GetRSSCPUCore + header checks "
             "(oracle/_ref/mosref --time: ref_frame, not ProcessPacket)")
-    return {"value": round(algo_bytes(tr, key) * r["passes"] / el / 1e9, 3), "unit": "GB/s", "cores": 1,
+    nt = int(r.get("threads", 1))
+    # every thread's frames over the longest thread's time (mosref reports the rate)
+    return {"value": round(algo_bytes(tr, key) / tr.n * r["mpkts"] * 1e6 / 1e9, 3), "unit": "GB/s", "cores": nt,
             "kind": "reference", "mpkts": round(r["mpkts"], 3),
-            "sample": f"{r['passes']} passes over one {tr.n}-frame batch ({el:.1f} s), mOS core/src {what}, 1 thread"}
+            "sample": f"{r['passes']} slice passes over one {tr.n}-frame batch ({el:.1f} s), mOS core/src {what}, "
+                      f"{nt} thread(s)" + (" over disjoint slices" if nt > 1 else "")}
 
 
 def cpu_baseline_row(tr: mosrx.Trace, key: str, min_s: float, O):
@@ -724,10 +732,13 @@ def cpu_rx_loop_leg(tr: mosrx.Trace, loops: int, forward: int, reps: int = 5, ti
 def measure_fw64(ctx, seconds: float):
     """BASELINE config #1: simple_firewall's rx path on ONE core, 10 000 x 60 B
     frames of one flow, the firewall's stack state (num_msp=1, forward=1,
-    num_queues=1, i40e map).  libpcap and the sample cannot be
-    built here, so the CPU-only run is timed as mOS's own
-    compiled per-frame functions (mosref --time) and as the oracle, both on one
-    core; the GPU classifying the same 10K batch is reported beside them."""
+    num_queues=1, i40e map).  The CPU baseline is the sample
+    itself: mOS's samples/simple_firewall compiled unmodified over the ENABLE_GPU
+    build with gpu_module_func replaying the trace (oracle/_ref/simple_firewall,
+    cpu_simple_firewall below: its rx loop on one core with mOS's ProcessPacket,
+    and with the GPU records); beside it mOS's own compiled per-frame functions
+    (mosref --time), ProcessPacket alone and the oracle, all on one core, and the
+    GPU classifying the same 10K batch."""
     tr = mosrx.Trace(mosrx.TRACE_FW64, 10_000)
     out = {"workload": "config #1: simple_firewall state, 1 core, 10k x 64B (60 B caplen), one flow",
            "batch": tr.n, "algo_bytes_per_batch": algo_bytes(tr)}
@@ -741,6 +752,9 @@ def measure_fw64(ctx, seconds: float):
     ref = cpu_reference(tr, "FW64", seconds, process_packet=True, forward=1)
     if ref:
         port["reference_processpacket"] = ref
+    sf = cpu_simple_firewall()
+    if sf:
+        port["simple_firewall"] = sf
     out["cpu_baseline"] = port
     ctx.set_params(mosrx.default_params())
     db = ctx.upload(tr.frames, tr.off, tr.len, frames_bytes=tr.frames_bytes, max_len=tr.max_len)
@@ -750,6 +764,47 @@ def measure_fw64(ctx, seconds: float):
                                   "method": "500 back-to-back launches over the resident 10K batch"}
     out["e2e_boundary"] = measure_fw64_boundary(tr)
     return out
+
+
+def cpu_simple_firewall(loops: int = 20, reps: int = 3, timeout: float = 120.0):
+    """BASELINE config #1 through the reference's own application, on one core:
+    mOS's samples/simple_firewall (unmodified, oracle/_ref/simple_firewall: the
+    ENABLE_GPU build of INTEGRATION.md §2, gpu_module_func replaying a pcap file
+    of config #1's 10K x 60 B trace and the rule flows of
+    tests/test_simple_firewall.py, `loops` times), `-n 1`.  Per-frame CPU time of
+    RunMainLoop's rx loop (core.c:902-907, timed per batch by oracle/sf_glue.c)
+    with mOS's ProcessPacket on every frame ("pp": the reference's CPU path) and
+    with the consumer of the GPU records ("gpu"), alternated `reps` times,
+    medians.  A reported baseline; None when the binary did not travel."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "simple_firewall")
+    if not os.access(exe, os.X_OK):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import tempfile
+    import pathlib
+    import test_simple_firewall as SF
+    frames = SF.firewall_frames()
+    ns = {"pp": [], "gpu": []}
+    with tempfile.TemporaryDirectory() as td:
+        for rep in range(reps):
+            for mode in ("pp", "gpu"):
+                tmp = pathlib.Path(td) / f"r{rep}"
+                tmp.mkdir(exist_ok=True)
+                try:
+                    r = SF.run_sample(exe, mode, tmp, frames, loops=loops, linger_ms=0)
+                except (AssertionError, OSError, ValueError, subprocess.TimeoutExpired) as e:
+                    print(f"[bench] simple_firewall leg failed: {str(e)[:300]}", file=sys.stderr)
+                    return None
+                ns[mode].append(r["result"]["rx_ns_per_frame"])
+    pp, gp = float(np.median(ns["pp"])), float(np.median(ns["gpu"]))
+    return {"value": round(1e3 / pp, 3), "unit": "Mpkt/s", "cores": 1, "kind": "reference",
+            "processpacket_ns_per_frame": round(pp, 1), "gpu_records_ns_per_frame": round(gp, 1),
+            "gpu_records_mpkts": round(1e3 / gp, 3),
+            "runs_ns": {k: [round(x, 1) for x in v] for k, v in ns.items()},
+            "sample": f"mOS samples/simple_firewall unmodified (-n 1) over gpu_module_func replaying "
+                      f"{len(frames)} frames x {loops} (config #1's 10K x 60 B flow + rule flows), rx loop "
+                      f"per-frame CPU time (core.c:902-907) with ProcessPacket (value) and with the GPU records, "
+                      f"{reps} alternated runs, medians"}
 
 
 def measure_fw64_boundary(tr: mosrx.Trace, loops: int = 50):
@@ -891,6 +946,48 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
                       f"{', ' + str(len(bpf)) + ' monitor filters installed: the fused classify + BPF queue kernel' if bpf else ''}), "
                       f"in-memory source replaying {tr.n} distinct frames; every batch crosses PCIe; device "
                       f"time = each kernel launch's dispatch-stamped duration (its frames were just copied in)"}
+
+
+def measure_backend_latency(key: str, group: int, rate_mpkts: float, cpu: int, seconds: float = 0.6,
+                            group_max_us: int = 0, warm_s: float = 0.15):
+    """Per-frame residency on the drop-in path: the backend
+    as measure_backend runs it (8-byte records, pipelined), fed by a paced source
+    (mosrx_source_paced: frame k arrives at t0 + k / rate, none is handed out
+    before it arrives, as a NIC ring fills at line rate) at `rate_mpkts`, the rx
+    loop polling (idle_us 0, as mOS's poll-mode loop does) with the census
+    consumer of the saturated legs.  Per frame: recv -> verdict available (its
+    batch returned by recv_pkts with records) and recv -> consumed (that plus its
+    share of the batch's walk), from the rx loop's probe (two clock reads per
+    batch, mosrx_rx_loop_opts.probe) after `warm_s` of warm-up.  Never the bench
+    value."""
+    batch = {"S64": 32_768, "M1500": 65_536, "IMIX": 262_144}[key]
+    kind = {"S64": mosrx.TRACE_S64, "M1500": mosrx.TRACE_M1500, "IMIX": mosrx.TRACE_IMIX}[key]
+    tr = mosrx.Trace(kind, batch * {"S64": 64, "M1500": 4, "IMIX": 2}[key])
+    rate = rate_mpkts * 1e6
+    src = mosrx.paced_source(mosrx.mem_source(tr.frames, tr.off, tr.len, loops=0), rate)
+    be = mosrx.GpuBackend([src], batch=batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
+                          group=group, compact=True, group_max_us=group_max_us)
+    probe = mosrx.LatencyProbe()
+    probe.src = src
+    probe.skip = int(rate * warm_s)
+    try:
+        t0 = time.perf_counter()
+        st = be.run_loop(idle_rounds=0, idle_us=0, max_us=int((seconds + warm_s) * 1e6), probe=probe)
+        dt = time.perf_counter() - t0
+        ms = be.stats()
+    finally:
+        be.close()
+    n = int(st.rx_packets)
+    t0n, nspf, rel = C.c_uint64(), C.c_double(), C.c_uint64()
+    out = {"offered_mpkts": round(rate_mpkts, 2), "delivered_mpkts": round(n / dt / 1e6, 2),
+           "frames_recorded": int(probe.recorded),
+           "avail_us": probe.percentiles("avail", (50, 99, 99.9)),
+           "consumed_us": probe.percentiles("done", (50, 99, 99.9)),
+           "avail_max_us": round(probe.avail_max_ns / 1e3, 1), "consumed_max_us": round(probe.done_max_ns / 1e3, 1),
+           "groups": int(ms.rx_groups), "mean_group_frames": round(ms.rx_frames / max(ms.rx_groups, 1), 1),
+           "max_group_frames": int(ms.max_group_frames), "group": group if group else "auto",
+           "group_max_us": group_max_us}
+    return out
 
 
 def measure_backend_threads(key: str, nthreads: int, group: int, frames_per_thread: int, device: int):
@@ -1058,6 +1155,15 @@ def main():
         ref = cpu_reference(traces[head], head, 10.0)
         if ref:
             cpu["reference"] = ref
+        # mOS's own code on one GPU's share of the host cores, beside
+        # the port's per_gpu_share: one pthread per disjoint slice
+        nt = cpu_share()[0]
+        if nt > 1:
+            ref = cpu_reference(traces[head], head, 10.0, threads=nt)
+            if ref:
+                ref["host_cpus"] = os.cpu_count()
+                ref["cpu_quota"] = cpu_quota()
+                cpu["reference_share"] = ref
         ref = cpu_reference(traces[head], head, 5.0, process_packet=True)
         if ref:
             cpu["reference_processpacket"] = ref
@@ -1160,7 +1266,8 @@ def headline_line(detail, h, head, results, e2e):
     cpu_line = None
     if cpu:
         cpu_line = _compact_cpu(cpu)
-        for leg in ("per_gpu_share", "job_share", "whole_host", "reference", "reference_processpacket"):
+        for leg in ("per_gpu_share", "job_share", "whole_host", "reference", "reference_share",
+                    "reference_processpacket"):
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("value", "unit", "cores", "host_cpus", "cpu_quota", "kind",
                                                           "mpkts") if k in cpu[leg]}
@@ -1177,6 +1284,8 @@ def headline_line(detail, h, head, results, e2e):
             sec[k] = {"gpu_mpkts": round(r["gpu_device_resident"]["mpkts"], 1),
                       "cpu_port_mpkts": cb.get("mpkts"),
                       "cpu_ref_processpacket_mpkts": (cb.get("reference_processpacket") or {}).get("mpkts"),
+                      "cpu_simple_firewall_mpkts": (cb.get("simple_firewall") or {}).get("value"),
+                      "simple_firewall_gpu_records_mpkts": (cb.get("simple_firewall") or {}).get("gpu_records_mpkts"),
                       "boundary_mpkts": round(r["e2e_boundary"]["mpkts"], 2)}
             continue
         # [Mpkt/s, launch us, roofline frac]; GB/s and the per-rank spread: the detail record

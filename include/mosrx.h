@@ -254,6 +254,9 @@ int  mosrx_classify_host_ex(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_
 #define MOSRX_NSLOT 2
 int  mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out);
 int  mosrx_classify_host_wait(mosrx_ctx *c, int slot);
+/* 1 when the slot's last submit has completed (its wait would not block) or
+ * nothing is outstanding on it, 0 while it runs, -errno on error. */
+int  mosrx_classify_host_ready(mosrx_ctx *c, int slot);
 
 /* The same with the pkt_info TCP fields into h_tcpinfo[n] (NULL: none). */
 int  mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out,

@@ -220,6 +220,12 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * mosrx_rx_state.rec_bytes says which form it has.  Not
 	                                                 * with tcpinfo.  Default 0 standalone, 1 in an mOS build
 	                                                 * left unconfigured (its consumer, mos_rx.c, reads both). */
+	uint32_t      group_max_us;                     /* latency budget of a group (0: none): it takes no more
+	                                                 * frames than, at this netdev's measured rates, cross PCIe
+	                                                 * and are classified within the budget, or than the rx
+	                                                 * loop walks within it (never under 4096 frames); any
+	                                                 * group mode.  A group is never waited for: a receive
+	                                                 * takes what has arrived.  DESIGN.md §5 (latency) */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
 #define MOSRX_GROUP_AUTO_BYTES  (512ull << 20)   /* per pipeline slot; 64 B frames: ~240 batches of 32K
@@ -275,6 +281,11 @@ typedef struct mosrx_gpu_module_stats {
 	                               whose pass failed are dropped and counted in tx_errors */
 	int32_t  cpu_node;          /* the core's NUMA node, -1 unknown */
 	int32_t  gpu_node;          /* its GPU's, -1 unknown */
+	uint64_t rx_groups;         /* groups handed out (one launch each) */
+	uint64_t max_group_frames;  /* frames of the largest of them */
+	uint64_t group_cap_frames;  /* the frame cap cfg.group_max_us gave the last group filled (0: none) */
+	double   ns_per_frame_host; /* the latency cap's rates: the host's time per frame of a group */
+	double   ns_per_byte_dev;   /*   and a group's submit -> records ready per frame byte (0: not measured) */
 } mosrx_gpu_module_stats;
 /* Time every kernel this thread's contexts launch (for the stats above). */
 int  mosrx_gpu_module_set_timing(struct mtcp_thread_context *ctx, int on);
@@ -306,11 +317,13 @@ int mosrx_rx_loop(const io_module_func *iom, struct mtcp_thread_context *ctx, in
  * only at max_pkts / max_us), or after `max_us` microseconds (0: no limit).
  * Every round ends with send_pkts on each netdev (core.c:999-1007), so frames
  * a consumer wrote with get_wptr leave in the same round. */
+struct mosrx_latency_probe;
 typedef struct mosrx_rx_loop_opts {
 	uint64_t max_pkts;
 	uint32_t idle_rounds;
 	uint32_t idle_us;
 	uint64_t max_us;
+	struct mosrx_latency_probe *probe;   /* NULL, or the residency of a paced source's frames (below) */
 } mosrx_rx_loop_opts;
 int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx, int nif,
                      const mosrx_rx_loop_opts *opts, mosrx_pkt_fn fn, void *arg, mosrx_rx_stats *st);
@@ -351,6 +364,37 @@ typedef struct mosrx_forwarder {
 int  mosrx_mos_forwards(const mosrx_result *res, int forward, uint32_t num_msp, uint32_t listener);
 void mosrx_forward_frame(void *arg, int ifidx, int index, const uint8_t *pkt, uint16_t len,
                          const mosrx_result *res);
+
+/* ---- residency of frames from a paced source (latency of the drop-in path) ----
+ * mosrx_source_paced: `inner`'s frames released at `rate_pps` -- frame k
+ * arrives at t0 + k * 1e9 / rate_pps, t0 being the first receive call -- and
+ * none before it arrives, as a NIC ring fills at line rate.  It takes `inner`
+ * over (closing it closes both).  Not for AF_PACKET sources (a live wire has its
+ * own pace).  mosrx_source_paced_info: t0 (CLOCK_MONOTONIC ns, 0 before the first
+ * receive), ns between arrivals, frames handed out. */
+mosrx_source *mosrx_source_paced(mosrx_source *inner, double rate_pps);
+int           mosrx_source_paced_info(const mosrx_source *s, uint64_t *t0_ns, double *ns_per_frame,
+                                      uint64_t *released);
+
+/* Residency of a paced source's frames through the rx loop
+ * (mosrx_rx_loop_opts.probe; one netdev): the k-th frame the loop receives is
+ * arrival k.  Per frame after the first `skip`: recv -> verdict available (the
+ * clock when recv_pkts returned its batch with the records) into avail_hist,
+ * and recv -> consumed (that clock plus the frame's share of the batch's walk,
+ * the walk taken as even over the batch) into done_hist.  Two clock reads per
+ * batch, nothing per frame.  Histogram bin of v ns: v below 16, else
+ * 16 * floor(log2 v) + the next 4 bits of v (6 % wide). */
+#define MOSRX_LAT_BINS 1024
+typedef struct mosrx_latency_probe {
+	const mosrx_source *src;      /* the paced source of the netdev (t0 and pace read at the first batch) */
+	uint64_t t0_ns;
+	double   ns_per_frame;
+	uint64_t skip;                /* warm-up frames not recorded */
+	uint64_t seen, recorded, batches;
+	uint64_t avail_max_ns, done_max_ns;
+	uint64_t avail_hist[MOSRX_LAT_BINS];
+	uint64_t done_hist[MOSRX_LAT_BINS];
+} mosrx_latency_probe;
 
 #ifdef __cplusplus
 }

@@ -8,10 +8,15 @@
  * recv_pkts (core.c:899) hands out the next classified batch; get_rptr
  * (core.c:905) the staged frames; the per-frame verdicts are read through
  * dev_ioctl(MOSRX_PKT_RX_RESULTS) or per packet through dev_ioctl(PKT_RX_RSS)
- * (dpdk_module.c:568-571).  Batches are received in groups of `group`
- * (cfg.group, default 1): a group's batches are staged back to back in one
- * pinned block and classified by ONE kernel launch (the batch queue), then
- * handed out one per recv_pkts, so small batches do not pay a launch each.
+ * (dpdk_module.c:568-571).  Batches are received in groups (cfg.group: a
+ * fixed count, or MOSRX_GROUP_AUTO, the default: every batch the source has
+ * ready, up to cfg.group_bytes of frames): a group's batches are staged back
+ * to back in one pinned block and classified by ONE kernel launch (the batch
+ * queue), then handed out one per recv_pkts, so small batches do not pay a
+ * launch each.  cfg.group_max_us bounds a group by time as well: no more
+ * frames than the measured PCIe + classify rate moves, or the host's rx loop
+ * walks, within that many microseconds (group_cap), so a frame's residency
+ * stays near a few times the budget at any load.
  * With `pipeline` set, the next group is received and classified while the
  * application consumes the current one, keeping the reference's pointer
  * lifetime (valid until the next recv_pkts).  A source that holds its frames
@@ -45,6 +50,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/mosrx_io_module.h"
 #include "mosrx_source.h"
@@ -105,6 +111,13 @@ struct if_state {
 	uint32_t cur_idx;         /* its batch exposed now */
 	int inflight;             /* group being classified, -1 none */
 	uint32_t gen;             /* bumped by SET_PARAMS / SET_BPF: older records are classified again */
+	/* the latency cap's rates (cfg.group_max_us), EWMAs: a group's submit ->
+	 * records ready per frame byte, and the host's time per frame from a group's
+	 * exposure to the recv_pkts that moves past it (the app's walk + the next
+	 * group's fill and submit) */
+	double ns_per_byte, ns_per_frame;
+	uint64_t t_submit[MOSRX_NSLOT], t_expose;
+	uint64_t cap_frames_last; /* the cap the last group_fill applied (UINT64_MAX: none) */
 	uint32_t nprog;           /* programs of the installed BPF set (0: none) */
 	/* TX: frames written through get_wptr, sent by send_pkts */
 	uint8_t *tx_buf;          /* tx_cap x TX_FRAME_LEN */
@@ -274,6 +287,10 @@ int mosrx_gpu_module_stats_of(struct mtcp_thread_context *ctx, mosrx_gpu_module_
 	if (!pv || !st)
 		return -EINVAL;
 	*st = pv->stats;
+	/* netdev 0's latency-cap state */
+	st->group_cap_frames = pv->ifs[0].cap_frames_last == UINT64_MAX ? 0 : pv->ifs[0].cap_frames_last;
+	st->ns_per_frame_host = pv->ifs[0].ns_per_frame;
+	st->ns_per_byte_dev = pv->ifs[0].ns_per_byte;
 	return 0;
 }
 
@@ -295,10 +312,29 @@ static void gpu_configure_from_mos(void)
 	cfg.num_ifs = (uint32_t)nd->num;
 	cfg.compact = 1;   /* mOS's consumer (mos_rx.c) reads 8-byte records */
 	for (i = 0; i < nd->num; i++) {
+		char var[64];
+		const char *pcap, *tx;
 		strncpy(cfg.if_names[i], nd->ent[i]->dev_name, sizeof(cfg.if_names[i]) - 1);
-		cfg.src[i] = mosrx_source_afpacket(cfg.if_names[i]);
+		/* offline replay: MOSRX_PCAP_<netdev>=file reads a capture instead of the
+		 * interface (MOSRX_PCAP_LOOPS times, default 1), MOSRX_TX_PCAP_<netdev>=file
+		 * dumps what mOS sends on it -- an unmodified mOS application run over a
+		 * recorded trace, e.g. BASELINE config #1's simple_firewall */
+		snprintf(var, sizeof(var), "MOSRX_PCAP_%s", cfg.if_names[i]);
+		pcap = getenv(var);
+		if (pcap) {
+			const char *loops = getenv("MOSRX_PCAP_LOOPS");
+			cfg.src[i] = mosrx_source_pcap(pcap, loops ? (uint32_t)strtoul(loops, NULL, 10) : 1);
+		} else {
+			cfg.src[i] = mosrx_source_afpacket(cfg.if_names[i]);
+		}
 		if (!cfg.src[i]) {   /* as pcap_create failing (pcap_module.c:140-144) */
-			fprintf(stderr, "[mosrx] gpu_module: interface '%s' not found (or no CAP_NET_RAW)\n", cfg.if_names[i]);
+			fprintf(stderr, "[mosrx] gpu_module: %s '%s' not found (or no CAP_NET_RAW)\n",
+			        pcap ? "capture" : "interface", pcap ? pcap : cfg.if_names[i]);
+			exit(EXIT_FAILURE);
+		}
+		snprintf(var, sizeof(var), "MOSRX_TX_PCAP_%s", cfg.if_names[i]);
+		if ((tx = getenv(var)) && mosrx_source_tx_pcap(cfg.src[i], tx)) {
+			fprintf(stderr, "[mosrx] gpu_module: TX dump '%s' cannot be written\n", tx);
 			exit(EXIT_FAILURE);
 		}
 	}
@@ -545,7 +581,7 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 
 /* Receive up to `batch` frames from the netdev's source into stage s, whose
  * descriptors start at *pos in the group block (advanced past what it used). */
-static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint64_t *pos)
+static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint64_t *pos, uint32_t max_n)
 {
 	const uint32_t mf = g_cfg.max_frame;
 	uint64_t at = (*pos + 255) & ~255ull, fpos = 2, cap;
@@ -560,7 +596,7 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
 	if (src && src->borrow) {         /* zero-copy: the source's pinned run is the batch */
 		const uint8_t *f = NULL;
 		uint64_t fb = 0;
-		s->n = src->borrow(src, g_cfg.batch, mf, &f, &fb, s->off, s->len);
+		s->n = src->borrow(src, max_n, mf, &f, &fb, s->off, s->len);
 		if (s->n) {
 			s->frames = (uint8_t *)f;
 			s->bytes = fb;
@@ -570,7 +606,7 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
 		}
 		fpos = 0;
 	} else if (src) {                 /* the source's batch form, or frame by frame (mosrx_source_fill) */
-		const int k = mosrx_source_fill(src, s->frames, cap, s->off, s->len, g_cfg.batch, mf, &s->bytes);
+		const int k = mosrx_source_fill(src, s->frames, cap, s->off, s->len, max_n, mf, &s->bytes);
 		s->n = k > 0 ? (uint32_t)k : 0;
 		if (k <= 0)
 			s->bytes = 2;
@@ -596,14 +632,50 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
  * short ends the group, so nothing waits for frames that are not there yet.
  * Filters or not, the group is one launch (the fused classify + BPF queue
  * kernel when a set is installed). */
+static uint64_t mono_ns(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+/* The latency cap (cfg.group_max_us): the frames and frame bytes a group may
+ * take so that, at the rates measured on this netdev so far, neither its
+ * transfer + classification nor the host's walk of it takes longer than the
+ * budget; never under MOSRX_GROUP_MIN_FRAMES (a group that small is all fixed
+ * costs).  UINT64_MAX when there is no budget or no measurement yet. */
+#define MOSRX_GROUP_MIN_FRAMES 4096u
+static void group_cap(const struct if_state *is, uint64_t *frames, uint64_t *bytes)
+{
+	const double budget = (double)g_cfg.group_max_us * 1e3;
+	*frames = *bytes = UINT64_MAX;
+	if (!g_cfg.group_max_us)
+		return;
+	if (is->ns_per_frame > 0) {
+		*frames = (uint64_t)(budget / is->ns_per_frame);
+		if (*frames < MOSRX_GROUP_MIN_FRAMES)
+			*frames = MOSRX_GROUP_MIN_FRAMES;
+	}
+	if (is->ns_per_byte > 0)
+		*bytes = (uint64_t)(budget / is->ns_per_byte);
+}
+
+static void ewma(double *e, double x)
+{
+	*e = *e > 0 ? 0.75 * *e + 0.25 * x : x;
+}
+
 static void group_fill(struct if_state *is, struct group *g)
 {
 	const uint32_t cap = g->cap_st;
-	uint64_t pos = 0, recs = 0, fbytes = 0;
+	uint64_t pos = 0, recs = 0, fbytes = 0, cap_frames, cap_bytes;
 	uint32_t i;
+	group_cap(is, &cap_frames, &cap_bytes);
+	is->cap_frames_last = cap_frames;
 	g->nst = 0;
 	for (i = 0; i < cap; i++) {
 		struct stage *s = &g->st[i];
+		const uint32_t want = cap_frames - recs < g_cfg.batch ? (uint32_t)(cap_frames - recs) : g_cfg.batch;
 		/* room for this stage: a worst-case one (explicit groups), or its
 		 * descriptors and one largest frame (auto: it stops where the block ends) */
 		const uint64_t need = g_cfg.group == MOSRX_GROUP_AUTO
@@ -611,7 +683,7 @@ static void group_fill(struct if_state *is, struct group *g)
 		                          : stage_bytes();
 		if (pos + need > g->blk_bytes || recs + g_cfg.batch > g->rec_cap)
 			break;
-		stage_fill(g, s, is->src, &pos);
+		stage_fill(g, s, is->src, &pos, want);
 		s->rec0 = (uint32_t)recs;
 		s->res = g->res + recs;
 		s->ti = g->ti ? g->ti + recs : NULL;
@@ -622,11 +694,29 @@ static void group_fill(struct if_state *is, struct group *g)
 		g->nst++;
 		recs += s->n;
 		fbytes += s->bytes;
-		if (s->n < g_cfg.batch)
+		if (s->n < want || recs >= cap_frames || fbytes >= cap_bytes)
 			break;
 		if (g_cfg.group == MOSRX_GROUP_AUTO && fbytes >= g->blk_bytes)
 			break;
 	}
+}
+
+static uint64_t group_frame_bytes(const struct group *g)
+{
+	uint64_t b = 0;
+	uint32_t i;
+	for (i = 0; i < g->nst; i++)
+		b += g->st[i].bytes;
+	return b;
+}
+
+static uint64_t group_frames(const struct group *g)
+{
+	uint64_t n = 0;
+	uint32_t i;
+	for (i = 0; i < g->nst; i++)
+		n += g->st[i].n;
+	return n;
 }
 
 /* Hand the group's borrowed runs back to the source (they are no longer exposed). */
@@ -775,8 +865,12 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 	}
 	/* the exposed group is done with (get_rptr pointers expire here) */
 	k = is->cur < 0 ? 0 : is->cur ^ 1;
-	if (is->cur >= 0)
+	if (is->cur >= 0) {
+		const uint64_t n = group_frames(&is->g[is->cur]);
+		if (n && is->t_expose)   /* the host's time per frame of this group (the latency cap's walk rate) */
+			ewma(&is->ns_per_frame, (double)(mono_ns() - is->t_expose) / (double)n);
 		group_recycle(&is->g[is->cur], is->src);
+	}
 	is->cur = -1;                     /* nothing exposed until a group is ready */
 	if (is->inflight < 0) {           /* nothing in flight: receive + classify now */
 		group_fill(is, &is->g[k]);
@@ -786,13 +880,23 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 			group_drop(pv, is, k);
 			return -1;
 		}
+		is->t_submit[k] = mono_ns();
 		is->inflight = k;
 	}
 	k = is->inflight;
 	is->inflight = -1;
-	if (group_wait(pv, is, k, 1)) {
-		group_drop(pv, is, k);
-		return -1;
+	{
+		/* the group's submit -> records ready, per frame byte: exact when the wait
+		 * blocks; an upper bound when the group was done before we came for it */
+		const int done = mosrx_classify_host_ready(is->mc, k) == 1;
+		if (group_wait(pv, is, k, 1)) {
+			group_drop(pv, is, k);
+			return -1;
+		}
+		const uint64_t b = group_frame_bytes(&is->g[k]);
+		const double x = b ? (double)(mono_ns() - is->t_submit[k]) / (double)b : 0;
+		if (b && (!done || is->ns_per_byte <= 0 || x < is->ns_per_byte))
+			ewma(&is->ns_per_byte, x);
 	}
 	/* classified in flight under a state that has changed since: again, under
 	 * the state the rx loop runs with now */
@@ -802,14 +906,23 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 	}
 	is->cur = k;
 	is->cur_idx = 0;
+	is->t_expose = mono_ns();
+	{
+		const uint64_t n = group_frames(&is->g[k]);
+		pv->stats.rx_groups++;
+		if (n > pv->stats.max_group_frames)
+			pv->stats.max_group_frames = n;
+	}
 	if (g_cfg.pipeline) {             /* classify the next group behind the app's work */
 		int nk = k ^ 1;
 		group_fill(is, &is->g[nk]);
 		if (is->g[nk].nst) {
-			if (group_submit(pv, is, nk, 0) == 0)
+			if (group_submit(pv, is, nk, 0) == 0) {
+				is->t_submit[nk] = mono_ns();
 				is->inflight = nk;
-			else
+			} else {
 				group_drop(pv, is, nk);
+			}
 		}
 	}
 	return (int32_t)is->g[k].st[0].n;

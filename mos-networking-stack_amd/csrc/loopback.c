@@ -681,6 +681,124 @@ int mosrx_source_afpacket_info(mosrx_source *s_, mosrx_afpacket_info *info)
 	return 0;
 }
 
+/* ---------------- paced arrivals ---------------- */
+/* A wire at a fixed frame rate in front of another source: frame k "arrives"
+ * at t0 + k / rate (t0: the first receive call) and is handed out by no
+ * receive before that, as a NIC ring fills at line rate.  What the backend
+ * receives per call is what has arrived by then, so group sizes follow the
+ * load; the latency probe (rx_loop.c) turns frame k's arrival into its
+ * residency.  The inner source keeps its receive forms (fill / borrow), capped
+ * at the frames that have arrived. */
+struct src_paced {
+	struct mosrx_source base;
+	struct mosrx_source *in;
+	double ns_per_frame;
+	uint64_t t0_ns, released;
+};
+
+static uint64_t mono_ns(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+/* frames that have arrived and were not handed out yet, at most max_n */
+static uint32_t paced_ready(struct src_paced *s, uint32_t max_n)
+{
+	uint64_t now = mono_ns(), arrived;
+	if (!s->t0_ns)
+		s->t0_ns = now;
+	arrived = (uint64_t)((double)(now - s->t0_ns) / s->ns_per_frame) + 1;
+	arrived = arrived > s->released ? arrived - s->released : 0;
+	return arrived < max_n ? (uint32_t)arrived : max_n;
+}
+
+static int paced_next(struct mosrx_source *s_, uint8_t *dst, uint32_t cap)
+{
+	struct src_paced *s = (struct src_paced *)s_;
+	int l;
+	if (!paced_ready(s, 1))
+		return 0;
+	l = s->in->next ? s->in->next(s->in, dst, cap) : 0;
+	s->released += l > 0;
+	return l;
+}
+
+static uint32_t paced_fill(struct mosrx_source *s_, uint8_t *frames, uint64_t cap, uint32_t *off, uint16_t *len,
+                           uint32_t max_n, uint32_t max_frame, uint64_t *end)
+{
+	struct src_paced *s = (struct src_paced *)s_;
+	const uint32_t n = paced_ready(s, max_n);
+	int k;
+	*end = 2;
+	if (!n)
+		return 0;
+	k = mosrx_source_fill(s->in, frames, cap, off, len, n, max_frame, end);
+	if (k <= 0)
+		return 0;
+	s->released += (uint32_t)k;
+	return (uint32_t)k;
+}
+
+static uint32_t paced_borrow(struct mosrx_source *s_, uint32_t max_n, uint32_t max_frame, const uint8_t **frames,
+                             uint64_t *frames_bytes, uint32_t *off, uint16_t *len)
+{
+	struct src_paced *s = (struct src_paced *)s_;
+	const uint32_t n = paced_ready(s, max_n);
+	uint32_t k;
+	if (!n)
+		return 0;
+	k = s->in->borrow(s->in, n, max_frame, frames, frames_bytes, off, len);
+	s->released += k;
+	return k;
+}
+
+static void paced_give_back(struct mosrx_source *s_)
+{
+	struct src_paced *s = (struct src_paced *)s_;
+	if (s->in->give_back)
+		s->in->give_back(s->in);
+}
+
+static void paced_close(struct mosrx_source *s_)
+{
+	struct src_paced *s = (struct src_paced *)s_;
+	mosrx_source_close(s->in);
+	free(s);
+}
+
+mosrx_source *mosrx_source_paced(mosrx_source *inner, double rate_pps)
+{
+	struct src_paced *s;
+	if (!inner || !(rate_pps > 0) || inner->close == afp_close)
+		return NULL;
+	s = calloc(1, sizeof(*s));
+	if (!s)
+		return NULL;
+	s->in = inner;
+	s->ns_per_frame = 1e9 / rate_pps;
+	s->base.next = paced_next;
+	s->base.fill = paced_fill;
+	if (inner->borrow) {
+		s->base.borrow = paced_borrow;
+		s->base.give_back = paced_give_back;
+	}
+	s->base.close = paced_close;
+	return &s->base;
+}
+
+int mosrx_source_paced_info(const mosrx_source *s_, uint64_t *t0_ns, double *ns_per_frame, uint64_t *released)
+{
+	const struct src_paced *s = (const struct src_paced *)s_;
+	if (!s_ || s_->close != paced_close)
+		return -EINVAL;
+	if (t0_ns) *t0_ns = s->t0_ns;
+	if (ns_per_frame) *ns_per_frame = s->ns_per_frame;
+	if (released) *released = s->released;
+	return 0;
+}
+
 /* ---------------- transmit ---------------- */
 /* A frame handed to send_pkts leaves through the source it belongs to: the
  * AF_PACKET socket (pcap_inject, pcap_module.c:67-79) or, when a TX dump is

@@ -201,10 +201,12 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 		    hipHostMalloc((void **)&c->slot[i].h_qdesc, MOSRX_MAX_GROUP * sizeof(mosrx_qdesc),
 		                  hipHostMallocDefault) != hipSuccess ||
 		    hipMalloc((void **)&c->slot[i].d_cnt, MOSRX_CNT_WORDS * 4) != hipSuccess ||
-		    hipHostMalloc((void **)&c->slot[i].h_cnt, MOSRX_CNT_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
+		    hipHostMalloc((void **)&c->slot[i].h_cnt, MOSRX_CNT_WORDS * 4, hipHostMallocDefault) != hipSuccess ||
+		    !(c->slot[i].h_prev = calloc(MOSRX_CNT_WORDS, 4))) {
 			mosrx_close(c);
 			return -ENODEV;
 		}
+		c->slot[i].cnt_dirty = 1;   /* the first launch on the slot zeroes its counters */
 	}
 	if ((rc = mosrx_set_params(c, p))) {
 		mosrx_close(c);
@@ -250,6 +252,7 @@ void mosrx_close(mosrx_ctx *c)
 		if (c->slot[i].h_qdesc) hipHostFree(c->slot[i].h_qdesc);
 		if (c->slot[i].d_cnt) hipFree(c->slot[i].d_cnt);
 		if (c->slot[i].h_cnt) hipHostFree(c->slot[i].h_cnt);
+		free(c->slot[i].h_prev);
 		if (c->slot[i].h_txc) hipHostFree(c->slot[i].h_txc);
 		slot_free(&c->slot[i]);
 	}
@@ -621,6 +624,21 @@ int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uin
 	return 0;
 }
 
+/* Before a launch that adds to the slot's reason counters: zero them only when
+ * their device value is not known to equal h_prev (mosrx_ctx.h); the launch
+ * leaves them unknown until its wait has taken its counts. */
+static hipError_t counters_arm(struct slot *s)
+{
+	if (s->cnt_dirty) {
+		hipError_t e = hipMemsetAsync(s->d_cnt, 0, MOSRX_CNT_WORDS * 4, s->stream);
+		if (e != hipSuccess)
+			return e;
+		memset(s->h_prev, 0, MOSRX_CNT_WORDS * 4);
+	}
+	s->cnt_dirty = 1;
+	return hipSuccess;
+}
+
 /* Enqueue one end-to-end batch on slot s: H2D frames+descriptors, kernel, D2H results. */
 /* h_fhash: flow hashes; h_match: the installed BPF set's match masks (one of
  * the two at most; both use the slot's per-frame u32 buffer); h_ti: pkt_info
@@ -646,7 +664,7 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 		HIPCHK(hipMemcpyAsync(s->d_off, b->off, (size_t)b->n * 4, hipMemcpyHostToDevice, s->stream));
 		HIPCHK(hipMemcpyAsync(s->d_len, b->len, (size_t)b->n * 2, hipMemcpyHostToDevice, s->stream));
 	}
-	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_CNT_WORDS * 4, s->stream));
+	HIPCHK(counters_arm(s));
 	if (c->timing) {
 		/* one launch: its dispatch stamps its own duration (no queueing gap before it);
 		 * the classify + BPF pair: events around both */
@@ -730,7 +748,6 @@ int mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mos
 	if (c->slot[slot].busy)
 		return -EBUSY;
 	if (b->n == 0) {
-		memset(c->slot[slot].h_cnt, 0, MOSRX_CNT_WORDS * 4);
 		c->slot[slot].busy = 2;   /* nothing enqueued */
 		return 0;
 	}
@@ -751,7 +768,6 @@ int mosrx_classify_bpf_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b,
 	if (c->slot[slot].busy)
 		return -EBUSY;
 	if (b->n == 0) {
-		memset(c->slot[slot].h_cnt, 0, MOSRX_CNT_WORDS * 4);
 		c->slot[slot].busy = 2;   /* nothing enqueued */
 		return 0;
 	}
@@ -781,11 +797,17 @@ int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
 		HIPCHK(hipEventSynchronize(s->done));
 	{
 		uint32_t r, k;
-		for (r = 0; r < MOSRX_R_COUNT; r++) {   /* the counter shards of the batch's workgroups */
-			uint32_t sum = 0;
+		for (r = 0; r < MOSRX_R_COUNT; r++)
+			c->h_cnt[r] = 0;
+		if (s->busy == 1) {
+			/* the batch's counts: what its launch added to every shard since the last wait */
 			for (k = 0; k < MOSRX_CNT_SHARDS; k++)
-				sum += s->h_cnt[k * MOSRX_CNT_STRIDE + r];
-			c->h_cnt[r] = sum;
+				for (r = 0; r < MOSRX_R_COUNT; r++) {
+					const uint32_t w = k * MOSRX_CNT_STRIDE + r;
+					c->h_cnt[r] += s->h_cnt[w] - s->h_prev[w];
+					s->h_prev[w] = s->h_cnt[w];
+				}
+			s->cnt_dirty = 0;
 		}
 	}
 	c->last_kernel_ms = -1.0f;
@@ -793,6 +815,17 @@ int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
 		c->last_kernel_ms = -1.0f;
 	s->busy = 0;
 	return 0;
+}
+
+int mosrx_classify_host_ready(mosrx_ctx *c, int slot)
+{
+	hipError_t e;
+	if (!c || slot < 0 || slot >= NSLOT)
+		return -EINVAL;
+	if (c->slot[slot].busy != 1)
+		return 1;
+	e = hipEventQuery(c->slot[slot].done);
+	return e == hipSuccess ? 1 : e == hipErrorNotReady ? 0 : -EIO;
 }
 
 int mosrx_set_timing(mosrx_ctx *c, int on)
@@ -908,7 +941,6 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 		                          mosrx__host_range_of(b[i].len, (uint64_t)b[i].n * 2)};
 	}
 	if (ntot == 0) {
-		memset(s->h_cnt, 0, MOSRX_CNT_WORDS * 4);
 		s->busy = 2;
 		return 0;
 	}
@@ -951,7 +983,7 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 		pre += b[i].n;
 	}
 	HIPCHK(hipMemcpyAsync(s->d_qdesc, s->h_qdesc, nb * sizeof(mosrx_qdesc), hipMemcpyHostToDevice, s->stream));
-	HIPCHK(hipMemsetAsync(s->d_cnt, 0, MOSRX_CNT_WORDS * 4, s->stream));
+	HIPCHK(counters_arm(s));
 	qp.desc = s->d_qdesc;
 	qp.tables = c->d_tables;
 	qp.counters = s->d_cnt;
@@ -1059,7 +1091,6 @@ int mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b, 
 	if (c->slot[slot].busy)
 		return -EBUSY;
 	if (b->n == 0) {
-		memset(c->slot[slot].h_cnt, 0, MOSRX_CNT_WORDS * 4);
 		c->slot[slot].busy = 2;
 		return 0;
 	}

@@ -44,7 +44,15 @@ struct slot {
 	uint32_t cap_n;
 	hipStream_t stream;
 	hipEvent_t done;
-	uint32_t *h_cnt;   /* MOSRX_R_COUNT, pinned: a D2H copy into pageable memory blocks the host */
+	uint32_t *h_cnt;   /* MOSRX_CNT_WORDS, pinned: a D2H copy into pageable memory blocks the host */
+	/* The counters only grow: a submit adds to d_cnt and copies it back into
+	 * h_cnt, and the wait takes the batch's counts as h_cnt - h_prev (u32
+	 * arithmetic, so wrapping is harmless), then keeps h_cnt as h_prev.  No
+	 * memset (a blit kernel and a dependent dispatch) per submit; cnt_dirty: the
+	 * device words are not h_prev (first use, a submit that failed after its
+	 * launch), and the next submit zeroes both. */
+	uint32_t *h_prev;
+	int cnt_dirty;
 	hipEvent_t kev0, kev1;     /* around the kernel of the last submit (when the context times) */
 	mosrx_qdesc *h_qdesc;      /* MOSRX_MAX_GROUP, pinned: a group's batch table */
 	mosrx_tx_check *h_txc;     /* pinned: the TX pass's check records (mosrx_tx_csum_host), h_txc_n of them */

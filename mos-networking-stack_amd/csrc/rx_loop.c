@@ -23,6 +23,9 @@
 
 #define ETHER_OVR 24
 
+static uint64_t now_ns(void);
+static void latency_batch(mosrx_latency_probe *p, uint64_t n, uint64_t t_avail, uint64_t t_end);
+
 static uint64_t now_us(void)
 {
 	struct timespec ts;
@@ -49,6 +52,7 @@ int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx,
 			mosrx_result one;
 			int32_t recv_cnt = iom->recv_pkts(ctx, rx_inf);
 			int32_t i;
+			const uint64_t t_avail = o->probe && recv_cnt > 0 ? now_ns() : 0;
 			if (recv_cnt < 0) {        /* RunMainLoop's for loop just skips it (core.c:899-902) */
 				st->recv_errors++;
 				continue;
@@ -73,6 +77,8 @@ int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx,
 					if (res8[i].reason < MOSRX_R_COUNT)
 						st->by_reason[res8[i].reason]++;
 				}
+				if (o->probe)
+					latency_batch(o->probe, (uint64_t)recv_cnt, t_avail, now_ns());
 				continue;
 			}
 			memset(&one, 0, sizeof(one));
@@ -98,6 +104,8 @@ int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx,
 				if (fn)
 					fn(arg, rx_inf, i, pkt, len, r);
 			}
+			if (o->probe)
+				latency_batch(o->probe, (uint64_t)recv_cnt, t_avail, now_ns());
 		}
 		if (iom->send_pkts)               /* core.c:999-1007: flush what the round wrote */
 			for (rx_inf = 0; rx_inf < nif; rx_inf++)
@@ -120,8 +128,100 @@ int mosrx_rx_loop_ex(const io_module_func *iom, struct mtcp_thread_context *ctx,
 int mosrx_rx_loop(const io_module_func *iom, struct mtcp_thread_context *ctx, int nif,
                   uint64_t max_pkts, mosrx_pkt_fn fn, void *arg, mosrx_rx_stats *st)
 {
-	const mosrx_rx_loop_opts o = {max_pkts, 1, 0, 0};   /* a finite source: stop at the first idle round */
+	const mosrx_rx_loop_opts o = {max_pkts, 1, 0, 0, NULL};   /* a finite source: stop at the first idle round */
 	return mosrx_rx_loop_ex(iom, ctx, nif, &o, fn, arg, st);
+}
+
+/* ---- per-frame residency of a paced source (mosrx_rx_loop_opts.probe) ----
+ * Frames from a paced source arrive at t0 + k * p and come through the
+ * backend in order, so the k-th frame the loop receives is arrival k.  Per
+ * batch of n frames starting at k0, the loop reads the clock twice: when
+ * recv_pkts has returned it with its records (t_avail) and when its walk ends
+ * (t_end).  Frame k0 + i then has
+ *   recv -> verdict available  t_avail - (t0 + (k0 + i) p)
+ *   recv -> consumed           t_avail + i (t_end - t_avail) / n - (t0 + (k0 + i) p)
+ * (the walk taken as even over the batch), both linear in i, so each batch
+ * goes into the log-spaced histograms by bins, not by frames: the probe costs
+ * the loop two clock reads per batch, nothing per frame. */
+static uint64_t now_ns(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+static uint32_t lat_bin(uint64_t v)
+{
+	uint32_t b;
+	if (v < 16)
+		return (uint32_t)v;
+	b = 63u - (uint32_t)__builtin_clzll(v);
+	return b * 16u + (uint32_t)((v >> (b - 4)) & 15u);
+}
+
+/* the lowest value of bin b + 1 (bins are contiguous and increasing) */
+static double bin_end(uint32_t b)
+{
+	uint32_t e;
+	if (b < 16)
+		return (double)(b + 1);
+	e = b / 16u;
+	return (double)(16u + b % 16u + 1u) * (double)(1ull << (e - 4));
+}
+
+/* values a + i d, i in [0, n), clamped at 0, counted into hist; returns the largest */
+static uint64_t hist_ramp(uint64_t *hist, double a, double d, uint64_t n)
+{
+	double lo = a, hi = a + d * (double)(n - 1);
+	uint64_t done = 0;
+	if (d < 0) {               /* count from the small end up: i runs backwards */
+		a = hi;
+		d = -d;
+		hi = lo;
+		lo = a;
+	}
+	while (done < n) {
+		const double v = lo + d * (double)done;
+		const uint32_t b = lat_bin(v > 0 ? (uint64_t)v : 0);
+		uint64_t k;
+		if (b >= MOSRX_LAT_BINS - 1 || d <= 0) {
+			k = n - done;
+		} else {
+			/* values of this bin: v + j d < bin_end(b) */
+			const double room = bin_end(b) - v;
+			k = room > 0 ? (uint64_t)(room / d) + 1 : 1;
+			if (k > n - done)
+				k = n - done;
+		}
+		hist[b < MOSRX_LAT_BINS ? b : MOSRX_LAT_BINS - 1] += k;
+		done += k;
+	}
+	return hi > 0 ? (uint64_t)hi : 0;
+}
+
+static void latency_batch(mosrx_latency_probe *p, uint64_t n, uint64_t t_avail, uint64_t t_end)
+{
+	uint64_t k0 = p->seen, skip = 0, m;
+	double a;
+	p->seen += n;
+	if (!p->t0_ns && p->src)
+		mosrx_source_paced_info(p->src, &p->t0_ns, &p->ns_per_frame, NULL);
+	if (k0 + n <= p->skip || !p->t0_ns)
+		return;
+	if (k0 < p->skip)
+		skip = p->skip - k0;
+	k0 += skip;
+	n -= skip;
+	a = (double)t_avail - ((double)p->t0_ns + (double)k0 * p->ns_per_frame);
+	m = hist_ramp(p->avail_hist, a, -p->ns_per_frame, n);
+	if (m > p->avail_max_ns)
+		p->avail_max_ns = m;
+	m = hist_ramp(p->done_hist, a + (double)skip * (double)(t_end - t_avail) / (double)(n + skip),
+	              (double)(t_end - t_avail) / (double)(n + skip) - p->ns_per_frame, n);
+	if (m > p->done_max_ns)
+		p->done_max_ns = m;
+	p->recorded += n;
+	p->batches++;
 }
 
 int mosrx_mos_forwards(const mosrx_result *res, int forward, uint32_t num_msp, uint32_t listener)

@@ -133,7 +133,7 @@ class ModuleCfg(C.Structure):
                 ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32),
                 ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32),
                 ("group_bytes", C.c_uint64), ("flowhash", C.c_int32), ("tx_csum", C.c_int32),
-                ("numa", C.c_int32), ("compact", C.c_int32)]
+                ("numa", C.c_int32), ("compact", C.c_int32), ("group_max_us", C.c_uint32)]
 
 
 class ModuleStats(C.Structure):
@@ -141,12 +141,42 @@ class ModuleStats(C.Structure):
                 ("tx_bytes", C.c_uint64), ("tx_errors", C.c_uint64), ("kernel_launches", C.c_uint64),
                 ("kernel_ms", C.c_double), ("rx_drops", C.c_uint64),
                 ("rx_reclassified", C.c_uint64), ("cpu", C.c_int32), ("device", C.c_int32),
-                ("tx_csum_offloaded", C.c_uint64), ("cpu_node", C.c_int32), ("gpu_node", C.c_int32)]
+                ("tx_csum_offloaded", C.c_uint64), ("cpu_node", C.c_int32), ("gpu_node", C.c_int32),
+                ("rx_groups", C.c_uint64), ("max_group_frames", C.c_uint64), ("group_cap_frames", C.c_uint64),
+                ("ns_per_frame_host", C.c_double), ("ns_per_byte_dev", C.c_double)]
+
+
+LAT_BINS = 1024
+
+
+class LatencyProbe(C.Structure):
+    """mosrx_latency_probe (include/mosrx_io_module.h): residency histograms of
+    frames from a paced source, filled by the rx loop (RxLoopOpts.probe)."""
+    _fields_ = [("src", C.c_void_p), ("t0_ns", C.c_uint64), ("ns_per_frame", C.c_double),
+                ("skip", C.c_uint64), ("seen", C.c_uint64), ("recorded", C.c_uint64), ("batches", C.c_uint64),
+                ("avail_max_ns", C.c_uint64), ("done_max_ns", C.c_uint64),
+                ("avail_hist", C.c_uint64 * LAT_BINS), ("done_hist", C.c_uint64 * LAT_BINS)]
+
+    @staticmethod
+    def bin_ns(b: int) -> float:
+        """The middle of histogram bin b, ns (16 bins per octave above 16 ns)."""
+        if b < 16:
+            return float(b)
+        e, m = b // 16, b % 16
+        return ((16 + m) + 0.5) * 2.0 ** (e - 4)
+
+    def percentiles(self, which: str = "avail", ps=(50, 99, 99.9)) -> dict:
+        h = np.array(getattr(self, which + "_hist")[:], dtype=np.float64)
+        tot = h.sum()
+        if tot == 0:
+            return {}
+        cum = np.cumsum(h) / tot
+        return {f"p{p:g}_us": round(self.bin_ns(int(np.searchsorted(cum, p / 100.0))) / 1e3, 2) for p in ps}
 
 
 class RxLoopOpts(C.Structure):
     _fields_ = [("max_pkts", C.c_uint64), ("idle_rounds", C.c_uint32), ("idle_us", C.c_uint32),
-                ("max_us", C.c_uint64)]
+                ("max_us", C.c_uint64), ("probe", C.c_void_p)]
 
 
 class AfpOpts(C.Structure):
@@ -262,6 +292,9 @@ def lib():
             "mosrx_gpu_module_bind": (I, [P, I]),
             "mosrx_rx_loop": (I, [P, P, I, U64, P, P, C.POINTER(RxStats)]),
             "mosrx_rx_loop_ex": (I, [P, P, I, C.POINTER(RxLoopOpts), P, P, C.POINTER(RxStats)]),
+            "mosrx_source_paced": (P, [P, C.c_double]),
+            "mosrx_source_paced_info": (I, [P, C.POINTER(U64), C.POINTER(C.c_double), C.POINTER(U64)]),
+            "mosrx_classify_host_ready": (I, [P, I]),
             "mosrx_mos_forwards": (I, [P, I, U32, U32]),
             "mosrx_device_count": (I, []),
             "mosrx_classify_host_submit_ex": (I, [P, I, C.POINTER(Batch), P, P]),
@@ -305,7 +338,25 @@ def lib():
             fn.restype = res
             fn.argtypes = args
         _lib = L
+        _sigs.update(sig)
     return _lib
+
+
+_sigs = {}
+
+
+def module_lib(path: str):
+    """Another build of gpu_module_func (e.g. the CPU test suite's build of the
+    module over a stand-in for the GPU): a CDLL whose mosrx_gpu_module_*
+    functions carry libmosrx's signatures, for GpuBackend(module_lib=...)."""
+    lib()
+    L = C.CDLL(path)
+    for name, (res, args) in _sigs.items():
+        if name.startswith("mosrx_gpu_module_"):
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+    return L
 
 
 def _chk(rc: int, what: str):
@@ -979,9 +1030,10 @@ class GpuBackend:
                  max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
                  ngpu: int = 1, bpf=None, group: int = 1, tcpinfo: bool = False, tx_batch: int = 64,
                  timing: bool = False, flowhash: bool = False, tx_csum: bool = False, compact: bool = False,
-                 group_bytes: int = 0):
+                 group_bytes: int = 0, group_max_us: int = 0, module_lib=None):
+        self.L = L = module_lib or lib()
         cfg = ModuleCfg()
-        lib().mosrx_gpu_module_cfg_default(C.byref(cfg))
+        L.mosrx_gpu_module_cfg_default(C.byref(cfg))
         cfg.num_ifs = len(sources)
         for i, s in enumerate(sources):
             cfg.src[i] = s
@@ -992,6 +1044,7 @@ class GpuBackend:
         cfg.tx_csum = int(tx_csum)
         cfg.compact = int(compact)          # 8-byte records (results8); 16-byte ones with filters
         cfg.group_bytes = group_bytes       # auto groups' frame bytes per launch (0: MOSRX_GROUP_AUTO_BYTES)
+        cfg.group_max_us = group_max_us     # a group's latency budget (0: none)
         if params is not None:
             cfg.params = params
         self.params = Params.from_buffer_copy(cfg.params)
@@ -1000,13 +1053,13 @@ class GpuBackend:
             self._bpf = _bpf_progs(bpf)          # kept alive until init_handle has installed them
             cfg.bpf_progs = C.addressof(self._bpf[0])
             cfg.bpf_nprog = len(bpf)
-        _chk(lib().mosrx_gpu_module_configure(C.byref(cfg)), "mosrx_gpu_module_configure")
+        _chk(L.mosrx_gpu_module_configure(C.byref(cfg)), "mosrx_gpu_module_configure")
         self.nif = len(sources)
         self.sources = list(sources)
-        self.m = gpu_module()
+        self.m = IoModuleFunc.in_dll(L, "gpu_module_func")
         self._ctx_obj = C.c_uint64(0xC0DE0000 + cpu)      # stands in for struct mtcp_thread_context *
         self.ctx = C.addressof(self._ctx_obj)
-        _chk(lib().mosrx_gpu_module_bind(self.ctx, cpu), "mosrx_gpu_module_bind")
+        _chk(L.mosrx_gpu_module_bind(self.ctx, cpu), "mosrx_gpu_module_bind")
         _VOIDFN(self.m.load_module_upper_half)()
         _CTXFN(self.m.init_handle)(self.ctx)
         self._recv = _RECVFN(self.m.recv_pkts)
@@ -1015,7 +1068,7 @@ class GpuBackend:
         self._wptr = _WPTRFN(self.m.get_wptr)
         self._send = _SENDFN(self.m.send_pkts)
         if timing:
-            _chk(lib().mosrx_gpu_module_set_timing(self.ctx, 1), "mosrx_gpu_module_set_timing")
+            _chk(L.mosrx_gpu_module_set_timing(self.ctx, 1), "mosrx_gpu_module_set_timing")
 
     def recv_pkts(self, ifidx: int = 0) -> int:
         return self._recv(self.ctx, ifidx)
@@ -1091,7 +1144,7 @@ class GpuBackend:
 
     def stats(self) -> ModuleStats:
         st = ModuleStats()
-        _chk(lib().mosrx_gpu_module_stats_of(self.ctx, C.byref(st)), "mosrx_gpu_module_stats_of")
+        _chk(self.L.mosrx_gpu_module_stats_of(self.ctx, C.byref(st)), "mosrx_gpu_module_stats_of")
         return st
 
     def forwarder(self, out_if: list[int], listener: bool = False) -> Forwarder:
@@ -1111,13 +1164,15 @@ class GpuBackend:
         return None if self._ioctl(self.ctx, ifidx, PKT_RX_RSS, C.byref(ri)) else ri.hash_value
 
     def run_loop(self, max_pkts: int = 0, idle_rounds: int = 1, idle_us: int = 0, max_us: int = 0,
-                 forward: Forwarder | None = None) -> RxStats:
-        """mosrx_rx_loop_ex over this backend; `forward`: the mosrx_forward_frame consumer."""
+                 forward: Forwarder | None = None, probe: LatencyProbe | None = None) -> RxStats:
+        """mosrx_rx_loop_ex over this backend; `forward`: the mosrx_forward_frame
+        consumer; `probe`: the residency of a paced source's frames (RxLoopOpts.probe)."""
         st = RxStats()
-        o = RxLoopOpts(max_pkts, idle_rounds, idle_us, max_us)
-        fn = C.cast(lib().mosrx_forward_frame, C.c_void_p) if forward is not None else None
-        _chk(lib().mosrx_rx_loop_ex(C.addressof(self.m), self.ctx, self.nif, C.byref(o), fn,
-                                    C.byref(forward) if forward is not None else None, C.byref(st)),
+        o = RxLoopOpts(max_pkts, idle_rounds, idle_us, max_us, C.addressof(probe) if probe is not None else None)
+        fn, arg = None, None
+        if forward is not None:
+            fn, arg = C.cast(lib().mosrx_forward_frame, C.c_void_p), C.byref(forward)
+        _chk(lib().mosrx_rx_loop_ex(C.addressof(self.m), self.ctx, self.nif, C.byref(o), fn, arg, C.byref(st)),
              "mosrx_rx_loop_ex")
         return st
 
@@ -1131,6 +1186,14 @@ class GpuBackend:
 
 
 SRC_BEST, SRC_FILL, SRC_PER_FRAME = 0, 1, 2
+
+
+def paced_source(inner: int, rate_pps: float) -> int:
+    """mosrx_source_paced: `inner`'s frames released at rate_pps (takes inner over)."""
+    s = lib().mosrx_source_paced(inner, float(rate_pps))
+    if not s:
+        raise MosrxError(22, "mosrx_source_paced")
+    return s
 
 
 def mem_source(frames: np.ndarray, off: np.ndarray, ln: np.ndarray, loops: int = 1, mode: int = SRC_BEST) -> int:

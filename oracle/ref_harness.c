@@ -50,15 +50,20 @@
  *   <seconds>; one JSON line.  The reference's per-frame rx cost as the rx loop
  *   pays it, stream lookup included.
  *
- * Usage: mosref --time <trace.in> <seconds>
- *   CPU baseline of the reference's own per-frame arithmetic on this host, one
- *   thread: the header checks of eth_in.c / ip_in.c / tcp.c, ip_fast_csum,
- *   TCPCalcChecksum, GetRSSHash and GetRSSCPUCore
- *   over every frame, passes repeated for at least <seconds>.  Prints one JSON
- *   line.  ProcessPacket itself is not timed: past the checksum it runs
- *   FindStream and the stateful flow engine (out of scope).
+ * Usage: mosref --time <trace.in> <seconds> [threads]
+ *   CPU baseline of the reference's own per-frame arithmetic on this host: the
+ *   header checks of eth_in.c / ip_in.c / tcp.c, ip_fast_csum, TCPCalcChecksum,
+ *   GetRSSHash and GetRSSCPUCore over every frame,
+ *   passes repeated for at least <seconds>.  Prints one JSON line.  With
+ *   `threads` > 1, one pthread per disjoint slice of the trace, all started
+ *   together, each repeating passes over its own slice (mOS's per-core
+ *   sharding: one mTCP thread per core, each on its own RSS queue's frames,
+ *   core.c:1369-1466); the rate is every thread's frames over the longest
+ *   thread's time.  ProcessPacket itself is not timed: past the checksum it
+ *   runs FindStream and the stateful flow engine (out of scope).
  */
 #include <arpa/inet.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -148,25 +153,80 @@ static double now_s(void)
 	return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
-static int time_mode(uint32_t n, const uint32_t *off, const uint16_t *len, const uint8_t *frames, int nq,
-                     double seconds)
+struct slice {
+	const uint32_t *off;
+	const uint16_t *len;
+	const uint8_t *frames;
+	uint32_t lo, hi;
+	int nq;
+	double seconds, el;
+	uint64_t passes;
+	uint32_t sink;
+	pthread_barrier_t *go;
+};
+
+static void *slice_run(void *arg)
 {
-	uint64_t passes = 0, bytes = 0;
+	struct slice *s = arg;
 	uint32_t i, sink = 0;
+	uint64_t passes = 0;
 	double t0, el;
-	for (i = 0; i < n; i++)
-		bytes += len[i];
+	pthread_barrier_wait(s->go);
 	t0 = now_s();
 	do {
-		for (i = 0; i < n; i++)
-			sink += ref_frame(frames + off[i], len[i], nq);
+		for (i = s->lo; i < s->hi; i++)
+			sink += ref_frame(s->frames + s->off[i], s->len[i], s->nq);
 		passes++;
 		el = now_s() - t0;
-	} while (el < seconds);
-	printf("{\"frames\": %u, \"passes\": %llu, \"seconds\": %.3f, \"mpkts\": %.4f, "
+	} while (el < s->seconds);
+	s->el = el;
+	s->passes = passes;
+	s->sink = sink;
+	return NULL;
+}
+
+static int time_mode(uint32_t n, const uint32_t *off, const uint16_t *len, const uint8_t *frames, int nq,
+                     double seconds, int threads)
+{
+	struct slice *sl;
+	pthread_t *th;
+	pthread_barrier_t go;
+	uint64_t frames_done = 0, bytes_done = 0, passes = 0;
+	uint32_t i, sink = 0;
+	double el = 0;
+	int t;
+	if (threads < 1 || (uint32_t)threads > n)
+		threads = 1;
+	sl = calloc((size_t)threads, sizeof(*sl));
+	th = calloc((size_t)threads, sizeof(*th));
+	if (!sl || !th || pthread_barrier_init(&go, NULL, (unsigned)threads))
+		return 1;
+	for (t = 0; t < threads; t++) {
+		sl[t] = (struct slice){off, len, frames, (uint32_t)((uint64_t)n * t / threads),
+		                       (uint32_t)((uint64_t)n * (t + 1) / threads), nq, seconds, 0, 0, 0, &go};
+		if (t && pthread_create(&th[t], NULL, slice_run, &sl[t]))
+			return 1;
+	}
+	slice_run(&sl[0]);
+	for (t = 1; t < threads; t++)
+		pthread_join(th[t], NULL);
+	for (t = 0; t < threads; t++) {
+		uint64_t b = 0;
+		for (i = sl[t].lo; i < sl[t].hi; i++)
+			b += len[i];
+		frames_done += (uint64_t)(sl[t].hi - sl[t].lo) * sl[t].passes;
+		bytes_done += b * sl[t].passes;
+		passes += sl[t].passes;
+		sink += sl[t].sink;
+		el = sl[t].el > el ? sl[t].el : el;
+	}
+	printf("{\"frames\": %u, \"threads\": %d, \"passes\": %llu, \"seconds\": %.3f, \"mpkts\": %.4f, "
 	       "\"caplen_gbps\": %.4f, \"sink\": %u}\n",
-	       n, (unsigned long long)passes, el, (double)n * passes / el / 1e6, (double)bytes * passes / el / 1e9,
+	       n, threads, (unsigned long long)passes, el, (double)frames_done / el / 1e6, (double)bytes_done / el / 1e9,
 	       sink);
+	pthread_barrier_destroy(&go);
+	free(sl);
+	free(th);
 	return 0;
 }
 
@@ -190,10 +250,12 @@ int main(int argc, char **argv)
 	static io_module_func null_iom;
 	static log_thread_context lg;
 
-	int timing = argc == 4 && !strcmp(argv[1], "--time");
+	int timing = (argc == 4 || argc == 5) && !strcmp(argv[1], "--time");
+	const int threads = timing && argc == 5 ? atoi(argv[4]) : 1;
 	const int timing_pp = argc == 4 && !strcmp(argv[1], "--time-pp");
 	if (argc != 3 && !timing && !timing_pp) {
-		fprintf(stderr, "usage: %s trace.in results.out | %s --time[-pp] trace.in seconds\n", argv[0], argv[0]);
+		fprintf(stderr, "usage: %s trace.in results.out | %s --time trace.in seconds [threads] | "
+		        "%s --time-pp trace.in seconds\n", argv[0], argv[0], argv[0]);
 		return 2;
 	}
 	if (timing_pp)
@@ -223,7 +285,7 @@ int main(int argc, char **argv)
 	fclose(in);
 	g_qmode = qmode;
 	if (timing)
-		return time_mode(n, off, len, frames, nq, atof(argv[2]));
+		return time_mode(n, off, len, frames, nq, atof(argv[2]), threads);
 
 	/* stack state: core.c:1079-1110 InitializeMTCPManager, reduced */
 	nd.num = (int)nlocal;

@@ -885,8 +885,20 @@ def measure_e2e(ctx, tr: mosrx.Trace, iters: int, sync=lambda: None):
                       "mosrx_source_fill), one H2D copy, kernel, D2H records; 2 streams"}
 
 
+_BACKEND_TRACES = {}
+
+
+def backend_trace(key: str, n: int) -> mosrx.Trace:
+    """The backend legs' trace of n frames (generated once per size: the auto
+    groups' traces are 1.3-2.3 GB)."""
+    if (key, n) not in _BACKEND_TRACES:
+        _BACKEND_TRACES[(key, n)] = mosrx.Trace({"S64": mosrx.TRACE_S64, "M1500": mosrx.TRACE_M1500,
+                                                 "IMIX": mosrx.TRACE_IMIX}[key], n)
+    return _BACKEND_TRACES[(key, n)]
+
+
 def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1, bpf=None,
-                    compact: bool = True, sync=lambda: None, group_bytes: int = 0):
+                    compact: bool = True, sync=lambda: None, group_bytes: int = 0, group_max_us: int | None = None):
     """The drop-in boundary's own rate: mosrx_rx_loop (RunMainLoop's rx section,
     core.c:897-909) over gpu_module_func (io_module.h:63-78) fed by an in-memory
     source replaying the trace — per group of batches: source -> pinned
@@ -899,18 +911,18 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
         # a group's batches must be distinct frames: replaying one batch would let
         # the group's copy carry it once and the kernel re-read it from cache
         # (group 0 = the module's default, auto: as many batches per launch as are
-        # ready, up to MOSRX_GROUP_AUTO_BYTES of frames -- ~240 of 64 B, 5 of 1500 B; more
+        # ready, up to MOSRX_GROUP_AUTO_BYTES of frames -- ~500 of 64 B, 10 of 1500 B; more
         # distinct batches than a launch takes, so no launch holds the same frames twice)
-        nb = group or {"S64": 320, "M1500": 10, "IMIX": 12}[key]
-        tr = mosrx.Trace({"S64": mosrx.TRACE_S64, "M1500": mosrx.TRACE_M1500,
-                          "IMIX": mosrx.TRACE_IMIX}[key], ctx_batch * nb)
+        nb = group or {"S64": 640, "M1500": 20, "IMIX": 24}[key]
+        tr = backend_trace(key, ctx_batch * nb)
     # warm-up (staging sized, module loaded): two launches' worth of frames, on top of
     # the timed part's frames_target
-    warm = 2 * ctx_batch * (group or (256 if key == "S64" else 6))
+    warm = 2 * ctx_batch * (group or (512 if key == "S64" else 12))
     loops = max(1, -(-(frames_target + warm) // tr.n))
     src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
+    cap = {} if group_max_us is None else {"group_max_us": group_max_us}
     be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
-                          group=group, timing=True, bpf=bpf, compact=compact, group_bytes=group_bytes)
+                          group=group, timing=True, bpf=bpf, compact=compact, group_bytes=group_bytes, **cap)
     try:
         be.run_loop(max_pkts=warm)
         st0 = be.stats()
@@ -1114,18 +1126,19 @@ def main():
         # configuration inside mOS: auto groups, 8-byte records (cfg.compact)
         # (frames through each leg: enough that the timed part holds several launches after the
         # warm-up's pipelined group -- an IMIX auto group is 3 batches of 100 MB)
-        target = {"S64": 64_000_000, "M1500": 3_000_000, "IMIX": 20_000_000}
+        target = {"S64": 128_000_000, "M1500": 6_000_000, "IMIX": 40_000_000}
         be, be_agg = {}, {}
         legs = [(k, dict(frames_target=target[k], group=0)) for k in ("M1500", "S64", "IMIX")]
-        legs += [("S64_rec16", dict(frames_target=64_000_000, group=0, compact=False)),   # 16-byte records
+        legs += [("S64_rec16", dict(frames_target=128_000_000, group=0, compact=False)),   # 16-byte records
                  ("S64_group1", dict(frames_target=16_000_000, group=1)),      # one launch per batch
                  # auto groups of half the default bytes (256 MiB of frames per launch, round 4's default)
-                 ("S64_auto256", dict(frames_target=32_000_000, group=0, group_bytes=256 << 20)),
+                 ("S64_auto512", dict(frames_target=64_000_000, group=0, group_bytes=512 << 20)),
                  ("S64_group128", dict(frames_target=32_000_000, group=128)),
                  # 8 monitor filters installed (mtcp_bind_monitor_filter): auto groups through the
-                 # fused classify + BPF queue kernel (16-byte records), as without filters
-                 ("S64_bpf", dict(frames_target=64_000_000, group=0, bpf=bpf_bench_programs())),
-                 ("IMIX_bpf", dict(frames_target=20_000_000, group=0, bpf=bpf_bench_programs())),
+                 # fused classify + BPF queue kernel's 8-byte-record (_c8) form, as without filters
+                 ("S64_bpf", dict(frames_target=128_000_000, group=0, bpf=bpf_bench_programs())),
+                 ("IMIX_bpf", dict(frames_target=40_000_000, group=0, bpf=bpf_bench_programs())),
+                 ("S64_group8", dict(frames_target=32_000_000, group=8)),
                  ("M1500_group1", dict(frames_target=2_000_000, group=1)),
                  ("M1500_group8", dict(frames_target=4_000_000, group=8))]
         for name, kw in legs:
@@ -1133,8 +1146,21 @@ def main():
             if k in traces:
                 be[name], be_agg[name] = dist.leg(lambda sync: measure_backend(traces[k], k, cpu=device, sync=sync,
                                                                                **kw))
+        _BACKEND_TRACES.clear()
         e2e["backend"] = be
         agg["backend"] = be_agg
+        # per-frame residency on the drop-in path (paced arrivals at 25 / 50 / 90 % of each
+        # configuration's saturated rate above; one GPU's host side: single-rank runs only)
+        if ws == 1:
+            lat = {}
+            for k in ("S64", "M1500"):
+                for g, name in ((0, k), (1, f"{k}_group1"), (8, f"{k}_group8")):
+                    if name not in be:
+                        continue
+                    for load in (0.25, 0.5, 0.9):
+                        lat[f"{name}@{int(load * 100)}"] = measure_backend_latency(k, g, load * be[name]["mpkts"],
+                                                                                  cpu=device)
+            e2e["backend_latency"] = lat
         e2e["aggregate"] = agg
         # one mTCP thread per core, each with its own context / source / rx loop
         # (one GPU's host side: single-rank runs only)
@@ -1224,11 +1250,12 @@ def main():
                    "resident_batches": h["resident_batches"],
                    "resident_bytes": h["resident_bytes"]},
         "roofline": h["roofline"],
-        "read_ceiling_gbps": read_ceiling,
+        "read_probe_gbps": read_ceiling,
         "numa": numa,
-        # the headline kernel's rate against the box's own streaming-read rate for
-        # launches of the ring's size (what the HBM delivers to a read-only kernel)
-        "frac_of_read_ceiling": (round(h["roofline"]["achieved"] / read_ceiling["launch_768MiB"], 4)
+        # the headline kernel's rate against the box's own streaming-read probe for
+        # launches of the ring's size: a comparison with a simple read-only kernel, not a
+        # ceiling (the classify kernel has read above it on some boxes)
+        "vs_read_probe": (round(h["roofline"]["achieved"] / read_ceiling["launch_768MiB"], 4)
                                  if read_ceiling and read_ceiling.get("launch_768MiB") else None),
         "cpu_baseline": cpu,
         "secondary": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in r.items()}
@@ -1298,7 +1325,7 @@ def headline_line(detail, h, head, results, e2e):
                     for k, v in e2e.items() if k in ("M1500", "S64")}
         be = e2e.get("backend") or {}
         e2e_line["backend"] = {k: {"mpkts": round(v["mpkts"], 1), "dev_frac": v.get("device_roofline_frac")}
-                               for k, v in be.items() if k not in ("S64_group128", "M1500_group8", "S64_auto256")}
+                               for k, v in be.items() if k not in ("S64_group128", "M1500_group8", "S64_auto512")}
         # the job's end-to-end rates: every rank's legs at once, all frames over the longest wall
         # (at N = 1 the same as the rank's own)
         ag = e2e.get("aggregate") if detail["n_gpus"] > 1 else None
@@ -1311,6 +1338,12 @@ def headline_line(detail, h, head, results, e2e):
                                                 if k in ("M1500", "S64", "IMIX")}
         if e2e.get("consumer"):
             e2e_line["consumer"] = e2e["consumer"]
+        if e2e.get("backend_latency"):
+            # recv -> verdict available, p50 / p99 us, at 25 / 50 / 90 % of the saturated rate
+            e2e_line["latency_fields"] = "offered Mpkt/s, avail p50 us, avail p99 us, consumed p99 us"
+            e2e_line["latency"] = {k: [v["offered_mpkts"], v["avail_us"].get("p50_us"), v["avail_us"].get("p99_us"),
+                                       v["consumed_us"].get("p99_us")]
+                                   for k, v in e2e["backend_latency"].items()}
     return {
         "metric": detail["metric"],
         "value": detail["value"],
@@ -1331,8 +1364,8 @@ def headline_line(detail, h, head, results, e2e):
         "roofline": {k: rf[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "launch_us",
                                          "launch_timing")},
         "per_rank_device_gbps": h["per_rank_device_gbps"],
-        "read_ceiling_gbps": detail["read_ceiling_gbps"],
-        "frac_of_read_ceiling": detail["frac_of_read_ceiling"],
+        "read_probe_gbps": detail["read_probe_gbps"],
+        "vs_read_probe": detail["vs_read_probe"],
         "cpu_baseline": cpu_line,
         "secondary_fields": "Mpkt/s, launch us, roofline frac[, one-launch rows: the stamp's reading for an "
                             "empty kernel of the same grid, us]",

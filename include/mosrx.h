@@ -254,6 +254,11 @@ int  mosrx_classify_host_ex(mosrx_ctx *c, const mosrx_batch *b, mosrx_result *h_
 #define MOSRX_NSLOT 2
 int  mosrx_classify_host_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, mosrx_result *h_out);
 int  mosrx_classify_host_wait(mosrx_ctx *c, int slot);
+/* Size both slots' device buffers for submits of up to `frames_bytes` of frame
+ * buffers (group copies included) and `n` frames, now: without it a slot grows
+ * on the first submit that needs more, which synchronises and reallocates (a
+ * stall of milliseconds in the middle of traffic).  -EBUSY while a slot runs. */
+int  mosrx_classify_host_reserve(mosrx_ctx *c, uint64_t frames_bytes, uint32_t n);
 /* 1 when the slot's last submit has completed (its wait would not block) or
  * nothing is outstanding on it, 0 while it runs, -errno on error. */
 int  mosrx_classify_host_ready(mosrx_ctx *c, int slot);
@@ -271,7 +276,7 @@ int  mosrx_classify_host_submit_ex(mosrx_ctx *c, int slot, const mosrx_batch *b,
  * h_tcpinfo[i] when h_tcpinfo is not NULL).  Wait with
  * mosrx_classify_host_wait; the counters are the group's sum.  Amortises the
  * launch for small batches the way an rx ring of several batches would. */
-#define MOSRX_MAX_GROUP 256
+#define MOSRX_MAX_GROUP 512
 int  mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
                                       mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo);
 /* The same, plus the flow-table hash of every frame into h_fhash[i] (NULL: none;

@@ -228,11 +228,12 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * takes what has arrived.  DESIGN.md §5 (latency) */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
-#define MOSRX_GROUP_AUTO_BYTES  (512ull << 20)   /* per pipeline slot; 64 B frames: ~240 batches of 32K
-                                                   * per launch, 1500 B: 5 of 64K.  Round 5: 256 MiB groups
-                                                   * of 64 B frames ran 0.43 us per batch on the device, 512
-                                                   * MiB ones 0.40 (the launch's ramp and drain spread
-                                                   * over twice the batches; profiles/r05/backend_groups) */
+#define MOSRX_GROUP_AUTO_BYTES  (1ull << 30)     /* per pipeline slot; 64 B frames: ~500 batches of 32K
+                                                   * per launch, 1500 B: 10 of 64K.  Measured (round 5-6,
+                                                   * profiles/r06/groups): 256 MiB groups of 64 B frames ran
+                                                   * 0.43 us per batch on the device, 512 MiB 0.40-0.42, 1 GiB
+                                                   * 0.41 (a launch's ramp and drain spread over more batches);
+                                                   * inside mOS scaled down to the pinned budget (auto_bytes) */
 
 void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg);
 int  mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg);

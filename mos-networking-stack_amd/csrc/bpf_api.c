@@ -209,7 +209,20 @@ void mosrx__note_stream(mosrx_ctx *c, hipStream_t s)
 	for (k = 0; k < c->nxs; k++)
 		if (s && s == c->xs[k])
 			return;
-	c->foreign_streams = 1;   /* a caller's stream (or the null stream): only a device sync covers it */
+	/* a caller's stream (or the null stream): an event after the launch just made */
+	for (k = 0; k < c->nfs && c->fstream[k] != s; k++)
+		;
+	if (k == c->nfs) {
+		if (k == MOSRX_FOREIGN ||
+		    (!c->fev[k] && hipEventCreateWithFlags(&c->fev[k], hipEventDisableTiming) != hipSuccess)) {
+			c->foreign_streams = 1;   /* no room: the drain syncs the device */
+			return;
+		}
+		c->fstream[k] = s;
+		c->nfs++;
+	}
+	if (hipEventRecord(c->fev[k], s) != hipSuccess)
+		c->foreign_streams = 1;
 }
 
 int mosrx__drain(mosrx_ctx *c)
@@ -219,8 +232,12 @@ int mosrx__drain(mosrx_ctx *c)
 	if (c->foreign_streams) {
 		HIPCHK(hipDeviceSynchronize());
 		c->foreign_streams = 0;
+		c->nfs = 0;
 		return 0;
 	}
+	for (k = 0; k < c->nfs; k++)
+		HIPCHK(hipEventSynchronize(c->fev[k]));
+	c->nfs = 0;
 	HIPCHK(hipStreamSynchronize(c->stream));
 	for (k = 0; k < NSLOT; k++)
 		HIPCHK(hipStreamSynchronize(c->slot[k].stream));
@@ -308,10 +325,10 @@ int mosrx__bpf_launch_dev(mosrx_ctx *c, const uint8_t *frames, uint64_t frames_b
                           const uint16_t *len, uint32_t n, uint32_t *match, hipStream_t s)
 {
 	mosrx_bparams bp = c->bpf;
+	int rc;
 	if (!n)
 		return 0;
 	mosrx__bpf_poll(c);
-	mosrx__note_stream(c, s);
 	bp.frames = frames;
 	bp.off = off;
 	bp.len = len;
@@ -320,12 +337,16 @@ int mosrx__bpf_launch_dev(mosrx_ctx *c, const uint8_t *frames, uint64_t frames_b
 	bp.frames_bytes = (uint32_t)frames_bytes;
 	bp.n = n;
 	if (c->bpf_fn)
-		return mosrx__bpf_jit_launch(c, &bp, s);
-	if (!c->d_bpf && bp.nprog)
+		rc = mosrx__bpf_jit_launch(c, &bp, s);
+	else if (!c->d_bpf && bp.nprog)
 		return -EINVAL;
-	if (c->d_bpf)
-		c->bpf_pool_used[(c->bpf_pool_next + MOSRX_BPF_POOL - 1) % MOSRX_BPF_POOL] = 1;
-	return mosrx_launch_bpf(&bp, (void *)s);
+	else {
+		if (c->d_bpf)
+			c->bpf_pool_used[(c->bpf_pool_next + MOSRX_BPF_POOL - 1) % MOSRX_BPF_POOL] = 1;
+		rc = mosrx_launch_bpf(&bp, (void *)s);
+	}
+	mosrx__note_stream(c, s);   /* (after the launch: its event covers it) */
+	return rc;
 }
 
 static int bpf_launch(mosrx_ctx *c, const mosrx_batch *b, const uint8_t *frames, const uint32_t *off,

@@ -1412,10 +1412,12 @@ int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hi
 	const unsigned threads = small ? 256u : 64u * (1u + MOSRX_STREAMERS);
 	mosrx_kparams k = *kp;
 	void *args[] = {&k};
+	int rc;
 	if (!f)
 		return -EINVAL;
-	mosrx__note_stream(c, s);
-	return module_launch(f, (kp->n + tile - 1) / tile, threads, s, args);
+	rc = module_launch(f, (kp->n + tile - 1) / tile, threads, s, args);
+	mosrx__note_stream(c, s);   /* (after the launch: its event covers it) */
+	return rc;
 }
 
 /* The fused kernel over a batch queue (qp's descriptors carry the masks). */
@@ -1432,10 +1434,12 @@ int mosrx__bpf_fused_queue_launch(mosrx_ctx *c, const mosrx_qparams *qp, uint32_
 	void *args[] = {&desc, &tpb, &nb, &q};
 	if (!f)
 		return -EINVAL;
+	int rc;
 	if (!total_tiles)
 		return 0;
-	mosrx__note_stream(c, s);
-	return module_launch(f, total_tiles, threads, s, args);
+	rc = module_launch(f, total_tiles, threads, s, args);
+	mosrx__note_stream(c, s);   /* (after the launch: its event covers it) */
+	return rc;
 }
 
 int mosrx__bpf_jit_launch(mosrx_ctx *c, const mosrx_bparams *bp, hipStream_t s)

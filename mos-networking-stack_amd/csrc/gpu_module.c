@@ -85,8 +85,10 @@ struct stage {
 	uint32_t msp, esp, gen, nprog, has_fh, has_ti;
 	int compact;              /* its records are mosrx_result8 (cfg.compact): RES8 */
 };
-/* A compact stage's records.  Set at submit (stage_records): a group's compact
- * records are packed back to back in 8-byte slots, so they come back in one copy. */
+/* A compact stage's records: group_submit re-points s->res into the group's
+ * array of 8-byte slots (packed back to back, so they come back in one copy);
+ * between group_fill and that submit s->res still points at a 16-byte slot, so
+ * RES8 is meaningful only once the stage was submitted (s->compact set). */
 #define RES8(s) ((mosrx_result8 *)(s)->res)
 
 struct group {
@@ -562,6 +564,16 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 				fprintf(stderr, "[mosrx] gpu_module: pinned staging allocation failed\n");
 				exit(EXIT_FAILURE);
 			}
+		/* the device side of the largest group, up front: a slot that grew in the
+		 * middle of traffic would stall the mTCP thread for milliseconds (the
+		 * copies' 256-byte run alignment: 3 runs per batch at most) */
+		{
+			const uint64_t fb = is->g[0].blk_bytes + (uint64_t)is->g[0].cap_st * 3 * 256;
+			const uint64_t n = is->g[0].rec_cap;
+			if ((rc = mosrx_classify_host_reserve(is->mc, fb, n > UINT32_MAX ? UINT32_MAX : (uint32_t)n)))
+				fprintf(stderr, "[mosrx] gpu_module: device staging not reserved (%s): slots grow on demand\n",
+				        mosrx_strerror(rc));
+		}
 		/* pinned when the TX rewrite copies it to the GPU and back (cfg.tx_csum) */
 		if (!g_cfg.tx_csum)
 			is->tx_buf = malloc((size_t)g_cfg.tx_batch * TX_FRAME_LEN);

@@ -238,6 +238,11 @@ void mosrx_close(mosrx_ctx *c)
 	hipSetDevice(c->device);
 	if (c->foreign_streams)   /* a caller's stream may still run the set's kernels: they go below */
 		hipDeviceSynchronize();
+	for (i = 0; i < (int)c->nfs; i++)
+		hipEventSynchronize(c->fev[i]);
+	for (i = 0; i < MOSRX_FOREIGN; i++)
+		if (c->fev[i])
+			hipEventDestroy(c->fev[i]);
 	if (c->stream)
 		hipStreamSynchronize(c->stream);
 	for (i = 0; i < NSLOT; i++) {
@@ -814,6 +819,21 @@ int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
 	if (s->busy == 1 && s->timed && hipEventElapsedTime(&c->last_kernel_ms, s->kev0, s->kev1) != hipSuccess)
 		c->last_kernel_ms = -1.0f;
 	s->busy = 0;
+	return 0;
+}
+
+int mosrx_classify_host_reserve(mosrx_ctx *c, uint64_t frames_bytes, uint32_t n)
+{
+	int i, rc;
+	if (!c || !n)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	for (i = 0; i < NSLOT; i++)
+		if (c->slot[i].busy)
+			return -EBUSY;
+	for (i = 0; i < NSLOT; i++)
+		if ((rc = mosrx__slot_reserve(c, &c->slot[i], frames_bytes, n)))
+			return rc;
 	return 0;
 }
 

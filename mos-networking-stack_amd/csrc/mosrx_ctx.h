@@ -90,7 +90,15 @@ struct mosrx_ctx {
 	hipStream_t xs[MOSRX_MAX_STREAMS];   /* timing streams (mosrx_time_op), created on first use */
 	hipEvent_t xdone[MOSRX_MAX_STREAMS];
 	uint32_t nxs;
-	int foreign_streams;             /* a set ran on a stream the context does not own since the last drain */
+	/* callers' streams a launch reading the installed set went to since the last
+	 * drain, each with an event recorded after that launch (mosrx__note_stream);
+	 * foreign_streams: more of them than the table holds, so the drain falls back
+	 * to a device-wide sync */
+#define MOSRX_FOREIGN 8
+	hipStream_t fstream[MOSRX_FOREIGN];
+	hipEvent_t fev[MOSRX_FOREIGN];
+	uint32_t nfs;
+	int foreign_streams;
 	int timing;                      /* record kernel events on the end-to-end path (mosrx_set_timing) */
 	float last_kernel_ms;            /* kernel time of the last waited submit, -1 if not timed */
 };
@@ -115,13 +123,15 @@ int mosrx__bpf_jit_hook_source(const mosrx_bpf_insn *insns, const mosrx_bparams 
 int mosrx__bpf_fused_launch(mosrx_ctx *c, const mosrx_kparams *kp, int small, hipStream_t s);
 int mosrx__slot_reserve(mosrx_ctx *c, struct slot *s, uint64_t frames_bytes, uint32_t n);
 /* A launch that reads the installed BPF set (its staged instructions or its
- * compiled module) is made on stream s: remembered when s is not one of the
- * context's own streams (a caller's stream), so that mosrx__drain waits for it. */
+ * compiled module) was just made on stream s: when s is not one of the
+ * context's own streams (a caller's stream), an event recorded on s after it
+ * lets mosrx__drain wait for exactly that work. */
 void mosrx__note_stream(mosrx_ctx *c, hipStream_t s);
 /* Every launch that may still read a staged instruction buffer or a compiled
- * module has finished: the context's own streams synchronised, and the whole
- * device when a caller's stream was used since the last drain.  Before a
- * buffer is rewritten or a module unloaded. */
+ * module has finished: the context's own streams synchronised, and the events
+ * noted on callers' streams since the last drain (the whole device only when
+ * more streams were used than the table holds).  Before a buffer is rewritten
+ * or a module unloaded. */
 int mosrx__drain(mosrx_ctx *c);
 
 /* The variant a launch of `n` frames in `bytes` runs: the context's, with the

@@ -295,6 +295,7 @@ def lib():
             "mosrx_source_paced": (P, [P, C.c_double]),
             "mosrx_source_paced_info": (I, [P, C.POINTER(U64), C.POINTER(C.c_double), C.POINTER(U64)]),
             "mosrx_classify_host_ready": (I, [P, I]),
+            "mosrx_classify_host_reserve": (I, [P, U64, U32]),
             "mosrx_mos_forwards": (I, [P, I, U32, U32]),
             "mosrx_device_count": (I, []),
             "mosrx_classify_host_submit_ex": (I, [P, I, C.POINTER(Batch), P, P]),
@@ -1042,7 +1043,7 @@ class GpuBackend:
         cfg.gpu_base, cfg.ngpu = gpu_base, ngpu
         cfg.group, cfg.tcpinfo, cfg.tx_batch, cfg.flowhash = group, int(tcpinfo), tx_batch, int(flowhash)
         cfg.tx_csum = int(tx_csum)
-        cfg.compact = int(compact)          # 8-byte records (results8); 16-byte ones with filters
+        cfg.compact = int(compact)          # 8-byte records (results8), with or without filters
         cfg.group_bytes = group_bytes       # auto groups' frame bytes per launch (0: MOSRX_GROUP_AUTO_BYTES)
         cfg.group_max_us = group_max_us     # a group's latency budget (0: none)
         if params is not None:

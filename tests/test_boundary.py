@@ -138,10 +138,11 @@ def test_gpu_module_config_validation():
     L = mosrx.lib()
     cfg = mosrx.ModuleCfg()
     L.mosrx_gpu_module_cfg_default(C.byref(cfg))
-    # group 0 = auto: as many batches per launch as the source has ready, up to group_bytes
+    # group 0 = auto: as many batches per launch as the source has ready, up to group_bytes;
+    # explicit groups 1..MOSRX_MAX_GROUP (512)
     assert (cfg.batch, cfg.tx_batch, cfg.group, cfg.group_bytes, cfg.pipeline) == (32768, 64, 0, 0, 1)
     cfg.num_ifs = 1
-    for field, bad in [("group", 257), ("max_frame", 63), ("num_ifs", 17), ("bpf_nprog", 33)]:
+    for field, bad in [("group", 513), ("max_frame", 63), ("num_ifs", 17), ("bpf_nprog", 33)]:
         c2 = mosrx.ModuleCfg.from_buffer_copy(cfg)
         setattr(c2, field, bad)
         assert L.mosrx_gpu_module_configure(C.byref(c2)) == -22, field

@@ -107,6 +107,14 @@ HINT = "auto"
 DISTINCT = 8     # distinct batch contents generated per rank (the rest are resident copies of them)
 
 
+_T0 = time.time()
+
+
+def progress(msg: str):
+    """One line on stderr per leg (a long run keeps writing while it works)."""
+    print(f"[bench +{time.time() - _T0:.0f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -1122,6 +1130,7 @@ def main():
         for k, iters in (("M1500", 60), ("S64", 800)):
             if k in traces:
                 e2e[k], agg[k] = dist.leg(lambda sync: measure_e2e(ctx, traces[k], iters, sync))
+                progress(f"e2e {k}: {e2e[k]['gbps']:.1f} GB/s {e2e[k]['mpkts']:.1f} Mpkt/s")
         # the gpu_module_func backend itself (host thread = this rank), the module's
         # configuration inside mOS: auto groups, 8-byte records (cfg.compact)
         # (frames through each leg: enough that the timed part holds several launches after the
@@ -1146,6 +1155,8 @@ def main():
             if k in traces:
                 be[name], be_agg[name] = dist.leg(lambda sync: measure_backend(traces[k], k, cpu=device, sync=sync,
                                                                                **kw))
+                progress(f"backend {name}: {be[name]['mpkts']:.1f} Mpkt/s, device frac "
+                         f"{be[name]['device_roofline_frac']}, {be[name]['batches_per_launch']} batches per launch")
         _BACKEND_TRACES.clear()
         e2e["backend"] = be
         agg["backend"] = be_agg
@@ -1158,8 +1169,10 @@ def main():
                     if name not in be:
                         continue
                     for load in (0.25, 0.5, 0.9):
-                        lat[f"{name}@{int(load * 100)}"] = measure_backend_latency(k, g, load * be[name]["mpkts"],
-                                                                                  cpu=device)
+                        r = lat[f"{name}@{int(load * 100)}"] = measure_backend_latency(k, g, load * be[name]["mpkts"],
+                                                                                      cpu=device)
+                        progress(f"latency {name} at {int(load * 100)} %: {r['delivered_mpkts']} Mpkt/s, avail "
+                                 f"{r['avail_us']}")
             e2e["backend_latency"] = lat
         e2e["aggregate"] = agg
         # one mTCP thread per core, each with its own context / source / rx loop
@@ -1171,6 +1184,7 @@ def main():
             if "M1500" in traces:
                 mt["M1500"] = [measure_backend_threads("M1500", t, 1, 2_000_000, device) for t in (1, 2, 4)]
             e2e["backend_threads"] = mt
+            progress("backend threads: " + ", ".join(f"{k} {[r['mpkts'] for r in v]}" for k, v in mt.items()))
     # the last barrier of the GPU legs: from here rank 0 alone runs the host-core
     # baselines, with no other rank's timed region in flight, and the others wait
     dist.barrier()
@@ -1178,6 +1192,8 @@ def main():
     if rank == 0 and not args.no_cpu:
         head = "M1500" if "M1500" in traces else keys[0]
         cpu = cpu_baseline(traces[head], head, min_s=10.0, ws=ws, host_cpus=host_cpus)
+        progress(f"cpu baseline (port): {cpu['value']} GB/s on 1 core, "
+                 f"{(cpu.get('per_gpu_share') or {}).get('value')} on one GPU's share")
         ref = cpu_reference(traces[head], head, 10.0)
         if ref:
             cpu["reference"] = ref
@@ -1193,6 +1209,7 @@ def main():
         ref = cpu_reference(traces[head], head, 5.0, process_packet=True)
         if ref:
             cpu["reference_processpacket"] = ref
+        progress("cpu baseline (mOS's own code) done")
         # mOS's whole rx loop with and without the GPU records (the CPU the GPU saves inside mOS)
         # 1500 B orphans under a monitor that forwards nothing: little besides the checks per frame
         rx = cpu_rx_loop_leg(orphan_segments(8192), 16, forward=0)
@@ -1206,6 +1223,7 @@ def main():
         rx = cpu_rx_loop_leg(mosrx.Trace(mosrx.TRACE_FW64, 10_000), 20, forward=1, monitors=0)
         if rx:
             cpu["mos_rx_loop_FW64_bare"] = rx
+        progress("mOS rx-loop legs done")
         for k in keys:
             if k != head:
                 results[k]["cpu_baseline"] = cpu_baseline(traces[k], k, min_s=2.0, shares=False)
@@ -1214,6 +1232,7 @@ def main():
                     if ref:
                         results[k]["cpu_baseline"]["reference"] = ref
         results["FW64"] = measure_fw64(ctx, 2.0)
+        progress("config #1 (simple_firewall) legs done")
     read_ceiling = None
     if rank == 0:
         # the box's streaming-read rate over a >= 1.5 GB working set (no Infinity-
@@ -1296,9 +1315,11 @@ def headline_line(detail, h, head, results, e2e):
         for leg in ("per_gpu_share", "job_share", "whole_host", "reference", "reference_share",
                     "reference_processpacket"):
             if cpu.get(leg):
-                cpu_line[leg] = {k: cpu[leg][k] for k in ("value", "unit", "cores", "host_cpus", "cpu_quota", "kind",
-                                                          "mpkts") if k in cpu[leg]}
-        for leg in ("mos_rx_loop_M1500", "mos_rx_loop_FW64", "mos_rx_loop_FW64_bare"):
+                # (host_cpus / cpu_quota once, on the per-GPU share; every leg's in the detail record)
+                keys = ("value", "unit", "cores", "kind", "mpkts") + (
+                    ("host_cpus", "cpu_quota") if leg == "per_gpu_share" else ())
+                cpu_line[leg] = {k: cpu[leg][k] for k in keys if k in cpu[leg]}
+        for leg in ("mos_rx_loop_M1500",):   # (config #1's rx-loop legs: the detail record and FW64 below)
             if cpu.get(leg):
                 cpu_line[leg] = {k: cpu[leg][k] for k in ("processpacket_ns_per_frame", "gpu_records_ns_per_frame",
                                                           "saved_ns_per_frame")}
@@ -1325,7 +1346,8 @@ def headline_line(detail, h, head, results, e2e):
                     for k, v in e2e.items() if k in ("M1500", "S64")}
         be = e2e.get("backend") or {}
         e2e_line["backend"] = {k: {"mpkts": round(v["mpkts"], 1), "dev_frac": v.get("device_roofline_frac")}
-                               for k, v in be.items() if k not in ("S64_group128", "M1500_group8", "S64_auto512")}
+                               for k, v in be.items()
+                               if k not in ("S64_group128", "M1500_group8", "S64_auto512", "S64_group8")}
         # the job's end-to-end rates: every rank's legs at once, all frames over the longest wall
         # (at N = 1 the same as the rank's own)
         ag = e2e.get("aggregate") if detail["n_gpus"] > 1 else None
@@ -1340,10 +1362,11 @@ def headline_line(detail, h, head, results, e2e):
             e2e_line["consumer"] = e2e["consumer"]
         if e2e.get("backend_latency"):
             # recv -> verdict available, p50 / p99 us, at 25 / 50 / 90 % of the saturated rate
-            e2e_line["latency_fields"] = "offered Mpkt/s, avail p50 us, avail p99 us, consumed p99 us"
-            e2e_line["latency"] = {k: [v["offered_mpkts"], v["avail_us"].get("p50_us"), v["avail_us"].get("p99_us"),
-                                       v["consumed_us"].get("p99_us")]
-                                   for k, v in e2e["backend_latency"].items()}
+            # (groups of 8: the detail record)
+            e2e_line["latency_fields"] = "offered Mpkt/s, recv->verdict p50 us, p99 us (detail: consumed, groups of 8)"
+            e2e_line["latency"] = {k: [round(v["offered_mpkts"], 1), round(v["avail_us"].get("p50_us", 0)),
+                                       round(v["avail_us"].get("p99_us", 0))]
+                                   for k, v in e2e["backend_latency"].items() if "group8" not in k}
     return {
         "metric": detail["metric"],
         "value": detail["value"],
@@ -1367,8 +1390,7 @@ def headline_line(detail, h, head, results, e2e):
         "read_probe_gbps": detail["read_probe_gbps"],
         "vs_read_probe": detail["vs_read_probe"],
         "cpu_baseline": cpu_line,
-        "secondary_fields": "Mpkt/s, launch us, roofline frac[, one-launch rows: the stamp's reading for an "
-                            "empty kernel of the same grid, us]",
+        "secondary_fields": "Mpkt/s, launch us, frac[, 1-launch rows: empty-kernel stamp us]",
         "secondary": sec,
         "e2e": e2e_line,
         "detail": "full record: stderr line '[bench-detail]' and --detail file",

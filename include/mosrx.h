@@ -314,6 +314,12 @@ int  mosrx_classify_host_group_submit_bpf(mosrx_ctx *c, int slot, const mosrx_ba
  * wait mosrx_last_kernel_ms gives that device time (-ENODATA if the last
  * waited submit was not timed). */
 int  mosrx_set_timing(mosrx_ctx *c, int on);
+/* Group submits (mosrx_classify_host_group_submit*) make the per-reason
+ * counters of mosrx_last_counters (on, the default) or not (off: no counter
+ * atomics in the kernel and no copy back per group; mosrx_last_counters then
+ * reads zeros after such a wait).  gpu_module_func turns them off: mOS counts
+ * NETSTAT from the records. */
+int  mosrx_set_counters(mosrx_ctx *c, int on);
 int  mosrx_last_kernel_ms(mosrx_ctx *c, float *ms);
 
 /* Per-reason counters of the last completed end-to-end batch (MOSRX_R_COUNT
@@ -340,6 +346,10 @@ int  mosrx_host_register(mosrx_ctx *c, void *hptr, size_t bytes, int flags);
 int  mosrx_host_unregister(mosrx_ctx *c, void *hptr);
 int  mosrx_memcpy_h2d(mosrx_ctx *c, void *dst, const void *src, size_t bytes);
 int  mosrx_memcpy_d2h(mosrx_ctx *c, void *dst, const void *src, size_t bytes);
+/* mosrx_memcpy_h2d done by the CUs instead of the SDMA engine: a kernel reads
+ * the pinned host memory over PCIe and writes HBM (src: hipHostMalloc'd or
+ * registered memory; -EINVAL otherwise).  Synchronous. */
+int  mosrx_memcpy_h2d_pull(mosrx_ctx *c, void *dst, const void *src, size_t bytes);
 void *mosrx_stream(mosrx_ctx *c);
 
 /* ---- timing helpers (HIP events on the context stream) -------------------- */

@@ -552,6 +552,10 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 			exit(EXIT_FAILURE);
 		}
 		is->params = g_cfg.params;
+		/* no per-group reason counters: mOS counts NETSTAT from the records (the
+		 * consumer, eth_in.c:42-45, :80-84), and their copy back is one more
+		 * operation in every group's chain */
+		mosrx_set_counters(is->mc, 0);
 		is->src = (cpu < MAX_THREADS && g_src_cpu[cpu][i]) ? g_src_cpu[cpu][i] : g_cfg.src[i];
 		is->cur = is->inflight = -1;
 		if (g_cfg.bpf_nprog && (rc = mosrx_bpf_set(is->mc, g_cfg.bpf_progs, g_cfg.bpf_nprog))) {
@@ -626,6 +630,15 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
 	} else {
 		s->bytes = 2;
 	}
+	/* a short batch's descriptors as one run, len[] right after off[n]: one copy
+	 * to the device instead of two (the reserved arrays' unused tails would keep
+	 * them apart); borrowed frames leave the block to the descriptors, so the
+	 * next stage's follow this one's and a group's descriptors are one run */
+	if (s->n && s->n < g_cfg.batch) {
+		uint16_t *len2 = (uint16_t *)(s->off + s->n);
+		memmove(len2, s->len, (size_t)s->n * 2);
+		s->len = len2;
+	}
 	/* the batch's real largest frame picks the kernel shape; equal frames packed
 	 * at one stride (the fill's back-to-back small frames, a ring of fixed-size
 	 * buffers) are handed over with that layout as a hint (mosrx_batch.layout) */
@@ -636,7 +649,7 @@ static void stage_fill(struct group *g, struct stage *s, mosrx_source *src, uint
 			s->stride = 0;
 	}
 	s->max_len = m;
-	*pos = at + fpos;
+	*pos = s->borrowed ? (uint64_t)((uint8_t *)(s->len + s->n) - g->blk) : at + fpos;
 }
 
 /* Receive a group: up to cap_st batches (auto: until the block's bytes of

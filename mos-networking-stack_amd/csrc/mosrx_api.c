@@ -705,6 +705,7 @@ static int host_enqueue(mosrx_ctx *c, struct slot *s, const mosrx_batch *b, mosr
 	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_CNT_WORDS * 4, hipMemcpyDeviceToHost, s->stream));
 	HIPCHK(hipEventRecord(s->done, s->stream));
 	s->busy = 1;
+	s->counted = 1;
 	return 0;
 }
 
@@ -804,7 +805,7 @@ int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
 		uint32_t r, k;
 		for (r = 0; r < MOSRX_R_COUNT; r++)
 			c->h_cnt[r] = 0;
-		if (s->busy == 1) {
+		if (s->busy == 1 && s->counted) {
 			/* the batch's counts: what its launch added to every shard since the last wait */
 			for (k = 0; k < MOSRX_CNT_SHARDS; k++)
 				for (r = 0; r < MOSRX_R_COUNT; r++) {
@@ -846,6 +847,14 @@ int mosrx_classify_host_ready(mosrx_ctx *c, int slot)
 		return 1;
 	e = hipEventQuery(c->slot[slot].done);
 	return e == hipSuccess ? 1 : e == hipErrorNotReady ? 0 : -EIO;
+}
+
+int mosrx_set_counters(mosrx_ctx *c, int on)
+{
+	if (!c)
+		return -EINVAL;
+	c->no_counters = !on;
+	return 0;
 }
 
 int mosrx_set_timing(mosrx_ctx *c, int on)
@@ -1003,10 +1012,11 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 		pre += b[i].n;
 	}
 	HIPCHK(hipMemcpyAsync(s->d_qdesc, s->h_qdesc, nb * sizeof(mosrx_qdesc), hipMemcpyHostToDevice, s->stream));
-	HIPCHK(counters_arm(s));
+	if (!c->no_counters)
+		HIPCHK(counters_arm(s));
 	qp.desc = s->d_qdesc;
 	qp.tables = c->d_tables;
-	qp.counters = s->d_cnt;
+	qp.counters = c->no_counters ? NULL : s->d_cnt;
 	qp.nb = nb;
 	qp.flags = c->kflags;
 	qp.tpb = tpb_ok ? tiles / nb : 0;
@@ -1061,9 +1071,11 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 		pre += n;
 		i = j;
 	}
-	HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_CNT_WORDS * 4, hipMemcpyDeviceToHost, s->stream));
+	if (!c->no_counters)
+		HIPCHK(hipMemcpyAsync(s->h_cnt, s->d_cnt, MOSRX_CNT_WORDS * 4, hipMemcpyDeviceToHost, s->stream));
 	HIPCHK(hipEventRecord(s->done, s->stream));
 	s->busy = 1;
+	s->counted = !c->no_counters;
 	return 0;
 }
 
@@ -1308,6 +1320,22 @@ int mosrx_memcpy_h2d(mosrx_ctx *c, void *dst, const void *src, size_t bytes)
 	if (!c)
 		return -EINVAL;
 	HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+int mosrx_launch_pull(void *dst, const void *src, uint64_t bytes, void *stream);
+
+int mosrx_memcpy_h2d_pull(mosrx_ctx *c, void *dst, const void *src, size_t bytes)
+{
+	void *dsrc = NULL;
+	if (!c || !dst || !src)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	if (hipHostGetDevicePointer(&dsrc, (void *)src, 0) != hipSuccess || !dsrc)
+		return -EINVAL;   /* not pinned host memory the device can reach */
+	if (mosrx_launch_pull(dst, dsrc, bytes, c->stream))
+		return -EIO;
 	HIPCHK(hipStreamSynchronize(c->stream));
 	return 0;
 }

@@ -53,6 +53,7 @@ struct slot {
 	 * launch), and the next submit zeroes both. */
 	uint32_t *h_prev;
 	int cnt_dirty;
+	int counted;               /* the last submit made reason counts (mosrx_set_counters) */
 	hipEvent_t kev0, kev1;     /* around the kernel of the last submit (when the context times) */
 	mosrx_qdesc *h_qdesc;      /* MOSRX_MAX_GROUP, pinned: a group's batch table */
 	mosrx_tx_check *h_txc;     /* pinned: the TX pass's check records (mosrx_tx_csum_host), h_txc_n of them */
@@ -100,6 +101,7 @@ struct mosrx_ctx {
 	uint32_t nfs;
 	int foreign_streams;
 	int timing;                      /* record kernel events on the end-to-end path (mosrx_set_timing) */
+	int no_counters;                 /* group submits make no reason counts (mosrx_set_counters) */
 	float last_kernel_ms;            /* kernel time of the last waited submit, -1 if not timed */
 };
 

@@ -1427,6 +1427,53 @@ extern "C" int mosrx_launch_read_bw(const void *p, uint64_t bytes, uint32_t *sin
 	return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// Host -> HBM pull by the CUs (mosrx_memcpy_h2d_pull): every lane reads 16-byte
+// chunks of pinned host memory over PCIe, PULL_U in flight, and stores them to
+// HBM; the byte head / tail outside the 16-byte grid by lane 0 of block 0.  The
+// SDMA engine's alternative for the backend's group copies.
+#define PULL_U 8
+__global__ __launch_bounds__(256) void mosrx_pull_kernel(uint8_t *dst, const uint8_t *src, uint64_t bytes)
+{
+	const uint64_t head = (16u - ((uintptr_t)dst & 15u)) & 15u;
+	const uint64_t h = head < bytes ? head : bytes;
+	const uint64_t n16 = (bytes - h) / 16u;
+	u32x4 *d = (u32x4 *)(dst + h);
+	const u32x4 *s = (const u32x4 *)(src + h);
+	const uint64_t step = (uint64_t)gridDim.x * 256u * PULL_U;
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u * PULL_U + threadIdx.x; i < n16; i += step) {
+		u32x4 v[PULL_U];
+#pragma unroll
+		for (int u = 0; u < PULL_U; u++) {
+			const uint64_t j = i + 256u * u;
+			if (j < n16)
+				v[u] = s[j];
+		}
+#pragma unroll
+		for (int u = 0; u < PULL_U; u++) {
+			const uint64_t j = i + 256u * u;
+			if (j < n16)
+				d[j] = v[u];
+		}
+	}
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		for (uint64_t k = 0; k < h; k++)
+			dst[k] = src[k];
+		for (uint64_t k = h + n16 * 16u; k < bytes; k++)
+			dst[k] = src[k];
+	}
+}
+
+extern "C" int mosrx_launch_pull(void *dst, const void *src, uint64_t bytes, void *stream)
+{
+	uint64_t g = bytes / (256u * PULL_U * 16u);
+	if (!bytes)
+		return 0;
+	g = g < 1 ? 1 : g > 4096 ? 4096 : g;
+	hipLaunchKernelGGL(mosrx_pull_kernel, dim3((uint32_t)g), dim3(256), 0, (hipStream_t)stream, (uint8_t *)dst,
+	                   (const uint8_t *)src, bytes);
+	return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 // An empty kernel of a classify launch's grid: its dispatch-stamped duration is
 // what the stamp itself reads for a launch that does nothing (mosrx_probe_stamp_floor;
 // the short rows' bench figures are stated against it).  Diagnostic only.

@@ -239,6 +239,7 @@ def lib():
             "mosrx_host_free": (I, [P, P]),
             "mosrx_memcpy_h2d": (I, [P, P, P, C.c_size_t]),
             "mosrx_memcpy_d2h": (I, [P, P, P, C.c_size_t]),
+            "mosrx_memcpy_h2d_pull": (I, [P, P, P, C.c_size_t]),
             "mosrx_stream": (P, [P]),
             "mosrx_time_dev": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
             "mosrx_time_dev_kernels": (I, [P, C.POINTER(Batch), U32, C.POINTER(P), U32, C.POINTER(C.c_float)]),
@@ -296,6 +297,7 @@ def lib():
             "mosrx_source_paced_info": (I, [P, C.POINTER(U64), C.POINTER(C.c_double), C.POINTER(U64)]),
             "mosrx_classify_host_ready": (I, [P, I]),
             "mosrx_classify_host_reserve": (I, [P, U64, U32]),
+            "mosrx_set_counters": (I, [P, I]),
             "mosrx_mos_forwards": (I, [P, I, U32, U32]),
             "mosrx_device_count": (I, []),
             "mosrx_classify_host_submit_ex": (I, [P, I, C.POINTER(Batch), P, P]),

@@ -77,6 +77,7 @@ int __wrap_mosrx_host_alloc(mosrx_ctx *mc, size_t bytes, void **p)
 int __wrap_mosrx_host_free(mosrx_ctx *mc, void *p) { (void)mc; free(p); return 0; }
 int __wrap_mosrx_classify_host_wait(mosrx_ctx *mc, int slot) { (void)mc; (void)slot; return 0; }
 int __wrap_mosrx_classify_host_ready(mosrx_ctx *mc, int slot) { (void)mc; (void)slot; return 1; }
+int __wrap_mosrx_set_counters(mosrx_ctx *mc, int on) { (void)mc; (void)on; return 0; }
 int __wrap_mosrx_classify_host_reserve(mosrx_ctx *mc, uint64_t fb, uint32_t n) { (void)mc; (void)fb; (void)n; return 0; }
 
 int __wrap_mosrx_bpf_set(mosrx_ctx *mc, const mosrx_bpf_prog *progs, uint32_t nprog)

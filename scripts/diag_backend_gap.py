@@ -84,14 +84,24 @@ elif phase.startswith("res_fresh"):
         a[:] = t.frames
         pins.append((p, a))
     spare = [mosrx.DevBuffer(ctx, len(t.frames)) for t in trs] if phase == "res_fresh_other" else None
+    copy_s = 0.0
     for i in range(60 if key == "M1500" else 20):
         j = i % len(qs)
+        t_c = time.perf_counter()
         for b in range(group):
             k = (j * group + b) % len(pins)
-            (spare[k] if spare else dbs[j * group + b].d_frames).upload(pins[k][1])
+            dst = spare[k] if spare else dbs[j * group + b].d_frames
+            if phase.endswith("_pull"):      # copied by the CUs (mosrx_memcpy_h2d_pull), not the SDMA engine
+                mosrx._chk(mosrx.lib().mosrx_memcpy_h2d_pull(ctx.handle, dst.ptr, pins[k][0], len(pins[k][1])), "pull")
+            else:
+                dst.upload(pins[k][1])
+        copy_s += time.perf_counter() - t_c
         if phase == "res_fresh_sleep10":
             time.sleep(0.01)
         us.append(1e3 * qs[j].time_dispatch(1))
+    nb = sum(len(pins[(jj * group + b) % len(pins)][1]) for jj in range(60 if key == "M1500" else 20)
+             for b in range(group))
+    print(f"{key} {phase}: copies {nb / copy_s / 1e9:.1f} GB/s (host-timed, synchronous)", flush=True)
     for p, _ in pins:
         ctx.host_free(p)
     for d in spare or []:

@@ -906,7 +906,8 @@ def backend_trace(key: str, n: int) -> mosrx.Trace:
 
 
 def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, group: int = 1, bpf=None,
-                    compact: bool = True, sync=lambda: None, group_bytes: int = 0, group_max_us: int | None = None):
+                    compact: bool = True, sync=lambda: None, group_bytes: int = 0, group_max_us: int | None = None,
+                    direct_kb: int | None = None):
     """The drop-in boundary's own rate: mosrx_rx_loop (RunMainLoop's rx section,
     core.c:897-909) over gpu_module_func (io_module.h:63-78) fed by an in-memory
     source replaying the trace — per group of batches: source -> pinned
@@ -929,6 +930,8 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
     loops = max(1, -(-(frames_target + warm) // tr.n))
     src = mosrx.mem_source(tr.frames, tr.off, tr.len, loops=loops)
     cap = {} if group_max_us is None else {"group_max_us": group_max_us}
+    if direct_kb is not None:
+        cap["direct_kb"] = direct_kb
     be = mosrx.GpuBackend([src], batch=ctx_batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
                           group=group, timing=True, bpf=bpf, compact=compact, group_bytes=group_bytes, **cap)
     try:
@@ -958,6 +961,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
             "distinct_frames": tr.n,
             "group": group if group else "auto", "batches_per_launch": round(batches / max(launches, 1), 2),
             "kernel_launches": int(launches), "batches": int(batches),
+            "direct_launches": int(st1.rx_direct_groups - st0.rx_direct_groups),
             "device_us_per_batch": round(dev_us, 3),
             "device_roofline_frac": round(ab / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if dev_us > 0 else None,
             "method": f"mosrx_rx_loop over gpu_module_func (pipelined, "
@@ -969,7 +973,7 @@ def measure_backend(tr: mosrx.Trace, key: str, frames_target: int, cpu: int, gro
 
 
 def measure_backend_latency(key: str, group: int, rate_mpkts: float, cpu: int, seconds: float = 0.6,
-                            group_max_us: int = 0, warm_s: float = 0.15):
+                            group_max_us: int = 0, warm_s: float = 0.15, direct_kb: int | None = None):
     """Per-frame residency on the drop-in path: the backend
     as measure_backend runs it (8-byte records, pipelined), fed by a paced source
     (mosrx_source_paced: frame k arrives at t0 + k / rate, none is handed out
@@ -986,7 +990,7 @@ def measure_backend_latency(key: str, group: int, rate_mpkts: float, cpu: int, s
     rate = rate_mpkts * 1e6
     src = mosrx.paced_source(mosrx.mem_source(tr.frames, tr.off, tr.len, loops=0), rate)
     be = mosrx.GpuBackend([src], batch=batch, max_frame=2048, pipeline=True, cpu=cpu, gpu_base=cpu,
-                          group=group, compact=True, group_max_us=group_max_us)
+                          group=group, compact=True, group_max_us=group_max_us, direct_kb=direct_kb)
     probe = mosrx.LatencyProbe()
     probe.src = src
     probe.skip = int(rate * warm_s)
@@ -1006,7 +1010,7 @@ def measure_backend_latency(key: str, group: int, rate_mpkts: float, cpu: int, s
            "avail_max_us": round(probe.avail_max_ns / 1e3, 1), "consumed_max_us": round(probe.done_max_ns / 1e3, 1),
            "groups": int(ms.rx_groups), "mean_group_frames": round(ms.rx_frames / max(ms.rx_groups, 1), 1),
            "max_group_frames": int(ms.max_group_frames), "group": group if group else "auto",
-           "group_max_us": group_max_us}
+           "group_max_us": group_max_us, "direct_groups": int(ms.rx_direct_groups)}
     return out
 
 

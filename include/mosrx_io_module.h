@@ -226,8 +226,15 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * loop walks within it (never under 4096 frames); any
 	                                                 * group mode.  A group is never waited for: a receive
 	                                                 * takes what has arrived.  DESIGN.md §5 (latency) */
+	uint32_t      direct_kb;                        /* groups of at most this many KiB of frames + descriptors
+	                                                 * launch with no copies: the kernel reads the pinned
+	                                                 * staging / the source's pinned buffers and writes the
+	                                                 * pinned records in place over PCIe (mosrx_set_direct).
+	                                                 * 0: every group is copied.  Default
+	                                                 * MOSRX_DIRECT_DEFAULT_KB */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
+#define MOSRX_DIRECT_DEFAULT_KB 1024
 #define MOSRX_GROUP_AUTO_BYTES  (1ull << 30)     /* per pipeline slot; 64 B frames: ~500 batches of 32K
                                                    * per launch, 1500 B: 10 of 64K.  Measured (round 5-6,
                                                    * profiles/r06/groups): 256 MiB groups of 64 B frames ran
@@ -287,6 +294,7 @@ typedef struct mosrx_gpu_module_stats {
 	uint64_t group_cap_frames;  /* the frame cap cfg.group_max_us gave the last group filled (0: none) */
 	double   ns_per_frame_host; /* the latency cap's rates: the host's time per frame of a group */
 	double   ns_per_byte_dev;   /*   and a group's submit -> records ready per frame byte (0: not measured) */
+	uint64_t rx_direct_groups;  /* groups of rx_groups that launched with no copies (cfg.direct_kb) */
 } mosrx_gpu_module_stats;
 /* Time every kernel this thread's contexts launch (for the stats above). */
 int  mosrx_gpu_module_set_timing(struct mtcp_thread_context *ctx, int on);

@@ -159,6 +159,7 @@ void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg)
 	cfg->group = MOSRX_GROUP_AUTO;
 	cfg->group_bytes = 0;
 	cfg->numa = 1;
+	cfg->direct_kb = MOSRX_DIRECT_DEFAULT_KB;
 	mosrx_params_default(&cfg->params);
 }
 
@@ -167,7 +168,7 @@ int mosrx_gpu_module_configure(const mosrx_gpu_module_cfg *cfg)
 	if (!cfg || cfg->num_ifs == 0 || cfg->num_ifs > MOSRX_MAX_DEVICES || cfg->batch == 0 ||
 	    cfg->max_frame < 64 || cfg->max_frame > 65535 || cfg->group > MOSRX_MAX_GROUP ||
 	    cfg->bpf_nprog > MOSRX_BPF_MAX_PROGS || cfg->params.num_local > MOSRX_MAX_LOCAL ||
-	    (cfg->compact && cfg->tcpinfo))
+	    (cfg->compact && cfg->tcpinfo) || cfg->direct_kb > (1u << 22))
 		return -EINVAL;
 	pthread_mutex_lock(&g_lock);
 	g_cfg = *cfg;
@@ -556,6 +557,9 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 		 * consumer, eth_in.c:42-45, :80-84), and their copy back is one more
 		 * operation in every group's chain */
 		mosrx_set_counters(is->mc, 0);
+		/* small groups (light load) with no copies: the kernel reads the pinned
+		 * staging and writes the pinned records in place */
+		mosrx_set_direct(is->mc, (uint64_t)g_cfg.direct_kb << 10);
 		is->src = (cpu < MAX_THREADS && g_src_cpu[cpu][i]) ? g_src_cpu[cpu][i] : g_cfg.src[i];
 		is->cur = is->inflight = -1;
 		if (g_cfg.bpf_nprog && (rc = mosrx_bpf_set(is->mc, g_cfg.bpf_progs, g_cfg.bpf_nprog))) {
@@ -937,6 +941,8 @@ static int32_t gpu_recv_pkts(struct mtcp_thread_context *ctx, int ifidx)
 		pv->stats.rx_groups++;
 		if (n > pv->stats.max_group_frames)
 			pv->stats.max_group_frames = n;
+		if (mosrx_slot_direct(is->mc, k) == 1)
+			pv->stats.rx_direct_groups++;
 	}
 	if (g_cfg.pipeline) {             /* classify the next group behind the app's work */
 		int nk = k ^ 1;

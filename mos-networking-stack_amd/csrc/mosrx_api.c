@@ -207,6 +207,11 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 			return -ENODEV;
 		}
 		c->slot[i].cnt_dirty = 1;   /* the first launch on the slot zeroes its counters */
+		{
+			void *d = NULL;
+			if (hipHostGetDevicePointer(&d, c->slot[i].h_qdesc, 0) == hipSuccess)
+				c->slot[i].hq_dev = (const mosrx_qdesc *)d;
+		}
 	}
 	if ((rc = mosrx_set_params(c, p))) {
 		mosrx_close(c);
@@ -857,6 +862,21 @@ int mosrx_set_counters(mosrx_ctx *c, int on)
 	return 0;
 }
 
+int mosrx_set_direct(mosrx_ctx *c, uint64_t max_bytes)
+{
+	if (!c)
+		return -EINVAL;
+	c->direct_max = max_bytes;
+	return 0;
+}
+
+int mosrx_slot_direct(mosrx_ctx *c, int slot)
+{
+	if (!c || slot < 0 || slot >= NSLOT)
+		return -EINVAL;
+	return c->slot[slot].direct;
+}
+
 int mosrx_set_timing(mosrx_ctx *c, int on)
 {
 	if (!c)
@@ -877,6 +897,7 @@ int mosrx_last_kernel_ms(mosrx_ctx *c, float *ms)
 
 /* ---- a group of host batches in one launch (gpu_module_func's rx ring) ---- */
 struct region { const uint8_t *lo; uint64_t len; int own; uint8_t *dev; uint64_t alloc; };
+struct out_dev { void *out, *ti, *fh, *match; };   /* a direct group's output arrays, device addresses */
 
 /* Device copies of every region of the group: regions in address order are
  * gathered into copy runs wherever the gap to the next one is under an eighth
@@ -921,6 +942,57 @@ static int group_copy(struct slot *s, struct region *r, uint32_t nr, uint64_t *d
 	return 0;
 }
 
+/* Direct groups (mosrx_set_direct): a group whose frames and descriptors
+ * total at most c->direct_max bytes, every region in a known pinned range
+ * with a device address (frame buffers 16-byte aligned, their extent rounded
+ * up to 16 bytes as the kernels' buffer resources do), is read by the kernel
+ * in place over PCIe: no H2D copy and no batch-table copy (the kernel reads
+ * the pinned table).  Each copy of the copying path is a blit or SDMA
+ * dispatch plus a queue handoff, 4-12 us apiece, ~80 us per group cycle with
+ * 3 blits and one SDMA copy (profiles/r06/cycle); a small group's PCIe
+ * transfer inside the kernel is shorter than that chain.  The regions' device
+ * addresses go into r[].dev; *bytes: the input bytes (the kernel-shape
+ * choice's byte count).  0: copy the group. */
+static int direct_regions(const mosrx_ctx *c, const struct slot *s, struct region *r, uint32_t nr, uint64_t *bytes)
+{
+	uint64_t in = 0;
+	uint32_t i;
+	for (i = 0; i < nr; i++)
+		in += r[i].len;
+	if (!c->direct_max || in > c->direct_max || !s->hq_dev)
+		return 0;
+	for (i = 0; i < nr; i++) {   /* r[]: (frames, off, len) per non-empty batch */
+		const int fr = i % 3 == 0;
+		if (fr && r[i].own)
+			return 0;
+		if (!(r[i].dev = (uint8_t *)mosrx__host_dev_of(r[i].lo, fr ? (r[i].len + 15) & ~(uint64_t)15 : r[i].len)))
+			return 0;
+	}
+	*bytes = in;
+	return 1;
+}
+
+/* The device addresses of a direct group's output arrays, when every one of
+ * them is pinned too: the kernel then writes them in place (no D2H copies). */
+static int direct_outputs(const mosrx_batch *b, uint32_t nb, mosrx_result *const *h_out, size_t rsz,
+                          mosrx_tcpinfo *const *h_ti, uint32_t *const *h_fh, uint32_t *const *h_match,
+                          struct out_dev *od)
+{
+	uint32_t i;
+	for (i = 0; i < nb; i++) {
+		const uint64_t n = b[i].n;
+		memset(&od[i], 0, sizeof(od[i]));
+		if (!n)
+			continue;
+		if (!(od[i].out = mosrx__host_dev_of(h_out[i], n * rsz)) ||
+		    (h_ti && !(od[i].ti = mosrx__host_dev_of(h_ti[i], n * sizeof(mosrx_tcpinfo)))) ||
+		    (h_fh && !(od[i].fh = mosrx__host_dev_of(h_fh[i], n * 4))) ||
+		    (h_match && !(od[i].match = mosrx__host_dev_of(h_match[i], n * 4))))
+			return 0;
+	}
+	return 1;
+}
+
 int mosrx_classify_host_group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t nb,
                                      mosrx_result *const *h_out, mosrx_tcpinfo *const *h_tcpinfo)
 {
@@ -942,8 +1014,9 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 	uint64_t dev_bytes = 0, pre = 0;
 	mosrx_qparams qp;
 	struct slot *s;
+	struct out_dev od[MOSRX_MAX_GROUP];
 	int rc, unknown = 0, kind, tpb_ok = 1;
-	int fused = 0, uni = 0;
+	int fused = 0, uni = 0, direct, out_direct;
 	if (!c || slot < 0 || slot >= NSLOT || !b || !h_out || nb == 0 || nb > MOSRX_MAX_GROUP ||
 	    (h_match && h_tcpinfo) || (compact && h_tcpinfo))
 		return -EINVAL;
@@ -971,14 +1044,21 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 	}
 	if (ntot == 0) {
 		s->busy = 2;
+		s->direct = 0;
 		return 0;
 	}
 	HIPCHK(hipSetDevice(c->device));
-	group_copy(s, r, nr, &dev_bytes, 0);
-	if ((rc = mosrx__slot_reserve(c, s, dev_bytes, ntot)))
+	direct = direct_regions(c, s, r, nr, &dev_bytes);
+	out_direct = direct && direct_outputs(b, nb, h_out, rsz, h_tcpinfo, h_fhash, h_match, od);
+	if (!direct) {
+		group_copy(s, r, nr, &dev_bytes, 0);
+		if ((rc = mosrx__slot_reserve(c, s, dev_bytes, ntot)))
+			return rc;
+		if ((rc = group_copy(s, r, nr, &dev_bytes, 1)))
+			return rc;
+	} else if (!out_direct && (rc = mosrx__slot_reserve(c, s, 0, ntot))) {
 		return rc;
-	if ((rc = group_copy(s, r, nr, &dev_bytes, 1)))
-		return rc;
+	}
 	kind = kind_of(c, unknown ? 0 : maxl, dev_bytes, ntot);   /* one shape for the whole group */
 	tile = MOSRX_KIND_FRAMES(kind);
 	if (h_match) {
@@ -996,6 +1076,14 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 		else
 			d->tinfo = h_tcpinfo ? s->d_ti + pre : NULL;
 		d->fhash = h_fhash ? s->d_fh + pre : NULL;
+		if (out_direct && b[i].n) {   /* the kernel writes the caller's pinned arrays in place */
+			d->out = (mosrx_result *)od[i].out;
+			if (fused)
+				d->bmatch = (uint32_t *)od[i].match;
+			else
+				d->tinfo = (mosrx_tcpinfo *)od[i].ti;
+			d->fhash = (uint32_t *)od[i].fh;
+		}
 		if (b[i].n) {
 			d->frames = r[nr].dev;
 			d->off = (const uint32_t *)r[nr + 1].dev;
@@ -1011,10 +1099,11 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 			tpb_ok = 0;
 		pre += b[i].n;
 	}
-	HIPCHK(hipMemcpyAsync(s->d_qdesc, s->h_qdesc, nb * sizeof(mosrx_qdesc), hipMemcpyHostToDevice, s->stream));
+	if (!direct)
+		HIPCHK(hipMemcpyAsync(s->d_qdesc, s->h_qdesc, nb * sizeof(mosrx_qdesc), hipMemcpyHostToDevice, s->stream));
 	if (!c->no_counters)
 		HIPCHK(counters_arm(s));
-	qp.desc = s->d_qdesc;
+	qp.desc = direct ? s->hq_dev : s->d_qdesc;
 	qp.tables = c->d_tables;
 	qp.counters = c->no_counters ? NULL : s->d_cnt;
 	qp.nb = nb;
@@ -1040,7 +1129,9 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 			return rc;
 		for (i = 0, pre = 0; h_match && i < nb; pre += b[i].n, i++)   /* the set per batch, same stream */
 			if ((rc = mosrx__bpf_launch_dev(c, s->h_qdesc[i].frames, b[i].frames_bytes, s->h_qdesc[i].off,
-			                                s->h_qdesc[i].len, b[i].n, s->d_match + pre, s->stream)))
+			                                s->h_qdesc[i].len, b[i].n,
+			                                out_direct && b[i].n ? (uint32_t *)od[i].match : s->d_match + pre,
+			                                s->stream)))
 				return rc;
 	}
 	mosrx__stamp_next(NULL, NULL);   /* (a stamp pair no launch took is not left for the next one) */
@@ -1048,7 +1139,7 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 		HIPCHK(hipEventRecord(s->kev1, s->stream));
 	s->timed = c->timing;
 	/* results: one copy when the host buffers follow each other, else per batch */
-	for (i = 0, pre = 0; i < nb;) {
+	for (i = 0, pre = 0; !out_direct && i < nb;) {
 		uint32_t j = i + 1;
 		uint64_t n = b[i].n;
 		while (j < nb && (uint8_t *)h_out[j] == (uint8_t *)h_out[j - 1] + b[j - 1].n * rsz &&
@@ -1076,6 +1167,7 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 	HIPCHK(hipEventRecord(s->done, s->stream));
 	s->busy = 1;
 	s->counted = !c->no_counters;
+	s->direct = direct;
 	return 0;
 }
 
@@ -1174,7 +1266,9 @@ int mosrx_dev_free(mosrx_ctx *c, void *dptr)
  * regions (3 per batch) by binary search under a read lock, so concurrent rx
  * threads do not serialise on it. */
 #define MAX_RANGES 4096
-static struct range { uintptr_t lo, hi; uint64_t id; int reg; } g_ranges[MAX_RANGES];
+/* dev: the range's device address (hipHostGetDevicePointer at add), 0 when
+ * the runtime gave none -- such a range is copied, never read in place */
+static struct range { uintptr_t lo, hi; uint64_t id; int reg; uintptr_t dev; } g_ranges[MAX_RANGES];
 static uint32_t g_nranges;
 static uint64_t g_range_seq;
 static uint64_t g_range_maxlen;   /* longest range ever added: no range starting further below can hold a */
@@ -1197,6 +1291,9 @@ static uint32_t range_upper(uintptr_t a)
 static int range_add(const void *p, uint64_t len, int reg)
 {
 	int rc = -ENOSPC;
+	void *dev = NULL;
+	if (p && hipHostGetDevicePointer(&dev, (void *)p, 0) != hipSuccess)
+		dev = NULL;
 	pthread_rwlock_wrlock(&g_range_lock);
 	if (p && len && g_nranges < MAX_RANGES) {
 		const uint32_t at = range_upper((uintptr_t)p);
@@ -1205,6 +1302,7 @@ static int range_add(const void *p, uint64_t len, int reg)
 		g_ranges[at].hi = (uintptr_t)p + len;
 		g_ranges[at].id = ++g_range_seq;
 		g_ranges[at].reg = reg;
+		g_ranges[at].dev = (uintptr_t)dev;
 		g_nranges++;
 		if (len > g_range_maxlen)
 			g_range_maxlen = len;
@@ -1259,6 +1357,26 @@ uint64_t mosrx__host_range_of(const void *p, uint64_t len)
 		}
 	pthread_rwlock_unlock(&g_range_lock);
 	return id;
+}
+
+/* The device address of [p, p + len) when a known range with a device
+ * address holds it (a direct group's region), else NULL. */
+void *mosrx__host_dev_of(const void *p, uint64_t len)
+{
+	const uintptr_t a = (uintptr_t)p, b = a + len;
+	void *dev = NULL;
+	uint32_t k;
+	if (b < a)
+		return NULL;
+	pthread_rwlock_rdlock(&g_range_lock);
+	for (k = range_upper(a); k-- > 0 && a - g_ranges[k].lo < g_range_maxlen;)
+		if (b <= g_ranges[k].hi) {
+			if (g_ranges[k].dev)
+				dev = (void *)(g_ranges[k].dev + (a - g_ranges[k].lo));
+			break;
+		}
+	pthread_rwlock_unlock(&g_range_lock);
+	return dev;
 }
 
 int mosrx_host_register(mosrx_ctx *c, void *hptr, size_t bytes, int flags)

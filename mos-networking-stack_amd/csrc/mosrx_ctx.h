@@ -59,6 +59,8 @@ struct slot {
 	mosrx_tx_check *h_txc;     /* pinned: the TX pass's check records (mosrx_tx_csum_host), h_txc_n of them */
 	uint32_t h_txc_n;
 	mosrx_qdesc *d_qdesc;
+	const mosrx_qdesc *hq_dev; /* h_qdesc's device address (a direct group's batch table), NULL: none */
+	int direct;                /* the last group submit was direct (mosrx_set_direct) */
 	int timed;
 	int busy;
 };
@@ -102,10 +104,12 @@ struct mosrx_ctx {
 	int foreign_streams;
 	int timing;                      /* record kernel events on the end-to-end path (mosrx_set_timing) */
 	int no_counters;                 /* group submits make no reason counts (mosrx_set_counters) */
+	uint64_t direct_max;             /* largest direct group, input bytes (mosrx_set_direct); 0: none */
 	float last_kernel_ms;            /* kernel time of the last waited submit, -1 if not timed */
 };
 
 int mosrx__check_batch(const mosrx_batch *b, int dev);
+void *mosrx__host_dev_of(const void *p, uint64_t len);
 int mosrx__bpf_jit_request(mosrx_ctx *c, const mosrx_bpf_insn *insns);
 int mosrx__bpf_jit_wait(mosrx_ctx *c);
 void mosrx__bpf_poll(mosrx_ctx *c);

@@ -133,7 +133,8 @@ class ModuleCfg(C.Structure):
                 ("params", Params), ("bpf_progs", C.c_void_p), ("bpf_nprog", C.c_uint32),
                 ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32),
                 ("group_bytes", C.c_uint64), ("flowhash", C.c_int32), ("tx_csum", C.c_int32),
-                ("numa", C.c_int32), ("compact", C.c_int32), ("group_max_us", C.c_uint32)]
+                ("numa", C.c_int32), ("compact", C.c_int32), ("group_max_us", C.c_uint32),
+                ("direct_kb", C.c_uint32)]
 
 
 class ModuleStats(C.Structure):
@@ -143,7 +144,8 @@ class ModuleStats(C.Structure):
                 ("rx_reclassified", C.c_uint64), ("cpu", C.c_int32), ("device", C.c_int32),
                 ("tx_csum_offloaded", C.c_uint64), ("cpu_node", C.c_int32), ("gpu_node", C.c_int32),
                 ("rx_groups", C.c_uint64), ("max_group_frames", C.c_uint64), ("group_cap_frames", C.c_uint64),
-                ("ns_per_frame_host", C.c_double), ("ns_per_byte_dev", C.c_double)]
+                ("ns_per_frame_host", C.c_double), ("ns_per_byte_dev", C.c_double),
+                ("rx_direct_groups", C.c_uint64)]
 
 
 LAT_BINS = 1024
@@ -298,6 +300,8 @@ def lib():
             "mosrx_classify_host_ready": (I, [P, I]),
             "mosrx_classify_host_reserve": (I, [P, U64, U32]),
             "mosrx_set_counters": (I, [P, I]),
+            "mosrx_set_direct": (I, [P, U64]),
+            "mosrx_slot_direct": (I, [P, I]),
             "mosrx_mos_forwards": (I, [P, I, U32, U32]),
             "mosrx_device_count": (I, []),
             "mosrx_classify_host_submit_ex": (I, [P, I, C.POINTER(Batch), P, P]),
@@ -804,8 +808,31 @@ class Context:
             _chk(lib().mosrx_classify_host_group_submit_bpf_c8(self.handle, slot, bs, n, o, f, m),
                  "mosrx_classify_host_group_submit_bpf_c8")
 
+    def group_submit_ex(self, slot: int, batches: list, outs: list, tinfo: list | None = None,
+                        fhash: list | None = None) -> None:
+        """mosrx_classify_host_group_submit_ex: 16-byte records into outs (host
+        pointers), pkt_info TCP fields and flow hashes when given."""
+        n = len(batches)
+        bs = (Batch * n)(*batches)
+        o = (C.c_void_p * n)(*outs)
+        ti = (C.c_void_p * n)(*tinfo) if tinfo is not None else None
+        f = (C.c_void_p * n)(*fhash) if fhash is not None else None
+        _chk(lib().mosrx_classify_host_group_submit_ex(self.handle, slot, bs, n, o, ti, f),
+             "mosrx_classify_host_group_submit_ex")
+
     def group_wait(self, slot: int) -> None:
         _chk(lib().mosrx_classify_host_wait(self.handle, slot), "mosrx_classify_host_wait")
+
+    def set_direct(self, max_bytes: int) -> None:
+        """mosrx_set_direct: group submits of at most max_bytes of pinned input run copy-free."""
+        _chk(lib().mosrx_set_direct(self.handle, int(max_bytes)), "mosrx_set_direct")
+
+    def slot_direct(self, slot: int) -> bool:
+        """mosrx_slot_direct: the slot's last group submit ran copy-free."""
+        rc = lib().mosrx_slot_direct(self.handle, slot)
+        if rc < 0:
+            _chk(rc, "mosrx_slot_direct")
+        return rc == 1
 
     def host_register(self, ptr: int, nbytes: int, flags: int = 0) -> None:
         _chk(lib().mosrx_host_register(self.handle, ptr, nbytes, flags), "mosrx_host_register")
@@ -1033,7 +1060,7 @@ class GpuBackend:
                  max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
                  ngpu: int = 1, bpf=None, group: int = 1, tcpinfo: bool = False, tx_batch: int = 64,
                  timing: bool = False, flowhash: bool = False, tx_csum: bool = False, compact: bool = False,
-                 group_bytes: int = 0, group_max_us: int = 0, module_lib=None):
+                 group_bytes: int = 0, group_max_us: int = 0, direct_kb: int | None = None, module_lib=None):
         self.L = L = module_lib or lib()
         cfg = ModuleCfg()
         L.mosrx_gpu_module_cfg_default(C.byref(cfg))
@@ -1048,6 +1075,8 @@ class GpuBackend:
         cfg.compact = int(compact)          # 8-byte records (results8), with or without filters
         cfg.group_bytes = group_bytes       # auto groups' frame bytes per launch (0: MOSRX_GROUP_AUTO_BYTES)
         cfg.group_max_us = group_max_us     # a group's latency budget (0: none)
+        if direct_kb is not None:
+            cfg.direct_kb = direct_kb       # copy-free groups up to this many KiB (0: none)
         if params is not None:
             cfg.params = params
         self.params = Params.from_buffer_copy(cfg.params)

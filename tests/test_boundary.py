@@ -97,7 +97,8 @@ def test_gpu_module_inside_mos_maps_gpus_by_mtcp_core(tmp_path):
     exe = tmp_path / "mos_boundary_map"
     objs = sorted(glob.glob(os.path.join(REF_OBJ, "*.o")))
     wraps = [f"-Wl,--wrap={s}" for s in ("mosrx_device_count", "mosrx_open", "mosrx_close", "mosrx_host_alloc",
-                                         "mosrx_host_free")]
+                                         "mosrx_host_free", "mosrx_set_counters", "mosrx_set_direct",
+                                         "mosrx_classify_host_reserve")]
     _run(["gcc", "-o", str(exe), str(hm), str(gm), *objs, *wraps, "-L" + PKG, "-lmosrx", "-Wl,-rpath," + PKG,
           "-lpthread", "-lrt"])
     for ndev, base, ngpu in [(1, 0, 0), (2, 0, 0), (4, 0, 0), (8, 0, 0), (8, 4, 0), (8, 2, 3)]:

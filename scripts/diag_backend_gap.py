@@ -64,6 +64,14 @@ else:
            for t in (trs[i % 8] for i in range(2 * group))]
     qs = [ctx.queue_ex(dbs[i:i + group], compact=True) for i in range(0, 2 * group, group)]
 bench.prewarm(lambda: qs[0].time(8, qs[1:], kernels=False), 0.5)
+watch = None
+if os.environ.get("MOSRX_DPM_WATCH"):   # sample the DPM clock levels through the phase (read-only sysfs)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import dpm_watch  # noqa: E402
+    watch = dpm_watch.Watch().start()
+    watch.label = "prewarmed"
+    time.sleep(0.05)
+    watch.label = phase
 us = []
 if phase == "res_b2b":
     for _ in range(5):
@@ -128,6 +136,12 @@ elif phase in ("res_dma_hostpages", "res_dma_devpages"):
 else:
     raise SystemExit(f"unknown phase {phase}")
 report(phase, us)
+if watch is not None:
+    watch.label = "after"
+    time.sleep(0.05)
+    watch.stop()
+    import json  # noqa: E402
+    print(f"{key} {phase} dpm: {json.dumps(watch.report())}", flush=True)
 for q in qs:
     q.destroy()
 for d in dbs:

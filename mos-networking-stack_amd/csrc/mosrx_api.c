@@ -965,7 +965,8 @@ static int direct_regions(const mosrx_ctx *c, const struct slot *s, struct regio
 		const int fr = i % 3 == 0;
 		if (fr && r[i].own)
 			return 0;
-		if (!(r[i].dev = (uint8_t *)mosrx__host_dev_of(r[i].lo, fr ? (r[i].len + 15) & ~(uint64_t)15 : r[i].len)))
+		if (!(r[i].dev = (uint8_t *)mosrx__host_dev_of(r[i].lo, fr ? (r[i].len + 15) & ~(uint64_t)15 : r[i].len,
+		                                               c->device)))
 			return 0;
 	}
 	*bytes = in;
@@ -974,7 +975,7 @@ static int direct_regions(const mosrx_ctx *c, const struct slot *s, struct regio
 
 /* The device addresses of a direct group's output arrays, when every one of
  * them is pinned too: the kernel then writes them in place (no D2H copies). */
-static int direct_outputs(const mosrx_batch *b, uint32_t nb, mosrx_result *const *h_out, size_t rsz,
+static int direct_outputs(int device, const mosrx_batch *b, uint32_t nb, mosrx_result *const *h_out, size_t rsz,
                           mosrx_tcpinfo *const *h_ti, uint32_t *const *h_fh, uint32_t *const *h_match,
                           struct out_dev *od)
 {
@@ -984,10 +985,10 @@ static int direct_outputs(const mosrx_batch *b, uint32_t nb, mosrx_result *const
 		memset(&od[i], 0, sizeof(od[i]));
 		if (!n)
 			continue;
-		if (!(od[i].out = mosrx__host_dev_of(h_out[i], n * rsz)) ||
-		    (h_ti && !(od[i].ti = mosrx__host_dev_of(h_ti[i], n * sizeof(mosrx_tcpinfo)))) ||
-		    (h_fh && !(od[i].fh = mosrx__host_dev_of(h_fh[i], n * 4))) ||
-		    (h_match && !(od[i].match = mosrx__host_dev_of(h_match[i], n * 4))))
+		if (!(od[i].out = mosrx__host_dev_of(h_out[i], n * rsz, device)) ||
+		    (h_ti && !(od[i].ti = mosrx__host_dev_of(h_ti[i], n * sizeof(mosrx_tcpinfo), device))) ||
+		    (h_fh && !(od[i].fh = mosrx__host_dev_of(h_fh[i], n * 4, device))) ||
+		    (h_match && !(od[i].match = mosrx__host_dev_of(h_match[i], n * 4, device))))
 			return 0;
 	}
 	return 1;
@@ -1049,7 +1050,7 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 	}
 	HIPCHK(hipSetDevice(c->device));
 	direct = direct_regions(c, s, r, nr, &dev_bytes);
-	out_direct = direct && direct_outputs(b, nb, h_out, rsz, h_tcpinfo, h_fhash, h_match, od);
+	out_direct = direct && direct_outputs(c->device, b, nb, h_out, rsz, h_tcpinfo, h_fhash, h_match, od);
 	if (!direct) {
 		group_copy(s, r, nr, &dev_bytes, 0);
 		if ((rc = mosrx__slot_reserve(c, s, dev_bytes, ntot)))
@@ -1267,8 +1268,10 @@ int mosrx_dev_free(mosrx_ctx *c, void *dptr)
  * threads do not serialise on it. */
 #define MAX_RANGES 4096
 /* dev: the range's device address (hipHostGetDevicePointer at add), 0 when
- * the runtime gave none -- such a range is copied, never read in place */
-static struct range { uintptr_t lo, hi; uint64_t id; int reg; uintptr_t dev; } g_ranges[MAX_RANGES];
+ * the runtime gave none -- such a range is copied, never read in place;
+ * dev_id: the HIP device current at add, the only one it is read in place by
+ * (a context on another GPU copies it) */
+static struct range { uintptr_t lo, hi; uint64_t id; int reg; uintptr_t dev; int dev_id; } g_ranges[MAX_RANGES];
 static uint32_t g_nranges;
 static uint64_t g_range_seq;
 static uint64_t g_range_maxlen;   /* longest range ever added: no range starting further below can hold a */
@@ -1292,7 +1295,8 @@ static int range_add(const void *p, uint64_t len, int reg)
 {
 	int rc = -ENOSPC;
 	void *dev = NULL;
-	if (p && hipHostGetDevicePointer(&dev, (void *)p, 0) != hipSuccess)
+	int dev_id = -1;
+	if (p && (hipGetDevice(&dev_id) != hipSuccess || hipHostGetDevicePointer(&dev, (void *)p, 0) != hipSuccess))
 		dev = NULL;
 	pthread_rwlock_wrlock(&g_range_lock);
 	if (p && len && g_nranges < MAX_RANGES) {
@@ -1303,6 +1307,7 @@ static int range_add(const void *p, uint64_t len, int reg)
 		g_ranges[at].id = ++g_range_seq;
 		g_ranges[at].reg = reg;
 		g_ranges[at].dev = (uintptr_t)dev;
+		g_ranges[at].dev_id = dev_id;
 		g_nranges++;
 		if (len > g_range_maxlen)
 			g_range_maxlen = len;
@@ -1359,9 +1364,10 @@ uint64_t mosrx__host_range_of(const void *p, uint64_t len)
 	return id;
 }
 
-/* The device address of [p, p + len) when a known range with a device
- * address holds it (a direct group's region), else NULL. */
-void *mosrx__host_dev_of(const void *p, uint64_t len)
+/* The address on HIP device `device` of [p, p + len) when a known range with
+ * a device address for that device holds it (a direct group's region), else
+ * NULL. */
+void *mosrx__host_dev_of(const void *p, uint64_t len, int device)
 {
 	const uintptr_t a = (uintptr_t)p, b = a + len;
 	void *dev = NULL;
@@ -1371,7 +1377,7 @@ void *mosrx__host_dev_of(const void *p, uint64_t len)
 	pthread_rwlock_rdlock(&g_range_lock);
 	for (k = range_upper(a); k-- > 0 && a - g_ranges[k].lo < g_range_maxlen;)
 		if (b <= g_ranges[k].hi) {
-			if (g_ranges[k].dev)
+			if (g_ranges[k].dev && g_ranges[k].dev_id == device)
 				dev = (void *)(g_ranges[k].dev + (a - g_ranges[k].lo));
 			break;
 		}
@@ -1417,6 +1423,7 @@ int mosrx_host_alloc(mosrx_ctx *c, size_t bytes, void **hptr)
 {
 	if (!c || !hptr)
 		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));   /* the range is read in place by this device (direct groups) */
 	if (hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault | hipHostMallocNumaUser) != hipSuccess &&
 	    hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
 		return -ENOMEM;

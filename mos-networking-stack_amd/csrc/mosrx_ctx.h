@@ -109,7 +109,7 @@ struct mosrx_ctx {
 };
 
 int mosrx__check_batch(const mosrx_batch *b, int dev);
-void *mosrx__host_dev_of(const void *p, uint64_t len);
+void *mosrx__host_dev_of(const void *p, uint64_t len, int device);
 int mosrx__bpf_jit_request(mosrx_ctx *c, const mosrx_bpf_insn *insns);
 int mosrx__bpf_jit_wait(mosrx_ctx *c);
 void mosrx__bpf_poll(mosrx_ctx *c);

@@ -331,10 +331,6 @@ int  mosrx_set_counters(mosrx_ctx *c, int on);
  * shortens the group cycle at light load.  mosrx_slot_direct: 1 when the
  * slot's last group submit went direct, 0 if not. */
 int  mosrx_set_direct(mosrx_ctx *c, uint64_t max_bytes);
-/* Waits (mosrx_classify_host_wait) poll the slot's completion event in a loop
- * (on) instead of the runtime's blocking wait (off, the default): for a
- * poll-mode thread such as mOS's rx loop, which owns its core. */
-int  mosrx_set_wait_spin(mosrx_ctx *c, int on);
 int  mosrx_slot_direct(mosrx_ctx *c, int slot);
 int  mosrx_last_kernel_ms(mosrx_ctx *c, float *ms);
 

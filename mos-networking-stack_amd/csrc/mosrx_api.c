@@ -182,8 +182,6 @@ int mosrx_open(int device, const mosrx_params *p, mosrx_ctx **out)
 	c->bpf_engine_req = MOSRX_BPF_ENGINE_JIT;
 	if (getenv("MOSRX_BPF_ENGINE") && atoi(getenv("MOSRX_BPF_ENGINE")) == 0)
 		c->bpf_engine_req = MOSRX_BPF_ENGINE_INTERP;
-	if (getenv("MOSRX_WAIT_SPIN"))
-		c->spin_wait = atoi(getenv("MOSRX_WAIT_SPIN")) != 0;
 	/* the timing streams are created right after the context stream: HIP maps
 	 * streams to hardware queues round robin (GPU_MAX_HW_QUEUES, 4 by default),
 	 * so the first three land on queues of their own */
@@ -806,19 +804,8 @@ int mosrx_classify_host_wait(mosrx_ctx *c, int slot)
 	s = &c->slot[slot];
 	if (!s->busy)
 		return -EINVAL;
-	if (s->busy == 1) {
-		if (c->spin_wait) {
-			/* poll mode (mosrx_set_wait_spin): query the slot's event until it
-			 * completes, as mOS's rx loop polls its NIC -- no sleep in the
-			 * runtime's wait, so the thread sees the records as soon as they land */
-			hipError_t e;
-			while ((e = hipEventQuery(s->done)) == hipErrorNotReady)
-				__builtin_ia32_pause();
-			HIPCHK(e);
-		} else {
-			HIPCHK(hipEventSynchronize(s->done));
-		}
-	}
+	if (s->busy == 1)
+		HIPCHK(hipEventSynchronize(s->done));
 	{
 		uint32_t r, k;
 		for (r = 0; r < MOSRX_R_COUNT; r++)
@@ -872,14 +859,6 @@ int mosrx_set_counters(mosrx_ctx *c, int on)
 	if (!c)
 		return -EINVAL;
 	c->no_counters = !on;
-	return 0;
-}
-
-int mosrx_set_wait_spin(mosrx_ctx *c, int on)
-{
-	if (!c)
-		return -EINVAL;
-	c->spin_wait = on ? 1 : 0;
 	return 0;
 }
 

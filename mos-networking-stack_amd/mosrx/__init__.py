@@ -301,7 +301,6 @@ def lib():
             "mosrx_classify_host_reserve": (I, [P, U64, U32]),
             "mosrx_set_counters": (I, [P, I]),
             "mosrx_set_direct": (I, [P, U64]),
-            "mosrx_set_wait_spin": (I, [P, I]),
             "mosrx_slot_direct": (I, [P, I]),
             "mosrx_mos_forwards": (I, [P, I, U32, U32]),
             "mosrx_device_count": (I, []),

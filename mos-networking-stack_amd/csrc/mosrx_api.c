@@ -974,7 +974,9 @@ static int direct_regions(const mosrx_ctx *c, const struct slot *s, struct regio
 }
 
 /* The device addresses of a direct group's output arrays, when every one of
- * them is pinned too: the kernel then writes them in place (no D2H copies). */
+ * them is pinned too and aligned to its element's store (16 / 8 bytes for the
+ * records, 4 for the side arrays): the kernel then writes them in place (no
+ * D2H copies). */
 static int direct_outputs(int device, const mosrx_batch *b, uint32_t nb, mosrx_result *const *h_out, size_t rsz,
                           mosrx_tcpinfo *const *h_ti, uint32_t *const *h_fh, uint32_t *const *h_match,
                           struct out_dev *od)
@@ -985,6 +987,9 @@ static int direct_outputs(int device, const mosrx_batch *b, uint32_t nb, mosrx_r
 		memset(&od[i], 0, sizeof(od[i]));
 		if (!n)
 			continue;
+		if (((uintptr_t)h_out[i] & (rsz - 1)) || (h_ti && ((uintptr_t)h_ti[i] & 3)) ||
+		    (h_fh && ((uintptr_t)h_fh[i] & 3)) || (h_match && ((uintptr_t)h_match[i] & 3)))
+			return 0;
 		if (!(od[i].out = mosrx__host_dev_of(h_out[i], n * rsz, device)) ||
 		    (h_ti && !(od[i].ti = mosrx__host_dev_of(h_ti[i], n * sizeof(mosrx_tcpinfo), device))) ||
 		    (h_fh && !(od[i].fh = mosrx__host_dev_of(h_fh[i], n * 4, device))) ||

@@ -181,7 +181,7 @@ def test_direct_only_within_its_bounds(gpu_ctx):
         # frames 2 bytes past a 16-byte boundary (offsets relative to the buffer),
         # descriptors aligned elsewhere in the block
         fr, o, ln, fb = parts[0]
-        fpos, opos = 4096 + 2, 6 << 20
+        fpos, opos = (7 << 19) + 2, 7 << 20     # past the staged batch (~3 MB)
         arr[fpos:fpos + fb] = fr[:fb]
         arr[opos:opos + 4 * t.n].view(np.uint32)[:] = o
         arr[opos + 4 * t.n:opos + 6 * t.n].view(np.uint16)[:] = ln
@@ -191,6 +191,17 @@ def test_direct_only_within_its_bounds(gpu_ctx):
         gpu_ctx.group_wait(0)
         assert not gpu_ctx.slot_direct(0)
         assert_records_equal(rec, ora, "unaligned")
+        # records 8 bytes off their 16-byte alignment: the inputs are read in place,
+        # the records made on the device and copied back (never stored misaligned)
+        rp2, rbuf = gpu_ctx.host_alloc(16 * t.n + 64)
+        try:
+            rec2 = rbuf[8:8 + 16 * t.n].view(mosrx.RESULT_DTYPE)
+            gpu_ctx.group_submit_ex(0, batches, [rp2 + 8])
+            gpu_ctx.group_wait(0)
+            assert gpu_ctx.slot_direct(0)
+            assert_records_equal(rec2, ora, "misaligned records")
+        finally:
+            gpu_ctx.host_free(rp2)
         # pageable frames and descriptors
         pfr = np.ascontiguousarray(fr)
         poff = np.ascontiguousarray(o, np.uint32)

@@ -1177,6 +1177,13 @@ def main():
                                                                                       cpu=device)
                         progress(f"latency {name} at {int(load * 100)} %: {r['delivered_mpkts']} Mpkt/s, avail "
                                  f"{r['avail_us']}")
+            # the same light-load points with every group copied (cfg.direct_kb 0): what the
+            # copy-free small groups gain, in the same run (the detail record only)
+            for k, g, name in (("S64", 0, "S64"), ("M1500", 1, "M1500_group1")):
+                if name in be:
+                    r = lat[f"{name}@25_copied"] = measure_backend_latency(k, g, 0.25 * be[name]["mpkts"], cpu=device,
+                                                                           direct_kb=0)
+                    progress(f"latency {name} at 25 %, every group copied: avail {r['avail_us']}")
             e2e["backend_latency"] = lat
         e2e["aggregate"] = agg
         # one mTCP thread per core, each with its own context / source / rx loop
@@ -1367,10 +1374,12 @@ def headline_line(detail, h, head, results, e2e):
         if e2e.get("backend_latency"):
             # recv -> verdict available, p50 / p99 us, at 25 / 50 / 90 % of the saturated rate
             # (groups of 8: the detail record)
-            e2e_line["latency_fields"] = "offered Mpkt/s, recv->verdict p50 us, p99 us (detail: consumed, groups of 8)"
+            e2e_line["latency_fields"] = ("offered Mpkt/s, recv->verdict p50 us, p99 us (detail: consumed, groups "
+                                          "of 8, every group copied)")
             e2e_line["latency"] = {k: [round(v["offered_mpkts"], 1), round(v["avail_us"].get("p50_us", 0)),
                                        round(v["avail_us"].get("p99_us", 0))]
-                                   for k, v in e2e["backend_latency"].items() if "group8" not in k}
+                                   for k, v in e2e["backend_latency"].items()
+                                   if "group8" not in k and "copied" not in k}
     return {
         "metric": detail["metric"],
         "value": detail["value"],

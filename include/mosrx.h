@@ -320,8 +320,9 @@ int  mosrx_set_timing(mosrx_ctx *c, int on);
  * reads zeros after such a wait).  gpu_module_func turns them off: mOS counts
  * NETSTAT from the records. */
 int  mosrx_set_counters(mosrx_ctx *c, int on);
-/* Direct groups: a group submit whose frames and descriptors total at most
- * max_bytes (0, the default: none), all of them in pinned memory the library
+/* Direct groups: a group submit of at most max_frames frames whose frames and
+ * descriptors total at most max_bytes (0, the default: none), all of them in
+ * pinned memory the library
  * knows (mosrx_host_alloc / mosrx_host_register, or a source's pinned
  * buffers) with 16-byte aligned frame buffers, launches with no copies: the
  * kernel reads them, and the batch table, in place over PCIe, and writes the
@@ -330,7 +331,7 @@ int  mosrx_set_counters(mosrx_ctx *c, int on);
  * the copy chain (a blit or SDMA dispatch and a queue handoff per copy), which
  * shortens the group cycle at light load.  mosrx_slot_direct: 1 when the
  * slot's last group submit went direct, 0 if not. */
-int  mosrx_set_direct(mosrx_ctx *c, uint64_t max_bytes);
+int  mosrx_set_direct(mosrx_ctx *c, uint64_t max_bytes, uint32_t max_frames);
 int  mosrx_slot_direct(mosrx_ctx *c, int slot);
 int  mosrx_last_kernel_ms(mosrx_ctx *c, float *ms);
 

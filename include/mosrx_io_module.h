@@ -232,8 +232,13 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * pinned records in place over PCIe (mosrx_set_direct).
 	                                                 * 0: every group is copied.  Default
 	                                                 * MOSRX_DIRECT_DEFAULT_KB */
+	uint32_t      direct_frames;                    /* ... and of at most this many frames (default
+	                                                 * MOSRX_DIRECT_DEFAULT_FRAMES) */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
+#define MOSRX_DIRECT_DEFAULT_FRAMES 16384   /* 64 B frames at 90 % load: auto groups of 31-49K frames
+                                             * read in place ran at the host's edge and once overloaded
+                                             * (p50 31 ms, profiles/r06/direct/); copied they hold */
 #define MOSRX_DIRECT_DEFAULT_KB 16384   /* measured (profiles/r06/direct): copy-free groups cut the
                                           * light-load p50 ~3x (64 B auto at 25 %: 108 -> 34 us) and
                                           * lift 64 B one-batch launches 257 -> 297 Mpkt/s; at 90 %

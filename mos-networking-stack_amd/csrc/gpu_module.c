@@ -160,6 +160,7 @@ void mosrx_gpu_module_cfg_default(mosrx_gpu_module_cfg *cfg)
 	cfg->group_bytes = 0;
 	cfg->numa = 1;
 	cfg->direct_kb = MOSRX_DIRECT_DEFAULT_KB;
+	cfg->direct_frames = MOSRX_DIRECT_DEFAULT_FRAMES;
 	mosrx_params_default(&cfg->params);
 }
 
@@ -559,7 +560,7 @@ static void gpu_init_handle(struct mtcp_thread_context *ctx)
 		mosrx_set_counters(is->mc, 0);
 		/* small groups (light load) with no copies: the kernel reads the pinned
 		 * staging and writes the pinned records in place */
-		mosrx_set_direct(is->mc, (uint64_t)g_cfg.direct_kb << 10);
+		mosrx_set_direct(is->mc, (uint64_t)g_cfg.direct_kb << 10, g_cfg.direct_frames);
 		is->src = (cpu < MAX_THREADS && g_src_cpu[cpu][i]) ? g_src_cpu[cpu][i] : g_cfg.src[i];
 		is->cur = is->inflight = -1;
 		if (g_cfg.bpf_nprog && (rc = mosrx_bpf_set(is->mc, g_cfg.bpf_progs, g_cfg.bpf_nprog))) {

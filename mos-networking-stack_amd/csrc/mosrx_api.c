@@ -862,11 +862,12 @@ int mosrx_set_counters(mosrx_ctx *c, int on)
 	return 0;
 }
 
-int mosrx_set_direct(mosrx_ctx *c, uint64_t max_bytes)
+int mosrx_set_direct(mosrx_ctx *c, uint64_t max_bytes, uint32_t max_frames)
 {
 	if (!c)
 		return -EINVAL;
 	c->direct_max = max_bytes;
+	c->direct_frames = max_frames;
 	return 0;
 }
 
@@ -943,7 +944,8 @@ static int group_copy(struct slot *s, struct region *r, uint32_t nr, uint64_t *d
 }
 
 /* Direct groups (mosrx_set_direct): a group whose frames and descriptors
- * total at most c->direct_max bytes, every region in a known pinned range
+ * total at most c->direct_max bytes in at most c->direct_frames frames, every
+ * region in a known pinned range
  * with a device address (frame buffers 16-byte aligned, their extent rounded
  * up to 16 bytes as the kernels' buffer resources do), is read by the kernel
  * in place over PCIe: no H2D copy and no batch-table copy (the kernel reads
@@ -953,13 +955,14 @@ static int group_copy(struct slot *s, struct region *r, uint32_t nr, uint64_t *d
  * transfer inside the kernel is shorter than that chain.  The regions' device
  * addresses go into r[].dev; *bytes: the input bytes (the kernel-shape
  * choice's byte count).  0: copy the group. */
-static int direct_regions(const mosrx_ctx *c, const struct slot *s, struct region *r, uint32_t nr, uint64_t *bytes)
+static int direct_regions(const mosrx_ctx *c, const struct slot *s, struct region *r, uint32_t nr, uint64_t ntot,
+                          uint64_t *bytes)
 {
 	uint64_t in = 0;
 	uint32_t i;
 	for (i = 0; i < nr; i++)
 		in += r[i].len;
-	if (!c->direct_max || in > c->direct_max || !s->hq_dev)
+	if (!c->direct_max || in > c->direct_max || ntot > c->direct_frames || !s->hq_dev)
 		return 0;
 	for (i = 0; i < nr; i++) {   /* r[]: (frames, off, len) per non-empty batch */
 		const int fr = i % 3 == 0;
@@ -1054,7 +1057,7 @@ static int group_submit(mosrx_ctx *c, int slot, const mosrx_batch *b, uint32_t n
 		return 0;
 	}
 	HIPCHK(hipSetDevice(c->device));
-	direct = direct_regions(c, s, r, nr, &dev_bytes);
+	direct = direct_regions(c, s, r, nr, ntot, &dev_bytes);
 	out_direct = direct && direct_outputs(c->device, b, nb, h_out, rsz, h_tcpinfo, h_fhash, h_match, od);
 	if (!direct) {
 		group_copy(s, r, nr, &dev_bytes, 0);

@@ -105,6 +105,7 @@ struct mosrx_ctx {
 	int timing;                      /* record kernel events on the end-to-end path (mosrx_set_timing) */
 	int no_counters;                 /* group submits make no reason counts (mosrx_set_counters) */
 	uint64_t direct_max;             /* largest direct group, input bytes (mosrx_set_direct); 0: none */
+	uint32_t direct_frames;          /*   and its most frames */
 	float last_kernel_ms;            /* kernel time of the last waited submit, -1 if not timed */
 };
 

@@ -134,7 +134,7 @@ class ModuleCfg(C.Structure):
                 ("tx_batch", C.c_uint32), ("tcpinfo", C.c_int32), ("group", C.c_uint32),
                 ("group_bytes", C.c_uint64), ("flowhash", C.c_int32), ("tx_csum", C.c_int32),
                 ("numa", C.c_int32), ("compact", C.c_int32), ("group_max_us", C.c_uint32),
-                ("direct_kb", C.c_uint32)]
+                ("direct_kb", C.c_uint32), ("direct_frames", C.c_uint32)]
 
 
 class ModuleStats(C.Structure):
@@ -300,7 +300,7 @@ def lib():
             "mosrx_classify_host_ready": (I, [P, I]),
             "mosrx_classify_host_reserve": (I, [P, U64, U32]),
             "mosrx_set_counters": (I, [P, I]),
-            "mosrx_set_direct": (I, [P, U64]),
+            "mosrx_set_direct": (I, [P, U64, U32]),
             "mosrx_slot_direct": (I, [P, I]),
             "mosrx_mos_forwards": (I, [P, I, U32, U32]),
             "mosrx_device_count": (I, []),
@@ -823,9 +823,10 @@ class Context:
     def group_wait(self, slot: int) -> None:
         _chk(lib().mosrx_classify_host_wait(self.handle, slot), "mosrx_classify_host_wait")
 
-    def set_direct(self, max_bytes: int) -> None:
-        """mosrx_set_direct: group submits of at most max_bytes of pinned input run copy-free."""
-        _chk(lib().mosrx_set_direct(self.handle, int(max_bytes)), "mosrx_set_direct")
+    def set_direct(self, max_bytes: int, max_frames: int = 0xFFFFFFFF) -> None:
+        """mosrx_set_direct: group submits of at most max_frames frames and max_bytes of
+        pinned input run copy-free."""
+        _chk(lib().mosrx_set_direct(self.handle, int(max_bytes), int(max_frames)), "mosrx_set_direct")
 
     def slot_direct(self, slot: int) -> bool:
         """mosrx_slot_direct: the slot's last group submit ran copy-free."""
@@ -1060,7 +1061,8 @@ class GpuBackend:
                  max_frame: int = 2048, pipeline: bool = True, cpu: int = 0, gpu_base: int = 0,
                  ngpu: int = 1, bpf=None, group: int = 1, tcpinfo: bool = False, tx_batch: int = 64,
                  timing: bool = False, flowhash: bool = False, tx_csum: bool = False, compact: bool = False,
-                 group_bytes: int = 0, group_max_us: int = 0, direct_kb: int | None = None, module_lib=None):
+                 group_bytes: int = 0, group_max_us: int = 0, direct_kb: int | None = None,
+                 direct_frames: int | None = None, module_lib=None):
         self.L = L = module_lib or lib()
         cfg = ModuleCfg()
         L.mosrx_gpu_module_cfg_default(C.byref(cfg))
@@ -1077,6 +1079,8 @@ class GpuBackend:
         cfg.group_max_us = group_max_us     # a group's latency budget (0: none)
         if direct_kb is not None:
             cfg.direct_kb = direct_kb       # copy-free groups up to this many KiB (0: none)
+        if direct_frames is not None:
+            cfg.direct_frames = direct_frames   # ... and up to this many frames
         if params is not None:
             cfg.params = params
         self.params = Params.from_buffer_copy(cfg.params)

@@ -79,7 +79,11 @@ int __wrap_mosrx_classify_host_wait(mosrx_ctx *mc, int slot) { (void)mc; (void)s
 int __wrap_mosrx_classify_host_ready(mosrx_ctx *mc, int slot) { (void)mc; (void)slot; return 1; }
 int __wrap_mosrx_set_counters(mosrx_ctx *mc, int on) { (void)mc; (void)on; return 0; }
 int __wrap_mosrx_classify_host_reserve(mosrx_ctx *mc, uint64_t fb, uint32_t n) { (void)mc; (void)fb; (void)n; return 0; }
-int __wrap_mosrx_set_direct(mosrx_ctx *mc, uint64_t max_bytes) { (void)mc; (void)max_bytes; return 0; }
+int __wrap_mosrx_set_direct(mosrx_ctx *mc, uint64_t max_bytes, uint32_t max_frames)
+{
+	(void)mc; (void)max_bytes; (void)max_frames;
+	return 0;
+}
 int __wrap_mosrx_slot_direct(mosrx_ctx *mc, int slot) { (void)mc; (void)slot; return 0; }
 
 int __wrap_mosrx_bpf_set(mosrx_ctx *mc, const mosrx_bpf_prog *progs, uint32_t nprog)

@@ -39,7 +39,7 @@ void __wrap_mosrx_close(mosrx_ctx *c) { free(c); }
 int __wrap_mosrx_host_alloc(mosrx_ctx *c, size_t bytes, void **p) { (void)c; *p = calloc(1, bytes); return *p ? 0 : -12; }
 int __wrap_mosrx_host_free(mosrx_ctx *c, void *p) { (void)c; free(p); return 0; }
 int __wrap_mosrx_set_counters(mosrx_ctx *c, int on) { (void)c; (void)on; return 0; }
-int __wrap_mosrx_set_direct(mosrx_ctx *c, uint64_t b) { (void)c; (void)b; return 0; }
+int __wrap_mosrx_set_direct(mosrx_ctx *c, uint64_t b, uint32_t f) { (void)c; (void)b; (void)f; return 0; }
 int __wrap_mosrx_classify_host_reserve(mosrx_ctx *c, uint64_t fb, uint32_t n) { (void)c; (void)fb; (void)n; return 0; }
 
 static void *init_thread(void *arg)

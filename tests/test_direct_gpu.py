@@ -159,9 +159,9 @@ def test_direct_reads_what_the_host_rewrote(gpu_ctx, memory):
 
 
 def test_direct_only_within_its_bounds(gpu_ctx):
-    """A group over the byte limit, a frame buffer off 16-byte alignment, or
-    pageable input is copied as before (slot_direct false), and its records are
-    the same."""
+    """A group over the byte or frame limit, a frame buffer off 16-byte
+    alignment, or pageable input is copied as before (slot_direct false), and
+    its records are the same."""
     t = mosrx.Trace(mosrx.TRACE_IMIX, 8_000, nflows=300, seed=4)
     gpu_ctx.set_params(mosrx.default_params())
     base, arr = gpu_ctx.host_alloc(8 << 20)
@@ -170,13 +170,14 @@ def test_direct_only_within_its_bounds(gpu_ctx):
         batches, parts = _stage(arr, base, t, 1)
         total = batches[0].frames_bytes + 6 * t.n
         ora = O.classify(parts[0][0][:parts[0][3]], parts[0][1], parts[0][2], O.params())
-        for limit, direct in ((total, True), (total - 1, False), (0, False)):
-            gpu_ctx.set_direct(limit)
+        for limit, frames, direct in ((total, t.n, True), (total - 1, t.n, False), (0, t.n, False),
+                                      (total, t.n - 1, False)):
+            gpu_ctx.set_direct(limit, frames)
             rec[...] = np.zeros(t.n, mosrx.RESULT_DTYPE)
             gpu_ctx.group_submit_ex(0, batches, [rp])
             gpu_ctx.group_wait(0)
-            assert gpu_ctx.slot_direct(0) == direct, limit
-            assert_records_equal(rec, ora, f"limit {limit}")
+            assert gpu_ctx.slot_direct(0) == direct, (limit, frames)
+            assert_records_equal(rec, ora, f"limit {limit} / {frames}")
         gpu_ctx.set_direct(BIG)
         # frames 2 bytes past a 16-byte boundary (offsets relative to the buffer),
         # descriptors aligned elsewhere in the block

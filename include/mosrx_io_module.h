@@ -236,9 +236,12 @@ typedef struct mosrx_gpu_module_cfg {
 	                                                 * MOSRX_DIRECT_DEFAULT_FRAMES) */
 } mosrx_gpu_module_cfg;
 #define MOSRX_GROUP_AUTO        0
-#define MOSRX_DIRECT_DEFAULT_FRAMES 16384   /* 64 B frames at 90 % load: auto groups of 31-49K frames
-                                             * read in place ran at the host's edge and once overloaded
-                                             * (p50 31 ms, profiles/r06/direct/); copied they hold */
+#define MOSRX_DIRECT_DEFAULT_FRAMES 0xFFFFFFFFu   /* no frame limit: a 16K limit made the 64 B 90 % points
+                                                   * worse (one batch per launch p50 / p99 58 / 84 -> 209 /
+                                                   * 303 us) and did not stop the auto groups' 90 % point
+                                                   * from overloading now and then, which it also does
+                                                   * with every group copied (1 run in 3 either way:
+                                                   * profiles/r06/direct/lat90_frames16k.txt) */
 #define MOSRX_DIRECT_DEFAULT_KB 16384   /* measured (profiles/r06/direct): copy-free groups cut the
                                           * light-load p50 ~3x (64 B auto at 25 %: 108 -> 34 us) and
                                           * lift 64 B one-batch launches 257 -> 297 Mpkt/s; at 90 %

@@ -142,7 +142,7 @@ def test_gpu_module_config_validation():
     # group 0 = auto: as many batches per launch as the source has ready, up to group_bytes;
     # explicit groups 1..MOSRX_MAX_GROUP (512)
     assert (cfg.batch, cfg.tx_batch, cfg.group, cfg.group_bytes, cfg.pipeline) == (32768, 64, 0, 0, 1)
-    assert (cfg.direct_kb, cfg.direct_frames) == (16384, 16384)   # copy-free groups up to 16 MiB and 16K frames
+    assert (cfg.direct_kb, cfg.direct_frames) == (16384, 0xFFFFFFFF)   # copy-free groups up to 16 MiB
     cfg.num_ifs = 1
     for field, bad in [("group", 513), ("max_frame", 63), ("num_ifs", 17), ("bpf_nprog", 33),
                        ("direct_kb", (1 << 22) + 1)]:

@@ -945,9 +945,9 @@ static int group_copy(struct slot *s, struct region *r, uint32_t nr, uint64_t *d
 
 /* Direct groups (mosrx_set_direct): a group whose frames and descriptors
  * total at most c->direct_max bytes in at most c->direct_frames frames, every
- * region in a known pinned range
- * with a device address (frame buffers 16-byte aligned, their extent rounded
- * up to 16 bytes as the kernels' buffer resources do), is read by the kernel
+ * region in a known pinned range with a device address for this context's GPU
+ * (frame buffers 16-byte aligned, their extent rounded up to 16 bytes as the
+ * kernels' buffer resources do), is read by the kernel
  * in place over PCIe: no H2D copy and no batch-table copy (the kernel reads
  * the pinned table).  Each copy of the copying path is a blit or SDMA
  * dispatch plus a queue handoff, 4-12 us apiece, ~80 us per group cycle with

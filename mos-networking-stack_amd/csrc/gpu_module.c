@@ -823,7 +823,10 @@ static int group_submit(struct gpu_priv *pv, struct if_state *is, int k, uint32_
 		return mosrx_classify_host_group_submit_c8(is->mc, k, b, nb, out8, g_cfg.flowhash ? fh : NULL);
 	if (is->nprog)
 		return mosrx_classify_host_group_submit_bpf(is->mc, k, b, nb, out, g_cfg.flowhash ? fh : NULL, mt);
-	if (nb == 1 && !g_cfg.flowhash)
+	/* one batch, no copy-free groups: the single-batch submit (no batch table:
+	 * the kernel takes the batch as arguments); with cfg.direct_kb a lone batch
+	 * takes the group path, which can run it with no copies */
+	if (nb == 1 && !g_cfg.flowhash && !g_cfg.direct_kb)
 		return mosrx_classify_host_submit_ex(is->mc, k, &b[0], out[0], ti[0]);
 	return mosrx_classify_host_group_submit_ex(is->mc, k, b, nb, out, g_cfg.tcpinfo ? ti : NULL,
 	                                           g_cfg.flowhash ? fh : NULL);

@@ -221,13 +221,15 @@ def test_direct_only_within_its_bounds(gpu_ctx):
 
 @pytest.mark.parametrize("mode", [mosrx.SRC_BEST, mosrx.SRC_FILL])
 @pytest.mark.parametrize("direct_kb", [0, 1024])
-def test_backend_small_groups_direct(mode, direct_kb):
+@pytest.mark.parametrize("group", [1, 2])
+def test_backend_small_groups_direct(mode, direct_kb, group):
     """gpu_module_func with cfg.direct_kb: groups under the limit launch copy-free
-    (stats.rx_direct_groups), lent (SRC_BEST) or staged (SRC_FILL); records and
-    frames equal the oracle over three replays either way."""
+    (stats.rx_direct_groups), lone batches included, lent (SRC_BEST) or staged
+    (SRC_FILL); records and frames equal the oracle over three replays either
+    way."""
     t = mosrx.Trace(mosrx.TRACE_IMIX, 9000, nflows=300, seed=2)
     src = mosrx.mem_source(t.frames, t.off, t.len, loops=3, mode=mode)
-    be = mosrx.GpuBackend([src], batch=1024, pipeline=True, cpu=5, group=2, direct_kb=direct_kb)
+    be = mosrx.GpuBackend([src], batch=1024, pipeline=True, cpu=5, group=group, direct_kb=direct_kb)
     try:
         ora = O.classify(t.frames, t.off, t.len, O.params())
         seen = 0
